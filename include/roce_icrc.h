@@ -1,0 +1,129 @@
+/*
+ * libroceicrc -- MI355X-native RoCEv2 Invariant-CRC engine, C ABI.
+ *
+ * What this replaces (reference = cqzhangyu/roce-test):
+ *   - calc_icrc()            p4/shuffle/shuffle_egress.p4:463-494 (the only ICRC
+ *                            arithmetic in the reference; its call is commented
+ *                            out at :669, so rewritten packets carry stale ICRCs)
+ *   - scripts/icrc/{disable,enable,query}-icrc.sh:12-41 (turn NIC ICRC checking
+ *                            off because of the above; with correct ICRCs that
+ *                            is no longer needed)
+ *   - the per-packet "ICRC of a Packet" hook python/simulator.py would call at
+ *     its wire crossings (simulator.py:49-55, 59-82) via ctypes.
+ * The reference has no FFI for this path; the signatures below follow its C++
+ * conventions instead: 0 / negative-errno returns (shuffle_endpoint.hpp:364-389,
+ * 447-471), errors reported, never aborting (logassert, common/logger.hpp:190),
+ * caller-owned buffers (huge_malloc MRs, common/huge_malloc.h:12-22).
+ *
+ * Packet convention: an "n-byte packet" is the L3 RoCEv2 packet with IPv4
+ * total_len = n: IPv4(20) || UDP(8) || BTH(12) || ext || payload+pad || ICRC(4)
+ * (p4/common/header.p4:42-112).  The ICRC covers 0xFF x 8 || L3[0, n-4) with the
+ * invariant fields masked; the returned value v is put on the wire as LE32(v)
+ * (shuffle_egress.p4:493), i.e. trailer bytes = v & 0xff, v >> 8, ...
+ *
+ * Errors: 0 = success, negative errno: -EINVAL (bad length / NULL / alignment),
+ * -ENODEV (no GPU), -ENOMEM, -EIO (HIP / RCCL failure).  Nothing aborts.
+ */
+#ifndef ROCE_ICRC_H
+#define ROCE_ICRC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RICRC_MIN_LEN 44u    /* IPv4 20 + UDP 8 + BTH 12 + ICRC 4 */
+#define RICRC_MAX_LEN 65535u /* IPv4 total_len is 16 bits */
+
+typedef struct ricrc_ctx ricrc_ctx;
+
+/* ------------------------------------------------------------ per packet (CPU)
+ * ricrc_one: ICRC of one L3 packet of n bytes (n >= 4; masks that fall beyond
+ * n-4 are skipped).  Pure, re-entrant, thread-safe.  Returns 0 for n < 4.
+ * Replaces calc_icrc() (shuffle_egress.p4:463-494) for the simulator's
+ * one-packet-at-a-time crossings, where a GPU launch would be pure overhead. */
+uint32_t ricrc_one(const uint8_t *l3, uint32_t n);
+
+/* 1 if the trailer holds the right ICRC, 0 if not, -EINVAL if n < 4 / NULL.
+ * The check NICs perform and scripts/icrc/disable-icrc.sh:27-33 turns off. */
+int ricrc_verify_one(const uint8_t *l3, uint32_t n);
+
+/* Writes the ICRC into the trailer (bytes n-4..n-1, LE32).  0 / -EINVAL. */
+int ricrc_stamp_one(uint8_t *l3, uint32_t n);
+
+/* 1 if l3 is a RoCEv2 packet this engine accepts: IPv4, IHL 5, protocol 17,
+ * UDP dport 4791, total_len == n, RICRC_MIN_LEN <= n (the ingress parser's
+ * accept path, p4/shuffle/shuffle_ingress_parser.p4:12-36, header.p4:14). */
+int ricrc_is_rocev2(const uint8_t *l3, uint32_t n);
+
+/* GF(2) helpers on the (un-inverted) CRC register -- the linear algebra behind
+ * incremental repair after header rewrites (shuffle_egress.p4:635-671):
+ *   ricrc_shift(reg, k)          = register advanced over k zero bytes
+ *   ricrc_combine(c1, c2, len2)  = ICRC-style crc32 of A||B from crc32(A),
+ *                                  crc32(B) and |B| (zlib crc32_combine). */
+uint32_t ricrc_shift(uint32_t reg, uint64_t nbytes);
+uint32_t ricrc_combine(uint32_t crc1, uint32_t crc2, uint64_t len2);
+
+/* ------------------------------------------------------------------ context
+ * n_gpus > 0: use devices 0..n_gpus-1; n_gpus < 0: every visible device;
+ * n_gpus == 0 -> -EINVAL.  No GPU -> -ENODEV (there is no CPU fallback).
+ * The context owns per-device streams, staging buffers and kernel state; it
+ * is not thread-safe (lock externally), exactly like the reference's
+ * endpoint objects. */
+int ricrc_create(ricrc_ctx **ctx, int n_gpus);
+/* Same, on an explicit device list (one process per GPU: pass {LOCAL_RANK}). */
+int ricrc_create_devices(ricrc_ctx **ctx, const int *devices, int n);
+void ricrc_destroy(ricrc_ctx *ctx);
+int ricrc_device_count(const ricrc_ctx *ctx);
+
+/* ------------------------------------------------------------- batch calls
+ * Packet i starts at base + (off ? off[i] : i * stride) + l3_offset and is
+ * len ? len[i] : (stride - l3_offset) bytes long; out[i] = its ICRC.
+ *
+ * ricrc_batch_host: host buffers in and out.  Packets are sharded over the
+ * context's GPUs by bytes, staged through pinned memory (or DMA'd directly if
+ * base was allocated by ricrc_host_alloc / is otherwise pinned), computed on
+ * the GPUs and copied back.  Synchronous.  Validates every length
+ * (RICRC_MIN_LEN..RICRC_MAX_LEN) before touching a GPU.
+ *
+ * ricrc_batch_device: device-resident batch on context device `dev`
+ * (pointers are device pointers on that device; off/len may be NULL).
+ * Asynchronous on `stream` (a hipStream_t; NULL = the context's stream for
+ * that device).  Lengths are not read on the host: a device length outside
+ * [4, RICRC_MAX_LEN] yields out[i] = 0.  16-byte aligned packet starts with a
+ * fixed length take the streaming kernel; anything else the general kernel. */
+int ricrc_batch_host(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *off, const uint32_t *len,
+                     uint32_t stride, uint64_t count, uint32_t l3_offset, uint32_t *out);
+int ricrc_batch_device(ricrc_ctx *ctx, int dev, const void *d_base, const uint64_t *d_off,
+                       const uint32_t *d_len, uint32_t stride, uint64_t count, uint32_t l3_offset,
+                       uint32_t *d_out, void *stream);
+
+/* Verify mode on the device: out[i] = 1 if packet i's trailer holds its ICRC,
+ * else 0.  Same addressing/asynchrony as ricrc_batch_device. */
+int ricrc_verify_device(ricrc_ctx *ctx, int dev, const void *d_base, const uint64_t *d_off,
+                        const uint32_t *d_len, uint32_t stride, uint64_t count, uint32_t l3_offset,
+                        uint32_t *d_out, void *stream);
+
+/* Pinned host memory for NIC-ring style buffers (the role of huge_malloc in
+ * common/huge_malloc.h:12-22).  NULL on failure. */
+void *ricrc_host_alloc(ricrc_ctx *ctx, uint64_t bytes);
+void ricrc_host_free(ricrc_ctx *ctx, void *p);
+
+/* Synthetic RoCEv2 SEND_ONLY batch generator on device `dev` (bench / tests):
+ * packet k of the buffer is global packet first+k, n bytes, at d_buf + k*stride.
+ * Header template of the reference (shuffle_ingress.p4:717-724,734-735),
+ * masked fields and payload seeded-random.  Asynchronous on `stream`. */
+int ricrc_synth_device(ricrc_ctx *ctx, int dev, uint64_t seed, uint64_t first, uint64_t count,
+                       uint32_t n, uint32_t stride, void *d_buf, void *stream);
+
+/* The context's own stream (a hipStream_t) for context device dev. */
+void *ricrc_stream(ricrc_ctx *ctx, int dev);
+
+const char *ricrc_strerror(int err);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ROCE_ICRC_H */

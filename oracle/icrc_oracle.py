@@ -1,0 +1,139 @@
+"""CPU oracle for the RoCEv2 Invariant CRC (ICRC) -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module, and only as a checker.  The product path (libroceicrc + HIP
+kernels) never routes through it.
+
+Parity status: the reference's own tests pin nothing at this boundary (it has
+no tests and its only ICRC is a disabled Tofino action), so the oracle is a
+spec restatement cross-checked three ways (zlib.crc32, a bitwise CRC-32, the
+CRC-32 residue) plus build-derived golden vectors and one hand-derived
+known-answer packet built from the reference's P4 header templates.
+-> "parity unpinned" in the sense of the task contract; see DESIGN.md §Oracle.
+
+Spec followed (all citations relative to the reference root):
+
+* ``p4/shuffle/shuffle_egress.p4:461``  ``Hash<bit<32>>(HashAlgorithm_t.CRC32)``:
+  CRC-32/IEEE, reflected poly 0xEDB88320, init 0xFFFFFFFF, xorout 0xFFFFFFFF
+  (Tofino's CRC32 preset; the SDE is not vendored -> restated, = zlib.crc32).
+* ``shuffle_egress.p4:465`` the 64-bit 0xFF..FF prefix (the masked LRH/GRH
+  stand-in of IBTA Annex A17 for RoCEv2).
+* ``shuffle_egress.p4:466-475`` IPv4: ver_ihl kept, diffserv -> 0xFF (:467),
+  total_len/id/flags kept, ttl -> 0xFF (:471), protocol kept, hdr_checksum ->
+  0xFFFF (:473), src/dst kept.
+* ``shuffle_egress.p4:477-480`` UDP: ports/length kept, checksum -> 0xFFFF.
+* ``shuffle_egress.p4:482-487`` BTH: opcode, se/m/pad/tver, pkey kept,
+  FECN/BECN/resv byte -> 0xFF (:485), dqpn and ackreq/psn kept.
+* ``shuffle_egress.p4:489-490`` every byte after BTH (extension headers,
+  payload, pad) is covered unmasked, up to the 4-byte ICRC trailer.
+* ``shuffle_egress.p4:493`` the 32-bit value is emitted byte-swapped, i.e. the
+  trailer holds the CRC little-endian.
+* Header layout offsets: ``p4/common/header.p4:42-53`` (ipv4_h, 20 B),
+  ``:67-72`` (udp_h, 8 B), ``:75-85`` (bth_h, 12 B).
+"""
+from __future__ import annotations
+
+import struct
+import zlib
+
+import numpy as np
+
+# L3 byte offsets forced to 0xFF before the CRC (shuffle_egress.p4:467,471,473,480,485)
+MASK_OFFSETS = (1, 8, 10, 11, 26, 27, 32)
+PREFIX = b"\xff" * 8                      # shuffle_egress.p4:465
+POLY_REFLECTED = 0xEDB88320
+CRC32_RESIDUE = 0x2144DF1C                # crc32(msg || LE32(crc32(msg))), any msg
+REGISTER_AFTER_PREFIX = 0xDEBB20E3        # ~crc32(8*0xFF): the rxe seed
+ROCE_UDP_PORT = 4791                      # header.p4:14
+MIN_PKT = 20 + 8 + 12 + 4                 # IPv4 + UDP + BTH + ICRC
+
+
+def masked_body(l3: bytes) -> bytes:
+    """The L3 bytes the ICRC covers, [0, n-4), with the invariant masks applied."""
+    n = len(l3)
+    if n < 4:
+        raise ValueError("packet shorter than the ICRC trailer")
+    b = bytearray(l3[: n - 4])
+    for o in MASK_OFFSETS:
+        if o < len(b):
+            b[o] = 0xFF
+    return bytes(b)
+
+
+def icrc(l3: bytes) -> int:
+    """ICRC value of one L3 RoCEv2 packet (trailer bytes = LE32 of the result).
+
+    Restates calc_icrc() (shuffle_egress.p4:463-494) with zlib's CRC-32, which
+    is the same parameter set as Tofino's HashAlgorithm_t.CRC32.
+    """
+    return zlib.crc32(PREFIX + masked_body(l3)) & 0xFFFFFFFF
+
+
+_BIT_TABLE = None
+
+
+def _crc32_bitwise(data: bytes, crc: int = 0xFFFFFFFF) -> int:
+    """Independent bit-at-a-time reflected CRC-32 register update (no table)."""
+    for byte in data:
+        crc ^= byte
+        for _ in range(8):
+            crc = (crc >> 1) ^ (POLY_REFLECTED if crc & 1 else 0)
+    return crc
+
+
+def icrc_bitwise(l3: bytes) -> int:
+    """Second, table-free formulation used to cross-check :func:`icrc`."""
+    return _crc32_bitwise(PREFIX + masked_body(l3)) ^ 0xFFFFFFFF
+
+
+def icrc_rxe(l3: bytes) -> int:
+    """Third formulation: Linux-rxe style seed 0xDEBB20E3 at IP byte 0."""
+    return _crc32_bitwise(masked_body(l3), REGISTER_AFTER_PREFIX) ^ 0xFFFFFFFF
+
+
+def residue_ok(l3: bytes) -> bool:
+    """CRC-32 over prefix||masked||trailer equals the CRC-32 residue 0x2144DF1C
+    (register 0xDEBB20E3 before xorout) iff the trailer (little-endian,
+    shuffle_egress.p4:493) holds the right ICRC."""
+    return (zlib.crc32(PREFIX + masked_body(l3) + bytes(l3[-4:])) & 0xFFFFFFFF) == CRC32_RESIDUE
+
+
+def stamp(l3: bytes) -> bytes:
+    """Return ``l3`` with its trailer replaced by the correct ICRC (LE32)."""
+    return bytes(l3[:-4]) + struct.pack("<I", icrc(l3))
+
+
+def icrc_batch(buf: np.ndarray, offsets=None, lengths=None, stride: int = 0,
+               count: int | None = None, l3_offset: int = 0) -> np.ndarray:
+    """Per-packet loop over a packed batch (same addressing as ricrc_batch_*)."""
+    mv = memoryview(np.ascontiguousarray(buf).reshape(-1).view(np.uint8))
+    if count is None:
+        count = len(offsets) if offsets is not None else len(mv) // stride
+    out = np.empty(count, dtype=np.uint32)
+    for i in range(count):
+        o = int(offsets[i]) if offsets is not None else i * stride
+        n = int(lengths[i]) if lengths is not None else stride - l3_offset
+        s = o + l3_offset
+        out[i] = icrc(mv[s: s + n].tobytes())
+    return out
+
+
+# --------------------------------------------------------------------------
+# GF(2) helpers (reflected representation: bit 31 = x^0) used by tests to
+# check the product's combine/shift helpers independently of the product.
+# --------------------------------------------------------------------------
+def gf_mul(a: int, b: int) -> int:
+    p = 0
+    for i in range(31, -1, -1):
+        if (a >> i) & 1:
+            p ^= b
+        b = (b >> 1) ^ (POLY_REFLECTED if b & 1 else 0)
+    return p
+
+
+def crc_shift(reg: int, nbytes: int) -> int:
+    """Register advanced over ``nbytes`` zero bytes (brute force)."""
+    for _ in range(nbytes):
+        for _ in range(8):
+            reg = (reg >> 1) ^ (POLY_REFLECTED if reg & 1 else 0)
+    return reg

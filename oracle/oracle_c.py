@@ -1,0 +1,78 @@
+"""ctypes binding of oracle/icrc_oracle.c -- TEST INFRASTRUCTURE ONLY.
+
+Used by tests/ (checker), __graft_entry__.smoke() (checker) and bench.py's
+cpu_baseline leg (the timed CPU port).  See icrc_oracle.c for the spec
+citations.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_SO = os.path.join(_HERE, "_build", "liboracle.so")
+_lib = None
+
+
+def build() -> str:
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+    return _SO
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_SO):
+            build()
+        L = ctypes.CDLL(_SO)
+        u8p, u32p, u64p = (ctypes.c_void_p,) * 3
+        for name in ("oracle_icrc_bitwise", "oracle_icrc_bytewise", "oracle_icrc_fast"):
+            f = getattr(L, name)
+            f.argtypes = [u8p, ctypes.c_uint32]
+            f.restype = ctypes.c_uint32
+        L.oracle_icrc_batch.argtypes = [u8p, u64p, u32p, ctypes.c_uint64, ctypes.c_uint64,
+                                        ctypes.c_uint32, u32p, ctypes.c_int, ctypes.c_int]
+        L.oracle_icrc_batch.restype = ctypes.c_int
+        L.oracle_synth_batch.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                         ctypes.c_uint32, ctypes.c_uint32, u8p]
+        L.oracle_synth_batch.restype = None
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+def icrc_one(pkt: bytes, kind: str = "fast") -> int:
+    buf = np.frombuffer(bytes(pkt), dtype=np.uint8)
+    fn = {"bitwise": lib().oracle_icrc_bitwise, "bytewise": lib().oracle_icrc_bytewise,
+          "fast": lib().oracle_icrc_fast}[kind]
+    return int(fn(buf.ctypes.data, len(pkt)))
+
+
+def icrc_batch(buf: np.ndarray, offsets=None, lengths=None, stride: int = 0, count=None,
+               l3_offset: int = 0, threads: int = 1, kind: str = "fast") -> np.ndarray:
+    buf = np.ascontiguousarray(buf).reshape(-1).view(np.uint8)
+    if offsets is not None:
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    if lengths is not None:
+        lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
+    if count is None:
+        count = len(offsets) if offsets is not None else buf.size // stride
+    out = np.empty(count, dtype=np.uint32)
+    k = {"bitwise": 0, "bytewise": 1, "fast": 2}[kind]
+    lib().oracle_icrc_batch(buf.ctypes.data, _ptr(offsets), _ptr(lengths), stride, count,
+                            l3_offset, out.ctypes.data, threads, k)
+    return out
+
+
+def synth_batch(seed: int, first: int, count: int, n: int, stride: int | None = None) -> np.ndarray:
+    """Host restatement of the device synthetic generator: (count, stride) uint8."""
+    stride = stride or n
+    buf = np.empty((count, stride), dtype=np.uint8)
+    lib().oracle_synth_batch(seed, first, count, n, stride, buf.ctypes.data)
+    return buf

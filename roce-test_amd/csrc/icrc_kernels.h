@@ -1,0 +1,50 @@
+// Kernel argument blocks and launchers shared by icrc_kernels.hip and the
+// host API (icrc_api.cpp).  Plain structs passed by value as kernargs.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ricrc {
+
+// Fixed-length batch, packet i at base + i*stride, 16-byte aligned.
+struct StreamArgs {
+  const uint8_t *base;  // first packet's L3 start
+  uint64_t stride;
+  uint64_t count;
+  uint32_t *out;
+  uint64_t n_iters;   // wave steps = ceil(count / (64 >> log2P2))
+  uint32_t len;       // n (L3 bytes incl. trailer)
+  uint32_t P;         // lanes per packet that hold data
+  uint32_t log2P2;    // lanes per packet rounded up to a power of two
+  uint32_t nw_last;   // words folded by the last lane of a packet
+  uint32_t verify;    // 0: out = ICRC, 1: out = (trailer == ICRC)
+  uint32_t K[64];     // per chunk c: x^(8 * bytes after chunk c)
+};
+
+// Any alignment / offsets / lengths.
+struct GeneralArgs {
+  const uint8_t *base;
+  const uint64_t *off;  // may be null (then p * stride)
+  const uint32_t *len;  // may be null (then fixed_len)
+  uint64_t stride;
+  uint64_t count;
+  uint32_t *out;
+  const uint32_t *inv_tab;  // x^(-8 z), z in [0, 4096)
+  uint32_t fixed_len;
+  uint32_t l3_offset;
+  uint32_t x4096;  // x^(8*4096)
+  uint32_t verify;
+  uint32_t K[64];  // x^(8*64*(63-lane))
+};
+
+struct SynthArgs {
+  uint8_t *buf;
+  uint64_t seed, first, count;
+  uint32_t n, stride;  // stride % 8 == 0, n <= stride
+};
+
+hipError_t launch_stream(const StreamArgs &a, int cpl, int grid, hipStream_t st);
+hipError_t launch_general(const GeneralArgs &a, int grid, hipStream_t st);
+hipError_t launch_synth(const SynthArgs &a, hipStream_t st);
+
+}  // namespace ricrc

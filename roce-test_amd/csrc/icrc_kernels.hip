@@ -1,0 +1,420 @@
+// gfx950 (MI355X / CDNA4) ICRC kernels of libroceicrc.
+//
+// Computes calc_icrc() of the reference (p4/shuffle/shuffle_egress.p4:463-494)
+// for whole batches of independent RoCEv2 packets held in HBM.  It is an
+// HBM-read-bound byte scan: no MFMA, one LDS table lookup per payload byte.
+//
+// Execution model:
+//  * Persistent grid, one 1024-thread workgroup (16 waves) per CU.  Each
+//    workgroup first builds 128 KiB of slice-by-4 CRC tables in LDS, then its
+//    waves stream packets until the batch is done.
+//  * LDS table layout: 32 copies of each 256-entry table, interleaved so that
+//    entry e of copy c sits at byte (e << 8) | (c << 2) of its 64 KiB region:
+//    ds_read_b32 from lane l hits bank (l & 31) whatever e is -> conflict
+//    free, and the address is ONE v_perm_b32 (the state byte lands in bits
+//    8..15, the lane's copy offset in bits 0..7, region in bit 16).
+//  * A lane folds one contiguous 64*CPL-byte chunk of a packet from a zero
+//    register (slice-by-4: 4 perms, 4 ds_read_b32, 2 v_bitop3 per word).
+//    Lane registers are re-aligned to the packet end by a GF(2) multiply by
+//    a per-lane constant x^(8 d) (32 x {v_bfe_i32, v_bitop3}) and XOR-reduced
+//    across the lanes of the packet with wave shuffles.
+//  * The 8 x 0xFF prefix is the start register 0xDEBB20E3, injected by XOR
+//    into the first data word (reg 0 ^ word ^ seed == seed-started fold).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "icrc_kernels.h"
+#include "icrc_math.h"
+
+namespace ricrc {
+
+__device__ constexpr SliceTables<4> g_tab = make_tables<4>();
+
+static constexpr int kWaves = 16;       // waves per workgroup
+static constexpr int kBlock = 64 * kWaves;
+static constexpr int kLdsWords = 32768;  // 128 KiB
+
+// ---------------------------------------------------------------- helpers
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ uint32_t and_xor(uint32_t a, uint32_t b, uint32_t c) {  // (a & b) ^ c
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x6A);
+}
+__device__ __forceinline__ uint32_t or_xor(uint32_t a, uint32_t b, uint32_t c) {  // (a | b) ^ c
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x56);
+}
+
+// Build the LDS tables: region 0 = {T3 | T2}, region 1 = {T1 | T0}, 256-byte
+// rows of 32 copies x 4 B per half.
+__device__ __forceinline__ void fill_tables(uint32_t *lds) {
+  for (int i = threadIdx.x; i < kLdsWords; i += blockDim.x) {
+    const int region = i >> 14, e = (i >> 6) & 255, half = (i >> 5) & 1;
+    const int t = region ? (half ? 0 : 1) : (half ? 2 : 3);
+    lds[i] = g_tab.t[t][e];
+  }
+}
+
+struct LaneTab {
+  uint32_t lo0, lo1;  // copy offsets for region 0 / region 1
+};
+
+__device__ __forceinline__ uint32_t lds_at(const uint32_t *lds, uint32_t byte_addr) {
+  return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(lds) + byte_addr);
+}
+
+// One slice-by-4 step: register after folding word w into register r.
+__device__ __forceinline__ uint32_t step4(const uint32_t *lds, LaneTab lt, uint32_t r, uint32_t w) {
+  const uint32_t x = r ^ w;
+  const uint32_t t3 = lds_at(lds, __builtin_amdgcn_perm(x, lt.lo0, 0x0C0C0400u));
+  const uint32_t t2 = lds_at(lds, __builtin_amdgcn_perm(x, lt.lo0, 0x0C0C0500u) + 128);
+  const uint32_t t1 = lds_at(lds, __builtin_amdgcn_perm(x, lt.lo1, 0x0C020600u));
+  const uint32_t t0 = lds_at(lds, __builtin_amdgcn_perm(x, lt.lo1, 0x0C020700u) + 128);
+  return xor3(t3, t2, xor3(t1, t0, 0u));
+}
+
+// r * K where Q[j] = K * x^(31-j) (bit j of r is the x^(31-j) coefficient).
+__device__ __forceinline__ uint32_t mul_basis(uint32_t r, const uint32_t (&Q)[32]) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (int j = 0; j < 32; ++j) {
+    const uint32_t m = (uint32_t)(((int32_t)(r << (31 - j))) >> 31);
+    acc = and_xor(m, Q[j], acc);
+  }
+  return acc;
+}
+
+__device__ __forceinline__ void make_basis(uint32_t K, uint32_t (&Q)[32]) {
+  Q[31] = K;
+#pragma unroll
+  for (int j = 30; j >= 0; --j) Q[j] = gf_mulx(Q[j + 1]);
+}
+
+__device__ __forceinline__ uint32_t gf_mul_dev(uint32_t a, uint32_t b) {
+  uint32_t p = 0;
+#pragma unroll 8
+  for (int i = 31; i >= 0; --i) {
+    const uint32_t m = (uint32_t)(((int32_t)(a << (31 - i))) >> 31);
+    p = and_xor(m, b, p);
+    b = gf_mulx(b);
+  }
+  return p;
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t word_of(const u32x4 &v, int i) { return v[i]; }
+
+// =======================================================================
+// Streaming kernel: fixed length, 16-byte aligned packet starts.
+// Lanes 0..P-1 of each group of P2 = 2^log2P2 lanes take consecutive
+// 64*CPL-byte chunks of one packet; a wave covers 64/P2 packets per step.
+// =======================================================================
+template <int CPL, bool PIPE>
+__global__ __launch_bounds__(kBlock) void icrc_stream_kernel(StreamArgs a) {
+  __shared__ uint32_t lds[kLdsWords];
+  fill_tables(lds);
+  __syncthreads();
+
+  constexpr int NP = 4 * CPL;   // 16-byte pieces per lane
+  constexpr int NW = 16 * CPL;  // words per lane
+  const int lane = threadIdx.x & 63;
+  const LaneTab lt{(uint32_t)(lane & 31) << 2, ((uint32_t)(lane & 31) << 2) | 0x10000u};
+  const uint32_t P2m1 = (1u << a.log2P2) - 1u;
+  const uint32_t c = lane & P2m1;      // chunk index inside the packet
+  const uint32_t g = lane >> a.log2P2;  // packet slot inside the wave
+  const uint32_t ppw = 64u >> a.log2P2;
+  const bool lane_valid = c < a.P;
+  const bool is_last = c + 1 == a.P;
+  const uint32_t nw_lane = !lane_valid ? 0u : is_last ? a.nw_last : (uint32_t)NW;
+
+  // First-chunk lanes apply the invariant masks and inject the seed.
+  const bool first = c == 0;
+  const uint32_t m0 = first ? kMaskW0 : 0u, m2 = first ? kMaskW2 : 0u;
+  const uint32_t m6 = first ? kMaskW6 : 0u, m8 = first ? kMaskW8 : 0u;
+  const uint32_t x0 = first ? kSeed : 0u;
+
+  uint32_t Q[32];
+  const bool multi = a.P > 1;
+  if (multi) make_basis(lane_valid ? a.K[c] : 0u, Q);
+
+  const uint64_t wave = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
+
+  // Loads are unconditional (no exec-masked branches, so the compiler can
+  // keep the next step's loads in flight with a counted vmcnt): lanes past
+  // the packet's data re-read their last 16-byte piece, lanes past the batch
+  // re-read the last packet.  Every address is a 16-byte aligned piece that
+  // holds at least one byte of a real packet, so it never leaves the buffer.
+  const uint32_t c_eff = lane_valid ? c : a.P - 1u;
+  const uint32_t kmax = (c_eff + 1 == a.P) ? (a.nw_last - 1u) >> 2 : (uint32_t)(NP - 1);
+  uint32_t poff[NP];
+#pragma unroll
+  for (int k = 0; k < NP; ++k) poff[k] = c_eff * (64u * CPL) + 16u * ((uint32_t)k < kmax ? (uint32_t)k : kmax);
+
+  auto load = [&](uint64_t it, u32x4 (&v)[NP]) {
+    const uint64_t p0 = it * ppw;  // wave-uniform first packet of this step
+    const uint64_t left = a.count - 1 - p0;
+    const uint32_t g_eff = (uint64_t)g < left ? g : (uint32_t)left;
+    const uint8_t *wbase = a.base + p0 * a.stride;
+    const uint32_t loff = g_eff * (uint32_t)a.stride;
+#pragma unroll
+    for (int k = 0; k < NP; ++k)
+      v[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(wbase + (loff + poff[k])));
+  };
+
+  auto fold = [&](uint64_t it, const u32x4 (&v)[NP]) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int j = 0; j < NW; ++j) {
+      uint32_t w = word_of(v[j >> 2], j & 3);
+      if (j == 0) w = or_xor(w, m0, x0);
+      if (j == 2) w |= m2;
+      if (j == 6) w |= m6;
+      if (j == 8) w |= m8;
+      const uint32_t rn = step4(lds, lt, r, w);
+      // Words below nw_last are valid in every valid lane (wave-uniform test);
+      // invalid lanes fold zeros into a zero register, which stays zero.
+      if ((uint32_t)j < a.nw_last) r = rn;
+      else r = ((uint32_t)j < nw_lane) ? rn : r;
+    }
+    if (multi) {
+      r = mul_basis(r, Q);
+      for (uint32_t s = 1; s <= P2m1; s <<= 1) r ^= __shfl_xor(r, (int)s);
+    }
+    // Every lane of a packet group holds the full register after the
+    // butterfly, and lanes past the batch recomputed the last packet, so all
+    // lanes store (identical values to identical addresses): no exec-masked
+    // store, no vmcnt drain at a branch join.
+    const uint64_t p0 = it * ppw;
+    const uint64_t left = a.count - 1 - p0;
+    const uint64_t p = p0 + ((uint64_t)g < left ? (uint64_t)g : left);
+    const uint32_t v_icrc = ~r;
+    if (a.verify) {
+      const uint32_t tr = *reinterpret_cast<const uint32_t *>(a.base + p * a.stride + a.len - 4);
+      a.out[p] = (tr == v_icrc) ? 1u : 0u;
+    } else {
+      a.out[p] = v_icrc;
+    }
+  };
+
+  if (PIPE) {
+    u32x4 cur[NP], nxt[NP];
+    uint64_t it = wave;
+    if (it < a.n_iters) load(it, cur);
+    for (; it < a.n_iters; it += nwaves) {
+      // Unconditional prefetch (the last step re-loads itself) so the compiler
+      // counts vmcnt exactly instead of draining at a branch join.
+      const uint64_t itn = it + nwaves < a.n_iters ? it + nwaves : it;
+      load(itn, nxt);
+      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the fold
+      fold(it, cur);
+#pragma unroll
+      for (int k = 0; k < NP; ++k) cur[k] = nxt[k];
+    }
+  } else {
+    for (uint64_t it = wave; it < a.n_iters; it += nwaves) {
+      u32x4 v[NP];
+      load(it, v);
+      fold(it, v);
+    }
+  }
+}
+
+// =======================================================================
+// General kernel: any alignment, per-packet offsets and/or lengths.
+// One wave per packet; the packet's bytes are covered by 4 KiB windows
+// aligned to 16 B below the packet start.  Bytes outside the packet are
+// zero, so the wave computes the register at the window end; windows are
+// chained with x^(8*4096) and the zero tail is removed with x^(-8 z).
+// =======================================================================
+__device__ __forceinline__ uint32_t byte_span_mask(int lo, int hi) {  // bytes [lo,hi) of a word
+  if (hi <= lo) return 0u;
+  const uint32_t h = hi >= 4 ? 0xFFFFFFFFu : ((1u << (8 * hi)) - 1u);
+  const uint32_t l = lo <= 0 ? 0u : ((1u << (8 * lo)) - 1u);
+  return h & ~l;
+}
+
+__device__ __forceinline__ uint32_t expand_nibble(uint32_t b) {
+  return ((b & 1u) ? 0x000000FFu : 0u) | ((b & 2u) ? 0x0000FF00u : 0u) | ((b & 4u) ? 0x00FF0000u : 0u) |
+         ((b & 8u) ? 0xFF000000u : 0u);
+}
+
+__global__ __launch_bounds__(kBlock) void icrc_general_kernel(GeneralArgs a) {
+  __shared__ uint32_t lds[kLdsWords];
+  fill_tables(lds);
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  const LaneTab lt{(uint32_t)(lane & 31) << 2, ((uint32_t)(lane & 31) << 2) | 0x10000u};
+  uint32_t Q[32];
+  make_basis(a.K[lane], Q);  // x^(8*64*(63-lane)): lane end -> window end
+
+  const uint64_t wave = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
+
+  for (uint64_t p = wave; p < a.count; p += nwaves) {
+    const uint64_t off = a.off ? a.off[p] : p * (uint64_t)a.stride;
+    const uint32_t n = a.len ? a.len[p] : a.fixed_len;
+    if (n < 4 || n > kMaxLen) {
+      if (lane == 0) a.out[p] = 0u;
+      continue;
+    }
+    const int M = (int)n - 4;
+    const uintptr_t start = (uintptr_t)a.base + off + a.l3_offset;
+    const uintptr_t a0 = start & ~(uintptr_t)15;
+    const int s = (int)(start - a0);
+    const int T = s + M;
+    const int nwin = T > 0 ? (T + 4095) >> 12 : 1;
+
+    uint32_t R = 0;
+    for (int w = 0; w < nwin; ++w) {
+      const uintptr_t lb = a0 + ((uintptr_t)w << 12) + ((uintptr_t)lane << 6);
+      const int rel0 = (int)(lb - start);  // packet-relative offset of the lane's first byte
+      u32x4 v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int pr = rel0 + 16 * k;
+        v[k] = u32x4{0u, 0u, 0u, 0u};
+        if (pr < M && pr + 16 > 0) v[k] = *reinterpret_cast<const u32x4 *>(lb + 16 * k);
+      }
+      const bool interior = rel0 >= 40 && rel0 + 64 <= M;
+      uint32_t r = 0;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        uint32_t wd = word_of(v[j >> 2], j & 3);
+        if (!interior) {
+          const int rel = rel0 + 4 * j;
+          const uint32_t vm = byte_span_mask(-rel, M - rel);
+          uint32_t mb = 0u;
+          if (rel > -4 && rel < 40) {
+            const uint64_t bits = rel >= 0 ? (kMaskBits >> rel) : (kMaskBits << (-rel));
+            mb = expand_nibble((uint32_t)bits & 0xFu) & vm;
+          }
+          uint32_t xp = 0u;
+          if (rel > -4 && rel < 4) xp = rel >= 0 ? (kSeed >> (8 * rel)) : (kSeed << (-8 * rel));
+          wd = ((wd & vm) | mb) ^ xp;
+        }
+        r = step4(lds, lt, r, wd);
+      }
+      r = mul_basis(r, Q);
+#pragma unroll
+      for (int sft = 1; sft < 64; sft <<= 1) r ^= __shfl_xor(r, sft);
+      R = w == 0 ? r : (gf_mul_dev(R, a.x4096) ^ r);
+    }
+    const int z = (nwin << 12) - T;  // zero bytes folded past the packet end
+    R = gf_mul_dev(R, a.inv_tab[z]);
+    if (lane == 0) {
+      const uint32_t v_icrc = ~R;
+      if (a.verify) {
+        const uint8_t *tb = reinterpret_cast<const uint8_t *>(start) + M;
+        const uint32_t tr = (uint32_t)tb[0] | ((uint32_t)tb[1] << 8) | ((uint32_t)tb[2] << 16) |
+                            ((uint32_t)tb[3] << 24);
+        a.out[p] = (tr == v_icrc) ? 1u : 0u;
+      } else {
+        a.out[p] = v_icrc;
+      }
+    }
+  }
+}
+
+// =======================================================================
+// Synthetic SEND_ONLY generator (bench/tests; restated on the CPU by
+// oracle/icrc_oracle.c:oracle_synth_packet).  One thread per 8-byte block.
+// =======================================================================
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ void synth_kernel(SynthArgs a) {
+  const uint64_t bpp = a.stride >> 3;  // 8-byte blocks per packet slot
+  const uint64_t total = a.count * bpp;
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = t / bpp, j = t - k * bpp, i = a.first + k;
+    uint64_t r = mix64(mix64(a.seed + i) + j);
+    const uint32_t b0 = (uint32_t)(j * 8);
+    if (b0 + 8 > a.n) {
+      const uint32_t keep = a.n > b0 ? a.n - b0 : 0u;
+      r = keep ? (r & (~0ull >> (64 - 8 * keep))) : 0ull;
+    }
+    if (b0 < 40 && a.n >= 40) {
+      uint8_t b[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) b[q] = (uint8_t)(r >> (8 * q));
+      const uint32_t n = a.n;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const uint32_t o = b0 + q;
+        uint8_t x = b[q];
+        switch (o) {
+          case 0: x = 0x45; break;
+          case 2: x = (uint8_t)(n >> 8); break;
+          case 3: x = (uint8_t)n; break;
+          case 4: x = 0x12; break;
+          case 5: x = 0x34; break;
+          case 6: x = 0x40; break;
+          case 7: x = 0x00; break;
+          case 9: x = 17; break;
+          case 12: x = 192; break;
+          case 13: x = 168; break;
+          case 14: x = 1; break;
+          case 15: x = 100; break;
+          case 16: x = 192; break;
+          case 17: x = 168; break;
+          case 18: x = 1; break;
+          case 19: x = (uint8_t)(1 + (i & 3)); break;
+          case 20: x = 0x45; break;
+          case 21: x = 0x7b; break;
+          case 22: x = 0x12; break;
+          case 23: x = 0xb7; break;
+          case 24: x = (uint8_t)((n - 20) >> 8); break;
+          case 25: x = (uint8_t)(n - 20); break;
+          case 28: x = 0x04; break;
+          case 29: x = 0x40; break;
+          case 30: x = 0xff; break;
+          case 31: x = 0xff; break;
+          case 36: x = 0; break;
+          case 37: x = (uint8_t)(i >> 16); break;
+          case 38: x = (uint8_t)(i >> 8); break;
+          case 39: x = (uint8_t)i; break;
+          default: break;
+        }
+        b[q] = x;
+      }
+      r = 0;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) r |= (uint64_t)b[q] << (8 * q);
+    }
+    *reinterpret_cast<uint64_t *>(a.buf + k * a.stride + j * 8) = r;
+  }
+}
+
+// ----------------------------------------------------------- host launchers
+hipError_t launch_stream(const StreamArgs &a, int cpl, int grid, hipStream_t st) {
+  const bool pipe = cpl == 1;
+  if (cpl == 1 && pipe) hipLaunchKernelGGL((icrc_stream_kernel<1, true>), dim3(grid), dim3(kBlock), 0, st, a);
+  else if (cpl == 2) hipLaunchKernelGGL((icrc_stream_kernel<2, false>), dim3(grid), dim3(kBlock), 0, st, a);
+  else if (cpl == 4) hipLaunchKernelGGL((icrc_stream_kernel<4, false>), dim3(grid), dim3(kBlock), 0, st, a);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t launch_general(const GeneralArgs &a, int grid, hipStream_t st) {
+  hipLaunchKernelGGL(icrc_general_kernel, dim3(grid), dim3(kBlock), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_synth(const SynthArgs &a, hipStream_t st) {
+  const uint64_t total = a.count * (a.stride >> 3);
+  uint64_t blocks = (total + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL(synth_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace ricrc

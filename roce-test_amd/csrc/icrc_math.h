@@ -1,0 +1,103 @@
+// GF(2) arithmetic and CRC-32 tables shared by the host library and the
+// gfx950 kernels of libroceicrc.
+//
+// Representation: the reflected CRC-32 register (poly 0xEDB88320, the
+// HashAlgorithm_t.CRC32 of p4/shuffle/shuffle_egress.p4:461).  Bit 31 of a
+// 32-bit value is the coefficient of x^0, bit 0 the coefficient of x^31, so
+// "advance the register over one zero bit" is multiplication by x.
+//
+// The register is linear over GF(2):   reg(A || B) = reg(A) * x^(8|B|) ^ reg0(B)
+// (reg0 = register started from 0).  Every kernel in this library is built on
+// that identity: lanes fold independent chunks from a zero register and the
+// partial registers are re-aligned by a multiplication by x^(8 d).
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define RICRC_HD __host__ __device__
+#else
+#define RICRC_HD
+#endif
+
+namespace ricrc {
+
+constexpr uint32_t kPoly = 0xEDB88320u;
+constexpr uint32_t kOne = 0x80000000u;          // x^0
+constexpr uint32_t kSeed = 0xDEBB20E3u;         // register after 8 x 0xFF from ~0 (shuffle_egress.p4:465)
+constexpr uint32_t kMinLen = 20 + 8 + 12 + 4;   // IPv4 + UDP + BTH + ICRC
+constexpr uint32_t kMaxLen = 65535;             // IPv4 total_len is 16 bits (header.p4:45)
+
+// Invariant-field masks as bits of a 64-bit "byte is forced to 0xFF" map over
+// L3 bytes [0,40): tos 1, ttl 8, IPv4 csum 10-11, UDP csum 26-27, BTH byte 4
+// at 32 (shuffle_egress.p4:467,471,473,480,485).
+constexpr uint64_t kMaskBits = (1ull << 1) | (1ull << 8) | (1ull << 10) | (1ull << 11) |
+                               (1ull << 26) | (1ull << 27) | (1ull << 32);
+// The same masks as little-endian OR-words for 4-aligned words 0, 2, 6, 8.
+constexpr uint32_t kMaskW0 = 0x0000FF00u;
+constexpr uint32_t kMaskW2 = 0xFFFF00FFu;
+constexpr uint32_t kMaskW6 = 0xFFFF0000u;
+constexpr uint32_t kMaskW8 = 0x000000FFu;
+
+RICRC_HD constexpr uint32_t gf_mulx(uint32_t a) { return (a >> 1) ^ ((a & 1u) ? kPoly : 0u); }
+
+// a * b mod P, both reflected.
+RICRC_HD constexpr uint32_t gf_mul(uint32_t a, uint32_t b) {
+  uint32_t p = 0;
+  for (int i = 31; i >= 0; --i) {
+    if ((a >> i) & 1u) p ^= b;
+    b = gf_mulx(b);
+  }
+  return p;
+}
+
+// x^(8 n) mod P by square-and-multiply.
+RICRC_HD constexpr uint32_t gf_x8n(uint64_t n) {
+  uint32_t r = kOne, sq = kOne >> 8;  // x^8
+  while (n) {
+    if (n & 1u) r = gf_mul(r, sq);
+    sq = gf_mul(sq, sq);
+    n >>= 1;
+  }
+  return r;
+}
+
+// x^-1 mod P = (P(x) + 1) / x: in normal order x^31 + (0x04C11DB7 >> 1);
+// reflected, that is bit 0 plus the reflected poly shifted left by one.
+constexpr uint32_t kXInv = (kPoly << 1) | 1u;
+
+// x^(-8 n) mod P.
+RICRC_HD constexpr uint32_t gf_xinv8n(uint64_t n) {
+  uint32_t r = kOne, sq = gf_mul(gf_mul(gf_mul(kXInv, kXInv), gf_mul(kXInv, kXInv)),
+                                 gf_mul(gf_mul(kXInv, kXInv), gf_mul(kXInv, kXInv)));
+  while (n) {
+    if (n & 1u) r = gf_mul(r, sq);
+    sq = gf_mul(sq, sq);
+    n >>= 1;
+  }
+  return r;
+}
+
+// Slice-by-N tables: T[k][b] = register after byte b followed by k zero
+// bytes, from a zero register (T[0] is the classic Sarwate table).
+template <int N>
+struct SliceTables {
+  uint32_t t[N][256];
+};
+
+template <int N>
+constexpr SliceTables<N> make_tables() {
+  SliceTables<N> s{};
+  for (uint32_t b = 0; b < 256; ++b) {
+    uint32_t c = b;
+    for (int k = 0; k < 8; ++k) c = (c >> 1) ^ ((c & 1u) ? kPoly : 0u);
+    s.t[0][b] = c;
+  }
+  for (int k = 1; k < N; ++k)
+    for (uint32_t b = 0; b < 256; ++b) s.t[k][b] = (s.t[k - 1][b] >> 8) ^ s.t[0][s.t[k - 1][b] & 0xFFu];
+  return s;
+}
+
+static_assert(gf_mul(kXInv, kOne >> 1) == kOne, "x * x^-1 must be 1");
+static_assert(make_tables<1>().t[0][1] == 0x77073096u, "Sarwate table");
+
+}  // namespace ricrc

@@ -1,0 +1,197 @@
+"""GPU parity: the gfx950 kernels (through the C ABI) against the CPU oracle.
+
+Bit-exact comparison on the same bytes: integer arithmetic, no tolerance.
+Inputs are built on the host (numpy, seeded) or by the device generator,
+copied where needed, and every kernel result is compared with
+oracle/icrc_oracle.c (itself pinned to zlib / the golden vectors by
+tests/test_oracle.py).  Covers the streaming kernel (fixed length, 16-B
+aligned), the general kernel (offsets, ragged lengths, any alignment,
+multi-window jumbo packets, Ethernet l3_offset), verify mode, the host-buffer
+path, and the full BASELINE headline size (1 M x 4096 B).
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import oracle_c  # noqa: E402
+import icrc_oracle  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0x1CEC0DE
+
+
+def _dev(a: np.ndarray):
+    return torch.from_numpy(np.ascontiguousarray(a)).to("cuda")
+
+
+def _out(count):
+    return torch.empty(count, dtype=torch.int32, device="cuda")
+
+
+def _host_u32(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy().view(np.uint32)
+
+
+def _stream():
+    return torch.cuda.current_stream()
+
+
+@pytest.mark.parametrize("n", [48, 64, 128, 256, 512, 1024, 1520, 2048, 4096, 4112, 8192, 9008, 16384])
+def test_stream_kernel_fixed(ctx, n):
+    count = 3000 if n <= 4096 else 600
+    host = oracle_c.synth_batch(SEED, 0, count, n)
+    want = oracle_c.icrc_batch(host, stride=n, threads=8)
+    d = _dev(host)
+    out = _out(count)
+    ctx.batch_device(d, count, out, stride=n, stream=_stream())
+    got = _host_u32(out)
+    np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("count", [1, 2, 63, 64, 65, 4097])
+def test_stream_kernel_tails(ctx, count):
+    """Partial last wave-steps and tiny batches (lanes past the batch)."""
+    for n in (64, 1024, 4096):
+        host = oracle_c.synth_batch(SEED + count, 7, count, n)
+        want = oracle_c.icrc_batch(host, stride=n)
+        out = _out(count)
+        ctx.batch_device(_dev(host), count, out, stride=n, stream=_stream())
+        np.testing.assert_array_equal(_host_u32(out), want)
+
+
+def test_device_synth_matches_host_restatement(ctx):
+    for n, stride in ((64, 64), (1024, 1024), (4096, 4096), (1000, 1008)):
+        count = 257
+        d = torch.empty(count * stride, dtype=torch.uint8, device="cuda")
+        ctx.synth_device(d, SEED, 1000, count, n, stride, stream=_stream())
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(d.cpu().numpy().reshape(count, stride),
+                                      oracle_c.synth_batch(SEED, 1000, count, n, stride))
+
+
+def _ragged(rng, count, lo, hi, align, l3_offset=0):
+    lens = rng.integers(lo, hi + 1, size=count).astype(np.uint32)
+    offs = np.zeros(count, dtype=np.uint64)
+    pos = int(rng.integers(0, 16))
+    for i in range(count):
+        pos += int(rng.integers(0, 40))
+        if align:
+            pos = (pos + align - 1) // align * align
+        offs[i] = pos
+        pos += int(lens[i]) + l3_offset
+    buf = rng.integers(0, 256, size=pos + 64, dtype=np.uint8)
+    return buf, offs, lens
+
+
+@pytest.mark.parametrize("lo,hi,align", [(4, 64, 1), (44, 300, 1), (44, 4096, 4), (44, 4096, 16),
+                                         (3000, 9100, 1), (9000, 20000, 1), (44, 65535, 1)])
+def test_general_kernel_ragged(ctx, lo, hi, align):
+    rng = np.random.default_rng(lo * 7 + hi)
+    count = 400 if hi <= 9100 else 40
+    buf, offs, lens = _ragged(rng, count, lo, hi, align)
+    want = oracle_c.icrc_batch(buf, offsets=offs, lengths=lens)
+    out = _out(count)
+    ctx.batch_device(_dev(buf), count, out, offsets=_dev(offs), lengths=_dev(lens), stream=_stream())
+    np.testing.assert_array_equal(_host_u32(out), want)
+
+
+def test_general_kernel_ethernet_offset(ctx):
+    """l3_offset = 14: L3 starts 2 bytes past a 16-byte boundary."""
+    rng = np.random.default_rng(14)
+    count, n = 500, 1024
+    frames = rng.integers(0, 256, size=(count, n + 14 + 2), dtype=np.uint8)  # 1040-B slots
+    stride = frames.shape[1]
+    want = oracle_c.icrc_batch(frames, stride=stride, l3_offset=14)
+    out = _out(count)
+    ctx.batch_device(_dev(frames), count, out, stride=stride, l3_offset=14, stream=_stream())
+    np.testing.assert_array_equal(_host_u32(out), want)
+
+
+def test_general_kernel_invalid_lengths_zero(ctx):
+    buf = np.arange(256, dtype=np.uint8)
+    offs = np.array([0, 16, 32], dtype=np.uint64)
+    lens = np.array([3, 0, 100], dtype=np.uint32)
+    out = _out(3)
+    ctx.batch_device(_dev(buf), 3, out, offsets=_dev(offs), lengths=_dev(lens), stream=_stream())
+    got = _host_u32(out)
+    assert got[0] == 0 and got[1] == 0
+    assert got[2] == icrc_oracle.icrc(buf[32:132].tobytes())
+
+
+@pytest.mark.parametrize("n", [64, 1024, 4096, 1000])
+def test_verify_mode(ctx, n):
+    """Stamp with the oracle, corrupt some packets, verify on the GPU."""
+    count = 1000
+    stride = (n + 15) // 16 * 16 if n % 16 else n
+    host = oracle_c.synth_batch(SEED, 0, count, n, stride)
+    icrcs = oracle_c.icrc_batch(host, stride=stride) if n == stride else \
+        oracle_c.icrc_batch(host, offsets=np.arange(count, dtype=np.uint64) * stride,
+                            lengths=np.full(count, n, np.uint32))
+    host[:, n - 4:n] = icrcs.view(np.uint8).reshape(count, 4)
+    bad = np.arange(0, count, 7)
+    flip_pos = 40 + (bad * 13) % (n - 44)   # an unmasked covered byte
+    host[bad, flip_pos] ^= 0x10
+    out = _out(count)
+    if n == stride:
+        ctx.batch_device(_dev(host), count, out, stride=n, stream=_stream(), verify=True)
+    else:
+        ctx.batch_device(_dev(host), count, out, offsets=_dev(np.arange(count, dtype=np.uint64) * stride),
+                         lengths=_dev(np.full(count, n, np.uint32)), stream=_stream(), verify=True)
+    got = _host_u32(out)
+    want = np.ones(count, np.uint32)
+    want[bad] = 0
+    np.testing.assert_array_equal(got, want)
+
+
+def test_mask_invariance_on_gpu(ctx):
+    """Changing tos/ttl/checksums/FECN byte must not change the device ICRC."""
+    count, n = 512, 1024
+    host = oracle_c.synth_batch(SEED, 0, count, n)
+    out1, out2 = _out(count), _out(count)
+    ctx.batch_device(_dev(host), count, out1, stride=n, stream=_stream())
+    for o in icrc_oracle.MASK_OFFSETS:
+        host[:, o] ^= 0x5A
+    ctx.batch_device(_dev(host), count, out2, stride=n, stream=_stream())
+    np.testing.assert_array_equal(_host_u32(out1), _host_u32(out2))
+
+
+def test_batch_host_paths(ctx):
+    rng = np.random.default_rng(5)
+    count, n = 2000, 4096
+    host = oracle_c.synth_batch(SEED, 0, count, n)
+    np.testing.assert_array_equal(ctx.batch_host(host, stride=n), oracle_c.icrc_batch(host, stride=n))
+    buf, offs, lens = _ragged(rng, 1500, 44, 4096, 1)
+    np.testing.assert_array_equal(ctx.batch_host(buf, offs, lens),
+                                  oracle_c.icrc_batch(buf, offsets=offs, lengths=lens))
+
+
+def test_batch_host_rejects_bad_lengths(ctx):
+    import roce_icrc
+
+    buf = np.zeros(4096, np.uint8)
+    with pytest.raises(roce_icrc.ICRCError):
+        ctx.batch_host(buf, offsets=np.array([0], np.uint64), lengths=np.array([43], np.uint32))
+
+
+@pytest.mark.slow
+def test_headline_full_size_bit_exact(ctx):
+    """BASELINE headline: 1,048,576 x 4096 B generated on the device, every
+    ICRC compared with the C oracle on the very same bytes (copied back)."""
+    count, n = 1 << 20, 4096
+    d = torch.empty(count * n, dtype=torch.uint8, device="cuda")
+    ctx.synth_device(d, SEED, 0, count, n, stream=_stream())
+    out = _out(count)
+    ctx.batch_device(d, count, out, stride=n, stream=_stream())
+    got = _host_u32(out)
+    host = d.cpu().numpy()
+    want = oracle_c.icrc_batch(host, stride=n, threads=16)
+    np.testing.assert_array_equal(got, want)
+    # size-independent check: stamping every ICRC makes every residue verify
+    host_pk = host.reshape(count, n)
+    host_pk[:, n - 4:] = got.view(np.uint8).reshape(count, 4)
+    d.copy_(torch.from_numpy(host))
+    ctx.batch_device(d, count, out, stride=n, stream=_stream(), verify=True)
+    assert int(_host_u32(out).sum()) == count
