@@ -42,7 +42,7 @@ struct Dev {
   int id = 0;
   int n_cu = 0;
   hipStream_t stream = nullptr;
-  uint32_t *d_inv = nullptr;  // x^(-8 z), z < 4096
+  uint32_t *d_inv = nullptr;  // x^(-8 z), z <= 4096
   Slot slot[2];
   bool staged = false;
 };
@@ -88,15 +88,15 @@ int init_dev(Dev &d) {
   HIP_TRY(hipGetDeviceProperties(&prop, d.id));
   d.n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
-  std::vector<uint32_t> inv(4096);
+  std::vector<uint32_t> inv(4097);  // z in [0, 4096]
   const uint32_t step = gf_xinv8n(1);
   uint32_t v = kOne;
-  for (int z = 0; z < 4096; ++z) {
+  for (int z = 0; z <= 4096; ++z) {
     inv[z] = v;
     v = gf_mul(v, step);
   }
-  HIP_TRY(hipMalloc(&d.d_inv, 4096 * sizeof(uint32_t)));
-  HIP_TRY(hipMemcpy(d.d_inv, inv.data(), 4096 * sizeof(uint32_t), hipMemcpyHostToDevice));
+  HIP_TRY(hipMalloc(&d.d_inv, 4097 * sizeof(uint32_t)));
+  HIP_TRY(hipMemcpy(d.d_inv, inv.data(), 4097 * sizeof(uint32_t), hipMemcpyHostToDevice));
   return 0;
 }
 

@@ -29,7 +29,7 @@ struct GeneralArgs {
   uint64_t stride;
   uint64_t count;
   uint32_t *out;
-  const uint32_t *inv_tab;  // x^(-8 z), z in [0, 4096)
+  const uint32_t *inv_tab;  // x^(-8 z), z in [0, 4096]
   uint32_t fixed_len;
   uint32_t l3_offset;
   uint32_t x4096;  // x^(8*4096)
