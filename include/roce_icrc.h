@@ -89,8 +89,8 @@ int ricrc_device_count(const ricrc_ctx *ctx);
  *
  * ricrc_batch_device: device-resident batch on context device `dev`
  * (pointers are device pointers on that device; off/len may be NULL).
- * Asynchronous on `stream` (a hipStream_t; NULL = the context's stream for
- * that device).  Lengths are not read on the host: a device length outside
+ * Asynchronous on `stream` (a hipStream_t; NULL = the HIP null stream;
+ * ricrc_stream() returns the context's own non-blocking stream).  Lengths are not read on the host: a device length outside
  * [4, RICRC_MAX_LEN] yields out[i] = 0.  16-byte aligned packet starts with a
  * fixed length take the streaming kernel; anything else the general kernel. */
 int ricrc_batch_host(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *off, const uint32_t *len,

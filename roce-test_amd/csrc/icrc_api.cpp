@@ -259,7 +259,7 @@ static int batch_device_impl(ricrc_ctx *ctx, int dev, const void *d_base, const 
   Dev &d = ctx->devs[dev];
   DeviceGuard g(d.id);
   if (!g.ok()) return -ENODEV;
-  hipStream_t st = stream ? (hipStream_t)stream : d.stream;
+  hipStream_t st = (hipStream_t)stream;  // NULL = the HIP null stream, like any HIP API
   return launch_batch(d, (const uint8_t *)d_base, d_off, d_len, stride, count, l3_offset, d_out, st, verify);
 }
 
@@ -283,7 +283,7 @@ int ricrc_synth_device(ricrc_ctx *ctx, int dev, uint64_t seed, uint64_t first, u
   DeviceGuard g(d.id);
   if (!g.ok()) return -ENODEV;
   SynthArgs a{(uint8_t *)d_buf, seed, first, count, n, stride};
-  return hip_err(launch_synth(a, stream ? (hipStream_t)stream : d.stream));
+  return hip_err(launch_synth(a, (hipStream_t)stream));
 }
 
 void *ricrc_host_alloc(ricrc_ctx *ctx, uint64_t bytes) {

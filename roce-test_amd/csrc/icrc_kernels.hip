@@ -229,6 +229,8 @@ __global__ __launch_bounds__(kBlock) void icrc_stream_kernel(StreamArgs a) {
 // chained with x^(8*4096) and the zero tail is removed with x^(-8 z).
 // =======================================================================
 __device__ __forceinline__ uint32_t byte_span_mask(int lo, int hi) {  // bytes [lo,hi) of a word
+  lo = lo < 0 ? 0 : lo;
+  hi = hi > 4 ? 4 : hi;
   if (hi <= lo) return 0u;
   const uint32_t h = hi >= 4 ? 0xFFFFFFFFu : ((1u << (8 * hi)) - 1u);
   const uint32_t l = lo <= 0 ? 0u : ((1u << (8 * lo)) - 1u);

@@ -1,0 +1,110 @@
+"""CPU check of the decomposition the gfx950 kernels use (no GPU needed).
+
+Both kernels split a packet into lane chunks folded from a zero register,
+re-align each chunk register with a GF(2) multiply by x^(8 d) and XOR the
+results; the general kernel additionally zero-extends the packet to 4 KiB
+windows (chained by x^(8*4096)) and removes the zero tail with x^(-8 z).
+These tests restate that algebra in pure Python -- using the oracle's
+independent gf_mul / crc_shift -- and check it against zlib on random
+packets, so a mistake in the *math* is caught on the CPU, before any GPU run.
+"""
+import random
+import zlib
+
+import icrc_oracle as o
+
+POLY = o.POLY_REFLECTED
+ONE = 0x80000000
+SEED_REG = o.REGISTER_AFTER_PREFIX
+
+
+def fold(reg, data: bytes):
+    for b in data:
+        reg ^= b
+        for _ in range(8):
+            reg = (reg >> 1) ^ (POLY if reg & 1 else 0)
+    return reg
+
+
+def x8n(n):
+    return o.crc_shift(ONE, n)
+
+
+def xinv():
+    return ((POLY << 1) & 0xFFFFFFFF) | 1
+
+
+def xinv8n(n):
+    r, s = ONE, xinv()
+    for _ in range(8 * n):
+        r = o.gf_mul(r, s)
+    return r
+
+
+def masked(pkt):
+    return bytearray(o.masked_body(pkt))
+
+
+def test_inverse_of_x():
+    assert o.gf_mul(xinv(), ONE >> 1) == ONE
+    for n in (1, 3, 17):
+        assert o.gf_mul(xinv8n(n), x8n(n)) == ONE
+
+
+def test_stream_kernel_decomposition():
+    """Lane c folds bytes [chunk*c, chunk*(c+1)) from 0 (lane 0 with the seed
+    injected into its first word); K_c = x^(8 * bytes after chunk c)."""
+    rng = random.Random(1)
+    for n in (44, 64, 100, 1024, 1500, 4096):
+        pkt = bytes(rng.randrange(256) for _ in range(n))
+        m = masked(pkt)
+        M = len(m)
+        for chunk in (64, 128, 256):
+            P = -(-M // chunk)
+            acc = 0
+            for c in range(P):
+                part = bytearray(m[chunk * c: min(chunk * (c + 1), M)])
+                if c == 0:
+                    for k in range(4):
+                        part[k] ^= (SEED_REG >> (8 * k)) & 0xFF
+                r = fold(0, part)
+                acc ^= o.gf_mul(r, x8n(M - min(chunk * (c + 1), M)))
+            assert acc ^ 0xFFFFFFFF == zlib.crc32(o.PREFIX + bytes(m))
+
+
+def test_general_kernel_decomposition():
+    """Zero-extended 4 KiB windows from a 16-byte aligned base below the
+    packet, seed injected at the packet start, tail removed by x^(-8 z)."""
+    rng = random.Random(2)
+    for n in (4, 5, 8, 44, 61, 300, 4096, 4100, 9001):
+        pkt = bytes(rng.randrange(256) for _ in range(n))
+        m = masked(pkt)
+        M = len(m)
+        for s in (0, 2, 7, 15):  # start offset above the aligned base
+            T = s + M
+            nwin = max(1, -(-T // 4096))
+            D = bytearray(4096 * nwin)
+            D[s: s + M] = m
+            for k in range(4):
+                D[s + k] ^= (SEED_REG >> (8 * k)) & 0xFF
+            R = 0
+            for w in range(nwin):
+                win = D[4096 * w: 4096 * (w + 1)]
+                Rw = 0
+                for lane in range(64):
+                    r = fold(0, win[64 * lane: 64 * lane + 64])
+                    Rw ^= o.gf_mul(r, x8n(64 * (63 - lane)))
+                R = Rw if w == 0 else (o.gf_mul(R, x8n(4096)) ^ Rw)
+            z = 4096 * nwin - T
+            R = o.gf_mul(R, xinv8n(z)) if z <= 64 else o.gf_mul(R, _xinv8n_fast(z))
+            assert R ^ 0xFFFFFFFF == zlib.crc32(o.PREFIX + bytes(m)), (n, s)
+
+
+def _xinv8n_fast(n):
+    r, sq, e = ONE, xinv8n(1), n
+    while e:
+        if e & 1:
+            r = o.gf_mul(r, sq)
+        sq = o.gf_mul(sq, sq)
+        e >>= 1
+    return r
