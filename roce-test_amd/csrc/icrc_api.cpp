@@ -9,6 +9,7 @@
 #include <errno.h>
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -170,6 +171,10 @@ int launch_batch(Dev &d, const uint8_t *base, const uint64_t *off, const uint32_
       }
       const uint64_t want = (a.n_iters + 15) / 16;
       const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)d.n_cu, want));
+      // Back-to-back packets of 64 * 2^j bytes: coalesced + LDS-transposed kernel.
+      const bool tsk = cpl == 1 && l3_offset == 0 && stride == fixed_len && (1u << a.log2P2) * 64u == stride &&
+                       ((uintptr_t)base % 16 == 0) && getenv("RICRC_NO_TSK") == nullptr;
+      if (tsk) return hip_err(launch_tsk(a, grid, st));
       return hip_err(launch_stream(a, cpl, grid, st));
     }
   }

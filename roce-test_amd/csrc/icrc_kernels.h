@@ -44,6 +44,7 @@ struct SynthArgs {
 };
 
 hipError_t launch_stream(const StreamArgs &a, int cpl, int grid, hipStream_t st);
+hipError_t launch_tsk(const StreamArgs &a, int grid, hipStream_t st);
 hipError_t launch_general(const GeneralArgs &a, int grid, hipStream_t st);
 hipError_t launch_synth(const SynthArgs &a, hipStream_t st);
 

@@ -160,7 +160,7 @@ __global__ __launch_bounds__(kBlock) void icrc_stream_kernel(StreamArgs a) {
     const uint32_t loff = g_eff * (uint32_t)a.stride;
 #pragma unroll
     for (int k = 0; k < NP; ++k)
-      v[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(wbase + (loff + poff[k])));
+      v[k] = *reinterpret_cast<const u32x4 *>(wbase + (loff + poff[k]));
   };
 
   auto fold = [&](uint64_t it, const u32x4 (&v)[NP]) {
@@ -218,6 +218,118 @@ __global__ __launch_bounds__(kBlock) void icrc_stream_kernel(StreamArgs a) {
       load(it, v);
       fold(it, v);
     }
+  }
+}
+
+
+// =======================================================================
+// Transposed streaming kernel (TSK): the headline path.
+// Packets of n = 64*P2 bytes (P2 = 1..64) back to back, so one wave step is
+// a contiguous 4 KiB region.  It is read with fully coalesced non-temporal
+// 16-byte buffer loads (lane l gets bytes 1024k + 16l: the only pattern that
+// streams at ~7 TB/s on MI355X -- the per-lane-chunk pattern with nt drops
+// to ~3.7 TB/s), then re-laid through a wave-private 2 KiB LDS
+// slot so each lane again holds one contiguous 64-byte chunk.  Loads that
+// would pass the end of the batch read zeros and out-of-batch stores are
+// dropped by the buffer range check, so the loop has no exec-masked memory
+// operation (no vmcnt drain at branch joins) and prefetches one step ahead.
+// =======================================================================
+static constexpr int kStageBytes = 2048;  // per wave
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+// Swizzled 16-byte slot of piece p inside a 2 KiB staging round: writes of 8
+// consecutive pieces stay in one 128-byte row, and the 4-piece chunk reads of
+// a ds_read_b128 lane group land in 16 distinct bank quads.
+__device__ __forceinline__ uint32_t stage_slot(uint32_t p) { return (p & ~3u) | ((p ^ (p >> 4)) & 3u); }
+
+__global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(StreamArgs a) {
+  __shared__ uint32_t lds[kLdsWords + kWaves * kStageBytes / 4];
+  fill_tables(lds);
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  char *stage = reinterpret_cast<char *>(lds) + kLdsWords * 4 + wid * kStageBytes;
+  const LaneTab lt{(uint32_t)(lane & 31) << 2, ((uint32_t)(lane & 31) << 2) | 0x10000u};
+  const uint32_t P2m1 = (1u << a.log2P2) - 1u;
+  const uint32_t c = lane & P2m1;
+  const uint32_t g = lane >> a.log2P2;
+  const uint32_t ppw = 64u >> a.log2P2;
+  const bool is_last = c == P2m1;
+  const bool first = c == 0;
+  const uint32_t m0 = first ? kMaskW0 : 0u, m2 = first ? kMaskW2 : 0u;
+  const uint32_t m6 = first ? kMaskW6 : 0u, m8 = first ? kMaskW8 : 0u;
+  const uint32_t x0 = first ? kSeed : 0u;
+  const bool multi = P2m1 != 0;
+  uint32_t Q[32];
+  if (multi) make_basis(a.K[c], Q);
+
+  // Staging addresses (bytes, relative to the wave's slot).
+  const uint32_t wr0 = 16u * stage_slot((uint32_t)lane), wr1 = 16u * stage_slot(64u + (uint32_t)lane);
+  uint32_t rd[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) rd[j] = 16u * stage_slot(4u * (uint32_t)(lane & 31) + j);
+  const int half = lane >> 5;
+
+  const uint64_t wave = (uint64_t)blockIdx.x * kWaves + wid;
+  const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
+  const uint64_t total = a.count * a.stride;
+
+  auto load = [&](uint64_t it, u32x4 (&v)[4]) {
+    const uint64_t off = it * 4096u;
+    const uint32_t rem = off < total ? (uint32_t)(total - off < 4096u ? total - off : 4096u) : 0u;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(a.base + (off < total ? off : 0), rem);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      v[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 1024 * k + 16 * lane, 0, 2));
+  };
+
+  auto step_it = [&](uint64_t it, const u32x4 (&v)[4]) {
+    u32x4 ch[4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      *reinterpret_cast<u32x4 *>(stage + wr0) = v[2 * h];
+      *reinterpret_cast<u32x4 *>(stage + wr1) = v[2 * h + 1];
+      if (half == h) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ch[j] = *reinterpret_cast<const u32x4 *>(stage + rd[j]);
+      }
+    }
+    uint32_t r = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      uint32_t w = ch[j >> 2][j & 3];
+      if (j == 0) w = or_xor(w, m0, x0);
+      if (j == 2) w |= m2;
+      if (j == 6) w |= m6;
+      if (j == 8) w |= m8;
+      const uint32_t rn = step4(lds, lt, r, w);
+      r = (j < 15 || !is_last) ? rn : r;  // the last lane's word 15 is the trailer
+    }
+    if (multi) {
+      r = mul_basis(r, Q);
+      for (uint32_t sft = 1; sft <= P2m1; sft <<= 1) r ^= __shfl_xor(r, (int)sft);
+    }
+    const uint32_t v_icrc = ~r;
+    const uint32_t val = a.verify ? (ch[3][3] == v_icrc ? 1u : 0u) : v_icrc;
+    const uint64_t p0 = it * ppw;
+    const uint32_t nout = p0 < a.count ? (uint32_t)(a.count - p0 < ppw ? a.count - p0 : ppw) : 0u;
+    const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out + (p0 < a.count ? p0 : 0), 4u * nout);
+    __builtin_amdgcn_raw_buffer_store_b32(val, ro, is_last ? 4u * g : 0x7FFFFFF0u, 0, 0);
+  };
+
+  uint64_t it = wave;
+  u32x4 cur[4], nxt[4];
+  load(it, cur);
+  for (; it < a.n_iters; it += nwaves) {
+    load(it + nwaves, nxt);  // past the batch: zero-length resource, reads 0
+    __builtin_amdgcn_sched_barrier(0);
+    step_it(it, cur);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
   }
 }
 
@@ -402,6 +514,11 @@ hipError_t launch_stream(const StreamArgs &a, int cpl, int grid, hipStream_t st)
   else if (cpl == 2) hipLaunchKernelGGL((icrc_stream_kernel<2, false>), dim3(grid), dim3(kBlock), 0, st, a);
   else if (cpl == 4) hipLaunchKernelGGL((icrc_stream_kernel<4, false>), dim3(grid), dim3(kBlock), 0, st, a);
   else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t launch_tsk(const StreamArgs &a, int grid, hipStream_t st) {
+  hipLaunchKernelGGL(icrc_tsk_kernel, dim3(grid), dim3(kBlock), 0, st, a);
   return hipGetLastError();
 }
 
