@@ -171,10 +171,27 @@ int launch_batch(Dev &d, const uint8_t *base, const uint64_t *off, const uint32_
       }
       const uint64_t want = (a.n_iters + 15) / 16;
       const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)d.n_cu, want));
-      // Back-to-back packets of 64 * 2^j bytes: coalesced + LDS-transposed kernel.
-      const bool tsk = cpl == 1 && l3_offset == 0 && stride == fixed_len && (1u << a.log2P2) * 64u == stride &&
-                       ((uintptr_t)base % 16 == 0) && getenv("RICRC_NO_TSK") == nullptr;
-      if (tsk) return hip_err(launch_tsk(a, grid, st));
+      // Back-to-back packets of 32 * 2^j bytes: coalesced + LDS-transposed kernel.
+      if (l3_offset == 0 && stride == fixed_len && fixed_len >= 64 && fixed_len <= 4096 &&
+          (fixed_len & (fixed_len - 1)) == 0 && ((uintptr_t)base % 16 == 0) && getenv("RICRC_NO_TSK") == nullptr) {
+        TskArgs t{};
+        t.base = base;
+        t.stride = stride;
+        t.count = count;
+        t.out = out;
+        t.n_iters = (count * stride + 4095) / 4096;
+        t.log2C = (uint32_t)ilog2_ceil(fixed_len / 32);
+        t.verify = verify ? 1u : 0u;
+        for (uint32_t p = 0; p < 128; ++p) {
+          const int64_t dd = (int64_t)M - 32 * (int64_t)(p + 1);
+          t.K[p] = p < fixed_len / 32 ? (dd >= 0 ? gf_x8n((uint64_t)dd) : gf_xinv8n((uint64_t)-dd)) : 0u;
+        }
+        const uint32_t y = gf_x8n(2048);
+        for (int j = 0; j < 32; ++j) t.YB[j] = gf_mul(y, 1u << j);
+        const uint64_t tw = (t.n_iters + 15) / 16;
+        const int tgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)d.n_cu, tw));
+        return hip_err(launch_tsk(t, tgrid, st));
+      }
       return hip_err(launch_stream(a, cpl, grid, st));
     }
   }

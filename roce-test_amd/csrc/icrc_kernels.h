@@ -21,6 +21,20 @@ struct StreamArgs {
   uint32_t K[64];     // per chunk c: x^(8 * bytes after chunk c)
 };
 
+// Back-to-back packets of n = 32 * 2^log2C bytes (2 <= 2^log2C <= 128),
+// 16-byte aligned: the coalesced + LDS-transposed kernel.
+struct TskArgs {
+  const uint8_t *base;
+  uint64_t stride;  // == n
+  uint64_t count;
+  uint32_t *out;
+  uint64_t n_iters;  // 4 KiB regions = ceil(count * n / 4096)
+  uint32_t log2C;
+  uint32_t verify;
+  uint32_t K[128];   // per chunk position: x^(8 (n - 4 - 32 (pos + 1)))
+  uint32_t YB[32];   // x^(8*2048) * x^(31-j): uniform basis for 4 KiB packets
+};
+
 // Any alignment / offsets / lengths.
 struct GeneralArgs {
   const uint8_t *base;
@@ -44,7 +58,7 @@ struct SynthArgs {
 };
 
 hipError_t launch_stream(const StreamArgs &a, int cpl, int grid, hipStream_t st);
-hipError_t launch_tsk(const StreamArgs &a, int grid, hipStream_t st);
+hipError_t launch_tsk(const TskArgs &a, int grid, hipStream_t st);
 hipError_t launch_general(const GeneralArgs &a, int grid, hipStream_t st);
 hipError_t launch_synth(const SynthArgs &a, hipStream_t st);
 

@@ -224,15 +224,19 @@ __global__ __launch_bounds__(kBlock) void icrc_stream_kernel(StreamArgs a) {
 
 // =======================================================================
 // Transposed streaming kernel (TSK): the headline path.
-// Packets of n = 64*P2 bytes (P2 = 1..64) back to back, so one wave step is
-// a contiguous 4 KiB region.  It is read with fully coalesced non-temporal
-// 16-byte buffer loads (lane l gets bytes 1024k + 16l: the only pattern that
-// streams at ~7 TB/s on MI355X -- the per-lane-chunk pattern with nt drops
-// to ~3.7 TB/s), then re-laid through a wave-private 2 KiB LDS
-// slot so each lane again holds one contiguous 64-byte chunk.  Loads that
-// would pass the end of the batch read zeros and out-of-batch stores are
-// dropped by the buffer range check, so the loop has no exec-masked memory
-// operation (no vmcnt drain at branch joins) and prefetches one step ahead.
+// Packets of n = 32*C bytes (C = 2..128 chunks of 32 B) back to back, so a
+// wave step is one contiguous 4 KiB region.  It is read with fully
+// coalesced non-temporal 16-byte buffer loads (lane l gets bytes 1024k+16l:
+// the only pattern that streams at ~7 TB/s on MI355X -- per-lane-chunk
+// loads with nt drop to ~3.7 TB/s) and re-laid through a
+// wave-private 2 KiB LDS slot in two rounds, so that in round h every lane
+// holds the contiguous 32-byte chunk 64h+l.  Each lane then folds its two
+// chunks as two independent 8-step chains (ILP against LDS latency).
+// Chunk registers are re-aligned by x^(8 d) with d = M - 32(pos+1) (the
+// packet's trailer word is zeroed, so the last chunk has d = -4, x^-32), and
+// XOR-reduced with DPP / permlane swaps (no LDS).  Loads past the batch read
+// zeros and out-of-batch stores are dropped by the buffer range check, so
+// the loop has no exec-masked memory op and prefetches one step ahead.
 // =======================================================================
 static constexpr int kStageBytes = 2048;  // per wave
 
@@ -240,39 +244,64 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, ui
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, (int)bytes, 0x00020000);
 }
 
-// Swizzled 16-byte slot of piece p inside a 2 KiB staging round: writes of 8
-// consecutive pieces stay in one 128-byte row, and the 4-piece chunk reads of
-// a ds_read_b128 lane group land in 16 distinct bank quads.
-__device__ __forceinline__ uint32_t stage_slot(uint32_t p) { return (p & ~3u) | ((p ^ (p >> 4)) & 3u); }
+// Swizzled 16-byte slot of piece p in a 2 KiB round: the 8-lane groups of
+// ds_write_b128 stay in one 128-byte row, and the 32-byte chunk reads of each
+// 16-lane ds_read_b128 group hit 16 distinct bank quads.
+__device__ __forceinline__ uint32_t stage_slot(uint32_t p) { return p ^ ((p >> 4) & 1u); }
 
-__global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(StreamArgs a) {
+// XOR of v over aligned groups of 2^levels lanes, result in every lane.
+__device__ __forceinline__ uint32_t group_xor(uint32_t v, uint32_t levels) {
+  if (levels > 0) v ^= __builtin_amdgcn_update_dpp(0u, v, 0xB1, 0xF, 0xF, true);   // quad_perm [1,0,3,2]
+  if (levels > 1) v ^= __builtin_amdgcn_update_dpp(0u, v, 0x4E, 0xF, 0xF, true);   // quad_perm [2,3,0,1]
+  if (levels > 2) v ^= __builtin_amdgcn_update_dpp(0u, v, 0x141, 0xF, 0xF, true);  // row_half_mirror
+  if (levels > 3) v ^= __builtin_amdgcn_update_dpp(0u, v, 0x140, 0xF, 0xF, true);  // row_mirror
+  if (levels > 4) {
+    const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    v = p[0] ^ p[1];
+  }
+  if (levels > 5) {
+    const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    v = p[0] ^ p[1];
+  }
+  return v;
+}
+
+// Per-lane word constants for one chain at packet chunk position pos.
+struct ChunkMask {
+  uint32_t mw0, xw0, m2, m6, keep7;
+};
+__device__ __forceinline__ ChunkMask chunk_mask(uint32_t pos, uint32_t last) {
+  ChunkMask m;
+  m.mw0 = pos == 0 ? kMaskW0 : (pos == 1 ? kMaskW8 : 0u);  // bytes 1 / 32
+  m.xw0 = pos == 0 ? kSeed : 0u;
+  m.m2 = pos == 0 ? kMaskW2 : 0u;
+  m.m6 = pos == 0 ? kMaskW6 : 0u;
+  m.keep7 = pos == last ? 0u : 0xFFFFFFFFu;  // trailer word of the packet
+  return m;
+}
+
+__global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
   __shared__ uint32_t lds[kLdsWords + kWaves * kStageBytes / 4];
   fill_tables(lds);
   __syncthreads();
 
-  const int lane = threadIdx.x & 63;
+  const uint32_t lane = threadIdx.x & 63;
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   char *stage = reinterpret_cast<char *>(lds) + kLdsWords * 4 + wid * kStageBytes;
-  const LaneTab lt{(uint32_t)(lane & 31) << 2, ((uint32_t)(lane & 31) << 2) | 0x10000u};
-  const uint32_t P2m1 = (1u << a.log2P2) - 1u;
-  const uint32_t c = lane & P2m1;
-  const uint32_t g = lane >> a.log2P2;
-  const uint32_t ppw = 64u >> a.log2P2;
-  const bool is_last = c == P2m1;
-  const bool first = c == 0;
-  const uint32_t m0 = first ? kMaskW0 : 0u, m2 = first ? kMaskW2 : 0u;
-  const uint32_t m6 = first ? kMaskW6 : 0u, m8 = first ? kMaskW8 : 0u;
-  const uint32_t x0 = first ? kSeed : 0u;
-  const bool multi = P2m1 != 0;
+  const LaneTab lt{(lane & 31) << 2, ((lane & 31) << 2) | 0x10000u};
+  const uint32_t log2C = a.log2C, Cm1 = (1u << log2C) - 1u;
+  const bool big = log2C == 7;  // 4 KiB packets: one packet per region
+  const uint32_t pos0 = big ? lane : (lane & Cm1), pos1 = big ? 64u + lane : (lane & Cm1);
+  const ChunkMask c0 = chunk_mask(pos0, Cm1), c1 = chunk_mask(pos1, Cm1);
+  const bool store0 = !big && pos0 == Cm1, store1 = pos1 == Cm1;
+  const uint32_t pk0 = big ? 0u : lane >> log2C, pk1 = big ? 0u : (64u + lane) >> log2C;
+  const uint32_t ppr = big ? 1u : 128u >> log2C;  // packets per 4 KiB region
+  const uint32_t levels = big ? 6u : log2C;
   uint32_t Q[32];
-  if (multi) make_basis(a.K[c], Q);
+  make_basis(a.K[pos1], Q);
 
-  // Staging addresses (bytes, relative to the wave's slot).
-  const uint32_t wr0 = 16u * stage_slot((uint32_t)lane), wr1 = 16u * stage_slot(64u + (uint32_t)lane);
-  uint32_t rd[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) rd[j] = 16u * stage_slot(4u * (uint32_t)(lane & 31) + j);
-  const int half = lane >> 5;
+  const uint32_t wr0 = 16u * stage_slot(lane), wr1 = 16u * stage_slot(64u + lane);
+  const uint32_t rd0 = 16u * stage_slot(2u * lane), rd1 = 16u * stage_slot(2u * lane + 1u);
 
   const uint64_t wave = (uint64_t)blockIdx.x * kWaves + wid;
   const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
@@ -288,37 +317,47 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(StreamArgs a) {
   };
 
   auto step_it = [&](uint64_t it, const u32x4 (&v)[4]) {
-    u32x4 ch[4];
+    u32x4 ch[2][2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       *reinterpret_cast<u32x4 *>(stage + wr0) = v[2 * h];
       *reinterpret_cast<u32x4 *>(stage + wr1) = v[2 * h + 1];
-      if (half == h) {
+      ch[h][0] = *reinterpret_cast<const u32x4 *>(stage + rd0);
+      ch[h][1] = *reinterpret_cast<const u32x4 *>(stage + rd1);
+    }
+    const uint32_t tr0 = ch[0][1][3], tr1 = ch[1][1][3];  // trailer words (last chunks)
+    ch[0][0][0] = or_xor(ch[0][0][0], c0.mw0, c0.xw0);
+    ch[1][0][0] = or_xor(ch[1][0][0], c1.mw0, c1.xw0);
+    ch[0][0][2] |= c0.m2;
+    ch[1][0][2] |= c1.m2;
+    ch[0][1][2] |= c0.m6;
+    ch[1][1][2] |= c1.m6;
+    ch[0][1][3] &= c0.keep7;
+    ch[1][1][3] &= c1.keep7;
+    uint32_t r0 = 0, r1 = 0;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) ch[j] = *reinterpret_cast<const u32x4 *>(stage + rd[j]);
-      }
+    for (int j = 0; j < 8; ++j) {
+      r0 = step4(lds, lt, r0, ch[0][j >> 2][j & 3]);
+      r1 = step4(lds, lt, r1, ch[1][j >> 2][j & 3]);
     }
-    uint32_t r = 0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      uint32_t w = ch[j >> 2][j & 3];
-      if (j == 0) w = or_xor(w, m0, x0);
-      if (j == 2) w |= m2;
-      if (j == 6) w |= m6;
-      if (j == 8) w |= m8;
-      const uint32_t rn = step4(lds, lt, r, w);
-      r = (j < 15 || !is_last) ? rn : r;  // the last lane's word 15 is the trailer
-    }
-    if (multi) {
-      r = mul_basis(r, Q);
-      for (uint32_t sft = 1; sft <= P2m1; sft <<= 1) r ^= __shfl_xor(r, (int)sft);
-    }
-    const uint32_t v_icrc = ~r;
-    const uint32_t val = a.verify ? (ch[3][3] == v_icrc ? 1u : 0u) : v_icrc;
-    const uint64_t p0 = it * ppw;
-    const uint32_t nout = p0 < a.count ? (uint32_t)(a.count - p0 < ppw ? a.count - p0 : ppw) : 0u;
+    const uint64_t p0 = it * ppr;
+    const uint32_t nout = p0 < a.count ? (uint32_t)(a.count - p0 < ppr ? a.count - p0 : ppr) : 0u;
     const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out + (p0 < a.count ? p0 : 0), 4u * nout);
-    __builtin_amdgcn_raw_buffer_store_b32(val, ro, is_last ? 4u * g : 0x7FFFFFF0u, 0, 0);
+    if (big) {
+      uint32_t acc = 0;  // r0 * x^(8*2048): chunk 64h+l sits 2 KiB before chunk 64+l
+#pragma unroll
+      for (int j = 0; j < 32; ++j) acc = and_xor((uint32_t)(((int32_t)(r0 << (31 - j))) >> 31), a.YB[j], acc);
+      const uint32_t r = group_xor(mul_basis(acc ^ r1, Q), 6);
+      const uint32_t val = a.verify ? (tr1 == ~r ? 1u : 0u) : ~r;
+      __builtin_amdgcn_raw_buffer_store_b32(val, ro, store1 ? 0u : 0x7FFFFFF0u, 0, 0);
+    } else {
+      const uint32_t s0 = group_xor(mul_basis(r0, Q), levels);
+      const uint32_t s1 = group_xor(mul_basis(r1, Q), levels);
+      const uint32_t v0 = a.verify ? (tr0 == ~s0 ? 1u : 0u) : ~s0;
+      const uint32_t v1 = a.verify ? (tr1 == ~s1 ? 1u : 0u) : ~s1;
+      __builtin_amdgcn_raw_buffer_store_b32(v0, ro, store0 ? 4u * pk0 : 0x7FFFFFF0u, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(v1, ro, store1 ? 4u * pk1 : 0x7FFFFFF0u, 0, 0);
+    }
   };
 
   uint64_t it = wave;
@@ -517,7 +556,7 @@ hipError_t launch_stream(const StreamArgs &a, int cpl, int grid, hipStream_t st)
   return hipGetLastError();
 }
 
-hipError_t launch_tsk(const StreamArgs &a, int grid, hipStream_t st) {
+hipError_t launch_tsk(const TskArgs &a, int grid, hipStream_t st) {
   hipLaunchKernelGGL(icrc_tsk_kernel, dim3(grid), dim3(kBlock), 0, st, a);
   return hipGetLastError();
 }
