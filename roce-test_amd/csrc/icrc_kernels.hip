@@ -70,18 +70,29 @@ __device__ __forceinline__ uint32_t step4(const uint32_t *lds, LaneTab lt, uint3
   const uint32_t t2 = lds_at(lds, __builtin_amdgcn_perm(x, lt.lo0, 0x0C0C0500u) + 128);
   const uint32_t t1 = lds_at(lds, __builtin_amdgcn_perm(x, lt.lo1, 0x0C020600u));
   const uint32_t t0 = lds_at(lds, __builtin_amdgcn_perm(x, lt.lo1, 0x0C020700u) + 128);
-  return xor3(t3, t2, xor3(t1, t0, 0u));
+  return xor3(t3, t2, t1 ^ t0);
+}
+
+// Same step, but returns (register ^ next word) directly: the word XOR rides
+// in the second v_bitop3, so a step is 4 v_perm + 2 v_bitop3 + 4 ds_read_b32.
+__device__ __forceinline__ uint32_t step4x(const uint32_t *lds, LaneTab lt, uint32_t x, uint32_t wnext) {
+  const uint32_t t3 = lds_at(lds, __builtin_amdgcn_perm(x, lt.lo0, 0x0C0C0400u));
+  const uint32_t t2 = lds_at(lds, __builtin_amdgcn_perm(x, lt.lo0, 0x0C0C0500u) + 128);
+  const uint32_t t1 = lds_at(lds, __builtin_amdgcn_perm(x, lt.lo1, 0x0C020600u));
+  const uint32_t t0 = lds_at(lds, __builtin_amdgcn_perm(x, lt.lo1, 0x0C020700u) + 128);
+  return xor3(t3, t2, xor3(t1, t0, wnext));
 }
 
 // r * K where Q[j] = K * x^(31-j) (bit j of r is the x^(31-j) coefficient).
+// Four independent accumulators keep the 32-term XOR off one dependency chain.
 __device__ __forceinline__ uint32_t mul_basis(uint32_t r, const uint32_t (&Q)[32]) {
-  uint32_t acc = 0;
+  uint32_t acc[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
   for (int j = 0; j < 32; ++j) {
     const uint32_t m = (uint32_t)(((int32_t)(r << (31 - j))) >> 31);
-    acc = and_xor(m, Q[j], acc);
+    acc[j & 3] = and_xor(m, Q[j], acc[j & 3]);
   }
-  return acc;
+  return xor3(acc[0], acc[1], acc[2] ^ acc[3]);
 }
 
 __device__ __forceinline__ void make_basis(uint32_t K, uint32_t (&Q)[32]) {
@@ -334,20 +345,22 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
     ch[1][1][2] |= c1.m6;
     ch[0][1][3] &= c0.keep7;
     ch[1][1][3] &= c1.keep7;
-    uint32_t r0 = 0, r1 = 0;
+    uint32_t r0 = ch[0][0][0], r1 = ch[1][0][0];  // register (0) ^ first word
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      r0 = step4(lds, lt, r0, ch[0][j >> 2][j & 3]);
-      r1 = step4(lds, lt, r1, ch[1][j >> 2][j & 3]);
+    for (int j = 1; j < 8; ++j) {
+      r0 = step4x(lds, lt, r0, ch[0][j >> 2][j & 3]);
+      r1 = step4x(lds, lt, r1, ch[1][j >> 2][j & 3]);
     }
+    r0 = step4x(lds, lt, r0, 0u);
+    r1 = step4x(lds, lt, r1, 0u);
     const uint64_t p0 = it * ppr;
     const uint32_t nout = p0 < a.count ? (uint32_t)(a.count - p0 < ppr ? a.count - p0 : ppr) : 0u;
     const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out + (p0 < a.count ? p0 : 0), 4u * nout);
     if (big) {
-      uint32_t acc = 0;  // r0 * x^(8*2048): chunk 64h+l sits 2 KiB before chunk 64+l
+      uint32_t acc[4] = {0u, 0u, 0u, r1};  // r0 * x^(8*2048) ^ r1: chunk l sits 2 KiB before chunk 64+l
 #pragma unroll
-      for (int j = 0; j < 32; ++j) acc = and_xor((uint32_t)(((int32_t)(r0 << (31 - j))) >> 31), a.YB[j], acc);
-      const uint32_t r = group_xor(mul_basis(acc ^ r1, Q), 6);
+      for (int j = 0; j < 32; ++j) acc[j & 3] = and_xor((uint32_t)(((int32_t)(r0 << (31 - j))) >> 31), a.YB[j], acc[j & 3]);
+      const uint32_t r = group_xor(mul_basis(xor3(acc[0], acc[1], acc[2] ^ acc[3]), Q), 6);
       const uint32_t val = a.verify ? (tr1 == ~r ? 1u : 0u) : ~r;
       __builtin_amdgcn_raw_buffer_store_b32(val, ro, store1 ? 0u : 0x7FFFFFF0u, 0, 0);
     } else {
