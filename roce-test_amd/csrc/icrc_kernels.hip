@@ -291,6 +291,10 @@ __device__ __forceinline__ ChunkMask chunk_mask(uint32_t pos, uint32_t last) {
   return m;
 }
 
+// ABL is a timing-only ablation mask used by tools/microbench (the product
+// instantiates ABL = 0 only): 1 no table fold, 2 no LDS transpose, 4 no lane
+// combine, 8 no global loads, 16 no stores.
+template <int ABL>
 __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
   __shared__ uint32_t lds[kLdsWords + kWaves * kStageBytes / 4];
   fill_tables(lds);
@@ -323,18 +327,28 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
     const uint32_t rem = off < total ? (uint32_t)(total - off < 4096u ? total - off : 4096u) : 0u;
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(a.base + (off < total ? off : 0), rem);
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      v[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 1024 * k + 16 * lane, 0, 2));
+    for (int k = 0; k < 4; ++k) {
+      if (ABL & 8) {
+        v[k] = u32x4{(uint32_t)it * 977u + k, lane, (uint32_t)it, 5u};
+      } else {
+        v[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 1024 * k + 16 * lane, 0, 2));
+      }
+    }
   };
 
   auto step_it = [&](uint64_t it, const u32x4 (&v)[4]) {
     u32x4 ch[2][2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      *reinterpret_cast<u32x4 *>(stage + wr0) = v[2 * h];
-      *reinterpret_cast<u32x4 *>(stage + wr1) = v[2 * h + 1];
-      ch[h][0] = *reinterpret_cast<const u32x4 *>(stage + rd0);
-      ch[h][1] = *reinterpret_cast<const u32x4 *>(stage + rd1);
+      if (ABL & 2) {
+        ch[h][0] = v[2 * h];
+        ch[h][1] = v[2 * h + 1];
+      } else {
+        *reinterpret_cast<u32x4 *>(stage + wr0) = v[2 * h];
+        *reinterpret_cast<u32x4 *>(stage + wr1) = v[2 * h + 1];
+        ch[h][0] = *reinterpret_cast<const u32x4 *>(stage + rd0);
+        ch[h][1] = *reinterpret_cast<const u32x4 *>(stage + rd1);
+      }
     }
     const uint32_t tr0 = ch[0][1][3], tr1 = ch[1][1][3];  // trailer words (last chunks)
     ch[0][0][0] = or_xor(ch[0][0][0], c0.mw0, c0.xw0);
@@ -348,28 +362,39 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
     uint32_t r0 = ch[0][0][0], r1 = ch[1][0][0];  // register (0) ^ first word
 #pragma unroll
     for (int j = 1; j < 8; ++j) {
-      r0 = step4x(lds, lt, r0, ch[0][j >> 2][j & 3]);
-      r1 = step4x(lds, lt, r1, ch[1][j >> 2][j & 3]);
+      if (ABL & 1) {
+        r0 = __builtin_amdgcn_perm(r0, ch[0][j >> 2][j & 3], 0x05040100u) ^ ch[0][j >> 2][j & 3];
+        r1 = __builtin_amdgcn_perm(r1, ch[1][j >> 2][j & 3], 0x05040100u) ^ ch[1][j >> 2][j & 3];
+      } else {
+        r0 = step4x(lds, lt, r0, ch[0][j >> 2][j & 3]);
+        r1 = step4x(lds, lt, r1, ch[1][j >> 2][j & 3]);
+      }
     }
-    r0 = step4x(lds, lt, r0, 0u);
-    r1 = step4x(lds, lt, r1, 0u);
+    if (!(ABL & 1)) {
+      r0 = step4x(lds, lt, r0, 0u);
+      r1 = step4x(lds, lt, r1, 0u);
+    }
     const uint64_t p0 = it * ppr;
     const uint32_t nout = p0 < a.count ? (uint32_t)(a.count - p0 < ppr ? a.count - p0 : ppr) : 0u;
     const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out + (p0 < a.count ? p0 : 0), 4u * nout);
-    if (big) {
+    if (ABL & 4) {
+      if (!(ABL & 16)) __builtin_amdgcn_raw_buffer_store_b32(r0 ^ r1, ro, store1 ? 0u : 0x7FFFFFF0u, 0, 0);
+    } else if (big) {
       uint32_t acc[4] = {0u, 0u, 0u, r1};  // r0 * x^(8*2048) ^ r1: chunk l sits 2 KiB before chunk 64+l
 #pragma unroll
       for (int j = 0; j < 32; ++j) acc[j & 3] = and_xor((uint32_t)(((int32_t)(r0 << (31 - j))) >> 31), a.YB[j], acc[j & 3]);
       const uint32_t r = group_xor(mul_basis(xor3(acc[0], acc[1], acc[2] ^ acc[3]), Q), 6);
       const uint32_t val = a.verify ? (tr1 == ~r ? 1u : 0u) : ~r;
-      __builtin_amdgcn_raw_buffer_store_b32(val, ro, store1 ? 0u : 0x7FFFFFF0u, 0, 0);
+      if (!(ABL & 16)) __builtin_amdgcn_raw_buffer_store_b32(val, ro, store1 ? 0u : 0x7FFFFFF0u, 0, 0);
     } else {
       const uint32_t s0 = group_xor(mul_basis(r0, Q), levels);
       const uint32_t s1 = group_xor(mul_basis(r1, Q), levels);
       const uint32_t v0 = a.verify ? (tr0 == ~s0 ? 1u : 0u) : ~s0;
       const uint32_t v1 = a.verify ? (tr1 == ~s1 ? 1u : 0u) : ~s1;
-      __builtin_amdgcn_raw_buffer_store_b32(v0, ro, store0 ? 4u * pk0 : 0x7FFFFFF0u, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b32(v1, ro, store1 ? 4u * pk1 : 0x7FFFFFF0u, 0, 0);
+      if (!(ABL & 16)) {
+        __builtin_amdgcn_raw_buffer_store_b32(v0, ro, store0 ? 4u * pk0 : 0x7FFFFFF0u, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(v1, ro, store1 ? 4u * pk1 : 0x7FFFFFF0u, 0, 0);
+      }
     }
   };
 
@@ -570,7 +595,7 @@ hipError_t launch_stream(const StreamArgs &a, int cpl, int grid, hipStream_t st)
 }
 
 hipError_t launch_tsk(const TskArgs &a, int grid, hipStream_t st) {
-  hipLaunchKernelGGL(icrc_tsk_kernel, dim3(grid), dim3(kBlock), 0, st, a);
+  hipLaunchKernelGGL(icrc_tsk_kernel<0>, dim3(grid), dim3(kBlock), 0, st, a);
   return hipGetLastError();
 }
 

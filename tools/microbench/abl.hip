@@ -1,0 +1,37 @@
+// Ablation timing of the TSK kernel (timing only: outputs are meaningless
+// for ABL != 0).  Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 abl.hip -o abl
+#include "../../roce-test_amd/csrc/icrc_kernels.hip"
+#include <stdio.h>
+#include <stdlib.h>
+using namespace ricrc;
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s\n", hipGetErrorString(e)); exit(1); } } while (0)
+template <int ABL> float run(TskArgs a, int grid, int reps) {
+  hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  hipLaunchKernelGGL(icrc_tsk_kernel<ABL>, dim3(grid), dim3(kBlock), 0, 0, a);
+  CK(hipDeviceSynchronize()); CK(hipEventRecord(e0));
+  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(icrc_tsk_kernel<ABL>, dim3(grid), dim3(kBlock), 0, 0, a);
+  CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); float ms; CK(hipEventElapsedTime(&ms, e0, e1)); return ms / reps;
+}
+int main() {
+  const uint64_t n = 4096, count = 1 << 20;
+  uint8_t *buf; uint32_t *out; CK(hipMalloc(&buf, n * count)); CK(hipMalloc(&out, 4 * count));
+  CK(hipMemset(buf, 0x3c, n * count));
+  hipDeviceProp_t p; CK(hipGetDeviceProperties(&p, 0));
+  TskArgs a{}; a.base = buf; a.stride = n; a.count = count; a.out = out; a.n_iters = count * n / 4096; a.log2C = 7;
+  for (int i = 0; i < 128; ++i) a.K[i] = 0x9E3779B9u * (i + 1);
+  for (int j = 0; j < 32; ++j) a.YB[j] = 0x85EBCA6Bu * (j + 3);
+  const int grid = p.multiProcessorCount;
+  auto rep = [&](const char *nm, float ms) { printf("%-36s %7.3f ms  %7.1f GB/s\n", nm, ms, n * count / (ms * 1e-3) / 1e9); };
+  rep("full", run<0>(a, grid, 10));
+  rep("no fold", run<1>(a, grid, 10));
+  rep("no transpose", run<2>(a, grid, 10));
+  rep("no combine", run<4>(a, grid, 10));
+  rep("no loads", run<8>(a, grid, 10));
+  rep("no loads, no transpose", run<8 | 2>(a, grid, 10));
+  rep("no fold, no combine (mem+transpose)", run<1 | 4>(a, grid, 10));
+  rep("no fold, no combine, no transpose", run<1 | 4 | 2>(a, grid, 10));
+  rep("fold only (no loads/transpose/comb)", run<8 | 2 | 4>(a, grid, 10));
+  rep("loads+fold (no transpose/comb)", run<2 | 4>(a, grid, 10));
+  rep("no stores", run<16>(a, grid, 10));
+  return 0;
+}
