@@ -277,6 +277,21 @@ __device__ __forceinline__ uint32_t group_xor(uint32_t v, uint32_t levels) {
   return v;
 }
 
+// Branch-free variant for a run-time group size: level k is applied through
+// a wave-uniform all-ones / zero mask, so the code stays one basic block and
+// the scheduler can interleave it with the next step's table lookups.
+__device__ __forceinline__ uint32_t group_xor_masked(uint32_t v, const uint32_t (&lm)[6]) {
+  v = and_xor(__builtin_amdgcn_update_dpp(0u, v, 0xB1, 0xF, 0xF, true), lm[0], v);
+  v = and_xor(__builtin_amdgcn_update_dpp(0u, v, 0x4E, 0xF, 0xF, true), lm[1], v);
+  v = and_xor(__builtin_amdgcn_update_dpp(0u, v, 0x141, 0xF, 0xF, true), lm[2], v);
+  v = and_xor(__builtin_amdgcn_update_dpp(0u, v, 0x140, 0xF, 0xF, true), lm[3], v);
+  const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  v = and_xor(p[0] ^ p[1] ^ v, lm[4], v);
+  const auto q = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  v = and_xor(q[0] ^ q[1] ^ v, lm[5], v);
+  return v;
+}
+
 // Per-lane word constants for one chain at packet chunk position pos.
 struct ChunkMask {
   uint32_t mw0, xw0, m2, m6, keep7;
@@ -294,7 +309,13 @@ __device__ __forceinline__ ChunkMask chunk_mask(uint32_t pos, uint32_t last) {
 // ABL is a timing-only ablation mask used by tools/microbench (the product
 // instantiates ABL = 0 only): 1 no table fold, 2 no LDS transpose, 4 no lane
 // combine, 8 no global loads, 16 no stores.
-template <int ABL>
+//
+// Software pipeline per wave: step i loads region i+1, transposes and folds
+// region i (LDS-bound) and, in the same basic block, finishes region i-1
+// (GF(2) re-alignment + DPP reduction + store, VALU-bound), so every wave's
+// instruction stream mixes both kinds of work instead of all 16 waves of a CU
+// marching through the LDS phase and then the VALU phase together.
+template <bool BIG, int ABL>
 __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
   __shared__ uint32_t lds[kLdsWords + kWaves * kStageBytes / 4];
   fill_tables(lds);
@@ -304,14 +325,18 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   char *stage = reinterpret_cast<char *>(lds) + kLdsWords * 4 + wid * kStageBytes;
   const LaneTab lt{(lane & 31) << 2, ((lane & 31) << 2) | 0x10000u};
-  const uint32_t log2C = a.log2C, Cm1 = (1u << log2C) - 1u;
-  const bool big = log2C == 7;  // 4 KiB packets: one packet per region
-  const uint32_t pos0 = big ? lane : (lane & Cm1), pos1 = big ? 64u + lane : (lane & Cm1);
-  const ChunkMask c0 = chunk_mask(pos0, Cm1), c1 = chunk_mask(pos1, Cm1);
-  const bool store0 = !big && pos0 == Cm1, store1 = pos1 == Cm1;
-  const uint32_t pk0 = big ? 0u : lane >> log2C, pk1 = big ? 0u : (64u + lane) >> log2C;
-  const uint32_t ppr = big ? 1u : 128u >> log2C;  // packets per 4 KiB region
-  const uint32_t levels = big ? 6u : log2C;
+  const uint32_t log2C = BIG ? 7u : a.log2C, Cm1 = (1u << log2C) - 1u;
+  const uint32_t pos0 = BIG ? lane : (lane & Cm1), pos1 = BIG ? 64u + lane : (lane & Cm1);
+  // For 4 KiB packets chain 1 (chunks 64..127) never holds header bytes and
+  // only lane 63 holds the trailer: keep those constants out of VGPRs.
+  const ChunkMask c0 = chunk_mask(pos0, BIG ? 0xFFFFFFFFu : Cm1);
+  const ChunkMask c1 = BIG ? ChunkMask{0u, 0u, 0u, 0u, lane == 63 ? 0u : 0xFFFFFFFFu} : chunk_mask(pos1, Cm1);
+  const bool store0 = !BIG && pos0 == Cm1, store1 = pos1 == Cm1;
+  const uint32_t pk0 = BIG ? 0u : lane >> log2C, pk1 = BIG ? 0u : (64u + lane) >> log2C;
+  const uint32_t ppr = BIG ? 1u : 128u >> log2C;  // packets per 4 KiB region
+  uint32_t lm[6];  // wave-uniform level masks of the segmented reduction (!BIG)
+#pragma unroll
+  for (int k = 0; k < 6; ++k) lm[k] = __builtin_amdgcn_readfirstlane((uint32_t)k < log2C ? 0xFFFFFFFFu : 0u);
   uint32_t Q[32];
   make_basis(a.K[pos1], Q);
 
@@ -336,7 +361,11 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
     }
   };
 
-  auto step_it = [&](uint64_t it, const u32x4 (&v)[4]) {
+  // Transpose + fold one region: chain registers and trailer words.
+  struct Folded {
+    uint32_t r0, r1, tr0, tr1;
+  };
+  auto fold = [&](const u32x4 (&v)[4]) -> Folded {
     u32x4 ch[2][2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -350,7 +379,9 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
         ch[h][1] = *reinterpret_cast<const u32x4 *>(stage + rd1);
       }
     }
-    const uint32_t tr0 = ch[0][1][3], tr1 = ch[1][1][3];  // trailer words (last chunks)
+    Folded f;
+    f.tr0 = ch[0][1][3];
+    f.tr1 = ch[1][1][3];  // trailer words (last chunks)
     ch[0][0][0] = or_xor(ch[0][0][0], c0.mw0, c0.xw0);
     ch[1][0][0] = or_xor(ch[1][0][0], c1.mw0, c1.xw0);
     ch[0][0][2] |= c0.m2;
@@ -374,23 +405,31 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
       r0 = step4x(lds, lt, r0, 0u);
       r1 = step4x(lds, lt, r1, 0u);
     }
+    f.r0 = r0;
+    f.r1 = r1;
+    return f;
+  };
+
+  // Re-align, reduce and store region `it` (it >= n_iters: store dropped).
+  auto finish = [&](uint64_t it, const Folded &f) {
     const uint64_t p0 = it * ppr;
     const uint32_t nout = p0 < a.count ? (uint32_t)(a.count - p0 < ppr ? a.count - p0 : ppr) : 0u;
     const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out + (p0 < a.count ? p0 : 0), 4u * nout);
     if (ABL & 4) {
-      if (!(ABL & 16)) __builtin_amdgcn_raw_buffer_store_b32(r0 ^ r1, ro, store1 ? 0u : 0x7FFFFFF0u, 0, 0);
-    } else if (big) {
-      uint32_t acc[4] = {0u, 0u, 0u, r1};  // r0 * x^(8*2048) ^ r1: chunk l sits 2 KiB before chunk 64+l
+      if (!(ABL & 16)) __builtin_amdgcn_raw_buffer_store_b32(f.r0 ^ f.r1, ro, store1 ? 0u : 0x7FFFFFF0u, 0, 0);
+    } else if (BIG) {
+      uint32_t acc[4] = {0u, 0u, 0u, f.r1};  // r0 * x^(8*2048) ^ r1: chunk l sits 2 KiB before chunk 64+l
 #pragma unroll
-      for (int j = 0; j < 32; ++j) acc[j & 3] = and_xor((uint32_t)(((int32_t)(r0 << (31 - j))) >> 31), a.YB[j], acc[j & 3]);
+      for (int j = 0; j < 32; ++j)
+        acc[j & 3] = and_xor((uint32_t)(((int32_t)(f.r0 << (31 - j))) >> 31), a.YB[j], acc[j & 3]);
       const uint32_t r = group_xor(mul_basis(xor3(acc[0], acc[1], acc[2] ^ acc[3]), Q), 6);
-      const uint32_t val = a.verify ? (tr1 == ~r ? 1u : 0u) : ~r;
+      const uint32_t val = a.verify ? (f.tr1 == ~r ? 1u : 0u) : ~r;
       if (!(ABL & 16)) __builtin_amdgcn_raw_buffer_store_b32(val, ro, store1 ? 0u : 0x7FFFFFF0u, 0, 0);
     } else {
-      const uint32_t s0 = group_xor(mul_basis(r0, Q), levels);
-      const uint32_t s1 = group_xor(mul_basis(r1, Q), levels);
-      const uint32_t v0 = a.verify ? (tr0 == ~s0 ? 1u : 0u) : ~s0;
-      const uint32_t v1 = a.verify ? (tr1 == ~s1 ? 1u : 0u) : ~s1;
+      const uint32_t s0 = group_xor_masked(mul_basis(f.r0, Q), lm);
+      const uint32_t s1 = group_xor_masked(mul_basis(f.r1, Q), lm);
+      const uint32_t v0 = a.verify ? (f.tr0 == ~s0 ? 1u : 0u) : ~s0;
+      const uint32_t v1 = a.verify ? (f.tr1 == ~s1 ? 1u : 0u) : ~s1;
       if (!(ABL & 16)) {
         __builtin_amdgcn_raw_buffer_store_b32(v0, ro, store0 ? 4u * pk0 : 0x7FFFFFF0u, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b32(v1, ro, store1 ? 4u * pk1 : 0x7FFFFFF0u, 0, 0);
@@ -398,16 +437,32 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
     }
   };
 
+  // Two register buffers used in turn (loop unrolled by two): no cur = nxt
+  // copies, which the scheduler would otherwise hoist right behind the
+  // prefetch and stall on it.
   uint64_t it = wave;
-  u32x4 cur[4], nxt[4];
-  load(it, cur);
-  for (; it < a.n_iters; it += nwaves) {
-    load(it + nwaves, nxt);  // past the batch: zero-length resource, reads 0
+  u32x4 bufA[4], bufB[4];
+  load(it, bufA);
+  Folded prev{0u, 0u, 0u, 0u};
+  uint64_t pit = a.n_iters;  // nothing to finish before the first fold
+  while (it < a.n_iters) {
+    load(it + nwaves, bufB);  // past the batch: zero-length resource, reads 0
     __builtin_amdgcn_sched_barrier(0);
-    step_it(it, cur);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
+    Folded f = fold(bufA);
+    finish(pit, prev);
+    prev = f;
+    pit = it;
+    it += nwaves;
+    if (it >= a.n_iters) break;
+    load(it + nwaves, bufA);
+    __builtin_amdgcn_sched_barrier(0);
+    f = fold(bufB);
+    finish(pit, prev);
+    prev = f;
+    pit = it;
+    it += nwaves;
   }
+  finish(pit, prev);
 }
 
 // =======================================================================
@@ -595,7 +650,8 @@ hipError_t launch_stream(const StreamArgs &a, int cpl, int grid, hipStream_t st)
 }
 
 hipError_t launch_tsk(const TskArgs &a, int grid, hipStream_t st) {
-  hipLaunchKernelGGL(icrc_tsk_kernel<0>, dim3(grid), dim3(kBlock), 0, st, a);
+  if (a.log2C == 7) hipLaunchKernelGGL((icrc_tsk_kernel<true, 0>), dim3(grid), dim3(kBlock), 0, st, a);
+  else hipLaunchKernelGGL((icrc_tsk_kernel<false, 0>), dim3(grid), dim3(kBlock), 0, st, a);
   return hipGetLastError();
 }
 
