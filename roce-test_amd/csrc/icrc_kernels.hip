@@ -361,11 +361,65 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
     }
   };
 
-  // Transpose + fold one region: chain registers and trailer words.
-  struct Folded {
-    uint32_t r0, r1, tr0, tr1;
+  // Re-alignment state of one folded region, advanced in 8 VALU slices.
+  struct Fin {
+    uint32_t r0, r1, tr0, tr1;  // chain registers, trailer words
+    uint32_t a0[4], a1[4];      // multiply accumulators
   };
-  auto fold = [&](const u32x4 (&v)[4]) -> Folded {
+  auto fin_init = [&](Fin &f) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) f.a0[k] = f.a1[k] = 0u;
+    if (BIG) f.a0[3] = f.r1;  // r0 * x^(8*2048) ^ r1
+  };
+  // Slice s (0..7) of the GF(2) products.  BIG: slices 0-3 fold r0 * y into
+  // a0, slices 4-7 multiply that by the lane constant into a1.  Otherwise
+  // each slice takes 4 bits of r0 * K and 4 bits of r1 * K.
+  auto fin_slice = [&](Fin &f, int sl) {
+    if (ABL & 4) return;
+    if (BIG) {
+      if (sl < 4) {
+#pragma unroll
+        for (int j = 8 * sl; j < 8 * sl + 8; ++j)
+          f.a0[j & 3] = and_xor((uint32_t)(((int32_t)(f.r0 << (31 - j))) >> 31), a.YB[j], f.a0[j & 3]);
+      } else {
+        if (sl == 4) f.r0 = xor3(f.a0[0], f.a0[1], f.a0[2] ^ f.a0[3]);
+#pragma unroll
+        for (int j = 8 * (sl - 4); j < 8 * (sl - 4) + 8; ++j)
+          f.a1[j & 3] = and_xor((uint32_t)(((int32_t)(f.r0 << (31 - j))) >> 31), Q[j], f.a1[j & 3]);
+      }
+    } else {
+#pragma unroll
+      for (int j = 4 * sl; j < 4 * sl + 4; ++j) {
+        f.a0[j & 3] = and_xor((uint32_t)(((int32_t)(f.r0 << (31 - j))) >> 31), Q[j], f.a0[j & 3]);
+        f.a1[j & 3] = and_xor((uint32_t)(((int32_t)(f.r1 << (31 - j))) >> 31), Q[j], f.a1[j & 3]);
+      }
+    }
+  };
+  // Reduce across the packet's lanes and store region `it` (>= n_iters: dropped).
+  auto fin_store = [&](uint64_t it, const Fin &f) {
+    const uint64_t p0 = it * ppr;
+    const uint32_t nout = p0 < a.count ? (uint32_t)(a.count - p0 < ppr ? a.count - p0 : ppr) : 0u;
+    const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out + (p0 < a.count ? p0 : 0), 4u * nout);
+    if (ABL & 16) return;
+    if (ABL & 4) {
+      __builtin_amdgcn_raw_buffer_store_b32(f.r0 ^ f.r1, ro, store1 ? 0u : 0x7FFFFFF0u, 0, 0);
+    } else if (BIG) {
+      const uint32_t r = group_xor(xor3(f.a1[0], f.a1[1], f.a1[2] ^ f.a1[3]), 6);
+      const uint32_t val = a.verify ? (f.tr1 == ~r ? 1u : 0u) : ~r;
+      __builtin_amdgcn_raw_buffer_store_b32(val, ro, store1 ? 0u : 0x7FFFFFF0u, 0, 0);
+    } else {
+      const uint32_t s0 = group_xor_masked(xor3(f.a0[0], f.a0[1], f.a0[2] ^ f.a0[3]), lm);
+      const uint32_t s1 = group_xor_masked(xor3(f.a1[0], f.a1[1], f.a1[2] ^ f.a1[3]), lm);
+      const uint32_t v0 = a.verify ? (f.tr0 == ~s0 ? 1u : 0u) : ~s0;
+      const uint32_t v1 = a.verify ? (f.tr1 == ~s1 ? 1u : 0u) : ~s1;
+      __builtin_amdgcn_raw_buffer_store_b32(v0, ro, store0 ? 4u * pk0 : 0x7FFFFFF0u, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(v1, ro, store1 ? 4u * pk1 : 0x7FFFFFF0u, 0, 0);
+    }
+  };
+
+  // Transpose + fold region `it` held in v, while finishing the previous
+  // region `pit` (state pf) in the shadow of each step's LDS table reads.
+  auto step = [&](const u32x4 (&v)[4], Fin &pf, uint64_t pit) -> Fin {
     u32x4 ch[2][2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -379,9 +433,9 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
         ch[h][1] = *reinterpret_cast<const u32x4 *>(stage + rd1);
       }
     }
-    Folded f;
+    Fin f;
     f.tr0 = ch[0][1][3];
-    f.tr1 = ch[1][1][3];  // trailer words (last chunks)
+    f.tr1 = ch[1][1][3];
     ch[0][0][0] = or_xor(ch[0][0][0], c0.mw0, c0.xw0);
     ch[1][0][0] = or_xor(ch[1][0][0], c1.mw0, c1.xw0);
     ch[0][0][2] |= c0.m2;
@@ -390,51 +444,35 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
     ch[1][1][2] |= c1.m6;
     ch[0][1][3] &= c0.keep7;
     ch[1][1][3] &= c1.keep7;
-    uint32_t r0 = ch[0][0][0], r1 = ch[1][0][0];  // register (0) ^ first word
+    uint32_t x0 = ch[0][0][0], x1 = ch[1][0][0];  // register (0) ^ first word
 #pragma unroll
-    for (int j = 1; j < 8; ++j) {
+    for (int j = 1; j <= 8; ++j) {
+      const uint32_t w0 = j < 8 ? ch[0][j >> 2][j & 3] : 0u, w1 = j < 8 ? ch[1][j >> 2][j & 3] : 0u;
       if (ABL & 1) {
-        r0 = __builtin_amdgcn_perm(r0, ch[0][j >> 2][j & 3], 0x05040100u) ^ ch[0][j >> 2][j & 3];
-        r1 = __builtin_amdgcn_perm(r1, ch[1][j >> 2][j & 3], 0x05040100u) ^ ch[1][j >> 2][j & 3];
+        x0 = __builtin_amdgcn_perm(x0, w0, 0x05040100u) ^ w0;
+        x1 = __builtin_amdgcn_perm(x1, w1, 0x05040100u) ^ w1;
+        fin_slice(pf, j - 1);
       } else {
-        r0 = step4x(lds, lt, r0, ch[0][j >> 2][j & 3]);
-        r1 = step4x(lds, lt, r1, ch[1][j >> 2][j & 3]);
+        const uint32_t t03 = lds_at(lds, __builtin_amdgcn_perm(x0, lt.lo0, 0x0C0C0400u));
+        const uint32_t t02 = lds_at(lds, __builtin_amdgcn_perm(x0, lt.lo0, 0x0C0C0500u) + 128);
+        const uint32_t t01 = lds_at(lds, __builtin_amdgcn_perm(x0, lt.lo1, 0x0C020600u));
+        const uint32_t t00 = lds_at(lds, __builtin_amdgcn_perm(x0, lt.lo1, 0x0C020700u) + 128);
+        const uint32_t t13 = lds_at(lds, __builtin_amdgcn_perm(x1, lt.lo0, 0x0C0C0400u));
+        const uint32_t t12 = lds_at(lds, __builtin_amdgcn_perm(x1, lt.lo0, 0x0C0C0500u) + 128);
+        const uint32_t t11 = lds_at(lds, __builtin_amdgcn_perm(x1, lt.lo1, 0x0C020600u));
+        const uint32_t t10 = lds_at(lds, __builtin_amdgcn_perm(x1, lt.lo1, 0x0C020700u) + 128);
+        __builtin_amdgcn_sched_barrier(0);
+        fin_slice(pf, j - 1);  // independent VALU work while the reads fly
+        __builtin_amdgcn_sched_barrier(0);
+        x0 = xor3(t03, t02, xor3(t01, t00, w0));
+        x1 = xor3(t13, t12, xor3(t11, t10, w1));
       }
     }
-    if (!(ABL & 1)) {
-      r0 = step4x(lds, lt, r0, 0u);
-      r1 = step4x(lds, lt, r1, 0u);
-    }
-    f.r0 = r0;
-    f.r1 = r1;
+    fin_store(pit, pf);
+    f.r0 = x0;
+    f.r1 = x1;
+    fin_init(f);
     return f;
-  };
-
-  // Re-align, reduce and store region `it` (it >= n_iters: store dropped).
-  auto finish = [&](uint64_t it, const Folded &f) {
-    const uint64_t p0 = it * ppr;
-    const uint32_t nout = p0 < a.count ? (uint32_t)(a.count - p0 < ppr ? a.count - p0 : ppr) : 0u;
-    const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out + (p0 < a.count ? p0 : 0), 4u * nout);
-    if (ABL & 4) {
-      if (!(ABL & 16)) __builtin_amdgcn_raw_buffer_store_b32(f.r0 ^ f.r1, ro, store1 ? 0u : 0x7FFFFFF0u, 0, 0);
-    } else if (BIG) {
-      uint32_t acc[4] = {0u, 0u, 0u, f.r1};  // r0 * x^(8*2048) ^ r1: chunk l sits 2 KiB before chunk 64+l
-#pragma unroll
-      for (int j = 0; j < 32; ++j)
-        acc[j & 3] = and_xor((uint32_t)(((int32_t)(f.r0 << (31 - j))) >> 31), a.YB[j], acc[j & 3]);
-      const uint32_t r = group_xor(mul_basis(xor3(acc[0], acc[1], acc[2] ^ acc[3]), Q), 6);
-      const uint32_t val = a.verify ? (f.tr1 == ~r ? 1u : 0u) : ~r;
-      if (!(ABL & 16)) __builtin_amdgcn_raw_buffer_store_b32(val, ro, store1 ? 0u : 0x7FFFFFF0u, 0, 0);
-    } else {
-      const uint32_t s0 = group_xor_masked(mul_basis(f.r0, Q), lm);
-      const uint32_t s1 = group_xor_masked(mul_basis(f.r1, Q), lm);
-      const uint32_t v0 = a.verify ? (f.tr0 == ~s0 ? 1u : 0u) : ~s0;
-      const uint32_t v1 = a.verify ? (f.tr1 == ~s1 ? 1u : 0u) : ~s1;
-      if (!(ABL & 16)) {
-        __builtin_amdgcn_raw_buffer_store_b32(v0, ro, store0 ? 4u * pk0 : 0x7FFFFFF0u, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(v1, ro, store1 ? 4u * pk1 : 0x7FFFFFF0u, 0, 0);
-      }
-    }
   };
 
   // Two register buffers used in turn (loop unrolled by two): no cur = nxt
@@ -443,26 +481,25 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
   uint64_t it = wave;
   u32x4 bufA[4], bufB[4];
   load(it, bufA);
-  Folded prev{0u, 0u, 0u, 0u};
+  Fin prev{};
+  fin_init(prev);
   uint64_t pit = a.n_iters;  // nothing to finish before the first fold
   while (it < a.n_iters) {
     load(it + nwaves, bufB);  // past the batch: zero-length resource, reads 0
     __builtin_amdgcn_sched_barrier(0);
-    Folded f = fold(bufA);
-    finish(pit, prev);
-    prev = f;
+    prev = step(bufA, prev, pit);
     pit = it;
     it += nwaves;
     if (it >= a.n_iters) break;
     load(it + nwaves, bufA);
     __builtin_amdgcn_sched_barrier(0);
-    f = fold(bufB);
-    finish(pit, prev);
-    prev = f;
+    prev = step(bufB, prev, pit);
     pit = it;
     it += nwaves;
   }
-  finish(pit, prev);
+#pragma unroll
+  for (int sl = 0; sl < 8; ++sl) fin_slice(prev, sl);
+  fin_store(pit, prev);
 }
 
 // =======================================================================

@@ -7,9 +7,9 @@ using namespace ricrc;
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s\n", hipGetErrorString(e)); exit(1); } } while (0)
 template <int ABL> float run(TskArgs a, int grid, int reps) {
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-  hipLaunchKernelGGL(icrc_tsk_kernel<true, ABL>, dim3(grid), dim3(kBlock), 0, 0, a);
+  hipLaunchKernelGGL((icrc_tsk_kernel<true, ABL>), dim3(grid), dim3(kBlock), 0, 0, a);
   CK(hipDeviceSynchronize()); CK(hipEventRecord(e0));
-  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(icrc_tsk_kernel<true, ABL>, dim3(grid), dim3(kBlock), 0, 0, a);
+  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL((icrc_tsk_kernel<true, ABL>), dim3(grid), dim3(kBlock), 0, 0, a);
   CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); float ms; CK(hipEventElapsedTime(&ms, e0, e1)); return ms / reps;
 }
 int main() {
