@@ -33,6 +33,7 @@ struct TskArgs {
   uint32_t verify;
   uint32_t K[128];   // per chunk position: x^(8 (n - 4 - 32 (pos + 1)))
   uint32_t YB[32];   // x^(8*2048) * x^(31-j): uniform basis for 4 KiB packets
+  uint64_t *stamps;  // diagnostic builds only (tools/microbench); null in the product
 };
 
 // Any alignment / offsets / lengths.

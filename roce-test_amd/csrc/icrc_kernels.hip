@@ -308,7 +308,8 @@ __device__ __forceinline__ ChunkMask chunk_mask(uint32_t pos, uint32_t last) {
 
 // ABL is a timing-only ablation mask used by tools/microbench (the product
 // instantiates ABL = 0 only): 1 no table fold, 2 no LDS transpose, 4 no lane
-// combine, 8 no global loads, 16 no stores.
+// combine, 8 no global loads, 16 no stores, 32 s_memtime stamps into
+// a.stamps (diagnostic: per wave {staging wait, fold, total} cycles).
 //
 // Software pipeline per wave: step i loads region i+1, transposes and folds
 // region i (LDS-bound) and, in the same basic block, finishes region i-1
@@ -419,7 +420,20 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
 
   // Transpose + fold region `it` held in v, while finishing the previous
   // region `pit` (state pf) in the shadow of each step's LDS table reads.
+  uint64_t st_stage = 0, st_fold = 0, st_t0 = 0, st_first = 0;
+  auto stamp = [&]() -> uint64_t {
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+  };
   auto step = [&](const u32x4 (&v)[4], Fin &pf, uint64_t pit) -> Fin {
+    uint64_t ts0 = 0;
+    if (ABL & 32) {
+      ts0 = stamp();
+      if (!st_first) st_first = ts0;
+    }
     u32x4 ch[2][2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -432,6 +446,12 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
         ch[h][0] = *reinterpret_cast<const u32x4 *>(stage + rd0);
         ch[h][1] = *reinterpret_cast<const u32x4 *>(stage + rd1);
       }
+    }
+    uint64_t ts1 = 0;
+    if (ABL & 32) {
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): staging data in registers
+      ts1 = stamp();
+      st_stage += ts1 - ts0;
     }
     Fin f;
     f.tr0 = ch[0][1][3];
@@ -471,6 +491,12 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
     fin_store(pit, pf);
     f.r0 = x0;
     f.r1 = x1;
+    if (ABL & 32) {
+      asm volatile("" ::"v"(x0), "v"(x1));
+      const uint64_t ts2 = stamp();
+      st_fold += ts2 - ts1;
+      st_t0 = ts2;
+    }
     fin_init(f);
     return f;
   };
@@ -500,6 +526,11 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
 #pragma unroll
   for (int sl = 0; sl < 8; ++sl) fin_slice(prev, sl);
   fin_store(pit, prev);
+  if ((ABL & 32) && lane == 0) {
+    a.stamps[3 * wave + 0] = st_stage;
+    a.stamps[3 * wave + 1] = st_fold;
+    a.stamps[3 * wave + 2] = st_t0 - st_first;
+  }
 }
 
 // =======================================================================

@@ -33,5 +33,21 @@ int main() {
   rep("fold only (no loads/transpose/comb)", run<8 | 2 | 4>(a, grid, 10));
   rep("loads+fold (no transpose/comb)", run<2 | 4>(a, grid, 10));
   rep("no stores", run<16>(a, grid, 10));
+  {
+    const int nw = grid * kWaves;
+    uint64_t *st; CK(hipMalloc(&st, 3 * 8 * nw)); a.stamps = st;
+    rep("stamps (diag)", run<32>(a, grid, 3));
+    rep("stamps no loads (diag)", run<32 | 8>(a, grid, 3));
+    uint64_t *h = (uint64_t *)malloc(3 * 8 * nw);
+    for (int v = 0; v < 2; ++v) {
+      if (v == 0) run<32>(a, grid, 1); else run<32 | 8>(a, grid, 1);
+      CK(hipMemcpy(h, st, 3 * 8 * nw, hipMemcpyDeviceToHost));
+      double s0 = 0, s1 = 0, s2 = 0;
+      for (int w = 0; w < nw; ++w) { s0 += h[3 * w]; s1 += h[3 * w + 1]; s2 += h[3 * w + 2]; }
+      const double iters = (double)a.n_iters / nw;
+      printf("%s per wave-iteration (ticks): staging+wait %.0f, fold+finish %.0f, total %.0f\n",
+             v == 0 ? "full    " : "no loads", s0 / nw / iters, s1 / nw / iters, s2 / nw / iters);
+    }
+  }
   return 0;
 }
