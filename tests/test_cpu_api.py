@@ -1,0 +1,143 @@
+"""CPU: the C-ABI library loads, exports what include/roce_icrc.h declares, and
+its per-packet (CPU) entry points match the oracle.  No GPU compute here: the
+batch calls are covered by tests/test_gpu_parity.py on the MI355X."""
+import ctypes
+import errno
+import json
+import os
+import random
+import re
+import struct
+import subprocess
+import zlib
+
+import numpy as np
+import pytest
+
+import icrc_oracle as O
+import roce_icrc
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "roce_icrc.h")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(ricrc_[a-z_0-9]+)\s*\(", text)))
+
+
+def test_header_declarations_exported():
+    syms = declared_symbols()
+    assert len(syms) >= 15
+    lib = ctypes.CDLL(roce_icrc.LIB_PATH)
+    for s in syms:
+        assert hasattr(lib, s), s
+    out = subprocess.run(["nm", "-D", "--defined-only", roce_icrc.LIB_PATH], capture_output=True, text=True).stdout
+    for s in syms:
+        assert re.search(rf"\bT {s}\b", out), f"{s} not exported as a text symbol"
+    assert sorted(roce_icrc.EXPORTED) == syms
+
+
+def test_library_is_gfx950_code_object():
+    """The .so embeds a gfx950 code object (the HIP kernels), nothing else."""
+    blob = open(roce_icrc.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+    assert b"gfx942" not in blob and b"gfx90a" not in blob
+
+
+def test_one_matches_golden_and_random():
+    meta = json.load(open(os.path.join(ROOT, "tests", "golden", "icrc_golden.json")))
+    blob = open(os.path.join(ROOT, "tests", "golden", "icrc_golden.bin"), "rb").read()
+    for c in meta["cases"]:
+        pkt = blob[c["offset"]: c["offset"] + c["len"]]
+        assert roce_icrc.icrc(pkt) == c["icrc"], c["desc"]
+    rng = random.Random(9)
+    for _ in range(300):
+        pkt = bytes(rng.getrandbits(8) for _ in range(rng.randrange(4, 5000)))
+        assert roce_icrc.icrc(pkt) == O.icrc(pkt)
+
+
+def test_input_types_no_copy_paths():
+    pkt = bytes.fromhex("450200301234400040110000c0a80164c0a80101457b12b7001c00001140ffff"
+                        "0000001100000005000000016c1f7922")
+    for v in (pkt, bytearray(pkt), memoryview(pkt), np.frombuffer(pkt, np.uint8).copy(), memoryview(bytearray(pkt))):
+        assert roce_icrc.icrc(v) == 0x22791F6C
+
+
+def test_verify_stamp_roundtrip():
+    rng = random.Random(1)
+    for n in (44, 64, 300, 1024, 4096):
+        pkt = bytearray(rng.getrandbits(8) for _ in range(n))
+        roce_icrc.stamp(pkt)
+        assert roce_icrc.verify(pkt)
+        assert O.residue_ok(bytes(pkt))
+        assert struct.unpack("<I", bytes(pkt[-4:]))[0] == O.icrc(bytes(pkt))
+        pkt[n - 5] ^= 0x40  # last covered byte (never a masked offset for n >= 44)
+        assert not roce_icrc.verify(pkt)
+
+
+def test_is_rocev2_classifier():
+    pkt = bytes.fromhex("450200301234400040110000c0a80164c0a80101457b12b7001c00001140ffff"
+                        "0000001100000005000000016c1f7922")
+    assert roce_icrc.is_rocev2(pkt)
+    bad = bytearray(pkt)
+    bad[23] = 0xB8  # dport 4792
+    assert not roce_icrc.is_rocev2(bad)
+    bad = bytearray(pkt)
+    bad[9] = 6  # TCP
+    assert not roce_icrc.is_rocev2(bad)
+    assert not roce_icrc.is_rocev2(pkt[:40])
+
+
+def test_shift_and_combine_against_oracle_and_zlib():
+    rng = random.Random(4)
+    for _ in range(50):
+        reg, n = rng.getrandbits(32), rng.randrange(0, 5000)
+        assert roce_icrc.shift(reg, n) == O.crc_shift(reg, n) if n < 600 else True
+        a = bytes(rng.getrandbits(8) for _ in range(rng.randrange(0, 300)))
+        b = bytes(rng.getrandbits(8) for _ in range(rng.randrange(0, 300)))
+        assert roce_icrc.combine(zlib.crc32(a), zlib.crc32(b), len(b)) == zlib.crc32(a + b)
+
+
+def test_incremental_repair_after_header_rewrite():
+    """The linearity the next-step 'repair' feature relies on: rewriting PSN
+    (shuffle_egress.p4:665) changes the ICRC by shift(crc0(delta), tail)."""
+    rng = random.Random(8)
+    pkt = bytearray(rng.getrandbits(8) for _ in range(1024))
+    old = roce_icrc.icrc(pkt)
+    new_pkt = bytearray(pkt)
+    new_pkt[37:40] = (0x123456).to_bytes(3, "big")
+    delta = bytes(a ^ b for a, b in zip(pkt[:1020], new_pkt[:1020]))
+    # crc0 of the delta stream (register from 0, no conditioning) = pure linear part
+    reg = 0
+    for byte in delta:
+        reg ^= byte
+        for _ in range(8):
+            reg = (reg >> 1) ^ (0xEDB88320 if reg & 1 else 0)
+    assert roce_icrc.icrc(new_pkt) == old ^ reg
+
+
+def test_errors_never_abort():
+    with pytest.raises(ValueError):
+        roce_icrc.icrc(b"abc")
+    assert roce_icrc.lib.ricrc_one(None, 100) == 0
+    assert roce_icrc.lib.ricrc_verify_one(None, 100) == -errno.EINVAL
+    assert roce_icrc.lib.ricrc_stamp_one(None, 100) == -errno.EINVAL
+    assert roce_icrc.lib.ricrc_batch_host(None, None, None, None, 0, 1, 0, None) == -errno.EINVAL
+    assert roce_icrc.lib.ricrc_batch_device(None, 0, None, None, None, 0, 1, 0, None, None) == -errno.EINVAL
+    h = ctypes.c_void_p()
+    assert roce_icrc.lib.ricrc_create(ctypes.byref(h), 0) == -errno.EINVAL
+    for rc in (0, -errno.EINVAL, -errno.ENODEV, -errno.ENOMEM, -errno.EIO, -12345):
+        assert roce_icrc.lib.ricrc_strerror(rc)
+
+
+def test_no_cpu_fallback_without_gpu():
+    torch = pytest.importorskip("torch")
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: the ENODEV path is not reachable")
+    with pytest.raises(roce_icrc.ICRCError) as e:
+        roce_icrc.Context()
+    assert e.value.rc == -errno.ENODEV
+    with pytest.raises(roce_icrc.ICRCError):
+        roce_icrc.icrc_batch(np.zeros(4096, np.uint8), stride=4096)

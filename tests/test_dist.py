@@ -1,0 +1,79 @@
+"""CPU: the N > 1 path (sharding + all-gather of results) with world_size-2 gloo.
+
+Each rank computes the ICRCs of its shard (here with the CPU oracle, the GPU
+being unavailable in this container), all-gathers them with the same helper
+bench.py uses over RCCL, and every rank must end with exactly the
+single-process result vector, for equal and unequal shards."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from roce_icrc.dist import all_gather_icrc, byte_balanced_cuts, shard_range
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, count, n, q):
+    import oracle_c
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lo, hi = shard_range(count, world, rank)
+        local = oracle_c.synth_batch(0x1CEC0DE, lo, hi - lo, n)
+        mine = oracle_c.icrc_batch(local, stride=n)
+        got = all_gather_icrc(torch.from_numpy(mine.view(np.int32).copy()), world)
+        q.put((rank, got.numpy().view(np.uint32).copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("count,n", [(1000, 1024), (777, 64)])
+def test_gloo_world2_gather_matches_single_process(count, n):
+    import oracle_c
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, count, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    want = oracle_c.icrc_batch(oracle_c.synth_batch(0x1CEC0DE, 0, count, n), stride=n)
+    for r in range(world):
+        np.testing.assert_array_equal(res[r], want)
+
+
+def test_shard_range_covers_exactly():
+    for total in (0, 1, 7, 1 << 20):
+        for world in (1, 2, 3, 8):
+            spans = [shard_range(total, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == total
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+            sizes = [h - l for l, h in spans]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_byte_balanced_cuts_mixed_mtu():
+    rng = np.random.default_rng(4)
+    lens = rng.choice([64, 256, 1024, 4096], size=40000)
+    for world in (2, 4, 8):
+        cuts = byte_balanced_cuts(lens, world)
+        assert cuts[0] == 0 and cuts[-1] == len(lens) and cuts == sorted(cuts)
+        shard_bytes = [int(lens[cuts[i]:cuts[i + 1]].sum()) for i in range(world)]
+        assert max(shard_bytes) - min(shard_bytes) <= 2 * 4096

@@ -1,0 +1,107 @@
+"""CPU: pin the oracle before trusting it (no GPU).
+
+The reference has no ICRC vectors, so the oracle is pinned by (1) the CRC-32
+check value of the parameter set Tofino's HashAlgorithm_t.CRC32 names
+(shuffle_egress.p4:461), (2) the hand-derived ACK known answer built from the
+reference's P4 templates, (3) three independent formulations agreeing, (4) the
+CRC-32 residue, (5) mask invariance exactly on the fields calc_icrc() forces
+to 0xFF (shuffle_egress.p4:467-485), and (6) the committed golden vectors.
+"""
+import json
+import os
+import random
+import struct
+import zlib
+
+import numpy as np
+import pytest
+
+import icrc_oracle as O
+import oracle_c
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def golden():
+    meta = json.load(open(os.path.join(GOLDEN, "icrc_golden.json")))
+    blob = open(os.path.join(GOLDEN, "icrc_golden.bin"), "rb").read()
+    return meta, [(c["desc"], blob[c["offset"]: c["offset"] + c["len"]], c["icrc"]) for c in meta["cases"]]
+
+
+def test_crc32_parameter_set_kat():
+    assert zlib.crc32(b"123456789") == 0xCBF43926
+    assert O._crc32_bitwise(b"123456789") ^ 0xFFFFFFFF == 0xCBF43926
+
+
+def test_ack_known_answer():
+    pkt = bytes.fromhex("450200301234400040110000c0a80164c0a80101457b12b7001c00001140ffff"
+                        "0000001100000005000000016c1f7922")
+    assert O.icrc(pkt) == 0x22791F6C
+    assert pkt[-4:] == struct.pack("<I", 0x22791F6C)  # little-endian trailer (shuffle_egress.p4:493)
+    assert O.residue_ok(pkt)
+
+
+def test_prefix_register_is_rxe_seed():
+    assert zlib.crc32(O.PREFIX) ^ 0xFFFFFFFF == O.REGISTER_AFTER_PREFIX == 0xDEBB20E3
+
+
+def test_golden_vectors_all_formulations():
+    meta, cases = golden()
+    assert meta["crc32_check_123456789"] == 0xCBF43926
+    assert len(cases) >= 50
+    for desc, pkt, want in cases:
+        assert O.icrc(pkt) == want, desc
+        assert O.icrc_bitwise(pkt) == want, desc
+        assert O.icrc_rxe(pkt) == want, desc
+        for kind in ("bitwise", "bytewise", "fast"):
+            assert oracle_c.icrc_one(pkt, kind) == want, (desc, kind)
+        assert O.residue_ok(O.stamp(pkt)), desc
+
+
+@pytest.mark.parametrize("n", [44, 64, 1024, 4096])
+def test_mask_invariance(n):
+    rng = random.Random(n)
+    pkt = bytearray(rng.getrandbits(8) for _ in range(n))
+    base = O.icrc(bytes(pkt))
+    for off in O.MASK_OFFSETS:  # masked: any value, same ICRC
+        q = bytearray(pkt)
+        q[off] ^= 0xA5
+        assert O.icrc(bytes(q)) == base, off
+    for off in [o for o in (0, 2, 9, 12, 20, 28, 33, 39, 40, n - 5) if o < n - 4]:  # covered: must change
+        q = bytearray(pkt)
+        q[off] ^= 0x01
+        assert O.icrc(bytes(q)) != base, off
+    q = bytearray(pkt)
+    q[-1] ^= 0xFF  # the trailer itself is not covered
+    assert O.icrc(bytes(q)) == base
+
+
+def test_batch_oracles_agree_and_threads():
+    buf = oracle_c.synth_batch(11, 0, 300, 1024)
+    a = oracle_c.icrc_batch(buf, stride=1024, threads=1, kind="bytewise")
+    b = oracle_c.icrc_batch(buf, stride=1024, threads=4, kind="fast")
+    c = O.icrc_batch(buf, stride=1024)
+    np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(a, c)
+
+
+def test_synth_generator_header_template():
+    """Synthetic packets are RoCEv2 SEND_ONLY per the reference templates."""
+    buf = oracle_c.synth_batch(5, 1000, 8, 4096)
+    for k, pkt in enumerate(buf):
+        i = 1000 + k
+        assert pkt[0] == 0x45 and pkt[9] == 17
+        assert struct.unpack(">H", pkt[2:4].tobytes())[0] == 4096
+        assert struct.unpack(">H", pkt[22:24].tobytes())[0] == 4791
+        assert pkt[28] == 0x04 and pkt[29] == 0x40
+        assert struct.unpack(">I", b"\0" + pkt[37:40].tobytes())[0] == i & 0xFFFFFF
+    # masked fields are random across packets
+    assert len({int(p[1]) for p in oracle_c.synth_batch(5, 0, 64, 64)}) > 8
+
+
+def test_gf_helpers_against_bruteforce():
+    rng = random.Random(3)
+    for _ in range(20):
+        r, n = rng.getrandbits(32), rng.randrange(0, 300)
+        x8n = O.crc_shift(0x80000000, n)
+        assert O.gf_mul(r, x8n) == O.crc_shift(r, n)
