@@ -8,8 +8,8 @@ kernel's per-dispatch values and applies the gfx950 correction of
 the bytes of a wide (16 B/lane) coalesced streaming read, so it is doubled;
 WRITE_SIZE is taken as reported (4 B per packet, small).  Both are in KiB.
 
-Writes profiles/pmc_traffic.json, which bench.py reports as roofline.traffic
-when the workload matches.  Usage (on the GPU box):
+Writes gpurun_out/pmc_traffic.json; copied into profiles/pmc_traffic.json it is
+what bench.py reports as roofline.traffic when the workload matches.  Usage (on the GPU box):
     python3 tools/pmc_traffic.py [--out profiles/pmc_traffic.json]
 """
 import argparse
@@ -32,7 +32,8 @@ def run_pass(counter, outdir):
     for f in glob.glob(os.path.join(outdir, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if "icrc" in row["Kernel_Name"] and row["Counter_Name"] == counter:
+                k = row["Kernel_Name"]
+                if "icrc_" in k and "synth" not in k and row["Counter_Name"] == counter:
                     vals.append(float(row["Counter_Value"]))
     if not vals:
         raise SystemExit(f"no {counter} rows for the icrc kernel")
@@ -41,7 +42,7 @@ def run_pass(counter, outdir):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "pmc_traffic.json"))
     ap.add_argument("--scratch", default=os.path.join(ROOT, "gpurun_out", "pmc_traffic"))
     a = ap.parse_args()
     fetch_kib, nf = run_pass("FETCH_SIZE", os.path.join(a.scratch, "fetch"))
