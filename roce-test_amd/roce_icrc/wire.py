@@ -56,14 +56,19 @@ def qpn_of(dqpn: int) -> int:
     return dqpn & 0xFFFFFF
 
 
+def _i(v) -> int:
+    """Plain Python int of a field (the reference mixes ints and numpy scalars)."""
+    return int(v) if v is not None else 0
+
+
 def _element(e) -> bytes:
     if e is None:
         return b"\x00" * 4
-    if isinstance(e, tuple):
-        dmac, ln, wb_off, dst_addr = e
+    if isinstance(e, (tuple, list)):
+        dmac, ln, wb_off, dst_addr = (_i(x) for x in e)
         return struct.pack(">HHIQ", dmac & 0xFFFF, ln & 0xFFFF, wb_off & 0xFFFFFFFF,
                            dst_addr & 0xFFFFFFFFFFFFFFFF)
-    return struct.pack(">I", int(e) & 0xFFFFFFFF)
+    return struct.pack(">I", _i(e) & 0xFFFFFFFF)
 
 
 def ipv4_checksum(hdr: bytes) -> int:
@@ -83,28 +88,28 @@ def encode(p) -> bytearray:
     ext = b""
     if op == 0x15:  # REPL: repl_h {flag, item_cnt, item_id} + items
         items = b"".join(_element(e) for e in data)
-        ext = struct.pack(">BBH", 0, len(data) & 0xFF, getattr(p, "si", 0) & 0xFFFF)
+        ext = struct.pack(">BBH", 0, len(data) & 0xFF, _i(getattr(p, "si", 0)) & 0xFFFF)
         payload = items
     else:
         if op in RETH_OPS:
-            ext += struct.pack(">QII", getattr(p, "addr", 0) & 0xFFFFFFFFFFFFFFFF, 0,
-                               getattr(p, "len", 0) & 0xFFFFFFFF)
+            ext += struct.pack(">QII", _i(getattr(p, "addr", 0)) & 0xFFFFFFFFFFFFFFFF, 0,
+                               _i(getattr(p, "len", 0)) & 0xFFFFFFFF)
         if op in AETH_OPS:
             syndrome = 0x60 if opname == "NAK" else 0x00
-            ext += struct.pack(">I", (syndrome << 24) | (getattr(p, "msn", 0) & 0xFFFFFF))
+            ext += struct.pack(">I", (syndrome << 24) | (_i(getattr(p, "msn", 0)) & 0xFFFFFF))
         payload = b"".join(_element(e) for e in data)
     pad = (-len(payload)) % 4
     payload += b"\x00" * pad
     n = 20 + 8 + 12 + len(ext) + len(payload) + 4
-    smac, dmac = getattr(p, "smac", 0), getattr(p, "dmac", 0)
+    smac, dmac = _i(getattr(p, "smac", 0)), _i(getattr(p, "dmac", 0))
     ip = bytearray(struct.pack(">BBHHHBBH4s4s", 0x45, 0x02, n, 0x1234, 0x4000, 64, 17, 0,
                                ip_of(smac), ip_of(dmac)))
     ip[10:12] = struct.pack(">H", ipv4_checksum(bytes(ip)))
     sport = VIR_UDP_PORT if (smac is None or smac < 0) else (0xC000 | (smac & 0x3FFF))
     udp = struct.pack(">HHHH", sport, ROCE_PORT, n - 20, 0)
-    psn = getattr(p, "psn", 0) & 0xFFFFFF
+    psn = _i(getattr(p, "psn", 0)) & 0xFFFFFF
     ackreq = 0x80 if getattr(p, "ackreq", 0) else 0
-    bth = struct.pack(">BBHI", op, 0x40 | (pad << 4), 0xFFFF, qpn_of(getattr(p, "dqpn", 0))) + \
+    bth = struct.pack(">BBHI", op, 0x40 | (pad << 4), 0xFFFF, qpn_of(_i(getattr(p, "dqpn", 0)))) + \
         struct.pack(">I", (ackreq << 24) | psn)
     return bytearray(ip + udp + bth + ext + payload + b"\x00\x00\x00\x00")
 
