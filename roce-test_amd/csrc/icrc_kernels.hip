@@ -428,50 +428,66 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
     __builtin_amdgcn_sched_barrier(0);
     return t;
   };
-  auto step = [&](const u32x4 (&v)[4], Fin &pf, uint64_t pit) -> Fin {
+
+  // Chunk registers of one region after the LDS transpose: ch[h][piece],
+  // chain h = 32-byte chunk 64h + lane.
+  struct Chunks {
+    u32x4 c[2][2];
+  };
+  auto stage_write = [&](const u32x4 (&v)[4], int h) {
+    if (ABL & 2) return;
+    *reinterpret_cast<u32x4 *>(stage + wr0) = v[2 * h];
+    *reinterpret_cast<u32x4 *>(stage + wr1) = v[2 * h + 1];
+  };
+  auto stage_read = [&](const u32x4 (&v)[4], Chunks &ch, int h) {
+    if (ABL & 2) {
+      ch.c[h][0] = v[2 * h];
+      ch.c[h][1] = v[2 * h + 1];
+      return;
+    }
+    ch.c[h][0] = *reinterpret_cast<const u32x4 *>(stage + rd0);
+    ch.c[h][1] = *reinterpret_cast<const u32x4 *>(stage + rd1);
+  };
+
+  // Fold region i (chunks `cc`) while (a) transposing region i+1 (loaded in
+  // `vn`) into `cn` through the LDS slot, and (b) finishing region i-1 (pf,
+  // pit) in VALU slices -- all in the shadow of the fold steps' table reads,
+  // so neither the transpose round trips nor the memory wait for region i+1
+  // sit on the wave's critical path.
+  auto step = [&](Chunks &cc, const u32x4 (&vn)[4], Chunks &cn, Fin &pf, uint64_t pit) -> Fin {
     uint64_t ts0 = 0;
     if (ABL & 32) {
       ts0 = stamp();
       if (!st_first) st_first = ts0;
     }
-    u32x4 ch[2][2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      if (ABL & 2) {
-        ch[h][0] = v[2 * h];
-        ch[h][1] = v[2 * h + 1];
-      } else {
-        *reinterpret_cast<u32x4 *>(stage + wr0) = v[2 * h];
-        *reinterpret_cast<u32x4 *>(stage + wr1) = v[2 * h + 1];
-        ch[h][0] = *reinterpret_cast<const u32x4 *>(stage + rd0);
-        ch[h][1] = *reinterpret_cast<const u32x4 *>(stage + rd1);
-      }
-    }
-    uint64_t ts1 = 0;
-    if (ABL & 32) {
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): staging data in registers
-      ts1 = stamp();
-      st_stage += ts1 - ts0;
-    }
     Fin f;
-    f.tr0 = ch[0][1][3];
-    f.tr1 = ch[1][1][3];
-    ch[0][0][0] = or_xor(ch[0][0][0], c0.mw0, c0.xw0);
-    ch[1][0][0] = or_xor(ch[1][0][0], c1.mw0, c1.xw0);
-    ch[0][0][2] |= c0.m2;
-    ch[1][0][2] |= c1.m2;
-    ch[0][1][2] |= c0.m6;
-    ch[1][1][2] |= c1.m6;
-    ch[0][1][3] &= c0.keep7;
-    ch[1][1][3] &= c1.keep7;
-    uint32_t x0 = ch[0][0][0], x1 = ch[1][0][0];  // register (0) ^ first word
+    f.tr0 = cc.c[0][1][3];
+    f.tr1 = cc.c[1][1][3];
+    uint32_t w[2][8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) w[h][j] = cc.c[h][j >> 2][j & 3];
+    w[0][0] = or_xor(w[0][0], c0.mw0, c0.xw0);
+    w[1][0] = or_xor(w[1][0], c1.mw0, c1.xw0);
+    w[0][2] |= c0.m2;
+    w[1][2] |= c1.m2;
+    w[0][6] |= c0.m6;
+    w[1][6] |= c1.m6;
+    w[0][7] &= c0.keep7;
+    w[1][7] &= c1.keep7;
+    uint32_t x0 = w[0][0], x1 = w[1][0];  // register (0) ^ first word
 #pragma unroll
     for (int j = 1; j <= 8; ++j) {
-      const uint32_t w0 = j < 8 ? ch[0][j >> 2][j & 3] : 0u, w1 = j < 8 ? ch[1][j >> 2][j & 3] : 0u;
+      const uint32_t w0 = j < 8 ? w[0][j] : 0u, w1 = j < 8 ? w[1][j] : 0u;
       if (ABL & 1) {
         x0 = __builtin_amdgcn_perm(x0, w0, 0x05040100u) ^ w0;
         x1 = __builtin_amdgcn_perm(x1, w1, 0x05040100u) ^ w1;
         fin_slice(pf, j - 1);
+        if (j == 3) stage_write(vn, 0);
+        if (j == 4) stage_read(vn, cn, 0);
+        if (j == 5) stage_write(vn, 1);
+        if (j == 6) stage_read(vn, cn, 1);
       } else {
         const uint32_t t03 = lds_at(lds, __builtin_amdgcn_perm(x0, lt.lo0, 0x0C0C0400u));
         const uint32_t t02 = lds_at(lds, __builtin_amdgcn_perm(x0, lt.lo0, 0x0C0C0500u) + 128);
@@ -481,6 +497,10 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
         const uint32_t t12 = lds_at(lds, __builtin_amdgcn_perm(x1, lt.lo0, 0x0C0C0500u) + 128);
         const uint32_t t11 = lds_at(lds, __builtin_amdgcn_perm(x1, lt.lo1, 0x0C020600u));
         const uint32_t t10 = lds_at(lds, __builtin_amdgcn_perm(x1, lt.lo1, 0x0C020700u) + 128);
+        if (j == 3) stage_write(vn, 0);  // region i+1, round 0 (waits for its load)
+        if (j == 4) stage_read(vn, cn, 0);
+        if (j == 5) stage_write(vn, 1);
+        if (j == 6) stage_read(vn, cn, 1);
         __builtin_amdgcn_sched_barrier(0);
         fin_slice(pf, j - 1);  // independent VALU work while the reads fly
         __builtin_amdgcn_sched_barrier(0);
@@ -494,32 +514,38 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
     if (ABL & 32) {
       asm volatile("" ::"v"(x0), "v"(x1));
       const uint64_t ts2 = stamp();
-      st_fold += ts2 - ts1;
+      st_fold += ts2 - ts0;
       st_t0 = ts2;
     }
     fin_init(f);
     return f;
   };
 
-  // Two register buffers used in turn (loop unrolled by two): no cur = nxt
-  // copies, which the scheduler would otherwise hoist right behind the
-  // prefetch and stall on it.
+  // Two load buffers and two chunk buffers used in turn (loop unrolled by
+  // two, no register copies): region r is loaded into L[r&1] two steps before
+  // it is folded and transposed into C[r&1] during the fold of region r-1.
   uint64_t it = wave;
-  u32x4 bufA[4], bufB[4];
-  load(it, bufA);
+  u32x4 LA[4], LB[4];
+  Chunks CA, CB;
+  load(it, LA);
+  load(it + nwaves, LB);
+  stage_write(LA, 0);
+  stage_read(LA, CA, 0);
+  stage_write(LA, 1);
+  stage_read(LA, CA, 1);
   Fin prev{};
   fin_init(prev);
   uint64_t pit = a.n_iters;  // nothing to finish before the first fold
   while (it < a.n_iters) {
-    load(it + nwaves, bufB);  // past the batch: zero-length resource, reads 0
+    load(it + 2 * nwaves, LA);  // LA was transposed into CA last step
     __builtin_amdgcn_sched_barrier(0);
-    prev = step(bufA, prev, pit);
+    prev = step(CA, LB, CB, prev, pit);
     pit = it;
     it += nwaves;
     if (it >= a.n_iters) break;
-    load(it + nwaves, bufA);
+    load(it + 2 * nwaves, LB);
     __builtin_amdgcn_sched_barrier(0);
-    prev = step(bufB, prev, pit);
+    prev = step(CB, LA, CA, prev, pit);
     pit = it;
     it += nwaves;
   }
