@@ -46,6 +46,15 @@ class ICRCError(RuntimeError):
 
 
 def _load():
+    # libroceicrc and PyTorch-ROCm each need a libamdhip64.so.7 (ROCm 7.2 from
+    # /opt/rocm, resp. torch's bundled copy) under the same SONAME: whichever
+    # is loaded first serves the whole process.  Load torch's first when it is
+    # installed so that torch tensors/streams and our kernels share one HIP
+    # runtime (the other order leaves torch with "No HIP GPUs are available").
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"libroceicrc.so not found at {LIB_PATH}; build it with "
