@@ -348,18 +348,22 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
   const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
   const uint64_t total = a.count * a.stride;
 
-  auto load = [&](uint64_t it, u32x4 (&v)[4]) {
+  auto region_rsrc = [&](uint64_t it) {
     const uint64_t off = it * 4096u;
     const uint32_t rem = off < total ? (uint32_t)(total - off < 4096u ? total - off : 4096u) : 0u;
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(a.base + (off < total ? off : 0), rem);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (ABL & 8) {
-        v[k] = u32x4{(uint32_t)it * 977u + k, lane, (uint32_t)it, 5u};
-      } else {
-        v[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 1024 * k + 16 * lane, 0, 2));
-      }
+    return make_rsrc(a.base + (off < total ? off : 0), rem);
+  };
+  auto load_piece = [&](__amdgpu_buffer_rsrc_t rs, uint64_t it, u32x4 (&v)[4], int k) {
+    if (ABL & 8) {
+      v[k] = u32x4{(uint32_t)it * 977u + k, lane, (uint32_t)it, 5u};
+    } else {
+      v[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 1024 * k + 16 * lane, 0, 2));
     }
+  };
+  auto load = [&](uint64_t it, u32x4 (&v)[4]) {
+    const __amdgpu_buffer_rsrc_t rs = region_rsrc(it);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) load_piece(rs, it, v, k);
   };
 
   // Re-alignment state of one folded region, advanced in 8 VALU slices.
@@ -454,7 +458,12 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
   // pit) in VALU slices -- all in the shadow of the fold steps' table reads,
   // so neither the transpose round trips nor the memory wait for region i+1
   // sit on the wave's critical path.
-  auto step = [&](Chunks &cc, const u32x4 (&vn)[4], Chunks &cn, Fin &pf, uint64_t pit) -> Fin {
+  // `ld`/`lit`: buffer to refill with region `lit`; its 4 loads are issued
+  // one per fold step (1-4), where an issue stall under memory back-pressure
+  // overlaps the step's own LDS wait instead of blocking the wave up front.
+  auto step = [&](Chunks &cc, const u32x4 (&vn)[4], Chunks &cn, Fin &pf, uint64_t pit, u32x4 (&ld)[4],
+                  uint64_t lit) -> Fin {
+    const __amdgpu_buffer_rsrc_t lrs = region_rsrc(lit);
     uint64_t ts0 = 0;
     if (ABL & 32) {
       ts0 = stamp();
@@ -484,6 +493,7 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
         x0 = __builtin_amdgcn_perm(x0, w0, 0x05040100u) ^ w0;
         x1 = __builtin_amdgcn_perm(x1, w1, 0x05040100u) ^ w1;
         fin_slice(pf, j - 1);
+        if (j <= 4) load_piece(lrs, lit, ld, j - 1);
         if (j == 3) stage_write(vn, 0);
         if (j == 4) stage_read(vn, cn, 0);
         if (j == 5) stage_write(vn, 1);
@@ -497,6 +507,7 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
         const uint32_t t12 = lds_at(lds, __builtin_amdgcn_perm(x1, lt.lo0, 0x0C0C0500u) + 128);
         const uint32_t t11 = lds_at(lds, __builtin_amdgcn_perm(x1, lt.lo1, 0x0C020600u));
         const uint32_t t10 = lds_at(lds, __builtin_amdgcn_perm(x1, lt.lo1, 0x0C020700u) + 128);
+        if (j <= 4) load_piece(lrs, lit, ld, j - 1);
         if (j == 3) stage_write(vn, 0);  // region i+1, round 0 (waits for its load)
         if (j == 4) stage_read(vn, cn, 0);
         if (j == 5) stage_write(vn, 1);
@@ -537,15 +548,11 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
   fin_init(prev);
   uint64_t pit = a.n_iters;  // nothing to finish before the first fold
   while (it < a.n_iters) {
-    load(it + 2 * nwaves, LA);  // LA was transposed into CA last step
-    __builtin_amdgcn_sched_barrier(0);
-    prev = step(CA, LB, CB, prev, pit);
+    prev = step(CA, LB, CB, prev, pit, LA, it + 2 * nwaves);  // LA was transposed into CA last step
     pit = it;
     it += nwaves;
     if (it >= a.n_iters) break;
-    load(it + 2 * nwaves, LB);
-    __builtin_amdgcn_sched_barrier(0);
-    prev = step(CB, LA, CA, prev, pit);
+    prev = step(CB, LA, CA, prev, pit, LB, it + 2 * nwaves);
     pit = it;
     it += nwaves;
   }
