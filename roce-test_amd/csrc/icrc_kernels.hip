@@ -309,7 +309,8 @@ __device__ __forceinline__ ChunkMask chunk_mask(uint32_t pos, uint32_t last) {
 // ABL is a timing-only ablation mask used by tools/microbench (the product
 // instantiates ABL = 0 only): 1 no table fold, 2 no LDS transpose, 4 no lane
 // combine, 8 no global loads, 16 no stores, 32 s_memtime stamps into
-// a.stamps (diagnostic: per wave {staging wait, fold, total} cycles).
+// a.stamps (diagnostic: per wave {staging wait, fold, total} cycles),
+// 64 no LDS drain at the step boundary, 256 s_sleep at the step boundary.
 //
 // Software pipeline per wave: step i loads region i+1, transposes and folds
 // region i (LDS-bound) and, in the same basic block, finishes region i-1
@@ -468,6 +469,20 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
     if (ABL & 32) {
       ts0 = stamp();
       if (!st_first) st_first = ts0;
+    }
+    if (!(ABL & 64)) {
+      // Drain this wave's LDS queue at the step boundary (lgkmcnt(0)): the
+      // transposed chunks of this region must be in registers anyway, and
+      // measured 8 % faster than letting the compiler's counted waits
+      // interleave the drain with the first table reads (tools/microbench).
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (ABL & 256) {  // experiment: short sleep at the step boundary
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_sched_barrier(0);
     }
     Fin f;
     f.tr0 = cc.c[0][1][3];

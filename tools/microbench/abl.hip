@@ -33,6 +33,9 @@ int main() {
   rep("fold only (no loads/transpose/comb)", run<8 | 2 | 4>(a, grid, 10));
   rep("loads+fold (no transpose/comb)", run<2 | 4>(a, grid, 10));
   rep("no stores", run<16>(a, grid, 10));
+  rep("exp: no drain at step", run<64>(a, grid, 10));
+  rep("exp: s_sleep 1 at step", run<256>(a, grid, 10));
+  rep("full again", run<0>(a, grid, 10));
   {
     const int nw = grid * kWaves;
     uint64_t *st; CK(hipMalloc(&st, 3 * 8 * nw)); a.stamps = st;
