@@ -310,7 +310,8 @@ __device__ __forceinline__ ChunkMask chunk_mask(uint32_t pos, uint32_t last) {
 // instantiates ABL = 0 only): 1 no table fold, 2 no LDS transpose, 4 no lane
 // combine, 8 no global loads, 16 no stores, 32 s_memtime stamps into
 // a.stamps (diagnostic: per wave {staging wait, fold, total} cycles),
-// 64 no LDS drain at the step boundary, 256 s_sleep at the step boundary.
+// 64 no LDS drain at the step boundary, 256 s_sleep at the step boundary,
+// 512 no per-region stores (results XOR-folded, one store per wave at exit).
 //
 // Software pipeline per wave: step i loads region i+1, transposes and folds
 // region i (LDS-bound) and, in the same basic block, finishes region i-1
@@ -345,13 +346,19 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
   const uint32_t wr0 = 16u * stage_slot(lane), wr1 = 16u * stage_slot(64u + lane);
   const uint32_t rd0 = 16u * stage_slot(2u * lane), rd1 = 16u * stage_slot(2u * lane + 1u);
 
+  // Each wave owns a contiguous block of regions, so its results are
+  // consecutive packets and (4 KiB packets) leave in coalesced 64-dword
+  // stores instead of one scattered dword per region.
   const uint64_t wave = (uint64_t)blockIdx.x * kWaves + wid;
   const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
   const uint64_t total = a.count * a.stride;
+  const uint64_t per_wave = (a.n_iters + nwaves - 1) / nwaves;
+  const uint64_t it_begin = wave * per_wave < a.n_iters ? wave * per_wave : a.n_iters;
+  const uint64_t it_end = it_begin + per_wave < a.n_iters ? it_begin + per_wave : a.n_iters;
 
-  auto region_rsrc = [&](uint64_t it) {
+  auto region_rsrc = [&](uint64_t it) {  // regions outside this wave's block read nothing
     const uint64_t off = it * 4096u;
-    const uint32_t rem = off < total ? (uint32_t)(total - off < 4096u ? total - off : 4096u) : 0u;
+    const uint32_t rem = (off < total && it < it_end) ? (uint32_t)(total - off < 4096u ? total - off : 4096u) : 0u;
     return make_rsrc(a.base + (off < total ? off : 0), rem);
   };
   auto load_piece = [&](__amdgpu_buffer_rsrc_t rs, uint64_t it, u32x4 (&v)[4], int k) {
@@ -402,7 +409,13 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
     }
   };
   // Reduce across the packet's lanes and store region `it` (>= n_iters: dropped).
+  uint32_t sink = 0;  // ABL & 512: results folded here, one store at the end
+  uint32_t res = 0;   // BIG: result of this wave's region it_begin + 64q + lane
   auto fin_store = [&](uint64_t it, const Fin &f) {
+    if (ABL & 512) {
+      sink ^= xor3(f.a1[0], f.a1[1], f.a1[2] ^ f.a1[3]) ^ xor3(f.a0[0], f.a0[1], f.a0[2] ^ f.a0[3]);
+      return;
+    }
     const uint64_t p0 = it * ppr;
     const uint32_t nout = p0 < a.count ? (uint32_t)(a.count - p0 < ppr ? a.count - p0 : ppr) : 0u;
     const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out + (p0 < a.count ? p0 : 0), 4u * nout);
@@ -412,7 +425,18 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
     } else if (BIG) {
       const uint32_t r = group_xor(xor3(f.a1[0], f.a1[1], f.a1[2] ^ f.a1[3]), 6);
       const uint32_t val = a.verify ? (f.tr1 == ~r ? 1u : 0u) : ~r;
-      __builtin_amdgcn_raw_buffer_store_b32(val, ro, store1 ? 0u : 0x7FFFFFF0u, 0, 0);
+      // Collect: lane (k mod 64) keeps the result of local region k; every
+      // 64th region (and the block's last) the whole group leaves in one
+      // coalesced store.  The store is issued every step with out-of-range
+      // offsets when not flushing, so no VMEM op sits under a branch.
+      const bool live = it < it_end;
+      const uint32_t k = (uint32_t)(it - it_begin) & 63u;
+      res = (live && lane == k) ? val : res;
+      const bool flush = live && (k == 63u || it + 1 == it_end);
+      const uint64_t g0 = it_begin + ((it - it_begin) & ~(uint64_t)63);
+      const uint32_t ng = live ? (uint32_t)(a.count - g0 < 64u ? a.count - g0 : 64u) : 0u;
+      const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.out + (live ? g0 : 0), 4u * ng);
+      __builtin_amdgcn_raw_buffer_store_b32(res, rg, (flush && lane <= k) ? 4u * lane : 0x7FFFFFF0u, 0, 0);
     } else {
       const uint32_t s0 = group_xor_masked(xor3(f.a0[0], f.a0[1], f.a0[2] ^ f.a0[3]), lm);
       const uint32_t s1 = group_xor_masked(xor3(f.a1[0], f.a1[1], f.a1[2] ^ f.a1[3]), lm);
@@ -550,11 +574,11 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
   // Two load buffers and two chunk buffers used in turn (loop unrolled by
   // two, no register copies): region r is loaded into L[r&1] two steps before
   // it is folded and transposed into C[r&1] during the fold of region r-1.
-  uint64_t it = wave;
+  uint64_t it = it_begin;
   u32x4 LA[4], LB[4];
   Chunks CA, CB;
   load(it, LA);
-  load(it + nwaves, LB);
+  load(it + 1, LB);
   stage_write(LA, 0);
   stage_read(LA, CA, 0);
   stage_write(LA, 1);
@@ -562,18 +586,19 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
   Fin prev{};
   fin_init(prev);
   uint64_t pit = a.n_iters;  // nothing to finish before the first fold
-  while (it < a.n_iters) {
-    prev = step(CA, LB, CB, prev, pit, LA, it + 2 * nwaves);  // LA was transposed into CA last step
+  while (it < it_end) {
+    prev = step(CA, LB, CB, prev, pit, LA, it + 2);  // LA was transposed into CA last step
     pit = it;
-    it += nwaves;
-    if (it >= a.n_iters) break;
-    prev = step(CB, LA, CA, prev, pit, LB, it + 2 * nwaves);
+    it += 1;
+    if (it >= it_end) break;
+    prev = step(CB, LA, CA, prev, pit, LB, it + 2);
     pit = it;
-    it += nwaves;
+    it += 1;
   }
 #pragma unroll
   for (int sl = 0; sl < 8; ++sl) fin_slice(prev, sl);
   fin_store(pit, prev);
+  if (ABL & 512) a.out[wave * 64 + lane] = sink;
   if ((ABL & 32) && lane == 0) {
     a.stamps[3 * wave + 0] = st_stage;
     a.stamps[3 * wave + 1] = st_fold;

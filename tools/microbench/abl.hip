@@ -14,7 +14,7 @@ template <int ABL> float run(TskArgs a, int grid, int reps) {
 }
 int main() {
   const uint64_t n = 4096, count = 1 << 20;
-  uint8_t *buf; uint32_t *out; CK(hipMalloc(&buf, n * count)); CK(hipMalloc(&out, 4 * count));
+  uint8_t *buf; uint32_t *out; CK(hipMalloc(&buf, n * count)); CK(hipMalloc(&out, 4 * count + (1 << 20)));
   CK(hipMemset(buf, 0x3c, n * count));
   hipDeviceProp_t p; CK(hipGetDeviceProperties(&p, 0));
   TskArgs a{}; a.base = buf; a.stride = n; a.count = count; a.out = out; a.n_iters = count * n / 4096; a.log2C = 7;
@@ -22,6 +22,10 @@ int main() {
   for (int j = 0; j < 32; ++j) a.YB[j] = 0x85EBCA6Bu * (j + 3);
   const int grid = p.multiProcessorCount;
   auto rep = [&](const char *nm, float ms) { printf("%-36s %7.3f ms  %7.1f GB/s\n", nm, ms, n * count / (ms * 1e-3) / 1e9); };
+  for (int r = 0; r < 3; ++r) { char nm[64]; snprintf(nm, 64, "full #%d (x20)", r); rep(nm, run<0>(a, grid, 20)); }
+  rep("exp: one store per wave", run<512>(a, grid, 20));
+  rep("full", run<0>(a, grid, 20));
+  rep("exp: one store per wave", run<512>(a, grid, 20));
   rep("full", run<0>(a, grid, 10));
   rep("no fold", run<1>(a, grid, 10));
   rep("no transpose", run<2>(a, grid, 10));
