@@ -424,7 +424,8 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
       __builtin_amdgcn_raw_buffer_store_b32(f.r0 ^ f.r1, ro, store1 ? 0u : 0x7FFFFFF0u, 0, 0);
     } else if (BIG) {
       const uint32_t r = group_xor(xor3(f.a1[0], f.a1[1], f.a1[2] ^ f.a1[3]), 6);
-      const uint32_t val = a.verify ? (f.tr1 == ~r ? 1u : 0u) : ~r;
+      const uint32_t trl = __builtin_amdgcn_readlane(f.tr1, 63);  // the trailer lives in lane 63
+      const uint32_t val = a.verify ? (trl == ~r ? 1u : 0u) : ~r;
       // Collect: lane (k mod 64) keeps the result of local region k; every
       // 64th region (and the block's last) the whole group leaves in one
       // coalesced store.  The store is issued every step with out-of-range

@@ -15,7 +15,13 @@ template <int ABL> float run(TskArgs a, int grid, int reps) {
 int main() {
   const uint64_t n = 4096, count = 1 << 20;
   uint8_t *buf; uint32_t *out; CK(hipMalloc(&buf, n * count)); CK(hipMalloc(&out, 4 * count + (1 << 20)));
-  CK(hipMemset(buf, 0x3c, n * count));
+  {  // random bytes (DVFS: constant data runs at a higher clock than real traffic)
+    uint8_t *h = (uint8_t *)malloc(n * count);
+    uint64_t x = 0x9E3779B97F4A7C15ull;
+    for (uint64_t i = 0; i < n * count / 8; ++i) { x ^= x << 13; x ^= x >> 7; x ^= x << 17; ((uint64_t *)h)[i] = x; }
+    CK(hipMemcpy(buf, h, n * count, hipMemcpyHostToDevice));
+    free(h);
+  }
   hipDeviceProp_t p; CK(hipGetDeviceProperties(&p, 0));
   TskArgs a{}; a.base = buf; a.stride = n; a.count = count; a.out = out; a.n_iters = count * n / 4096; a.log2C = 7;
   for (int i = 0; i < 128; ++i) a.K[i] = 0x9E3779B9u * (i + 1);
