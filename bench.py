@@ -35,8 +35,10 @@ SEED = 0x1CEC0DE
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    # The first ~20 launches of a fresh process run ~10 % slower (clock / TLB
+    # ramp measured in tools/microbench/abl.hip); 40 untimed steps cover it.
+    ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--count", type=int, default=1 << 20, help="packets per GPU")
     ap.add_argument("--size", type=int, default=4096, help="L3 packet bytes (IPv4 total_len)")
     ap.add_argument("--no-gather", action="store_true", help="skip the RCCL all-gather at N>1")
@@ -48,7 +50,7 @@ def parse():
 def load_traffic(size, count):
     """HBM bytes per launch measured by a separate rocprofv3 --pmc pass
     (profiles/*pmc*.json, produced by tools/pmc_traffic.py), or None."""
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")  # from tools/pmc_traffic.py
     try:
         with open(p) as f:
             d = json.load(f)

@@ -17,6 +17,10 @@ fi
 timeout -k 10 300 python bench.py ${BENCH_ARGS:-} > "$OUT/bench.json" 2> "$OUT/bench.err"; ok $? bench
 cat "$OUT/bench.json"
 if [ "${SKIP_PROF:-0}" != 1 ]; then
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --steps 20 --warmup 3 --no-cpu > "$OUT/prof.log" 2>&1; ok $? rocprof
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --no-cpu > "$OUT/prof.log" 2>&1; ok $? rocprof
   find "$OUT/prof" -name '*kernel_stats.csv' -exec cat {} \;
+fi
+if [ "${SKIP_PMC:-0}" != 1 ]; then
+  timeout -k 10 600 python3 tools/pmc_traffic.py --out "$OUT/pmc_traffic.json" --scratch "$OUT/pmc_scratch" > "$OUT/pmc.log" 2>&1; ok $? pmc
+  cat "$OUT/pmc_traffic.json"
 fi
