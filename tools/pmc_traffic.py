@@ -45,6 +45,7 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "pmc_traffic.json"))
     ap.add_argument("--scratch", default=os.path.join(ROOT, "gpurun_out", "pmc_traffic"))
     a = ap.parse_args()
+    a.out, a.scratch = os.path.abspath(a.out), os.path.abspath(a.scratch)
     fetch_kib, nf = run_pass("FETCH_SIZE", os.path.join(a.scratch, "fetch"))
     write_kib, nw = run_pass("WRITE_SIZE", os.path.join(a.scratch, "write"))
     count, size = 1 << 20, 4096
