@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--count", type=int, default=1 << 20, help="packets per GPU")
     ap.add_argument("--size", type=int, default=4096, help="L3 packet bytes (IPv4 total_len)")
     ap.add_argument("--no-gather", action="store_true", help="skip the RCCL all-gather at N>1")
+    ap.add_argument("--overlap-gather", action="store_true",
+                    help="run step i's all-gather async, overlapping step i+1's kernel (default: in-stream)")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="wall budget of the CPU baseline")
     ap.add_argument("--no-cpu", action="store_true")
     return ap.parse_args()
@@ -104,46 +106,76 @@ def main():
 
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    distributed = "MASTER_ADDR" in os.environ  # launched by torch.distributed.run
+    if distributed:
         dist.init_process_group("nccl", device_id=dev)
     ctx = roce_icrc.Context(devices=[local])
 
     count, size = args.count, args.size
     stream = torch.cuda.current_stream()
     pk = torch.empty(count * size, dtype=torch.uint8, device=dev)
-    out = torch.empty(count, dtype=torch.int32, device=dev)
+    # Rank r owns global packets [r*count, (r+1)*count) (dist.shard_range of
+    # world*count): generated on its own device from the global index.
     ctx.synth_device(pk, SEED, rank * count, count, size, stream=stream)
-    gathered = torch.empty(world * count, dtype=torch.int32, device=dev) if world > 1 else None
-    do_gather = world > 1 and not args.no_gather
+    do_gather = distributed and not args.no_gather
+    # Double-buffered results.  Default: the all-gather is ordered after the
+    # kernel on the compute stream.  --overlap-gather: step i's all-gather
+    # runs async on RCCL's stream, overlapping step i+1's kernel, and a buffer
+    # is reused only after the gather that read it has been waited for.  (Each
+    # ICRC block fills a whole CU's LDS, so RCCL blocks compete for whole CUs;
+    # measured in DESIGN.md.)
+    outs = [torch.empty(count, dtype=torch.int32, device=dev) for _ in range(2)]
+    gathered = [torch.empty(world * count, dtype=torch.int32, device=dev) for _ in range(2)] if do_gather else None
+    pending = [None, None]
 
-    def step(ev=None):
+    def step(i, ev=None):
+        b = i & 1
+        if pending[b] is not None:
+            pending[b].wait()  # the current stream waits for the gather that read outs[b]
+            pending[b] = None
         if ev is not None:
             ev[0].record(stream)
-        ctx.batch_device(pk, count, out, stride=size, stream=stream)
+        ctx.batch_device(pk, count, outs[b], stride=size, stream=stream)
         if ev is not None:
             ev[1].record(stream)
         if do_gather:
-            dist.all_gather_into_tensor(gathered, out)
+            if args.overlap_gather:
+                pending[b] = dist.all_gather_into_tensor(gathered[b], outs[b], async_op=True)
+            else:
+                dist.all_gather_into_tensor(gathered[b], outs[b])
 
-    for _ in range(args.warmup):
-        step()
+    def drain():
+        for b in range(2):
+            if pending[b] is not None:
+                pending[b].wait()
+                pending[b] = None
+
+    for i in range(args.warmup):
+        step(i)
+    drain()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(args.steps)]
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(evs[i])
+        step(i, evs[i])
+    drain()
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+    out = outs[(args.steps - 1) & 1]
+    if do_gather:  # every rank holds all world*count ICRCs in packet order
+        g = gathered[(args.steps - 1) & 1]
+        if not torch.equal(g[rank * count:(rank + 1) * count], out):
+            raise SystemExit("bench: all-gathered ICRCs do not contain this rank's shard")
 
-    if world > 1:
+    if distributed:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
@@ -168,7 +200,8 @@ def main():
         "dtype": "u8",
         "data": "synthetic (device-generated RoCEv2 SEND_ONLY packets, seeded; reference P4 header template)",
         "config": {"workload": f"{count} x {size} B RoCEv2 packets per GPU, device-resident, "
-                               f"streaming ICRC kernel" + (" + RCCL all-gather of ICRCs" if do_gather else ""),
+                               f"streaming ICRC kernel" + (" + RCCL all-gather of ICRCs" + (" (overlapped)" if args.overlap_gather else "")
+                                                           if do_gather else ""),
                    "packets_per_gpu": count, "packet_bytes": size,
                    "parallelism": f"dp{world}" + (" (all-gather u32 results)" if do_gather else "")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -186,7 +219,7 @@ def main():
     if rank == 0:
         print(json.dumps(result), flush=True)
     ctx.close()
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 

@@ -82,9 +82,10 @@ int ricrc_device_count(const ricrc_ctx *ctx);
  * len ? len[i] : (stride - l3_offset) bytes long; out[i] = its ICRC.
  *
  * ricrc_batch_host: host buffers in and out.  Packets are sharded over the
- * context's GPUs by bytes, staged through pinned memory (or DMA'd directly if
- * base was allocated by ricrc_host_alloc / is otherwise pinned), computed on
- * the GPUs and copied back.  Synchronous.  Validates every length
+ * context's GPUs by bytes, staged through pinned memory by parallel CPU
+ * copies (or DMA'd directly if base was allocated by ricrc_host_alloc /
+ * registered with ricrc_host_register / is otherwise pinned), computed on
+ * the GPUs and copied back; chunks are double-buffered per GPU.  Synchronous.  Validates every length
  * (RICRC_MIN_LEN..RICRC_MAX_LEN) before touching a GPU.
  *
  * ricrc_batch_device: device-resident batch on context device `dev`
@@ -106,9 +107,19 @@ int ricrc_verify_device(ricrc_ctx *ctx, int dev, const void *d_base, const uint6
                         uint32_t *d_out, void *stream);
 
 /* Pinned host memory for NIC-ring style buffers (the role of huge_malloc in
- * common/huge_malloc.h:12-22).  NULL on failure. */
+ * common/huge_malloc.h:12-22).  NULL on failure.  ricrc_batch_host DMAs
+ * straight out of such memory (no CPU copy) whenever a chunk's packets form
+ * an ascending span -- a fixed stride, or ring offsets with little slack. */
 void *ricrc_host_alloc(ricrc_ctx *ctx, uint64_t bytes);
 void ricrc_host_free(ricrc_ctx *ctx, void *p);
+
+/* Pin an existing host buffer (e.g. a hugepage NIC ring from huge_malloc,
+ * common/huge_malloc.h:12-22, or a numpy array) for the lifetime of the
+ * registration, so ricrc_batch_host reads it by DMA.  0, -EINVAL (NULL, zero
+ * size, already registered / not registered), -ENOMEM, -EIO.  Registrations
+ * still live at ricrc_destroy are released there. */
+int ricrc_host_register(ricrc_ctx *ctx, void *p, uint64_t bytes);
+int ricrc_host_unregister(ricrc_ctx *ctx, void *p);
 
 /* Synthetic RoCEv2 SEND_ONLY batch generator on device `dev` (bench / tests):
  * packet k of the buffer is global packet first+k, n bytes, at d_buf + k*stride.

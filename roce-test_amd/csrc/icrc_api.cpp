@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "../../include/roce_icrc.h"
@@ -36,6 +37,7 @@ struct Slot {
   uint64_t *h_off = nullptr;
   uint32_t *h_len = nullptr;
   uint32_t *h_out = nullptr;
+  hipStream_t st = nullptr;  // per slot: chunk k+1's H2D overlaps chunk k's kernel/D2H
   hipEvent_t done = nullptr;
 };
 
@@ -43,7 +45,8 @@ struct Dev {
   int id = 0;
   int n_cu = 0;
   hipStream_t stream = nullptr;
-  uint32_t *d_inv = nullptr;  // x^(-8 z), z <= 4096
+  uint32_t *d_inv = nullptr;   // x^(-8 z), z <= 4096
+  uint32_t *d_invb = nullptr;  // row z: multiplication basis of x^(-8 z) (32 words), z <= 4096
   Slot slot[2];
   bool staged = false;
 };
@@ -76,8 +79,15 @@ uint32_t x8n_host(uint64_t n) { return gf_x8n(n); }
 
 }  // namespace
 
+struct HostRange {
+  uintptr_t lo, hi;
+  bool owned;  // ricrc_host_alloc (else ricrc_host_register)
+};
+
 struct ricrc_ctx {
   std::vector<Dev> devs;
+  std::vector<HostRange> pinned;  // host ranges the DMA engines may read directly
+  int host_threads = 1;           // CPU copy threads for pageable host batches
 };
 
 namespace {
@@ -98,6 +108,13 @@ int init_dev(Dev &d) {
   }
   HIP_TRY(hipMalloc(&d.d_inv, 4097 * sizeof(uint32_t)));
   HIP_TRY(hipMemcpy(d.d_inv, inv.data(), 4097 * sizeof(uint32_t), hipMemcpyHostToDevice));
+  std::vector<uint32_t> rows(4097 * 32);
+  for (int z = 0; z <= 4096; ++z) {
+    const Basis b = make_const_basis(inv[z]);
+    std::copy(b.q, b.q + 32, rows.begin() + 32 * z);
+  }
+  HIP_TRY(hipMalloc(&d.d_invb, rows.size() * sizeof(uint32_t)));
+  HIP_TRY(hipMemcpy(d.d_invb, rows.data(), rows.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
   return 0;
 }
 
@@ -113,6 +130,7 @@ int ensure_staging(Dev &d) {
     HIP_TRY(hipHostMalloc(&s.h_off, kStagePkts * sizeof(uint64_t), hipHostMallocDefault));
     HIP_TRY(hipHostMalloc(&s.h_len, kStagePkts * sizeof(uint32_t), hipHostMallocDefault));
     HIP_TRY(hipHostMalloc(&s.h_out, kStagePkts * sizeof(uint32_t), hipHostMallocDefault));
+    HIP_TRY(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
   }
   d.staged = true;
@@ -125,8 +143,10 @@ void free_dev(Dev &d) {
     if (s.done) (void)hipEventSynchronize(s.done), (void)hipEventDestroy(s.done);
     (void)hipFree(s.d_buf), (void)hipFree(s.d_off), (void)hipFree(s.d_len), (void)hipFree(s.d_out);
     (void)hipHostFree(s.h_buf), (void)hipHostFree(s.h_off), (void)hipHostFree(s.h_len), (void)hipHostFree(s.h_out);
+    if (s.st) (void)hipStreamDestroy(s.st);
   }
   (void)hipFree(d.d_inv);
+  (void)hipFree(d.d_invb);
   if (d.stream) (void)hipStreamDestroy(d.stream);
 }
 
@@ -195,6 +215,35 @@ int launch_batch(Dev &d, const uint8_t *base, const uint64_t *off, const uint32_
       return hip_err(launch_stream(a, cpl, grid, st));
     }
   }
+  if (getenv("RICRC_GENERAL_WAVE") == nullptr) {
+    // Ragged kernel: pieces from a device-side scan of the descriptors, or
+    // arithmetic when every packet has the same length and 16-byte phase.
+    RaggedArgs r{};
+    r.base = base;
+    r.off = off;
+    r.len = len;
+    r.stride = stride;
+    r.count = count;
+    r.out = out;
+    r.inv_tab = d.d_inv;
+    r.inv_basis = d.d_invb;
+    r.fixed_len = fixed_len;
+    r.l3_offset = l3_offset;
+    r.verify = verify ? 1u : 0u;
+    for (uint32_t l = 0; l < 64; ++l) r.K[l] = x8n_host(64ull * (63 - l));
+    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)d.n_cu, (count + 63) / 64));
+    if (!off && !len && stride % 16 == 0) {
+      r.P = ragged_pieces((uintptr_t)base + l3_offset, fixed_len);
+      return hip_err(launch_ragged(r, grid, st));
+    }
+    uint64_t *ps = nullptr;
+    HIP_TRY(hipMallocAsync((void **)&ps, (count + 1) * sizeof(uint64_t), st));
+    r.ps = ps;
+    hipError_t e = ragged_piece_scan(r, ps, st);
+    if (e == hipSuccess) e = launch_ragged(r, grid, st);
+    const hipError_t e2 = hipFreeAsync(ps, st);
+    return hip_err(e != hipSuccess ? e : e2);
+  }
   GeneralArgs g{};
   g.base = base;
   g.off = off;
@@ -229,6 +278,12 @@ int ricrc_create_devices(ricrc_ctx **ctx, const int *devices, int n) {
     if (devices[i] < 0 || devices[i] >= avail) return -ENODEV;
   ricrc_ctx *c = new (std::nothrow) ricrc_ctx;
   if (!c) return -ENOMEM;
+  {
+    const unsigned hw = std::thread::hardware_concurrency();
+    int t = (int)std::min(16u, std::max(1u, hw));
+    if (const char *e = getenv("RICRC_HOST_THREADS")) t = std::max(1, std::min(64, atoi(e)));
+    c->host_threads = t;
+  }
   c->devs.resize(n);
   for (int i = 0; i < n; ++i) {
     c->devs[i].id = devices[i];
@@ -260,6 +315,10 @@ int ricrc_create(ricrc_ctx **ctx, int n_gpus) {
 void ricrc_destroy(ricrc_ctx *ctx) {
   if (!ctx) return;
   for (Dev &d : ctx->devs) free_dev(d);
+  for (const HostRange &r : ctx->pinned) {
+    if (r.owned) (void)hipHostFree((void *)r.lo);
+    else (void)hipHostUnregister((void *)r.lo);
+  }
   delete ctx;
 }
 
@@ -311,18 +370,108 @@ int ricrc_synth_device(ricrc_ctx *ctx, int dev, uint64_t seed, uint64_t first, u
 void *ricrc_host_alloc(ricrc_ctx *ctx, uint64_t bytes) {
   if (!ctx || bytes == 0) return nullptr;
   void *p = nullptr;
-  if (hipHostMalloc(&p, bytes, hipHostMallocPortable) != hipSuccess) return nullptr;
+  if (hipHostMalloc(&p, bytes, hipHostMallocPortable) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  ctx->pinned.push_back({(uintptr_t)p, (uintptr_t)p + bytes, true});
   return p;
 }
 
 void ricrc_host_free(ricrc_ctx *ctx, void *p) {
-  (void)ctx;
-  if (p) (void)hipHostFree(p);
+  if (!ctx || !p) return;
+  for (size_t i = 0; i < ctx->pinned.size(); ++i)
+    if (ctx->pinned[i].owned && ctx->pinned[i].lo == (uintptr_t)p) {
+      ctx->pinned.erase(ctx->pinned.begin() + i);
+      (void)hipHostFree(p);
+      return;
+    }
 }
 
-// Host batches: the batch is cut into byte-balanced shards, one per device;
-// each device walks its shard in chunks that alternate between two staging
-// slots so the CPU gather of chunk k+1 overlaps H2D + kernel + D2H of chunk k.
+int ricrc_host_register(ricrc_ctx *ctx, void *p, uint64_t bytes) {
+  if (!ctx || !p || bytes == 0) return -EINVAL;
+  const uintptr_t lo = (uintptr_t)p, hi = lo + bytes;
+  for (const HostRange &r : ctx->pinned)
+    if (lo < r.hi && r.lo < hi) return -EINVAL;  // overlaps a context range (HIP itself may accept it)
+  const hipError_t e = hipHostRegister(p, bytes, hipHostRegisterPortable);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return e == hipErrorHostMemoryAlreadyRegistered ? -EINVAL : (e == hipErrorOutOfMemory ? -ENOMEM : -EIO);
+  }
+  ctx->pinned.push_back({(uintptr_t)p, (uintptr_t)p + bytes, false});
+  return 0;
+}
+
+int ricrc_host_unregister(ricrc_ctx *ctx, void *p) {
+  if (!ctx || !p) return -EINVAL;
+  for (size_t i = 0; i < ctx->pinned.size(); ++i)
+    if (!ctx->pinned[i].owned && ctx->pinned[i].lo == (uintptr_t)p) {
+      ctx->pinned.erase(ctx->pinned.begin() + i);
+      return hipHostUnregister(p) == hipSuccess ? 0 : ((void)hipGetLastError(), -EIO);
+    }
+  return -EINVAL;
+}
+
+}  // extern "C"
+
+namespace {
+
+// True if [p, p+n) lies in host memory the DMA engines can read without a
+// CPU bounce: a context range (ricrc_host_alloc / ricrc_host_register) or
+// memory some other owner pinned (hipHostMalloc / hipHostRegister, e.g. a
+// torch pinned tensor), as reported by the HIP pointer attributes.
+bool dma_readable(const ricrc_ctx *ctx, const void *p, uint64_t n) {
+  const uintptr_t lo = (uintptr_t)p, hi = lo + n;
+  for (const HostRange &r : ctx->pinned)
+    if (lo >= r.lo && hi <= r.hi) return true;
+  hipPointerAttribute_t at;
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  if (at.type != hipMemoryTypeHost) return false;
+  uintptr_t rs = 0;
+  size_t rn = 0;
+  if (hipPointerGetAttribute(&rs, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, (hipDeviceptr_t)p) != hipSuccess ||
+      hipPointerGetAttribute(&rn, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, (hipDeviceptr_t)p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return lo >= rs && hi <= rs + rn;
+}
+
+// Run fn(lo, hi) over [0, n) on up to `threads` threads (the caller is one).
+template <class F>
+void par_for(uint64_t n, int threads, uint64_t grain, F fn) {
+  const uint64_t t = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)threads, n / std::max<uint64_t>(1, grain)));
+  if (t <= 1) {
+    fn(0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  th.reserve(t - 1);
+  for (uint64_t k = 1; k < t; ++k) th.emplace_back(fn, n * k / t, n * (k + 1) / t);
+  fn(0, n / t);
+  for (auto &x : th) x.join();
+}
+
+}  // namespace
+
+extern "C" {
+
+// Host batches (host in, host out; the NIC-ring path of SURVEY §8f-4).  The
+// batch is cut into byte-balanced shards, one per device; each device walks
+// its shard in chunks alternating between two staging slots with their own
+// streams, so chunk k+1's CPU copy + H2D overlap chunk k's kernel + D2H.
+// A chunk reaches the device in one of three ways:
+//   span/DMA   the packets form a contiguous, ascending span (fixed stride,
+//              or a ring of ascending offsets with little slack) in
+//              DMA-readable memory: one hipMemcpyAsync straight from the
+//              caller's buffer, no CPU copy;
+//   span/copy  same span in pageable memory: parallel memcpy into the pinned
+//              slot, then one DMA;
+//   gather     anything else: packets copied one by one (in parallel) into
+//              the pinned slot, 16-byte aligned, with new offsets.
 int ricrc_batch_host(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *off, const uint32_t *len,
                      uint32_t stride, uint64_t count, uint32_t l3_offset, uint32_t *out) {
   if (!ctx || ctx->devs.empty()) return -EINVAL;
@@ -330,11 +479,13 @@ int ricrc_batch_host(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *off, c
   if (!base || !out) return -EINVAL;
   if (!off && stride == 0) return -EINVAL;
   auto pkt_len = [&](uint64_t i) -> uint64_t { return len ? len[i] : (uint64_t)stride - l3_offset; };
-  auto pkt_start = [&](uint64_t i) -> uint64_t { return (off ? off[i] : i * (uint64_t)stride) + l3_offset; };
+  auto frame = [&](uint64_t i) -> uint64_t { return off ? off[i] : i * (uint64_t)stride; };
   if (!len && stride <= l3_offset) return -EINVAL;
+  uint64_t total = 0;
   for (uint64_t i = 0; i < count; ++i) {
     const uint64_t n = pkt_len(i);
     if (n < kMinLen || n > kMaxLen) return -EINVAL;
+    total += n;
   }
   const int ndev = (int)ctx->devs.size();
   for (Dev &d : ctx->devs) {
@@ -342,8 +493,6 @@ int ricrc_batch_host(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *off, c
     if (rc) return rc;
   }
   // Byte-balanced shard boundaries.
-  uint64_t total = 0;
-  for (uint64_t i = 0; i < count; ++i) total += pkt_len(i);
   std::vector<uint64_t> cut(ndev + 1, count);
   cut[0] = 0;
   {
@@ -354,7 +503,6 @@ int ricrc_batch_host(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *off, c
       while (k < ndev && acc * ndev >= total * k) cut[k++] = i + 1;
     }
   }
-  // Per device cursor; round-robin chunk issue across devices.
   struct Cur {
     uint64_t next, end;
     int slot;
@@ -363,6 +511,7 @@ int ricrc_batch_host(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *off, c
   };
   std::vector<Cur> cur(ndev);
   for (int k = 0; k < ndev; ++k) cur[k] = Cur{cut[k], cut[k + 1], 0, {0, 0}, {0, 0}, {false, false}};
+  const int T = ctx->host_threads;
 
   auto drain = [&](Dev &d, Cur &c, int s) -> int {
     if (!c.pend[s]) return 0;
@@ -386,31 +535,69 @@ int ricrc_batch_host(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *off, c
       int rc = drain(d, c, s);
       if (rc) return rc;
       Slot &sl = d.slot[s];
-      // Gather packets [lo, hi) into the pinned slot, 16-byte aligned each.
       const uint64_t lo = c.next;
-      uint64_t hi = lo, bytes = 0;
+      // Span plan: the largest [lo, hi) whose frames ascend without overlap
+      // and whose byte span [frame(lo), end of hi-1) fits the slot with at
+      // most 25 % slack.  The span lands at d_buf + pad so that packet lo's
+      // L3 header is 16-byte aligned on the device (so are the others when
+      // the frames are 16 apart, e.g. a fixed stride).
+      const uint64_t s_lo = frame(lo);
+      const uint64_t pad = (16u - (l3_offset & 15u)) & 15u;
+      uint64_t hi = lo, s_hi = s_lo, used = 0;
       while (hi < c.end && hi - lo < kStagePkts) {
-        const uint64_t n = pkt_len(hi), padded = (n + 15) & ~15ull;
-        if (bytes + padded > kStageBytes) break;
-        sl.h_off[hi - lo] = bytes;
-        sl.h_len[hi - lo] = (uint32_t)n;
-        memcpy(sl.h_buf + bytes, base + pkt_start(hi), n);
-        bytes += padded;
+        const uint64_t fs = frame(hi), fe = fs + l3_offset + pkt_len(hi);
+        if (fs < s_hi && hi > lo) break;  // not ascending / overlapping
+        if (fe - s_lo > kStageBytes) break;
+        s_hi = fe;
+        used += pkt_len(hi);
         ++hi;
       }
-      const uint64_t m = hi - lo;
-      HIP_TRY(hipMemcpyAsync(sl.d_buf, sl.h_buf, bytes, hipMemcpyHostToDevice, d.stream));
-      const bool uniform = !len && !off;  // contiguous fixed-size -> streaming kernel
-      if (uniform && (pkt_len(lo) % 16 == 0)) {
-        rc = launch_batch(d, sl.d_buf, nullptr, nullptr, pkt_len(lo), m, 0, sl.d_out, d.stream, false);
+      const bool span = hi > lo && (s_hi - s_lo) <= used + used / 4 + 64;
+      uint64_t m, bytes;
+      uint32_t kl3 = l3_offset;
+      if (span) {
+        m = hi - lo;
+        bytes = s_hi - s_lo;
+        const uint8_t *src = base + s_lo;
+        if (dma_readable(ctx, src, bytes)) {
+          HIP_TRY(hipMemcpyAsync(sl.d_buf + pad, src, bytes, hipMemcpyHostToDevice, sl.st));
+        } else {
+          par_for(bytes, T, 4u << 20, [&](uint64_t a, uint64_t b) { memcpy(sl.h_buf + a, src + a, b - a); });
+          HIP_TRY(hipMemcpyAsync(sl.d_buf + pad, sl.h_buf, bytes, hipMemcpyHostToDevice, sl.st));
+        }
+        if (off || len)
+          for (uint64_t i = lo; i < hi; ++i) sl.h_off[i - lo] = frame(i) - s_lo + pad;
       } else {
-        HIP_TRY(hipMemcpyAsync(sl.d_off, sl.h_off, m * sizeof(uint64_t), hipMemcpyHostToDevice, d.stream));
-        HIP_TRY(hipMemcpyAsync(sl.d_len, sl.h_len, m * sizeof(uint32_t), hipMemcpyHostToDevice, d.stream));
-        rc = launch_batch(d, sl.d_buf, sl.d_off, sl.d_len, 0, m, 0, sl.d_out, d.stream, false);
+        // Gather: packed L3 packets, 16-byte aligned each.
+        hi = lo;
+        bytes = 0;
+        while (hi < c.end && hi - lo < kStagePkts) {
+          const uint64_t padded = (pkt_len(hi) + 15) & ~15ull;
+          if (bytes + padded > kStageBytes) break;
+          sl.h_off[hi - lo] = bytes;
+          bytes += padded;
+          ++hi;
+        }
+        m = hi - lo;
+        par_for(m, T, 4096, [&](uint64_t a, uint64_t b) {
+          for (uint64_t i = a; i < b; ++i)
+            memcpy(sl.h_buf + sl.h_off[i], base + frame(lo + i) + l3_offset, pkt_len(lo + i));
+        });
+        HIP_TRY(hipMemcpyAsync(sl.d_buf, sl.h_buf, bytes, hipMemcpyHostToDevice, sl.st));
+        kl3 = 0;
+      }
+      const bool fixed = span && !off && !len;  // frames at i*stride from d_buf + pad
+      if (fixed) {
+        rc = launch_batch(d, sl.d_buf + pad, nullptr, nullptr, stride, m, kl3, sl.d_out, sl.st, false);
+      } else {
+        HIP_TRY(hipMemcpyAsync(sl.d_off, sl.h_off, m * sizeof(uint64_t), hipMemcpyHostToDevice, sl.st));
+        for (uint64_t i = 0; i < m; ++i) sl.h_len[i] = (uint32_t)pkt_len(lo + i);
+        HIP_TRY(hipMemcpyAsync(sl.d_len, sl.h_len, m * sizeof(uint32_t), hipMemcpyHostToDevice, sl.st));
+        rc = launch_batch(d, sl.d_buf, sl.d_off, sl.d_len, 0, m, kl3, sl.d_out, sl.st, false);
       }
       if (rc) return rc;
-      HIP_TRY(hipMemcpyAsync(sl.h_out, sl.d_out, m * sizeof(uint32_t), hipMemcpyDeviceToHost, d.stream));
-      HIP_TRY(hipEventRecord(sl.done, d.stream));
+      HIP_TRY(hipMemcpyAsync(sl.h_out, sl.d_out, m * sizeof(uint32_t), hipMemcpyDeviceToHost, sl.st));
+      HIP_TRY(hipEventRecord(sl.done, sl.st));
       c.pend[s] = true;
       c.pend_lo[s] = lo;
       c.pend_hi[s] = hi;

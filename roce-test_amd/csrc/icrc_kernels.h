@@ -52,6 +52,37 @@ struct GeneralArgs {
   uint32_t K[64];  // x^(8*64*(63-lane))
 };
 
+// Ragged batches (any alignment, per-packet offsets and/or lengths): the
+// batch is cut into 64-byte pieces, packet by packet -- packet i covers
+// pieces [ps[i], ps[i+1]) laid from its start rounded down to 16 B -- and a
+// wave step maps 64 consecutive pieces onto its 64 lanes, however many
+// packets they belong to.
+struct RaggedArgs {
+  const uint8_t *base;
+  const uint64_t *off;     // may be null (then p * stride)
+  const uint32_t *len;     // may be null (then fixed_len)
+  const uint64_t *ps;      // exclusive prefix of pieces, count + 1 entries; null: uniform
+  uint64_t stride;
+  uint64_t count;
+  uint32_t *out;
+  const uint32_t *inv_tab;    // x^(-8 z), z in [0, 4096]
+  const uint32_t *inv_basis;  // row z (32 words): basis of x^(-8 z), z in [0, 4096]
+  uint32_t fixed_len;
+  uint32_t l3_offset;
+  uint32_t verify;
+  uint32_t P;              // pieces per packet when ps == null
+  uint32_t K[64];          // x^(8*64*(63-lane)): lane piece end -> step end
+};
+
+// Pieces of a packet of n bytes whose L3 header starts at address `start`:
+// the CRC'd bytes [0, n-4) plus the start's offset inside its 16-byte unit,
+// in 64-byte pieces (at least one; invalid lengths get one and yield 0).
+__host__ __device__ inline uint32_t ragged_pieces(uintptr_t start, uint32_t n) {
+  if (n < 4 || n > 65535) return 1u;
+  const uint32_t p = ((uint32_t)(start & 15u) + (n - 4u) + 63u) >> 6;
+  return p ? p : 1u;
+}
+
 struct SynthArgs {
   uint8_t *buf;
   uint64_t seed, first, count;
@@ -61,6 +92,10 @@ struct SynthArgs {
 hipError_t launch_stream(const StreamArgs &a, int cpl, int grid, hipStream_t st);
 hipError_t launch_tsk(const TskArgs &a, int grid, hipStream_t st);
 hipError_t launch_general(const GeneralArgs &a, int grid, hipStream_t st);
+hipError_t launch_ragged(const RaggedArgs &a, int grid, hipStream_t st);
+// ps[0..count] = exclusive prefix of ragged_pieces over the batch (stream
+// ordered; temporary storage from the stream-ordered allocator).
+hipError_t ragged_piece_scan(const RaggedArgs &a, uint64_t *ps, hipStream_t st);
 hipError_t launch_synth(const SynthArgs &a, hipStream_t st);
 
 }  // namespace ricrc

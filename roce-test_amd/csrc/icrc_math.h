@@ -77,6 +77,18 @@ RICRC_HD constexpr uint32_t gf_xinv8n(uint64_t n) {
   return r;
 }
 
+// Multiplication basis of a constant K: q[j] = K * x^(31-j), so that
+// r * K = XOR over set bits j of r of q[j] (bit j is the x^(31-j) term).
+struct Basis {
+  uint32_t q[32];
+};
+RICRC_HD constexpr Basis make_const_basis(uint32_t K) {
+  Basis b{};
+  b.q[31] = K;
+  for (int j = 30; j >= 0; --j) b.q[j] = gf_mulx(b.q[j + 1]);
+  return b;
+}
+
 // Slice-by-N tables: T[k][b] = register after byte b followed by k zero
 // bytes, from a zero register (T[0] is the classic Sarwate table).
 template <int N>

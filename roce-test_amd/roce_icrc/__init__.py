@@ -35,7 +35,7 @@ EXPORTED = (
     "ricrc_one", "ricrc_verify_one", "ricrc_stamp_one", "ricrc_is_rocev2", "ricrc_shift",
     "ricrc_combine", "ricrc_create", "ricrc_create_devices", "ricrc_destroy", "ricrc_device_count", "ricrc_batch_host",
     "ricrc_batch_device", "ricrc_verify_device", "ricrc_host_alloc", "ricrc_host_free",
-    "ricrc_synth_device", "ricrc_stream", "ricrc_strerror",
+    "ricrc_host_register", "ricrc_host_unregister", "ricrc_synth_device", "ricrc_stream", "ricrc_strerror",
 )
 
 
@@ -78,6 +78,8 @@ def _load():
         "ricrc_verify_device": ([vp, i32, vp, vp, vp, u32, u64, u32, vp, vp], i32),
         "ricrc_host_alloc": ([vp, u64], vp),
         "ricrc_host_free": ([vp, vp], None),
+        "ricrc_host_register": ([vp, vp, u64], i32),
+        "ricrc_host_unregister": ([vp, vp], i32),
         "ricrc_synth_device": ([vp, i32, u64, u64, u64, u32, u32, vp, vp], i32),
         "ricrc_stream": ([vp, i32], vp),
         "ricrc_strerror": ([i32], ctypes.c_char_p),
@@ -263,6 +265,20 @@ class Context:
 
     def host_free(self, arr: np.ndarray) -> None:
         lib.ricrc_host_free(self._h, arr.ctypes.data)
+
+    def host_register(self, arr: np.ndarray) -> None:
+        """Pin an existing contiguous host array (a NIC ring) so host batches
+        read it by DMA; undo with :meth:`host_unregister`."""
+        if not arr.flags["C_CONTIGUOUS"]:
+            raise ValueError("host_register needs a contiguous array")
+        rc = lib.ricrc_host_register(self._h, arr.ctypes.data, arr.nbytes)
+        if rc:
+            raise ICRCError(rc, "ricrc_host_register")
+
+    def host_unregister(self, arr: np.ndarray) -> None:
+        rc = lib.ricrc_host_unregister(self._h, arr.ctypes.data)
+        if rc:
+            raise ICRCError(rc, "ricrc_host_unregister")
 
 
 def icrc_batch(buf, offsets=None, lengths=None, stride: int = 0, l3_offset: int = 0,

@@ -168,6 +168,70 @@ def test_batch_host_paths(ctx):
                                   oracle_c.icrc_batch(buf, offsets=offs, lengths=lens))
 
 
+def test_batch_host_multi_chunk_pinned_and_registered(ctx):
+    """> one 256 MiB staging chunk (slot alternation), through each route:
+    pageable span (parallel CPU copy), pinned span (ricrc_host_alloc, direct
+    DMA) and registered span (ricrc_host_register, direct DMA)."""
+    count, n = 70000, 4096  # 287 MB -> 2 chunks
+    host = oracle_c.synth_batch(SEED, 7, count, n)
+    want = oracle_c.icrc_batch(host, stride=n, threads=8)
+    np.testing.assert_array_equal(ctx.batch_host(host, stride=n), want)
+    pinned = ctx.host_alloc(host.size)
+    try:
+        pinned[:] = host.reshape(-1)
+        np.testing.assert_array_equal(ctx.batch_host(pinned, stride=n), want)
+    finally:
+        ctx.host_free(pinned)
+    ring = host.reshape(-1).copy()
+    ctx.host_register(ring)
+    try:
+        np.testing.assert_array_equal(ctx.batch_host(ring, stride=n), want)
+    finally:
+        ctx.host_unregister(ring)
+
+
+@pytest.mark.parametrize("registered", [False, True])
+def test_batch_host_ring_and_gather(ctx, registered):
+    """Ragged ring (ascending offsets, small gaps, Ethernet l3_offset) takes
+    the span route; the same packets with shuffled offsets take the gather
+    route; fixed stride with per-packet lengths takes the span route with
+    device offsets.  All bit-exact."""
+    rng = np.random.default_rng(11)
+    buf, offs, lens = _ragged(rng, 3000, 44, 4096, 1, l3_offset=14)
+    want = oracle_c.icrc_batch(buf, offsets=offs, lengths=lens, l3_offset=14)
+    if registered:
+        ctx.host_register(buf)
+    try:
+        np.testing.assert_array_equal(ctx.batch_host(buf, offs, lens, l3_offset=14), want)
+        perm = rng.permutation(len(offs))
+        np.testing.assert_array_equal(ctx.batch_host(buf, offs[perm], lens[perm], l3_offset=14), want[perm])
+    finally:
+        if registered:
+            ctx.host_unregister(buf)
+    stride = 2048
+    count = 1000
+    fr = rng.integers(0, 256, size=count * stride + 64, dtype=np.uint8)
+    ln = rng.integers(44, stride - 14 + 1, size=count).astype(np.uint32)
+    want = oracle_c.icrc_batch(fr, lengths=ln, stride=stride, count=count, l3_offset=14)
+    np.testing.assert_array_equal(ctx.batch_host(fr, lengths=ln, stride=stride, l3_offset=14, count=count), want)
+    want = oracle_c.icrc_batch(fr, stride=stride, count=count, l3_offset=14)
+    np.testing.assert_array_equal(ctx.batch_host(fr, stride=stride, l3_offset=14, count=count), want)
+
+
+def test_host_register_errors(ctx):
+    import roce_icrc
+
+    a = np.zeros(1 << 16, np.uint8)
+    ctx.host_register(a)
+    try:
+        with pytest.raises(roce_icrc.ICRCError):
+            ctx.host_register(a)
+    finally:
+        ctx.host_unregister(a)
+    with pytest.raises(roce_icrc.ICRCError):
+        ctx.host_unregister(a)
+
+
 def test_batch_host_rejects_bad_lengths(ctx):
     import roce_icrc
 

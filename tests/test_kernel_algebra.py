@@ -108,3 +108,56 @@ def _xinv8n_fast(n):
         sq = o.gf_mul(sq, sq)
         e >>= 1
     return r
+
+
+def test_ragged_kernel_decomposition():
+    """The ragged kernel's algebra (icrc_kernels.hip icrc_ragged_kernel):
+    packets cut into 64-byte pieces from their 16-byte aligned base, 64
+    consecutive pieces per wave step regardless of packet boundaries, lane l
+    aligned to the step end by x^(512 (63-l)), packets reduced as
+    P[last] ^ P[first-1] of a prefix XOR, packets open at lane 63 carried into
+    the next step by x^(8*4096), and the last lane's x^-(8 z + 512 (63-l))."""
+    rng = random.Random(3)
+    sizes = [4, 5, 44, 48, 61, 64, 100, 256, 1024, 4096, 4100, 9001, 64, 64, 44, 300] * 2
+    rng.shuffle(sizes)
+    pkts, pieces = [], []  # pieces: (packet index, bytes)
+    for i, n in enumerate(sizes):
+        pkt = bytes(rng.randrange(256) for _ in range(n))
+        m = masked(pkt)
+        M, s = len(m), rng.randrange(16)
+        P = max(1, (s + M + 63) // 64)
+        D = bytearray(64 * P)
+        D[s: s + M] = m
+        for k in range(4):
+            D[s + k] ^= (SEED_REG >> (8 * k)) & 0xFF
+        pkts.append((m, s, P))
+        pieces += [(i, D[64 * k: 64 * k + 64]) for k in range(P)]
+    got, carry = {}, 0
+    for g in range(0, len(pieces), 64):
+        step = pieces[g: g + 64]
+        vals = []
+        for lane, (_, d) in enumerate(step):
+            r = fold(0, d)
+            vals.append(o.gf_mul(r, x8n(64 * (63 - lane))))
+        vals[0] ^= carry
+        pre, acc = [], 0
+        for v in vals:
+            acc ^= v
+            pre.append(acc)
+        carry = 0
+        for lane, (i, _) in enumerate(step):
+            first = next(l for l in range(64) if step[l][0] == i)
+            seg = pre[lane] ^ (pre[first - 1] if first > 0 else 0)
+            last_here = lane + 1 == len(step) or step[lane + 1][0] != i
+            if not last_here:
+                continue
+            ends = g + lane + 1 == len(pieces) or pieces[g + lane + 1][0] != i
+            if ends:
+                m, s, P = pkts[i]
+                z = 64 * P - s - len(m)
+                got[i] = o.gf_mul(seg, _xinv8n_fast(z + 64 * (63 - lane))) ^ 0xFFFFFFFF
+            else:  # open at lane 63
+                assert lane == 63
+                carry = o.gf_mul(seg, x8n(4096))
+    for i, (m, _, _) in enumerate(pkts):
+        assert got[i] == zlib.crc32(o.PREFIX + bytes(m)), (i, len(m))
