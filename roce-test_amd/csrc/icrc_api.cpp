@@ -46,7 +46,7 @@ struct Dev {
   int n_cu = 0;
   hipStream_t stream = nullptr;
   uint32_t *d_inv = nullptr;   // x^(-8 z), z <= 4096
-  uint32_t *d_invb = nullptr;  // row z: multiplication basis of x^(-8 z) (32 words), z <= 4096
+  uint32_t *d_inv4 = nullptr;  // t: x^(8 (k - t)), k = 0..3, t <= 4096
   Slot slot[2];
   bool staged = false;
 };
@@ -108,13 +108,11 @@ int init_dev(Dev &d) {
   }
   HIP_TRY(hipMalloc(&d.d_inv, 4097 * sizeof(uint32_t)));
   HIP_TRY(hipMemcpy(d.d_inv, inv.data(), 4097 * sizeof(uint32_t), hipMemcpyHostToDevice));
-  std::vector<uint32_t> rows(4097 * 32);
-  for (int z = 0; z <= 4096; ++z) {
-    const Basis b = make_const_basis(inv[z]);
-    std::copy(b.q, b.q + 32, rows.begin() + 32 * z);
-  }
-  HIP_TRY(hipMalloc(&d.d_invb, rows.size() * sizeof(uint32_t)));
-  HIP_TRY(hipMemcpy(d.d_invb, rows.data(), rows.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  std::vector<uint32_t> inv4(4097 * 4);  // t, k: x^(8 (k - t))
+  for (int t = 0; t <= 4096; ++t)
+    for (int k = 0; k < 4; ++k) inv4[4 * t + k] = k >= t ? gf_x8n((uint64_t)(k - t)) : gf_xinv8n((uint64_t)(t - k));
+  HIP_TRY(hipMalloc(&d.d_inv4, inv4.size() * sizeof(uint32_t)));
+  HIP_TRY(hipMemcpy(d.d_inv4, inv4.data(), inv4.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
   return 0;
 }
 
@@ -146,7 +144,7 @@ void free_dev(Dev &d) {
     if (s.st) (void)hipStreamDestroy(s.st);
   }
   (void)hipFree(d.d_inv);
-  (void)hipFree(d.d_invb);
+  (void)hipFree(d.d_inv4);
   if (d.stream) (void)hipStreamDestroy(d.stream);
 }
 
@@ -226,7 +224,7 @@ int launch_batch(Dev &d, const uint8_t *base, const uint64_t *off, const uint32_
     r.count = count;
     r.out = out;
     r.inv_tab = d.d_inv;
-    r.inv_basis = d.d_invb;
+    r.inv4 = reinterpret_cast<const u32x4_t *>(d.d_inv4);
     r.fixed_len = fixed_len;
     r.l3_offset = l3_offset;
     r.verify = verify ? 1u : 0u;

@@ -6,6 +6,10 @@
 
 namespace ricrc {
 
+struct u32x4_t {
+  uint32_t v[4];
+};
+
 // Fixed-length batch, packet i at base + i*stride, 16-byte aligned.
 struct StreamArgs {
   const uint8_t *base;  // first packet's L3 start
@@ -65,8 +69,8 @@ struct RaggedArgs {
   uint64_t stride;
   uint64_t count;
   uint32_t *out;
-  const uint32_t *inv_tab;    // x^(-8 z), z in [0, 4096]
-  const uint32_t *inv_basis;  // row z (32 words): basis of x^(-8 z), z in [0, 4096]
+  const uint32_t *inv_tab;  // x^(-8 z), z in [0, 4096]
+  const u32x4_t *inv4;      // entry t: x^(8 (k - t)) for k = 0..3, t in [0, 4096]
   uint32_t fixed_len;
   uint32_t l3_offset;
   uint32_t verify;

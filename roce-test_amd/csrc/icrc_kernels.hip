@@ -615,12 +615,12 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
 // chained with x^(8*4096) and the zero tail is removed with x^(-8 z).
 // =======================================================================
 __device__ __forceinline__ uint32_t byte_span_mask(int lo, int hi) {  // bytes [lo,hi) of a word
-  lo = lo < 0 ? 0 : lo;
-  hi = hi > 4 ? 4 : hi;
-  if (hi <= lo) return 0u;
-  const uint32_t h = hi >= 4 ? 0xFFFFFFFFu : ((1u << (8 * hi)) - 1u);
-  const uint32_t l = lo <= 0 ? 0u : ((1u << (8 * lo)) - 1u);
-  return h & ~l;
+  // Branch-free: 64-bit shifts of 0xFFFFFFFF handle the 0- and 32-bit ends.
+  const uint32_t l = (uint32_t)(lo < 0 ? 0 : lo > 4 ? 4 : lo);
+  const uint32_t h = (uint32_t)(hi < 0 ? 0 : hi > 4 ? 4 : hi);
+  const uint32_t keep_hi = (uint32_t)(0xFFFFFFFFull >> (32u - 8u * h));
+  const uint32_t keep_lo = (uint32_t)(0xFFFFFFFFull << (8u * l));
+  return keep_hi & keep_lo;
 }
 
 __device__ __forceinline__ uint32_t expand_nibble(uint32_t b) {
@@ -743,7 +743,6 @@ __device__ __forceinline__ uint32_t gload4_unaligned(uintptr_t addr) {
   return *reinterpret_cast<gptr_u32_unaligned>(addr);
 }
 
-__device__ constexpr Basis g_x256 = make_const_basis(gf_x8n(32));
 __device__ constexpr Basis g_x4096 = make_const_basis(gf_x8n(4096));
 
 // r * K for a wave-uniform r and a constant basis: scalar ALU code.
@@ -774,7 +773,10 @@ __device__ __forceinline__ uint32_t wave_prefix_xor(uint32_t v, uint32_t lane) {
 // the kernel owns) so the compiler counts vmcnt instead of draining at a
 // branch join.  MODE: 0 uniform (no descriptors), 1 offsets + lengths,
 // 2 offsets only, 3 lengths only.
-template <int MODE, int kRaggedBlock>
+// ABL: timing-only ablation mask for tools/microbench/ragged_abl.hip (the
+// product instantiates 0): 1 no table fold, 2 no finish slices, 4 no piece
+// loads, 8 no word masking.
+template <int MODE, int kRaggedBlock, int ABL = 0>
 __global__ __launch_bounds__(kRaggedBlock) void icrc_ragged_kernel(RaggedArgs a) {
   constexpr bool UNI = MODE == 0, HAS_OFF = MODE == 1 || MODE == 2, HAS_LEN = MODE == 1 || MODE == 3;
   // 128 KiB slice tables + the lanes' alignment bases (8 KiB, shared by all
@@ -793,10 +795,10 @@ __global__ __launch_bounds__(kRaggedBlock) void icrc_ragged_kernel(RaggedArgs a)
   const uint32_t lane = threadIdx.x & 63;
   const LaneTab lt{(lane & 31) << 2, ((lane & 31) << 2) | 0x10000u};
   const u32x4 *qrow = reinterpret_cast<const u32x4 *>(lds + kLdsWords) + lane;
-  auto mul_lane = [&](uint32_t r) -> uint32_t {  // r * x^(512 (63 - lane))
-    uint32_t acc[4] = {0u, 0u, 0u, 0u};
+  // Half h of r * x^(512 (63 - lane)): basis words 16h..16h+15 from LDS.
+  auto mul_lane_part = [&](uint32_t r, int h, uint32_t (&acc)[4]) {
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
+    for (int q = 4 * h; q < 4 * h + 4; ++q) {
       const u32x4 b = qrow[64 * q];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -805,7 +807,6 @@ __global__ __launch_bounds__(kRaggedBlock) void icrc_ragged_kernel(RaggedArgs a)
         acc[i] = and_xor(mk, b[i], acc[i]);
       }
     }
-    return xor3(acc[0], acc[1], acc[2] ^ acc[3]);
   };
 
   const uint64_t wave = (uint64_t)blockIdx.x * (kRaggedBlock / 64) + (threadIdx.x >> 6);
@@ -839,16 +840,17 @@ __global__ __launch_bounds__(kRaggedBlock) void icrc_ragged_kernel(RaggedArgs a)
 
   // Lane j's view of packet pc + j (clamped into [p0, p1)).
   struct Desc {
-    uint64_t s;       // first piece (g_end past the wave's packets)
+    int32_t rel;      // first piece - step's first piece, capped at 64 (past the wave's packets: 64)
     uintptr_t start;  // L3 start address
     uint32_t n;
   };
-  auto load_desc = [&](uint64_t pc) -> Desc {
+  auto load_desc = [&](uint64_t pc, uint64_t gstep) -> Desc {
     const uint64_t pj = pc + lane;
     const bool in = pj < p1;
     const uint64_t pjc = in ? pj : p1 - 1;
     Desc d;
-    d.s = in ? PS(pjc) : g_end;
+    const int64_t r64 = (int64_t)((in ? PS(pjc) : g_end) - gstep);
+    d.rel = r64 > 64 ? 64 : (int32_t)r64;
     d.start = (uintptr_t)a.base + (HAS_OFF ? a.off[pjc] : pjc * a.stride) + a.l3_offset;
     d.n = HAS_LEN ? a.len[pjc] : a.fixed_len;
     return d;
@@ -863,8 +865,7 @@ __global__ __launch_bounds__(kRaggedBlock) void icrc_ragged_kernel(RaggedArgs a)
     bool live;
   };
   auto map_step = [&](const Desc &d, uint64_t g) -> Map {
-    const int64_t r64 = (int64_t)(d.s - g);
-    const int32_t relj = r64 > 64 ? 64 : (int32_t)r64;
+    const int32_t relj = d.rel;
     const int32_t tgt = (lane >= 1 && relj < 64) ? relj : 0;
     const uint32_t recv = (uint32_t)__builtin_amdgcn_ds_permute(tgt << 2, 1);
     const uint64_t starts = __ballot(recv != 0u) | 1ull;
@@ -898,41 +899,48 @@ __global__ __launch_bounds__(kRaggedBlock) void icrc_ragged_kernel(RaggedArgs a)
     for (int q = 0; q < 4; ++q) {
       const int ru = rel0 + 16 * q;
       const bool use = ok && ru < M && ru + 16 > 0;
-      v[q] = gload16(use ? pbase + 16 * q : safe);
+      if (ABL & 4) v[q] = u32x4{(uint32_t)rel0, (uint32_t)M, lane, (uint32_t)q};
+      else v[q] = gload16(use ? pbase + 16 * q : safe);
     }
   };
 
-  uint32_t carry = 0;  // open packet's XOR, aligned to the previous step's end
   // End lanes' x^-(8 z + 512 (63 - lane)) and trailers, loaded at the start
   // of the step's stage -- before the next step's prefetch, so waiting for
   // them never waits for the prefetch (gfx9 loads retire in order).  Every
   // lane loads (others read entry 0 / the table), so no memory op sits under
   // a divergent branch: a branch join would make the compiler drain vmcnt to
   // zero and serialise the pipeline.
-  auto load_fin = [&](const Map &m, uint32_t &C, uint32_t &T) {
+  auto load_fin = [&](const Map &m, u32x4 &C, uint32_t &T) {
     const bool e = is_end_of(m);
     const uint32_t M = (m.n >= 4u && m.n <= kMaxLen) ? m.n - 4u : 0u;
     const uint32_t z = 64u * ragged_pieces(m.start, m.n) - (uint32_t)(m.start & 15u) - M;
-    C = gload4_unaligned((uintptr_t)(a.inv_tab + (e ? z + 64u * (63u - lane) : 0u)));
+    C = gload16((uintptr_t)(a.inv4 + (e ? z + 64u * (63u - lane) : 0u)));
     T = gload4_unaligned(e ? m.start + M : safe);
   };
-  auto process = [&](const Map &m, const u32x4 (&v)[4], uint32_t C, uint32_t T, uint64_t pc) {
+
+  // Part A of a step: mask the piece's words (wave-uniform branches, before
+  // the interleaved block).
+  auto mask_words = [&](const Map &m, const u32x4 (&v)[4], uint32_t (&w)[16]) {
     const bool valid = m.n >= 4u && m.n <= kMaxLen;
     const int M = valid ? (int)m.n - 4 : 0;
     const int s = (int)(m.start & 15u);
-    const uint32_t P = ragged_pieces(m.start, m.n);
     const int k = (int)lane - m.rel;
-    const bool is_end = m.live && (uint32_t)k + 1u == P;
     const bool first = m.live && k == 0;
     const int rel0 = 64 * k - s;  // packet-relative offset of the lane's first byte
-    uint32_t w[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) w[j] = word_of(v[j >> 2], j & 3);
     // Bytes outside [0, n-4) -> 0 (misaligned head of a first piece, tail
-    // of a last piece), only when some lane of the wave has such a piece.
+    // of a last piece), only when some lane of the wave has such a piece;
+    // whole-word selects when every boundary in the wave is 4-byte aligned.
     if (__ballot(rel0 < 0 || rel0 + 64 > M)) {
+      if (__ballot(((s | M) & 3) != 0) == 0) {
+        const int lo = -rel0, hi = M - rel0;  // valid bytes of the piece: [lo, hi)
 #pragma unroll
-      for (int j = 0; j < 16; ++j) w[j] &= byte_span_mask(-(rel0 + 4 * j), M - (rel0 + 4 * j));
+        for (int j = 0; j < 16; ++j) w[j] = (4 * j >= lo && 4 * j < hi) ? w[j] : 0u;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) w[j] &= byte_span_mask(-(rel0 + 4 * j), M - (rel0 + 4 * j));
+      }
     }
     // Invariant masks + seed on first pieces.  Fast path: every first piece
     // starts 16-byte aligned and holds all masked bytes (n >= 37).
@@ -956,59 +964,136 @@ __global__ __launch_bounds__(kRaggedBlock) void icrc_ragged_kernel(RaggedArgs a)
         }
       }
     }
-    // Fold the 64-byte piece as two independent 32-byte chains (ILP against
-    // LDS latency) joined by x^256, and align it to the step end.
-    uint32_t ra = 0u, rb = 0u;
+  };
+
+  // Part B of a step, run during the next step's fold: align to the step
+  // end, per-packet XOR, end-lane correction, store, carry.
+  struct Fin {
+    Map m;
+    uint32_t r, T;  // r: the piece's register
+    u32x4 C;  // x^(-8 t + 8 k), k = 0..3: starts of four independent multiply chains
+    uint64_t pc;
+    // in flight between slices (C doubles as the chains' running multiples)
+    uint32_t seg;
+    uint32_t acc[4];
+  };
+  uint32_t carry = 0;  // open packet's XOR, aligned to the previous step's end
+  auto fin_slice = [&](Fin &f, int sl) {
+    switch (sl) {
+      case 0:
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      ra = step4(lds, lt, ra, w[j]);
-      rb = step4(lds, lt, rb, w[8 + j]);
+        for (int k = 0; k < 4; ++k) f.acc[k] = 0u;
+        mul_lane_part(f.r, 0, f.acc);  // align to the step end, basis words 0..15
+        break;
+      case 1: {
+        mul_lane_part(f.r, 1, f.acc);  // basis words 16..31
+        uint32_t val = f.m.live ? xor3(f.acc[0], f.acc[1], f.acc[2] ^ f.acc[3]) : 0u;
+        if (lane == 0) val ^= carry;
+        const uint32_t pre = wave_prefix_xor(val, lane);
+        const int first_lane = f.m.rel > 0 ? f.m.rel : 0;  // packet's first lane in this step
+        const uint32_t before = (uint32_t)__builtin_amdgcn_ds_bpermute((first_lane - 1) << 2, (int)pre);
+        f.seg = pre ^ (first_lane == 0 ? 0u : before);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) f.acc[k] = 0u;
+        break;
+      }
+      case 2:
+      case 3:
+      case 4:
+      case 5: {  // register = seg * x^-(8 z + 512 (63 - lane)): chain k takes bits 31-8k..24-8k
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int bit = 31 - 8 * k - (2 * (sl - 2) + i);
+            const uint32_t mk = (uint32_t)(((int32_t)(f.seg << (31 - bit))) >> 31);
+            f.acc[k] = and_xor(mk, f.C[k], f.acc[k]);
+            f.C[k] = gf_mulx(f.C[k]);
+          }
+        }
+        break;
+      }
+      case 6: {
+        const bool valid = f.m.n >= 4u && f.m.n <= kMaxLen;
+        const bool is_end = is_end_of(f.m);
+        const uint32_t v_icrc = ~xor3(f.acc[0], f.acc[1], f.acc[2] ^ f.acc[3]);
+        const uint32_t o = !valid ? 0u : a.verify ? (f.T == v_icrc ? 1u : 0u) : v_icrc;
+        // Range-checked store: other lanes' offsets are out of range and dropped.
+        const uint32_t ooff = is_end ? (uint32_t)(f.pc + f.m.idx) * 4u : 0x7FFFFFF0u;
+        const __amdgpu_buffer_rsrc_t out_rsrc =
+            make_rsrc(a.out, a.count < (1ull << 30) ? (uint32_t)a.count * 4u : 0xFFFFFFF0u);
+        __builtin_amdgcn_raw_buffer_store_b32(o, out_rsrc, (int)ooff, 0, 0);
+        break;
+      }
+      default: {  // packet open at lane 63: carry it (wave-uniform, scalar ALU)
+        const bool open63 = __builtin_amdgcn_readlane((int)(f.m.live && !is_end_of(f.m)), 63) != 0;
+        const uint32_t seg63 = (uint32_t)__builtin_amdgcn_readlane((int)f.seg, 63);
+        carry = open63 ? mul_const_uniform(seg63, g_x4096) : 0u;
+        break;
+      }
     }
-    uint32_t val = m.live ? mul_lane(mul_basis(ra, g_x256.q) ^ rb) : 0u;
-    if (lane == 0) val ^= carry;
-    const uint32_t pre = wave_prefix_xor(val, lane);
-    const int f = m.rel > 0 ? m.rel : 0;  // packet's first lane in this step
-    const uint32_t before = (uint32_t)__builtin_amdgcn_ds_bpermute((f - 1) << 2, (int)pre);
-    const uint32_t seg = pre ^ (f == 0 ? 0u : before);
-    // End lanes: register = seg * x^-(8 z + 512 (63 - lane)), stored through a
-    // range-checked buffer (other lanes' offsets are out of range and
-    // dropped) -- straight-line, like the loads.
-    const uint32_t v_icrc = ~gf_mul_dev(seg, C);
-    const uint32_t o = !valid ? 0u : a.verify ? (T == v_icrc ? 1u : 0u) : v_icrc;
-    const uint32_t ooff = is_end ? (uint32_t)(pc + m.idx) * 4u : 0x7FFFFFF0u;
-    const __amdgpu_buffer_rsrc_t out_rsrc = make_rsrc(a.out, a.count < (1ull << 30) ? (uint32_t)a.count * 4u : 0xFFFFFFF0u);
-    __builtin_amdgcn_raw_buffer_store_b32(o, out_rsrc, (int)ooff, 0, 0);
-    // Packet open at lane 63: carry it (wave-uniform, scalar ALU).
-    const bool open63 = __builtin_amdgcn_readlane((int)(m.live && !is_end), 63) != 0;
-    const uint32_t seg63 = (uint32_t)__builtin_amdgcn_readlane((int)seg, 63);
-    carry = open63 ? mul_const_uniform(seg63, g_x4096) : 0u;
   };
 
   uint64_t g = PS(p0), pc = p0;
-  Map mA = map_step(load_desc(pc), g);
+  Map mA = map_step(load_desc(pc, g), g);
   uint64_t pcn = next_pc(mA, pc);
-  Desc dn = load_desc(pcn);
-  u32x4 vA[4], vB[4];
+  Desc dn = load_desc(pcn, g + 64);
+  u32x4 v[4];  // pieces of the step being started; refilled with the next step's once masked
   Map mB;
-  load_pieces(mA, vA);
-  // One pipeline stage: map the next step into (mn, vn), fold the current.
-  auto stage = [&](const Map &mc, const u32x4 (&vc)[4], Map &mn, u32x4 (&vn)[4]) -> bool {
-    uint32_t C, T;
-    load_fin(mc, C, T);
+  load_pieces(mA, v);
+  Fin prev{};
+  prev.m.live = false;  // pipeline primer: no lane ends or carries
+  prev.m.n = 0;
+  prev.m.rel = 0;
+  prev.m.idx = 0;
+  prev.m.start = safe;
+
+  // One pipeline stage: mask this step's words, map + prefetch the next
+  // step (into the same piece registers), then fold this step interleaved
+  // slice by slice with the finish of the previous one.
+  auto stage = [&](const Map &mc, Map &mn) -> bool {
+    Fin cur;
+    cur.m = mc;
+    cur.pc = pc;
+    load_fin(mc, cur.C, cur.T);
+    uint32_t w[16];
+    if (ABL & 8) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) w[j] = word_of(v[j >> 2], j & 3);
+    } else {
+      mask_words(mc, v, w);
+    }
     const uint64_t gn = g + 64;
     mn = map_step(dn, gn);
     const uint64_t pcnn = next_pc(mn, pcn);
-    dn = load_desc(pcnn);
-    load_pieces(mn, vn);
-    __builtin_amdgcn_sched_barrier(0);  // next step's loads go out before this step's fold
-    process(mc, vc, C, T, pc);
+    dn = load_desc(pcnn, gn + 64);
+    load_pieces(mn, v);
+    __builtin_amdgcn_sched_barrier(0);
+    // One 16-step chain: its LDS latency hides behind the interleaved
+    // finish work (measured faster than two chains joined by x^256).
+    uint32_t r = 0u;
+#pragma unroll
+    for (int sl = 0; sl < 8; ++sl) {
+      if (ABL & 1) {
+        r ^= w[2 * sl] ^ w[2 * sl + 1];
+      } else {
+        r = step4(lds, lt, r, w[2 * sl]);
+        r = step4(lds, lt, r, w[2 * sl + 1]);
+      }
+      if (!(ABL & 2)) fin_slice(prev, sl);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    cur.r = r;
+    prev = cur;
     pc = pcn;
     pcn = pcnn;
     g = gn;
     return gn < g_end;
   };
-  while (stage(mA, vA, mB, vB) && stage(mB, vB, mA, vA)) {
+  while (stage(mA, mB) && stage(mB, mA)) {
   }
+#pragma unroll
+  for (int sl = 0; sl < 8; ++sl) fin_slice(prev, sl);
 }
 
 // =======================================================================
