@@ -93,7 +93,8 @@ int ricrc_device_count(const ricrc_ctx *ctx);
  * Asynchronous on `stream` (a hipStream_t; NULL = the HIP null stream;
  * ricrc_stream() returns the context's own non-blocking stream).  Lengths are not read on the host: a device length outside
  * [4, RICRC_MAX_LEN] yields out[i] = 0.  16-byte aligned packet starts with a
- * fixed length take the streaming kernel; anything else the general kernel. */
+ * fixed length take the streaming kernels; anything else (offsets, lengths,
+ * any alignment or mix of sizes) the ragged kernel, several packets per wave. */
 int ricrc_batch_host(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *off, const uint32_t *len,
                      uint32_t stride, uint64_t count, uint32_t l3_offset, uint32_t *out);
 int ricrc_batch_device(ricrc_ctx *ctx, int dev, const void *d_base, const uint64_t *d_off,

@@ -213,51 +213,34 @@ int launch_batch(Dev &d, const uint8_t *base, const uint64_t *off, const uint32_
       return hip_err(launch_stream(a, cpl, grid, st));
     }
   }
-  if (getenv("RICRC_GENERAL_WAVE") == nullptr) {
-    // Ragged kernel: pieces from a device-side scan of the descriptors, or
-    // arithmetic when every packet has the same length and 16-byte phase.
-    RaggedArgs r{};
-    r.base = base;
-    r.off = off;
-    r.len = len;
-    r.stride = stride;
-    r.count = count;
-    r.out = out;
-    r.inv_tab = d.d_inv;
-    r.inv4 = reinterpret_cast<const u32x4_t *>(d.d_inv4);
-    r.fixed_len = fixed_len;
-    r.l3_offset = l3_offset;
-    r.verify = verify ? 1u : 0u;
-    for (uint32_t l = 0; l < 64; ++l) r.K[l] = x8n_host(64ull * (63 - l));
-    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)d.n_cu, (count + 63) / 64));
-    if (!off && !len && stride % 16 == 0) {
-      r.P = ragged_pieces((uintptr_t)base + l3_offset, fixed_len);
-      return hip_err(launch_ragged(r, grid, st));
-    }
-    uint64_t *ps = nullptr;
-    HIP_TRY(hipMallocAsync((void **)&ps, (count + 1) * sizeof(uint64_t), st));
-    r.ps = ps;
-    hipError_t e = ragged_piece_scan(r, ps, st);
-    if (e == hipSuccess) e = launch_ragged(r, grid, st);
-    const hipError_t e2 = hipFreeAsync(ps, st);
-    return hip_err(e != hipSuccess ? e : e2);
+  // Everything else: the ragged kernel.  Pieces from a device-side scan of
+  // the descriptors, or arithmetic when every packet has the same length and
+  // 16-byte phase.
+  RaggedArgs r{};
+  r.base = base;
+  r.off = off;
+  r.len = len;
+  r.stride = stride;
+  r.count = count;
+  r.out = out;
+  r.inv_tab = d.d_inv;
+  r.inv4 = reinterpret_cast<const u32x4_t *>(d.d_inv4);
+  r.fixed_len = fixed_len;
+  r.l3_offset = l3_offset;
+  r.verify = verify ? 1u : 0u;
+  for (uint32_t l = 0; l < 64; ++l) r.K[l] = x8n_host(64ull * (63 - l));
+  const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)d.n_cu, (count + 63) / 64));
+  if (!off && !len && stride % 16 == 0) {
+    r.P = ragged_pieces((uintptr_t)base + l3_offset, fixed_len);
+    return hip_err(launch_ragged(r, grid, st));
   }
-  GeneralArgs g{};
-  g.base = base;
-  g.off = off;
-  g.len = len;
-  g.stride = stride;
-  g.count = count;
-  g.out = out;
-  g.inv_tab = d.d_inv;
-  g.fixed_len = fixed_len;
-  g.l3_offset = l3_offset;
-  g.x4096 = x8n_host(4096);
-  g.verify = verify ? 1u : 0u;
-  for (uint32_t l = 0; l < 64; ++l) g.K[l] = x8n_host(64ull * (63 - l));
-  const uint64_t want = (count + 15) / 16;
-  const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)d.n_cu, want));
-  return hip_err(launch_general(g, grid, st));
+  uint64_t *ps = nullptr;
+  HIP_TRY(hipMallocAsync((void **)&ps, (count + 1) * sizeof(uint64_t), st));
+  r.ps = ps;
+  hipError_t e = ragged_piece_scan(r, ps, st);
+  if (e == hipSuccess) e = launch_ragged(r, grid, st);
+  const hipError_t e2 = hipFreeAsync(ps, st);
+  return hip_err(e != hipSuccess ? e : e2);
 }
 
 }  // namespace

@@ -40,21 +40,6 @@ struct TskArgs {
   uint64_t *stamps;  // diagnostic builds only (tools/microbench); null in the product
 };
 
-// Any alignment / offsets / lengths.
-struct GeneralArgs {
-  const uint8_t *base;
-  const uint64_t *off;  // may be null (then p * stride)
-  const uint32_t *len;  // may be null (then fixed_len)
-  uint64_t stride;
-  uint64_t count;
-  uint32_t *out;
-  const uint32_t *inv_tab;  // x^(-8 z), z in [0, 4096]
-  uint32_t fixed_len;
-  uint32_t l3_offset;
-  uint32_t x4096;  // x^(8*4096)
-  uint32_t verify;
-  uint32_t K[64];  // x^(8*64*(63-lane))
-};
 
 // Ragged batches (any alignment, per-packet offsets and/or lengths): the
 // batch is cut into 64-byte pieces, packet by packet -- packet i covers
@@ -95,7 +80,6 @@ struct SynthArgs {
 
 hipError_t launch_stream(const StreamArgs &a, int cpl, int grid, hipStream_t st);
 hipError_t launch_tsk(const TskArgs &a, int grid, hipStream_t st);
-hipError_t launch_general(const GeneralArgs &a, int grid, hipStream_t st);
 hipError_t launch_ragged(const RaggedArgs &a, int grid, hipStream_t st);
 // ps[0..count] = exclusive prefix of ragged_pieces over the batch (stream
 // ordered; temporary storage from the stream-ordered allocator).

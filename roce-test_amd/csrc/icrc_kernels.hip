@@ -608,11 +608,7 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
 }
 
 // =======================================================================
-// General kernel: any alignment, per-packet offsets and/or lengths.
-// One wave per packet; the packet's bytes are covered by 4 KiB windows
-// aligned to 16 B below the packet start.  Bytes outside the packet are
-// zero, so the wave computes the register at the window end; windows are
-// chained with x^(8*4096) and the zero tail is removed with x^(-8 z).
+// Byte-level helpers for packets that do not start or end on a word.
 // =======================================================================
 __device__ __forceinline__ uint32_t byte_span_mask(int lo, int hi) {  // bytes [lo,hi) of a word
   // Branch-free: 64-bit shifts of 0xFFFFFFFF handle the 0- and 32-bit ends.
@@ -626,84 +622,6 @@ __device__ __forceinline__ uint32_t byte_span_mask(int lo, int hi) {  // bytes [
 __device__ __forceinline__ uint32_t expand_nibble(uint32_t b) {
   return ((b & 1u) ? 0x000000FFu : 0u) | ((b & 2u) ? 0x0000FF00u : 0u) | ((b & 4u) ? 0x00FF0000u : 0u) |
          ((b & 8u) ? 0xFF000000u : 0u);
-}
-
-__global__ __launch_bounds__(kBlock) void icrc_general_kernel(GeneralArgs a) {
-  __shared__ uint32_t lds[kLdsWords];
-  fill_tables(lds);
-  __syncthreads();
-
-  const int lane = threadIdx.x & 63;
-  const LaneTab lt{(uint32_t)(lane & 31) << 2, ((uint32_t)(lane & 31) << 2) | 0x10000u};
-  uint32_t Q[32];
-  make_basis(a.K[lane], Q);  // x^(8*64*(63-lane)): lane end -> window end
-
-  const uint64_t wave = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
-  const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
-
-  for (uint64_t p = wave; p < a.count; p += nwaves) {
-    const uint64_t off = a.off ? a.off[p] : p * (uint64_t)a.stride;
-    const uint32_t n = a.len ? a.len[p] : a.fixed_len;
-    if (n < 4 || n > kMaxLen) {
-      if (lane == 0) a.out[p] = 0u;
-      continue;
-    }
-    const int M = (int)n - 4;
-    const uintptr_t start = (uintptr_t)a.base + off + a.l3_offset;
-    const uintptr_t a0 = start & ~(uintptr_t)15;
-    const int s = (int)(start - a0);
-    const int T = s + M;
-    const int nwin = T > 0 ? (T + 4095) >> 12 : 1;
-
-    uint32_t R = 0;
-    for (int w = 0; w < nwin; ++w) {
-      const uintptr_t lb = a0 + ((uintptr_t)w << 12) + ((uintptr_t)lane << 6);
-      const int rel0 = (int)(lb - start);  // packet-relative offset of the lane's first byte
-      u32x4 v[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int pr = rel0 + 16 * k;
-        v[k] = u32x4{0u, 0u, 0u, 0u};
-        if (pr < M && pr + 16 > 0) v[k] = *reinterpret_cast<const u32x4 *>(lb + 16 * k);
-      }
-      const bool interior = rel0 >= 40 && rel0 + 64 <= M;
-      uint32_t r = 0;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        uint32_t wd = word_of(v[j >> 2], j & 3);
-        if (!interior) {
-          const int rel = rel0 + 4 * j;
-          const uint32_t vm = byte_span_mask(-rel, M - rel);
-          uint32_t mb = 0u;
-          if (rel > -4 && rel < 40) {
-            const uint64_t bits = rel >= 0 ? (kMaskBits >> rel) : (kMaskBits << (-rel));
-            mb = expand_nibble((uint32_t)bits & 0xFu) & vm;
-          }
-          uint32_t xp = 0u;
-          if (rel > -4 && rel < 4) xp = rel >= 0 ? (kSeed >> (8 * rel)) : (kSeed << (-8 * rel));
-          wd = ((wd & vm) | mb) ^ xp;
-        }
-        r = step4(lds, lt, r, wd);
-      }
-      r = mul_basis(r, Q);
-#pragma unroll
-      for (int sft = 1; sft < 64; sft <<= 1) r ^= __shfl_xor(r, sft);
-      R = w == 0 ? r : (gf_mul_dev(R, a.x4096) ^ r);
-    }
-    const int z = (nwin << 12) - T;  // zero bytes folded past the packet end
-    R = gf_mul_dev(R, a.inv_tab[z]);
-    if (lane == 0) {
-      const uint32_t v_icrc = ~R;
-      if (a.verify) {
-        const uint8_t *tb = reinterpret_cast<const uint8_t *>(start) + M;
-        const uint32_t tr = (uint32_t)tb[0] | ((uint32_t)tb[1] << 8) | ((uint32_t)tb[2] << 16) |
-                            ((uint32_t)tb[3] << 24);
-        a.out[p] = (tr == v_icrc) ? 1u : 0u;
-      } else {
-        a.out[p] = v_icrc;
-      }
-    }
-  }
 }
 
 // =======================================================================
@@ -1187,24 +1105,12 @@ hipError_t launch_tsk(const TskArgs &a, int grid, hipStream_t st) {
   return hipGetLastError();
 }
 
-template <int NT>
-static void launch_ragged_nt(const RaggedArgs &a, int grid, hipStream_t st) {
-  const dim3 b(NT);
-  if (!a.ps) hipLaunchKernelGGL((icrc_ragged_kernel<0, NT>), dim3(grid), b, 0, st, a);
-  else if (a.off && a.len) hipLaunchKernelGGL((icrc_ragged_kernel<1, NT>), dim3(grid), b, 0, st, a);
-  else if (a.off) hipLaunchKernelGGL((icrc_ragged_kernel<2, NT>), dim3(grid), b, 0, st, a);
-  else hipLaunchKernelGGL((icrc_ragged_kernel<3, NT>), dim3(grid), b, 0, st, a);
-}
-
 hipError_t launch_ragged(const RaggedArgs &a, int grid, hipStream_t st) {
-  const char *e = getenv("RICRC_RAGGED_NT");
-  if (e && atoi(e) == 512) launch_ragged_nt<512>(a, grid, st);
-  else launch_ragged_nt<1024>(a, grid, st);
-  return hipGetLastError();
-}
-
-hipError_t launch_general(const GeneralArgs &a, int grid, hipStream_t st) {
-  hipLaunchKernelGGL(icrc_general_kernel, dim3(grid), dim3(kBlock), 0, st, a);
+  const dim3 b(1024);
+  if (!a.ps) hipLaunchKernelGGL((icrc_ragged_kernel<0, 1024>), dim3(grid), b, 0, st, a);
+  else if (a.off && a.len) hipLaunchKernelGGL((icrc_ragged_kernel<1, 1024>), dim3(grid), b, 0, st, a);
+  else if (a.off) hipLaunchKernelGGL((icrc_ragged_kernel<2, 1024>), dim3(grid), b, 0, st, a);
+  else hipLaunchKernelGGL((icrc_ragged_kernel<3, 1024>), dim3(grid), b, 0, st, a);
   return hipGetLastError();
 }
 

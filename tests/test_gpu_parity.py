@@ -5,7 +5,7 @@ Inputs are built on the host (numpy, seeded) or by the device generator,
 copied where needed, and every kernel result is compared with
 oracle/icrc_oracle.c (itself pinned to zlib / the golden vectors by
 tests/test_oracle.py).  Covers the streaming kernel (fixed length, 16-B
-aligned), the general kernel (offsets, ragged lengths, any alignment,
+aligned), the ragged kernel (offsets, ragged lengths, any alignment,
 multi-window jumbo packets, Ethernet l3_offset), verify mode, the host-buffer
 path, and the full BASELINE headline size (1 M x 4096 B).
 """
@@ -88,7 +88,7 @@ def _ragged(rng, count, lo, hi, align, l3_offset=0):
 
 @pytest.mark.parametrize("lo,hi,align", [(4, 64, 1), (44, 300, 1), (44, 4096, 4), (44, 4096, 16),
                                          (3000, 9100, 1), (9000, 20000, 1), (44, 65535, 1)])
-def test_general_kernel_ragged(ctx, lo, hi, align):
+def test_ragged_kernel_lengths(ctx, lo, hi, align):
     rng = np.random.default_rng(lo * 7 + hi)
     count = 400 if hi <= 9100 else 40
     buf, offs, lens = _ragged(rng, count, lo, hi, align)
@@ -98,7 +98,7 @@ def test_general_kernel_ragged(ctx, lo, hi, align):
     np.testing.assert_array_equal(_host_u32(out), want)
 
 
-def test_general_kernel_ethernet_offset(ctx):
+def test_ragged_kernel_ethernet_offset(ctx):
     """l3_offset = 14: L3 starts 2 bytes past a 16-byte boundary."""
     rng = np.random.default_rng(14)
     count, n = 500, 1024
@@ -110,7 +110,7 @@ def test_general_kernel_ethernet_offset(ctx):
     np.testing.assert_array_equal(_host_u32(out), want)
 
 
-def test_general_kernel_invalid_lengths_zero(ctx):
+def test_ragged_kernel_invalid_lengths_zero(ctx):
     buf = np.arange(256, dtype=np.uint8)
     offs = np.array([0, 16, 32], dtype=np.uint64)
     lens = np.array([3, 0, 100], dtype=np.uint32)
@@ -119,6 +119,58 @@ def test_general_kernel_invalid_lengths_zero(ctx):
     got = _host_u32(out)
     assert got[0] == 0 and got[1] == 0
     assert got[2] == icrc_oracle.icrc(buf[32:132].tobytes())
+
+
+def test_ragged_kernel_c4_mix_many_waves(ctx):
+    """BASELINE C4 shape (sizes uniform over 64/256/1024/4096, packed back to
+    back): enough packets that every wave owns a range and the per-wave
+    64-ary searches take several rounds; plus long runs of 64-byte packets
+    (64 packets in one wave step)."""
+    rng = np.random.default_rng(4)
+    count = 200_000
+    lens = rng.choice(np.array([64, 256, 1024, 4096], np.uint32), size=count)
+    lens[1000:9000] = 64
+    offs = np.zeros(count, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    total = int(offs[-1] + lens[-1])
+    buf = np.empty(total + 64, np.uint8)
+    buf[:] = rng.integers(0, 256, size=buf.size, dtype=np.uint8)
+    want = oracle_c.icrc_batch(buf, offsets=offs, lengths=lens, threads=16)
+    out = _out(count)
+    ctx.batch_device(_dev(buf), count, out, offsets=_dev(offs), lengths=_dev(lens), stream=_stream())
+    np.testing.assert_array_equal(_host_u32(out), want)
+
+
+def test_ragged_kernel_offsets_only_and_lengths_only(ctx):
+    """Descriptor modes: offsets with a fixed length (stride - l3_offset), and
+    per-packet lengths at a fixed stride."""
+    rng = np.random.default_rng(23)
+    count, stride = 3000, 1536
+    frames = rng.integers(0, 256, size=count * stride + 64, dtype=np.uint8)
+    perm = rng.permutation(count).astype(np.uint64)
+    offs = perm * stride + 3  # scattered, odd alignment
+    want = oracle_c.icrc_batch(frames, offsets=offs, lengths=np.full(count, 1000, np.uint32))
+    out = _out(count)
+    ctx.batch_device(_dev(frames), count, out, stride=1000, offsets=_dev(offs), stream=_stream())
+    np.testing.assert_array_equal(_host_u32(out), want)
+    lens = rng.integers(44, stride - 14 + 1, size=count).astype(np.uint32)
+    want = oracle_c.icrc_batch(frames, lengths=lens, stride=stride, count=count, l3_offset=14)
+    ctx.batch_device(_dev(frames), count, out, stride=stride, lengths=_dev(lens), l3_offset=14,
+                     stream=_stream())
+    np.testing.assert_array_equal(_host_u32(out), want)
+
+
+def test_ragged_kernel_uniform_misaligned_stride(ctx):
+    """Fixed stride with the L3 start off 16-byte alignment (no descriptors:
+    arithmetic piece map), several pieces per packet, many packets."""
+    rng = np.random.default_rng(9)
+    for n, l3, stride in ((1500, 14, 1520), (64, 2, 80), (4096, 6, 4112)):
+        count = 20000 if n < 2000 else 5000
+        frames = rng.integers(0, 256, size=count * stride + 64, dtype=np.uint8)
+        want = oracle_c.icrc_batch(frames, stride=stride, count=count, l3_offset=l3, threads=16)
+        out = _out(count)
+        ctx.batch_device(_dev(frames), count, out, stride=stride, l3_offset=l3, stream=_stream())
+        np.testing.assert_array_equal(_host_u32(out), want, err_msg=f"n={n} l3={l3}")
 
 
 @pytest.mark.parametrize("n", [64, 1024, 4096, 1000])

@@ -5,7 +5,7 @@ reference python/simulator.py for seeds 1-3, captured by
 tests/golden/gen_sim_stream.py with ICRCs from the oracle.  Here: the adapter
 re-serialises every Packet to the same bytes, ricrc_one (ctypes) reproduces
 every ICRC, the verify path accepts them, corruption is caught, and (GPU) the
-whole stream as one ragged batch through the general kernel matches."""
+whole stream as one ragged batch through the ragged kernel matches."""
 import json
 import os
 import queue

@@ -6,7 +6,7 @@ Device-resident (HIP-event kernel time, inputs already in HBM):
     headline 4096 B) through the default dispatch (TSK kernel) and, for
     comparison, with RICRC_NO_TSK=1 (the stride/offset streaming kernel);
   * the C4 ragged mix (N uniform over {64,256,1024,4096}, packed, uint64
-    offsets + uint32 lengths) through the general kernel.
+    offsets + uint32 lengths) through the ragged kernel.
 Host-resident (ricrc_batch_host: host in, host out; PCIe-inclusive):
   * pageable numpy input, pinned (ricrc_host_alloc) input, registered input.
 
@@ -131,7 +131,7 @@ def main():
     check_sample(np, oracle_c, buf[:span].cpu().numpy(), offs[:ns], lens[:ns],
                  out[:ns].cpu().numpy().view(np.uint32), "C4 ragged")
     alg = nbytes + 16 * count
-    emit(path="device", kernel="general (ragged C4 mix)", packets=count, bytes=nbytes, kernel_ms=round(ms, 4),
+    emit(path="device", kernel="ragged (C4 mix)", packets=count, bytes=nbytes, kernel_ms=round(ms, 4),
          gib_s=round(nbytes / (ms * 1e-3) / 2**30, 1), hbm_frac=round(alg / (ms * 1e-3) / 8e12, 4))
     host_ragged = (buf.cpu().numpy(), offs, lens, out.cpu().numpy().view(np.uint32).copy())
     del buf, out, d_offs, d_lens
