@@ -428,16 +428,19 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
       const uint32_t val = a.verify ? (trl == ~r ? 1u : 0u) : ~r;
       // Collect: lane (k mod 64) keeps the result of local region k; every
       // 64th region (and the block's last) the whole group leaves in one
-      // coalesced store.  The store is issued every step with out-of-range
-      // offsets when not flushing, so no VMEM op sits under a branch.
+      // coalesced store, under a wave-uniform branch.  Stores share vmcnt
+      // with loads and retire in order, so a store issued every step (even
+      // a dropped out-of-range one) would make each prefetch wait for a
+      // write acknowledgement: measured 4 % of the kernel.
       const bool live = it < it_end;
       const uint32_t k = (uint32_t)(it - it_begin) & 63u;
       res = (live && lane == k) ? val : res;
-      const bool flush = live && (k == 63u || it + 1 == it_end);
-      const uint64_t g0 = it_begin + ((it - it_begin) & ~(uint64_t)63);
-      const uint32_t ng = live ? (uint32_t)(a.count - g0 < 64u ? a.count - g0 : 64u) : 0u;
-      const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.out + (live ? g0 : 0), 4u * ng);
-      __builtin_amdgcn_raw_buffer_store_b32(res, rg, (flush && lane <= k) ? 4u * lane : 0x7FFFFFF0u, 0, 0);
+      if (live && (k == 63u || it + 1 == it_end)) {  // it, it_begin, it_end: wave-uniform
+        const uint64_t g0 = it_begin + ((it - it_begin) & ~(uint64_t)63);
+        const uint32_t ng = (uint32_t)(a.count - g0 < 64u ? a.count - g0 : 64u);
+        const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.out + g0, 4u * ng);
+        __builtin_amdgcn_raw_buffer_store_b32(res, rg, lane <= k ? 4u * lane : 0x7FFFFFF0u, 0, 0);
+      }
     } else {
       const uint32_t s0 = group_xor_masked(xor3(f.a0[0], f.a0[1], f.a0[2] ^ f.a0[3]), lm);
       const uint32_t s1 = group_xor_masked(xor3(f.a1[0], f.a1[1], f.a1[2] ^ f.a1[3]), lm);
@@ -693,7 +696,8 @@ __device__ __forceinline__ uint32_t wave_prefix_xor(uint32_t v, uint32_t lane) {
 // 2 offsets only, 3 lengths only.
 // ABL: timing-only ablation mask for tools/microbench/ragged_abl.hip (the
 // product instantiates 0): 1 no table fold, 2 no finish slices, 4 no piece
-// loads, 8 no word masking.
+// loads, 8 no word masking, 32 no result stores (folded into one per wave),
+// 64 no end-lane multiply, 128 no carry multiply, 256 no lane alignment.
 template <int MODE, int kRaggedBlock, int ABL = 0>
 __global__ __launch_bounds__(kRaggedBlock) void icrc_ragged_kernel(RaggedArgs a) {
   constexpr bool UNI = MODE == 0, HAS_OFF = MODE == 1 || MODE == 2, HAS_LEN = MODE == 1 || MODE == 3;
@@ -896,15 +900,17 @@ __global__ __launch_bounds__(kRaggedBlock) void icrc_ragged_kernel(RaggedArgs a)
     uint32_t acc[4];
   };
   uint32_t carry = 0;  // open packet's XOR, aligned to the previous step's end
+  uint32_t sink = 0;   // ABL & 32: results folded here instead of stored
   auto fin_slice = [&](Fin &f, int sl) {
     switch (sl) {
       case 0:
 #pragma unroll
         for (int k = 0; k < 4; ++k) f.acc[k] = 0u;
-        mul_lane_part(f.r, 0, f.acc);  // align to the step end, basis words 0..15
+        if (ABL & 256) f.acc[0] = f.r;
+        else mul_lane_part(f.r, 0, f.acc);  // align to the step end, basis words 0..15
         break;
       case 1: {
-        mul_lane_part(f.r, 1, f.acc);  // basis words 16..31
+        if (!(ABL & 256)) mul_lane_part(f.r, 1, f.acc);  // basis words 16..31
         uint32_t val = f.m.live ? xor3(f.acc[0], f.acc[1], f.acc[2] ^ f.acc[3]) : 0u;
         if (lane == 0) val ^= carry;
         const uint32_t pre = wave_prefix_xor(val, lane);
@@ -919,6 +925,10 @@ __global__ __launch_bounds__(kRaggedBlock) void icrc_ragged_kernel(RaggedArgs a)
       case 3:
       case 4:
       case 5: {  // register = seg * x^-(8 z + 512 (63 - lane)): chain k takes bits 31-8k..24-8k
+        if (ABL & 64) {
+          f.acc[sl - 2] ^= f.seg ^ f.C[sl - 2];
+          break;
+        }
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
 #pragma unroll
@@ -938,15 +948,19 @@ __global__ __launch_bounds__(kRaggedBlock) void icrc_ragged_kernel(RaggedArgs a)
         const uint32_t o = !valid ? 0u : a.verify ? (f.T == v_icrc ? 1u : 0u) : v_icrc;
         // Range-checked store: other lanes' offsets are out of range and dropped.
         const uint32_t ooff = is_end ? (uint32_t)(f.pc + f.m.idx) * 4u : 0x7FFFFFF0u;
-        const __amdgpu_buffer_rsrc_t out_rsrc =
-            make_rsrc(a.out, a.count < (1ull << 30) ? (uint32_t)a.count * 4u : 0xFFFFFFF0u);
-        __builtin_amdgcn_raw_buffer_store_b32(o, out_rsrc, (int)ooff, 0, 0);
+        if (ABL & 32) {
+          sink ^= o;
+        } else {
+          const __amdgpu_buffer_rsrc_t out_rsrc =
+              make_rsrc(a.out, a.count < (1ull << 30) ? (uint32_t)a.count * 4u : 0xFFFFFFF0u);
+          __builtin_amdgcn_raw_buffer_store_b32(o, out_rsrc, (int)ooff, 0, 0);
+        }
         break;
       }
       default: {  // packet open at lane 63: carry it (wave-uniform, scalar ALU)
         const bool open63 = __builtin_amdgcn_readlane((int)(f.m.live && !is_end_of(f.m)), 63) != 0;
         const uint32_t seg63 = (uint32_t)__builtin_amdgcn_readlane((int)f.seg, 63);
-        carry = open63 ? mul_const_uniform(seg63, g_x4096) : 0u;
+        carry = open63 ? ((ABL & 128) ? seg63 : mul_const_uniform(seg63, g_x4096)) : 0u;
         break;
       }
     }
@@ -1012,6 +1026,7 @@ __global__ __launch_bounds__(kRaggedBlock) void icrc_ragged_kernel(RaggedArgs a)
   }
 #pragma unroll
   for (int sl = 0; sl < 8; ++sl) fin_slice(prev, sl);
+  if (ABL & 32) a.out[wave % a.count] = sink;
 }
 
 // =======================================================================

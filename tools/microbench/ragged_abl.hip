@@ -56,6 +56,11 @@ int main(int argc, char **argv) {
   rep("no fold, no finish, no mask", run<1, 11>(a, grid, 10));
   rep("only map (no fold/finish/mask/loads)", run<1, 15>(a, grid, 10));
   rep("no loads, no mask (compute)", run<1, 12>(a, grid, 10));
+  rep("no stores (one per wave)", run<1, 32>(a, grid, 10));
+  rep("no end multiply", run<1, 64>(a, grid, 10));
+  rep("no carry multiply", run<1, 128>(a, grid, 10));
+  rep("no lane alignment", run<1, 256>(a, grid, 10));
+  rep("no end/carry/lane multiplies", run<1, 64 | 128 | 256>(a, grid, 10));
   rep("full again", run<1, 0>(a, grid, 10));
   return 0;
 }
