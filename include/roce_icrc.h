@@ -57,6 +57,39 @@ int ricrc_stamp_one(uint8_t *l3, uint32_t n);
  * accept path, p4/shuffle/shuffle_ingress_parser.p4:12-36, header.p4:14). */
 int ricrc_is_rocev2(const uint8_t *l3, uint32_t n);
 
+/* ------------------------------------------------------- address families
+ * The reference is IPv4-only (header.p4:42-53, shuffle_ingress_parser.p4:16-19)
+ * and every entry point without a flags argument keeps exactly its masks.
+ * The *_ex entry points take one of:
+ *   RICRC_F_IPV4  IPv4 masks (as the plain entry points);
+ *   RICRC_F_IPV6  RoCEv2 over IPv6: traffic class + flow label (L3 byte 0 low
+ *                 nibble, bytes 1-3), hop limit (7), UDP checksum (46-47),
+ *                 BTH byte 4 (52) forced to ones -- IBTA Annex A17 as the
+ *                 Linux rxe driver applies it (rxe_icrc.c);
+ *   RICRC_F_AUTO  per packet from the IP version nibble (6: IPv6, else IPv4).
+ * Any other value: -EINVAL (per-packet calls returning a value: 0). */
+#define RICRC_F_IPV4 0u
+#define RICRC_F_IPV6 1u
+#define RICRC_F_AUTO 2u
+
+uint32_t ricrc_one_ex(const uint8_t *l3, uint32_t n, uint32_t flags);
+int ricrc_verify_one_ex(const uint8_t *l3, uint32_t n, uint32_t flags);
+int ricrc_stamp_one_ex(uint8_t *l3, uint32_t n, uint32_t flags);
+
+/* 4: RoCEv2 over IPv4 (as ricrc_is_rocev2), 6: RoCEv2 over IPv6 (version 6,
+ * next header 17, payload length n-40, UDP dport 4791), 0: neither. */
+int ricrc_classify(const uint8_t *l3, uint32_t n);
+
+/* Incremental repair after a header rewrite (the switch's PSN/MSN/opcode
+ * patches, shuffle_egress.p4:635-671): l3 is the packet AFTER the rewrite,
+ * bytes [off, off+len) held old_bytes before it and old_icrc was its ICRC.
+ * *new_icrc = the rewritten packet's ICRC in O(len), not O(n):
+ * old ^ shift(crc0(masked delta), n-4-off-len).  0, or -EINVAL (NULL,
+ * n < 4, range past n-4, bad flags, or an AUTO rewrite that changes the IP
+ * version). */
+int ricrc_repair_one(const uint8_t *l3, uint32_t n, uint32_t off, const uint8_t *old_bytes, uint32_t len,
+                     uint32_t old_icrc, uint32_t flags, uint32_t *new_icrc);
+
 /* GF(2) helpers on the (un-inverted) CRC register -- the linear algebra behind
  * incremental repair after header rewrites (shuffle_egress.p4:635-671):
  *   ricrc_shift(reg, k)          = register advanced over k zero bytes

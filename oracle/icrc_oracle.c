@@ -31,7 +31,13 @@
 
 #define POLY 0xEDB88320u
 
-static const int kMask[] = {1, 8, 10, 11, 26, 27, 32};
+/* {L3 offset, OR value}.  IPv4: shuffle_egress.p4:467,471,473,480,485.
+ * IPv6 (not in the IPv4-only reference): IBTA Annex A17 as Linux rxe applies
+ * it (rxe_icrc.c): priority nibble (byte 0 low), flow label bytes 1-3, hop
+ * limit 7, UDP checksum 46-47, BTH byte 4 at 52. */
+static const int kMaskV4[][2] = {{1, 0xFF}, {8, 0xFF}, {10, 0xFF}, {11, 0xFF}, {26, 0xFF}, {27, 0xFF}, {32, 0xFF}};
+static const int kMaskV6[][2] = {{0, 0x0F}, {1, 0xFF}, {2, 0xFF}, {3, 0xFF}, {7, 0xFF}, {46, 0xFF}, {47, 0xFF}, {52, 0xFF}};
+#define HEAD 56 /* every masked byte of either family lies in [0, 56) */
 
 static uint32_t bit_update(uint32_t crc, const uint8_t *p, size_t n) {
   for (size_t i = 0; i < n; ++i) {
@@ -55,42 +61,55 @@ static void init_tables(void) {
       T[t][b] = (T[t - 1][b] >> 8) ^ T[0][T[t - 1][b] & 0xFF];
 }
 
-/* First min(n-4, 40) bytes with the invariant masks applied. */
-static size_t masked_head(const uint8_t *l3, uint32_t n, uint8_t head[40]) {
-  size_t m = n - 4, h = m < 40 ? m : 40;
+/* family: 0 IPv4, 1 IPv6, 2 per packet from the version nibble. */
+static int fam_of(const uint8_t *l3, uint32_t n, int family) {
+  if (family == 2) return (n > 0 && (l3[0] >> 4) == 6) ? 1 : 0;
+  return family == 1 ? 1 : 0;
+}
+
+/* First min(n-4, HEAD) bytes with the invariant masks applied. */
+static size_t masked_head(const uint8_t *l3, uint32_t n, int family, uint8_t head[HEAD]) {
+  size_t m = n - 4, h = m < HEAD ? m : HEAD;
   memcpy(head, l3, h);
-  for (size_t i = 0; i < sizeof(kMask) / sizeof(kMask[0]); ++i)
-    if ((size_t)kMask[i] < h) head[kMask[i]] = 0xFF;
+  if (fam_of(l3, n, family)) {
+    for (size_t i = 0; i < sizeof(kMaskV6) / sizeof(kMaskV6[0]); ++i)
+      if ((size_t)kMaskV6[i][0] < h) head[kMaskV6[i][0]] |= (uint8_t)kMaskV6[i][1];
+  } else {
+    for (size_t i = 0; i < sizeof(kMaskV4) / sizeof(kMaskV4[0]); ++i)
+      if ((size_t)kMaskV4[i][0] < h) head[kMaskV4[i][0]] |= (uint8_t)kMaskV4[i][1];
+  }
   return h;
 }
 
-uint32_t oracle_icrc_bitwise(const uint8_t *l3, uint32_t n) {
+uint32_t oracle_icrc_bitwise_ex(const uint8_t *l3, uint32_t n, int family) {
   if (n < 4) return 0;
   static const uint8_t ff[8] = {0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF};
-  uint8_t head[40];
-  size_t h = masked_head(l3, n, head);
+  uint8_t head[HEAD];
+  size_t h = masked_head(l3, n, family, head);
   uint32_t c = bit_update(0xFFFFFFFFu, ff, 8);
   c = bit_update(c, head, h);
   c = bit_update(c, l3 + h, (n - 4) - h);
   return ~c;
 }
+uint32_t oracle_icrc_bitwise(const uint8_t *l3, uint32_t n) { return oracle_icrc_bitwise_ex(l3, n, 0); }
 
 static uint32_t byte_update(uint32_t c, const uint8_t *p, size_t n) {
   for (size_t i = 0; i < n; ++i) c = T[0][(c ^ p[i]) & 0xFF] ^ (c >> 8);
   return c;
 }
 
-uint32_t oracle_icrc_bytewise(const uint8_t *l3, uint32_t n) {
+uint32_t oracle_icrc_bytewise_ex(const uint8_t *l3, uint32_t n, int family) {
   pthread_once(&g_once, init_tables);
   if (n < 4) return 0;
   static const uint8_t ff[8] = {0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF};
-  uint8_t head[40];
-  size_t h = masked_head(l3, n, head);
+  uint8_t head[HEAD];
+  size_t h = masked_head(l3, n, family, head);
   uint32_t c = byte_update(0xFFFFFFFFu, ff, 8);
   c = byte_update(c, head, h);
   c = byte_update(c, l3 + h, (n - 4) - h);
   return ~c;
 }
+uint32_t oracle_icrc_bytewise(const uint8_t *l3, uint32_t n) { return oracle_icrc_bytewise_ex(l3, n, 0); }
 
 static uint32_t s8_update(uint32_t c, const uint8_t *p, size_t n) {
   while (n >= 8) {
@@ -106,19 +125,20 @@ static uint32_t s8_update(uint32_t c, const uint8_t *p, size_t n) {
   return byte_update(c, p, n);
 }
 
-uint32_t oracle_icrc_fast(const uint8_t *l3, uint32_t n) {
+uint32_t oracle_icrc_fast_ex(const uint8_t *l3, uint32_t n, int family) {
   pthread_once(&g_once, init_tables);
   if (n < 4) return 0;
-  uint8_t head[40];
-  size_t h = masked_head(l3, n, head);
+  uint8_t head[HEAD];
+  size_t h = masked_head(l3, n, family, head);
   uint32_t c = 0xDEBB20E3u; /* register after the 8 x 0xFF prefix */
   c = s8_update(c, head, h);
   c = s8_update(c, l3 + h, (n - 4) - h);
   return ~c;
 }
+uint32_t oracle_icrc_fast(const uint8_t *l3, uint32_t n) { return oracle_icrc_fast_ex(l3, n, 0); }
 
 /* ---------------------------------------------------------------- batch */
-typedef uint32_t (*icrc_fn)(const uint8_t *, uint32_t);
+typedef uint32_t (*icrc_fn)(const uint8_t *, uint32_t, int);
 
 struct job {
   const uint8_t *base;
@@ -128,6 +148,7 @@ struct job {
   uint32_t l3_offset;
   uint32_t *out;
   icrc_fn fn;
+  int family;
 };
 
 static void *run_job(void *arg) {
@@ -135,17 +156,18 @@ static void *run_job(void *arg) {
   for (uint64_t i = j->lo; i < j->hi; ++i) {
     uint64_t o = j->off ? j->off[i] : i * j->stride;
     uint32_t n = j->len ? j->len[i] : (uint32_t)(j->stride - j->l3_offset);
-    j->out[i] = j->fn(j->base + o + j->l3_offset, n);
+    j->out[i] = j->fn(j->base + o + j->l3_offset, n, j->family);
   }
   return NULL;
 }
 
-/* kind: 0 = bitwise, 1 = bytewise, 2 = slice-by-8.  Returns 0. */
-int oracle_icrc_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len,
-                      uint64_t stride, uint64_t count, uint32_t l3_offset, uint32_t *out,
-                      int threads, int kind) {
+/* kind: 0 = bitwise, 1 = bytewise, 2 = slice-by-8; family: 0 IPv4, 1 IPv6,
+ * 2 per packet.  Returns 0. */
+int oracle_icrc_batch_ex(const uint8_t *base, const uint64_t *off, const uint32_t *len,
+                         uint64_t stride, uint64_t count, uint32_t l3_offset, uint32_t *out,
+                         int threads, int kind, int family) {
   pthread_once(&g_once, init_tables);
-  icrc_fn fn = kind == 0 ? oracle_icrc_bitwise : kind == 1 ? oracle_icrc_bytewise : oracle_icrc_fast;
+  icrc_fn fn = kind == 0 ? oracle_icrc_bitwise_ex : kind == 1 ? oracle_icrc_bytewise_ex : oracle_icrc_fast_ex;
   if (threads < 1) threads = 1;
   if ((uint64_t)threads > count) threads = count ? (int)count : 1;
   pthread_t tid[256];
@@ -153,13 +175,19 @@ int oracle_icrc_batch(const uint8_t *base, const uint64_t *off, const uint32_t *
   if (threads > 256) threads = 256;
   for (int t = 0; t < threads; ++t) {
     jobs[t] = (struct job){base, off, len, stride, count * t / threads, count * (t + 1) / threads,
-                           l3_offset, out, fn};
+                           l3_offset, out, fn, family};
     if (threads == 1) run_job(&jobs[0]);
     else pthread_create(&tid[t], NULL, run_job, &jobs[t]);
   }
   if (threads > 1)
     for (int t = 0; t < threads; ++t) pthread_join(tid[t], NULL);
   return 0;
+}
+
+int oracle_icrc_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len,
+                      uint64_t stride, uint64_t count, uint32_t l3_offset, uint32_t *out,
+                      int threads, int kind) {
+  return oracle_icrc_batch_ex(base, off, len, stride, count, l3_offset, out, threads, kind, 0);
 }
 
 /* ------------------------------------------------- synthetic generator

@@ -40,6 +40,14 @@ import numpy as np
 
 # L3 byte offsets forced to 0xFF before the CRC (shuffle_egress.p4:467,471,473,480,485)
 MASK_OFFSETS = (1, 8, 10, 11, 26, 27, 32)
+# RoCEv2 over IPv6 -- not in the IPv4-only reference (header.p4:42-53).  Spec:
+# IBTA Annex A17 ICRC invariant fields, as the Linux rxe driver applies them
+# (drivers/infiniband/sw/rxe/rxe_icrc.c: ip6h->priority = 0xf (byte 0 low
+# nibble), ip6h->flow_lbl[0..2] = 0xff (bytes 1-3), ip6h->hop_limit = 0xff
+# (byte 7), udph->check = 0xffff (bytes 40+6, 40+7), bth->qpn |= ~QPN_MASK
+# (BTH byte 4 at 48+4)).  OR-values per L3 offset.
+MASKS_V6 = ((0, 0x0F), (1, 0xFF), (2, 0xFF), (3, 0xFF), (7, 0xFF), (46, 0xFF), (47, 0xFF), (52, 0xFF))
+MASKS_V4 = tuple((o, 0xFF) for o in MASK_OFFSETS)
 PREFIX = b"\xff" * 8                      # shuffle_egress.p4:465
 POLY_REFLECTED = 0xEDB88320
 CRC32_RESIDUE = 0x2144DF1C                # crc32(msg || LE32(crc32(msg))), any msg
@@ -48,25 +56,34 @@ ROCE_UDP_PORT = 4791                      # header.p4:14
 MIN_PKT = 20 + 8 + 12 + 4                 # IPv4 + UDP + BTH + ICRC
 
 
-def masked_body(l3: bytes) -> bytes:
+def family_of(l3: bytes, family: str = "v4") -> str:
+    """'v4' / 'v6', or for 'auto' the IP version nibble (6 -> 'v6', else 'v4')."""
+    if family == "auto":
+        return "v6" if len(l3) and (l3[0] >> 4) == 6 else "v4"
+    if family not in ("v4", "v6"):
+        raise ValueError(family)
+    return family
+
+
+def masked_body(l3: bytes, family: str = "v4") -> bytes:
     """The L3 bytes the ICRC covers, [0, n-4), with the invariant masks applied."""
     n = len(l3)
     if n < 4:
         raise ValueError("packet shorter than the ICRC trailer")
     b = bytearray(l3[: n - 4])
-    for o in MASK_OFFSETS:
+    for o, v in (MASKS_V6 if family_of(l3, family) == "v6" else MASKS_V4):
         if o < len(b):
-            b[o] = 0xFF
+            b[o] |= v
     return bytes(b)
 
 
-def icrc(l3: bytes) -> int:
+def icrc(l3: bytes, family: str = "v4") -> int:
     """ICRC value of one L3 RoCEv2 packet (trailer bytes = LE32 of the result).
 
     Restates calc_icrc() (shuffle_egress.p4:463-494) with zlib's CRC-32, which
     is the same parameter set as Tofino's HashAlgorithm_t.CRC32.
     """
-    return zlib.crc32(PREFIX + masked_body(l3)) & 0xFFFFFFFF
+    return zlib.crc32(PREFIX + masked_body(l3, family)) & 0xFFFFFFFF
 
 
 _BIT_TABLE = None
@@ -81,30 +98,30 @@ def _crc32_bitwise(data: bytes, crc: int = 0xFFFFFFFF) -> int:
     return crc
 
 
-def icrc_bitwise(l3: bytes) -> int:
+def icrc_bitwise(l3: bytes, family: str = "v4") -> int:
     """Second, table-free formulation used to cross-check :func:`icrc`."""
-    return _crc32_bitwise(PREFIX + masked_body(l3)) ^ 0xFFFFFFFF
+    return _crc32_bitwise(PREFIX + masked_body(l3, family)) ^ 0xFFFFFFFF
 
 
-def icrc_rxe(l3: bytes) -> int:
+def icrc_rxe(l3: bytes, family: str = "v4") -> int:
     """Third formulation: Linux-rxe style seed 0xDEBB20E3 at IP byte 0."""
-    return _crc32_bitwise(masked_body(l3), REGISTER_AFTER_PREFIX) ^ 0xFFFFFFFF
+    return _crc32_bitwise(masked_body(l3, family), REGISTER_AFTER_PREFIX) ^ 0xFFFFFFFF
 
 
-def residue_ok(l3: bytes) -> bool:
+def residue_ok(l3: bytes, family: str = "v4") -> bool:
     """CRC-32 over prefix||masked||trailer equals the CRC-32 residue 0x2144DF1C
     (register 0xDEBB20E3 before xorout) iff the trailer (little-endian,
     shuffle_egress.p4:493) holds the right ICRC."""
-    return (zlib.crc32(PREFIX + masked_body(l3) + bytes(l3[-4:])) & 0xFFFFFFFF) == CRC32_RESIDUE
+    return (zlib.crc32(PREFIX + masked_body(l3, family) + bytes(l3[-4:])) & 0xFFFFFFFF) == CRC32_RESIDUE
 
 
-def stamp(l3: bytes) -> bytes:
+def stamp(l3: bytes, family: str = "v4") -> bytes:
     """Return ``l3`` with its trailer replaced by the correct ICRC (LE32)."""
-    return bytes(l3[:-4]) + struct.pack("<I", icrc(l3))
+    return bytes(l3[:-4]) + struct.pack("<I", icrc(l3, family))
 
 
 def icrc_batch(buf: np.ndarray, offsets=None, lengths=None, stride: int = 0,
-               count: int | None = None, l3_offset: int = 0) -> np.ndarray:
+               count: int | None = None, l3_offset: int = 0, family: str = "v4") -> np.ndarray:
     """Per-packet loop over a packed batch (same addressing as ricrc_batch_*)."""
     mv = memoryview(np.ascontiguousarray(buf).reshape(-1).view(np.uint8))
     if count is None:
@@ -114,7 +131,7 @@ def icrc_batch(buf: np.ndarray, offsets=None, lengths=None, stride: int = 0,
         o = int(offsets[i]) if offsets is not None else i * stride
         n = int(lengths[i]) if lengths is not None else stride - l3_offset
         s = o + l3_offset
-        out[i] = icrc(mv[s: s + n].tobytes())
+        out[i] = icrc(mv[s: s + n].tobytes(), family)
     return out
 
 

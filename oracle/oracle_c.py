@@ -29,13 +29,13 @@ def lib():
             build()
         L = ctypes.CDLL(_SO)
         u8p, u32p, u64p = (ctypes.c_void_p,) * 3
-        for name in ("oracle_icrc_bitwise", "oracle_icrc_bytewise", "oracle_icrc_fast"):
+        for name in ("oracle_icrc_bitwise_ex", "oracle_icrc_bytewise_ex", "oracle_icrc_fast_ex"):
             f = getattr(L, name)
-            f.argtypes = [u8p, ctypes.c_uint32]
+            f.argtypes = [u8p, ctypes.c_uint32, ctypes.c_int]
             f.restype = ctypes.c_uint32
-        L.oracle_icrc_batch.argtypes = [u8p, u64p, u32p, ctypes.c_uint64, ctypes.c_uint64,
-                                        ctypes.c_uint32, u32p, ctypes.c_int, ctypes.c_int]
-        L.oracle_icrc_batch.restype = ctypes.c_int
+        L.oracle_icrc_batch_ex.argtypes = [u8p, u64p, u32p, ctypes.c_uint64, ctypes.c_uint64,
+                                           ctypes.c_uint32, u32p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.oracle_icrc_batch_ex.restype = ctypes.c_int
         L.oracle_synth_batch.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                          ctypes.c_uint32, ctypes.c_uint32, u8p]
         L.oracle_synth_batch.restype = None
@@ -47,15 +47,18 @@ def _ptr(a):
     return None if a is None else a.ctypes.data
 
 
-def icrc_one(pkt: bytes, kind: str = "fast") -> int:
+FAMILY = {"v4": 0, "v6": 1, "auto": 2}
+
+
+def icrc_one(pkt: bytes, kind: str = "fast", family: str = "v4") -> int:
     buf = np.frombuffer(bytes(pkt), dtype=np.uint8)
-    fn = {"bitwise": lib().oracle_icrc_bitwise, "bytewise": lib().oracle_icrc_bytewise,
-          "fast": lib().oracle_icrc_fast}[kind]
-    return int(fn(buf.ctypes.data, len(pkt)))
+    fn = {"bitwise": lib().oracle_icrc_bitwise_ex, "bytewise": lib().oracle_icrc_bytewise_ex,
+          "fast": lib().oracle_icrc_fast_ex}[kind]
+    return int(fn(buf.ctypes.data, len(pkt), FAMILY[family]))
 
 
 def icrc_batch(buf: np.ndarray, offsets=None, lengths=None, stride: int = 0, count=None,
-               l3_offset: int = 0, threads: int = 1, kind: str = "fast") -> np.ndarray:
+               l3_offset: int = 0, threads: int = 1, kind: str = "fast", family: str = "v4") -> np.ndarray:
     buf = np.ascontiguousarray(buf).reshape(-1).view(np.uint8)
     if offsets is not None:
         offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
@@ -65,8 +68,8 @@ def icrc_batch(buf: np.ndarray, offsets=None, lengths=None, stride: int = 0, cou
         count = len(offsets) if offsets is not None else buf.size // stride
     out = np.empty(count, dtype=np.uint32)
     k = {"bitwise": 0, "bytewise": 1, "fast": 2}[kind]
-    lib().oracle_icrc_batch(buf.ctypes.data, _ptr(offsets), _ptr(lengths), stride, count,
-                            l3_offset, out.ctypes.data, threads, k)
+    lib().oracle_icrc_batch_ex(buf.ctypes.data, _ptr(offsets), _ptr(lengths), stride, count,
+                               l3_offset, out.ctypes.data, threads, k, FAMILY[family])
     return out
 
 

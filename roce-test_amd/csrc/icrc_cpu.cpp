@@ -5,8 +5,9 @@
 // It restates calc_icrc() (p4/shuffle/shuffle_egress.p4:463-494) with a
 // slice-by-16 table fold; the 8 x 0xFF prefix (:465) is folded into the
 // starting register kSeed, the masked fields (:467-485) are applied to a
-// 40-byte copy of the header, and everything after it (:489-490) is folded
-// straight from the caller's buffer.
+// copy of the header, and everything after it (:489-490) is folded straight
+// from the caller's buffer.  The *_ex variants add RoCEv2 over IPv6 (masks of
+// IBTA Annex A17 / Linux rxe) and per-packet family detection.
 #include <errno.h>
 #include <string.h>
 
@@ -37,36 +38,80 @@ uint32_t fold_bytes(uint32_t c, const uint8_t *p, size_t n) {
   return c;
 }
 
-// Register over 0xFF x 8 || masked L3[0, n-4); n >= 4.
-uint32_t icrc_register(const uint8_t *l3, uint32_t n) {
-  const size_t m = n - 4, h = m < 40 ? m : 40;
-  uint8_t head[40];
+uint32_t family_of(const uint8_t *l3, uint32_t n, uint32_t flags) {
+  if (flags == ricrc::kFamAuto) return (n > 0 && (l3[0] >> 4) == 6) ? ricrc::kFamV6 : ricrc::kFamV4;
+  return flags == ricrc::kFamV6 ? ricrc::kFamV6 : ricrc::kFamV4;
+}
+
+// Register over 0xFF x 8 || masked L3[0, n-4); n >= 4.  The masked bytes
+// (either family) all lie in the first kMaskSpan bytes: they are applied to a
+// copy of that head, the rest is folded from the caller's buffer.
+uint32_t icrc_register(const uint8_t *l3, uint32_t n, uint32_t fam) {
+  const size_t m = n - 4, h = m < ricrc::kMaskSpan ? m : ricrc::kMaskSpan;
+  uint8_t head[ricrc::kMaskSpan];
   memcpy(head, l3, h);
-  for (int i = 0; i < 40; ++i)
-    if (((ricrc::kMaskBits >> i) & 1u) && (size_t)i < h) head[i] = 0xFF;
+  for (size_t i = 0; i < h; ++i) head[i] |= (uint8_t)ricrc::mask_byte(fam, (uint32_t)i);
   uint32_t c = fold_bytes(ricrc::kSeed, head, h);
   return fold_bytes(c, l3 + h, m - h);
 }
+
+bool flags_ok(uint32_t flags) { return flags <= ricrc::kFamAuto; }
 
 }  // namespace
 
 extern "C" {
 
-uint32_t ricrc_one(const uint8_t *l3, uint32_t n) {
-  if (!l3 || n < 4) return 0;
-  return ~icrc_register(l3, n);
+uint32_t ricrc_one_ex(const uint8_t *l3, uint32_t n, uint32_t flags) {
+  if (!l3 || n < 4 || !flags_ok(flags)) return 0;
+  return ~icrc_register(l3, n, family_of(l3, n, flags));
 }
 
-int ricrc_verify_one(const uint8_t *l3, uint32_t n) {
-  if (!l3 || n < 4) return -EINVAL;
-  return ricrc_one(l3, n) == load_le32(l3 + n - 4) ? 1 : 0;
+uint32_t ricrc_one(const uint8_t *l3, uint32_t n) { return ricrc_one_ex(l3, n, RICRC_F_IPV4); }
+
+int ricrc_verify_one_ex(const uint8_t *l3, uint32_t n, uint32_t flags) {
+  if (!l3 || n < 4 || !flags_ok(flags)) return -EINVAL;
+  return ricrc_one_ex(l3, n, flags) == load_le32(l3 + n - 4) ? 1 : 0;
 }
 
-int ricrc_stamp_one(uint8_t *l3, uint32_t n) {
-  if (!l3 || n < 4) return -EINVAL;
-  const uint32_t v = ricrc_one(l3, n);
+int ricrc_verify_one(const uint8_t *l3, uint32_t n) { return ricrc_verify_one_ex(l3, n, RICRC_F_IPV4); }
+
+int ricrc_stamp_one_ex(uint8_t *l3, uint32_t n, uint32_t flags) {
+  if (!l3 || n < 4 || !flags_ok(flags)) return -EINVAL;
+  const uint32_t v = ricrc_one_ex(l3, n, flags);
   memcpy(l3 + n - 4, &v, 4);  // little-endian host == LE32 on the wire
   return 0;
+}
+
+int ricrc_stamp_one(uint8_t *l3, uint32_t n) { return ricrc_stamp_one_ex(l3, n, RICRC_F_IPV4); }
+
+int ricrc_repair_one(const uint8_t *l3, uint32_t n, uint32_t off, const uint8_t *old_bytes, uint32_t len,
+                     uint32_t old_icrc, uint32_t flags, uint32_t *new_icrc) {
+  if (!l3 || !old_bytes || !new_icrc || n < 4 || !flags_ok(flags)) return -EINVAL;
+  const uint32_t m = n - 4;
+  if (off > m || len > m - off) return -EINVAL;  // only covered bytes [0, n-4) can change
+  const uint32_t fam = family_of(l3, n, flags);
+  if (flags == ricrc::kFamAuto && off == 0 && len > 0 && (old_bytes[0] >> 4) != (l3[0] >> 4))
+    return -EINVAL;  // the rewrite changed the address family: recompute instead
+  // Linearity: the register moves by crc0(delta) advanced over the covered
+  // bytes after the range; masked bytes contribute nothing to either side.
+  uint32_t c = 0;
+  for (uint32_t i = 0; i < len; ++i) {
+    const uint32_t mb = ricrc::mask_byte(fam, off + i);
+    const uint8_t d = (uint8_t)((l3[off + i] ^ old_bytes[i]) & ~mb);
+    c = kT.t[0][(c ^ d) & 0xFF] ^ (c >> 8);
+  }
+  *new_icrc = old_icrc ^ ricrc_shift(c, (uint64_t)(m - off - len));
+  return 0;
+}
+
+int ricrc_classify(const uint8_t *l3, uint32_t n) {
+  if (!l3 || n < 4) return 0;
+  if (ricrc_is_rocev2(l3, n)) return 4;
+  // IPv6: version 6, next header UDP, payload length = n - 40, dport 4791.
+  if (n < 40 + 8 + 12 + 4 || (l3[0] >> 4) != 6 || l3[6] != 17) return 0;
+  if (((uint32_t)l3[4] << 8 | l3[5]) != n - 40) return 0;
+  if (((uint32_t)l3[42] << 8 | l3[43]) != 4791) return 0;
+  return 6;
 }
 
 int ricrc_is_rocev2(const uint8_t *l3, uint32_t n) {

@@ -38,6 +38,29 @@ constexpr uint32_t kMaskW2 = 0xFFFF00FFu;
 constexpr uint32_t kMaskW6 = 0xFFFF0000u;
 constexpr uint32_t kMaskW8 = 0x000000FFu;
 
+// IPv6 (RoCEv2 over IPv6; not in the IPv4-only reference, header.p4:42-53):
+// the invariant fields of IBTA Annex A17 as the Linux rxe driver masks them
+// (rxe_icrc.c) -- traffic class + flow label (byte 0 low nibble, bytes 1-3),
+// hop limit 7, UDP checksum 46-47, BTH byte 4 at 52.  OR-words for 4-aligned
+// words 0, 1, 11, 13.
+constexpr uint32_t kMaskV6W0 = 0xFFFFFF0Fu;
+constexpr uint32_t kMaskV6W1 = 0xFF000000u;
+constexpr uint32_t kMaskV6W11 = 0xFFFF0000u;
+constexpr uint32_t kMaskV6W13 = 0x000000FFu;
+
+// Address families (the flags of the *_ex entry points, include/roce_icrc.h).
+enum Family : uint32_t { kFamV4 = 0, kFamV6 = 1, kFamAuto = 2 };
+constexpr uint32_t kMaskSpan = 56;  // every masked byte of either family lies in L3 [0, 56)
+
+// OR-word w (bytes 4w..4w+3) of a family's masks.
+RICRC_HD constexpr uint32_t mask_word(uint32_t fam, uint32_t w) {
+  return fam == kFamV6 ? (w == 0 ? kMaskV6W0 : w == 1 ? kMaskV6W1 : w == 11 ? kMaskV6W11 : w == 13 ? kMaskV6W13 : 0u)
+                       : (w == 0 ? kMaskW0 : w == 2 ? kMaskW2 : w == 6 ? kMaskW6 : w == 8 ? kMaskW8 : 0u);
+}
+RICRC_HD constexpr uint32_t mask_byte(uint32_t fam, uint32_t i) {
+  return i < kMaskSpan ? (mask_word(fam, i >> 2) >> (8 * (i & 3))) & 0xFFu : 0u;
+}
+
 RICRC_HD constexpr uint32_t gf_mulx(uint32_t a) { return (a >> 1) ^ ((a & 1u) ? kPoly : 0u); }
 
 // a * b mod P, both reflected.

@@ -33,6 +33,7 @@ MAX_LEN = 65535
 
 EXPORTED = (
     "ricrc_one", "ricrc_verify_one", "ricrc_stamp_one", "ricrc_is_rocev2", "ricrc_shift",
+    "ricrc_one_ex", "ricrc_verify_one_ex", "ricrc_stamp_one_ex", "ricrc_classify", "ricrc_repair_one",
     "ricrc_combine", "ricrc_create", "ricrc_create_devices", "ricrc_destroy", "ricrc_device_count", "ricrc_batch_host",
     "ricrc_batch_device", "ricrc_verify_device", "ricrc_host_alloc", "ricrc_host_free",
     "ricrc_host_register", "ricrc_host_unregister", "ricrc_synth_device", "ricrc_stream", "ricrc_strerror",
@@ -67,6 +68,11 @@ def _load():
         "ricrc_verify_one": ([u8p, u32], i32),
         "ricrc_stamp_one": ([u8p, u32], i32),
         "ricrc_is_rocev2": ([u8p, u32], i32),
+        "ricrc_one_ex": ([u8p, u32, u32], u32),
+        "ricrc_verify_one_ex": ([u8p, u32, u32], i32),
+        "ricrc_stamp_one_ex": ([u8p, u32, u32], i32),
+        "ricrc_classify": ([u8p, u32], i32),
+        "ricrc_repair_one": ([u8p, u32, u32, u8p, u32, u32, u32, ctypes.POINTER(u32)], i32),
         "ricrc_shift": ([u32, u64], u32),
         "ricrc_combine": ([u32, u32, u64], u32),
         "ricrc_create": ([ctypes.POINTER(vp), i32], i32),
@@ -111,34 +117,66 @@ def _buf(pkt):
 
 
 # ------------------------------------------------------------------ per packet
-def icrc(pkt) -> int:
+# Address families of the *_ex entry points (include/roce_icrc.h): the
+# reference is IPv4-only, and "v4" (the default) is exactly its masks.
+FAMILIES = {"v4": 0, "v6": 1, "auto": 2}
+
+
+def _fam(family: str) -> int:
+    try:
+        return FAMILIES[family]
+    except KeyError:
+        raise ValueError(f"family must be one of {sorted(FAMILIES)}, not {family!r}") from None
+
+
+def icrc(pkt, family: str = "v4") -> int:
     """ICRC of one L3 RoCEv2 packet (bytes / bytearray / memoryview / uint8 array).
 
-    Wire trailer = little-endian bytes of the result (shuffle_egress.p4:493)."""
+    Wire trailer = little-endian bytes of the result (shuffle_egress.p4:493).
+    ``family``: "v4" (the reference's IPv4 masks), "v6" (RoCEv2 over IPv6) or
+    "auto" (per packet from the IP version nibble)."""
     p, n, _keep = _buf(pkt)
     if n < 4:
         raise ValueError("packet shorter than the 4-byte ICRC trailer")
-    return int(lib.ricrc_one(p, n))
+    return int(lib.ricrc_one_ex(p, n, _fam(family)))
 
 
-def verify(pkt) -> bool:
+def verify(pkt, family: str = "v4") -> bool:
     """True iff the packet's trailer carries its ICRC (what a NIC checks)."""
     p, n, _keep = _buf(pkt)
-    rc = lib.ricrc_verify_one(p, n)
+    rc = lib.ricrc_verify_one_ex(p, n, _fam(family))
     if rc < 0:
-        raise ICRCError(rc, "ricrc_verify_one")
+        raise ICRCError(rc, "ricrc_verify_one_ex")
     return rc == 1
 
 
-def stamp(pkt: bytearray) -> bytearray:
+def stamp(pkt: bytearray, family: str = "v4") -> bytearray:
     """Write the ICRC into the trailer of a mutable packet, in place; returns it."""
     if not isinstance(pkt, (bytearray, memoryview, np.ndarray)):
         raise TypeError("stamp() needs a mutable buffer (bytearray / memoryview / uint8 array)")
     p, n, _keep = _buf(pkt)
-    rc = lib.ricrc_stamp_one(p, n)
+    rc = lib.ricrc_stamp_one_ex(p, n, _fam(family))
     if rc < 0:
-        raise ICRCError(rc, "ricrc_stamp_one")
+        raise ICRCError(rc, "ricrc_stamp_one_ex")
     return pkt
+
+
+def classify(pkt) -> int:
+    """4 (RoCEv2 over IPv4), 6 (RoCEv2 over IPv6) or 0."""
+    p, n, _keep = _buf(pkt)
+    return int(lib.ricrc_classify(p, n))
+
+
+def repair(pkt, off: int, old_bytes, old_icrc: int, family: str = "v4") -> int:
+    """ICRC of ``pkt`` (already rewritten) from its pre-rewrite ICRC, given the
+    old contents of the rewritten range [off, off + len(old_bytes)): O(len)."""
+    p, n, _keep = _buf(pkt)
+    q, m, _keep2 = _buf(bytes(old_bytes))
+    out = ctypes.c_uint32()
+    rc = lib.ricrc_repair_one(p, n, off, q, m, old_icrc & 0xFFFFFFFF, _fam(family), ctypes.byref(out))
+    if rc < 0:
+        raise ICRCError(rc, "ricrc_repair_one")
+    return int(out.value)
 
 
 def is_rocev2(pkt) -> bool:

@@ -78,8 +78,19 @@ def ipv4_checksum(hdr: bytes) -> int:
     return (~s) & 0xFFFF
 
 
-def encode(p) -> bytearray:
-    """Serialise a reference ``Packet`` into an L3 RoCEv2 packet (trailer zeroed)."""
+def ip6_of(mac: int) -> bytes:
+    """IPv6 address of an endpoint for the IPv6 variant: fd00::192.168.1.x
+    (unique-local prefix + the IPv4 address of :func:`ip_of`)."""
+    return bytes([0xFD] + [0] * 11) + ip_of(mac)
+
+
+def encode(p, ipv6: bool = False, tclass: int = 0x02, flow: int = 0, hop: int = 64) -> bytearray:
+    """Serialise a reference ``Packet`` into an L3 RoCEv2 packet (trailer zeroed).
+
+    ``ipv6=True`` builds RoCEv2 over IPv6 instead (not in the IPv4-only
+    reference): a 40-byte IPv6 header (version 6, ``tclass``, ``flow``,
+    payload length, next header 17, ``hop``) in place of IPv4, then the same
+    UDP / BTH / extension / payload bytes."""
     opname = getattr(p, "opcode", "")
     if opname not in OPCODES:
         raise ValueError(f"unknown opcode {opname!r}")
@@ -100,13 +111,18 @@ def encode(p) -> bytearray:
         payload = b"".join(_element(e) for e in data)
     pad = (-len(payload)) % 4
     payload += b"\x00" * pad
-    n = 20 + 8 + 12 + len(ext) + len(payload) + 4
+    iph = 40 if ipv6 else 20
+    n = iph + 8 + 12 + len(ext) + len(payload) + 4
     smac, dmac = _i(getattr(p, "smac", 0)), _i(getattr(p, "dmac", 0))
-    ip = bytearray(struct.pack(">BBHHHBBH4s4s", 0x45, 0x02, n, 0x1234, 0x4000, 64, 17, 0,
-                               ip_of(smac), ip_of(dmac)))
-    ip[10:12] = struct.pack(">H", ipv4_checksum(bytes(ip)))
+    if ipv6:
+        vtf = (6 << 28) | ((tclass & 0xFF) << 20) | (flow & 0xFFFFF)
+        ip = bytearray(struct.pack(">IHBB16s16s", vtf, n - 40, 17, hop & 0xFF, ip6_of(smac), ip6_of(dmac)))
+    else:
+        ip = bytearray(struct.pack(">BBHHHBBH4s4s", 0x45, 0x02, n, 0x1234, 0x4000, 64, 17, 0,
+                                   ip_of(smac), ip_of(dmac)))
+        ip[10:12] = struct.pack(">H", ipv4_checksum(bytes(ip)))
     sport = VIR_UDP_PORT if (smac is None or smac < 0) else (0xC000 | (smac & 0x3FFF))
-    udp = struct.pack(">HHHH", sport, ROCE_PORT, n - 20, 0)
+    udp = struct.pack(">HHHH", sport, ROCE_PORT, n - iph, 0)
     psn = _i(getattr(p, "psn", 0)) & 0xFFFFFF
     ackreq = 0x80 if getattr(p, "ackreq", 0) else 0
     bth = struct.pack(">BBHI", op, 0x40 | (pad << 4), 0xFFFF, qpn_of(_i(getattr(p, "dqpn", 0)))) + \
