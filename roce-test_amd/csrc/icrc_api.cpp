@@ -189,6 +189,26 @@ int launch_batch(Dev &d, const uint8_t *base, const uint64_t *off, const uint32_
       }
       const uint64_t want = (a.n_iters + 15) / 16;
       const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)d.n_cu, want));
+      // Back-to-back 1, 2 or 4 KiB packets: the strided-chain kernel (no LDS
+      // transpose), as long as each wave's span fits a 31-bit buffer offset.
+      if (l3_offset == 0 && stride == fixed_len && (fixed_len == 1024 || fixed_len == 2048 || fixed_len == 4096) &&
+          ((uintptr_t)base % 16 == 0) && getenv("RICRC_NO_SCK") == nullptr) {
+        const uint64_t groups = (count + 7) / 8;
+        const int sgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)d.n_cu, (groups + 15) / 16));
+        const uint64_t waves = 16ull * (uint64_t)sgrid;
+        if ((groups + waves - 1) / waves * 8ull * fixed_len < (1ull << 31)) {
+          SckArgs k{};
+          k.base = base;
+          k.count = count;
+          k.out = out;
+          k.n = fixed_len;
+          k.verify = verify ? 1u : 0u;
+          const uint32_t xi = gf_xinv8n(4);
+          for (int j = 0; j < 32; ++j) k.XB[j] = gf_mul(xi, 1u << j);
+          for (int s = 0; s < 8; ++s) k.QS[s] = gf_xinv8n(16ull * s + 4);
+          return hip_err(launch_sck(k, sgrid, st));
+        }
+      }
       // Back-to-back packets of 32 * 2^j bytes: coalesced + LDS-transposed kernel.
       if (l3_offset == 0 && stride == fixed_len && fixed_len >= 64 && fixed_len <= 4096 &&
           (fixed_len & (fixed_len - 1)) == 0 && ((uintptr_t)base % 16 == 0) && getenv("RICRC_NO_TSK") == nullptr) {

@@ -40,6 +40,18 @@ struct TskArgs {
   uint64_t *stamps;  // diagnostic builds only (tools/microbench); null in the product
 };
 
+// Back-to-back packets of n = 128 * L bytes (L = 8, 16, 32), 16-byte aligned:
+// the strided-chain kernel.  8 lanes per packet, 8 packets per wave group.
+struct SckArgs {
+  const uint8_t *base;
+  uint64_t count;
+  uint32_t *out;
+  uint32_t n;        // == stride
+  uint32_t verify;
+  uint32_t XB[32];   // basis of x^-32 (Horner step between a lane's chains)
+  uint32_t QS[8];    // x^(-32 (4 s + 1)): lane slot s's chain 0 -> packet end
+  uint64_t *stamps;  // diagnostic builds only (tools/microbench); null in the product
+};
 
 // Ragged batches (any alignment, per-packet offsets and/or lengths): the
 // batch is cut into 64-byte pieces, packet by packet -- packet i covers
@@ -80,6 +92,8 @@ struct SynthArgs {
 
 hipError_t launch_stream(const StreamArgs &a, int cpl, int grid, hipStream_t st);
 hipError_t launch_tsk(const TskArgs &a, int grid, hipStream_t st);
+// Returns hipErrorInvalidValue for an n it has no instantiation for.
+hipError_t launch_sck(const SckArgs &a, int grid, hipStream_t st);
 hipError_t launch_ragged(const RaggedArgs &a, int grid, hipStream_t st);
 // ps[0..count] = exclusive prefix of ragged_pieces over the batch (stream
 // ordered; temporary storage from the stream-ordered allocator).

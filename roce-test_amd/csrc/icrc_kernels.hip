@@ -47,11 +47,11 @@ __device__ __forceinline__ uint32_t or_xor(uint32_t a, uint32_t b, uint32_t c) {
 
 // Build the LDS tables: region 0 = {T3 | T2}, region 1 = {T1 | T0}, 256-byte
 // rows of 32 copies x 4 B per half.
-__device__ __forceinline__ void fill_tables(uint32_t *lds) {
+__device__ __forceinline__ void fill_tables(uint32_t *lds, const SliceTables<4> &tab = g_tab) {
   for (int i = threadIdx.x; i < kLdsWords; i += blockDim.x) {
     const int region = i >> 14, e = (i >> 6) & 255, half = (i >> 5) & 1;
     const int t = region ? (half ? 0 : 1) : (half ? 2 : 3);
-    lds[i] = g_tab.t[t][e];
+    lds[i] = tab.t[t][e];
   }
 }
 
@@ -611,6 +611,202 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
 }
 
 // =======================================================================
+// Strided-chain kernel (SCK): the headline path, packets of n = 128 L bytes
+// back to back (L = 8, 16, 32: 1, 2, 4 KiB).
+//
+// A wave takes 8 packets at a time (a "group", 8 n bytes); lane 8 g + s
+// belongs to packet g of the group and owns the 16-byte slot s of every
+// 128-byte line of it.  Load k of a group is one buffer_load_dwordx4 that
+// reads line k of all 8 packets -- whole 128-byte lines, which streams as
+// fast as 1 KiB-contiguous loads on MI355X (tools/microbench/mb_lines.hip)
+// -- and lands, with no LDS transpose, as one fold step for each of the
+// lane's 4 chains: chain j = 4 s + i folds words j, j + 32, j + 64, ... of
+// its packet, one word per line, so a fold step is "XOR the word, advance
+// the register 128 bytes" with the slice-by-4 tables T_124..T_127 in LDS
+// (same conflict-free layout as above).  Four independent chains per lane
+// and no cross-lane traffic while folding.
+//
+// Algebra (tests/test_kernel_algebra.py::test_strided_chain_decomposition):
+// with the trailer word zeroed, register = XOR_j r_j x^-32(j+1).  A lane
+// combines its chains by Horner in x^-32 (uniform basis, SGPRs), multiplies
+// once by x^-32(4 s + 1) (lane basis) and the 8 lanes of a packet XOR-reduce
+// with three DPP steps.  That finish (4 GF(2) multiplies per lane per group,
+// 4 per 8 packets instead of the transposed kernel's 2 per packet) runs in 8
+// VALU slices inside the first fold steps of the next group.  Loads run D
+// lines ahead through a rotating register ring; past the wave's span the
+// buffer range check returns zeros, so no load is ever exec-masked.
+// Results: lane l keeps packet 8 (l & 7) + (l >> 3) of each block of 8
+// groups and the block leaves in one coalesced 64-dword store.
+//
+// ABL (timing-only ablations for tools/microbench; the product uses 0):
+// 1 no table fold, 2 no finish, 8 no global loads, 16 no stores.
+// =======================================================================
+constexpr SliceTables<4> make_stride_tables(uint64_t gap) {
+  SliceTables<4> s = make_tables<4>();
+  const uint32_t g = gf_x8n(gap);
+  for (int k = 0; k < 4; ++k)
+    for (int b = 0; b < 256; ++b) s.t[k][b] = gf_mul(s.t[k][b], g);
+  return s;
+}
+__device__ constexpr SliceTables<4> g_tab128 = make_stride_tables(124);  // word + 124 bytes = one line
+
+template <int L, int ABL>
+__global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
+  __shared__ uint32_t lds[kLdsWords];
+  fill_tables(lds, g_tab128);
+  __syncthreads();
+
+  constexpr int D = 8;  // lines in flight per wave
+  static_assert(L % D == 0, "ring indices must repeat every group");
+  constexpr uint32_t N = 128u * L, GB = 8u * N;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const LaneTab lt{(lane & 31) << 2, ((lane & 31) << 2) | 0x10000u};
+  const uint32_t s = lane & 7;
+  const uint32_t mw0 = s == 0 ? kMaskW0 : (s == 2 ? kMaskW8 : 0u);  // bytes 1 / 32
+  const uint32_t xw0 = s == 0 ? kSeed : 0u;
+  const uint32_t mw2 = s == 0 ? kMaskW2 : (s == 1 ? kMaskW6 : 0u);  // bytes 8, 10-11 / 26-27
+  const uint32_t keep3 = s == 7 ? 0u : 0xFFFFFFFFu;                  // the trailer word
+  uint32_t qs = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) qs = s == (uint32_t)k ? a.QS[k] : qs;
+  uint32_t Q[32];
+  make_basis(qs, Q);
+
+  const uint64_t wave = (uint64_t)blockIdx.x * kWaves + wid;
+  const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
+  const uint64_t G = (a.count + 7) >> 3;
+  const uint64_t per = (G + nwaves - 1) / nwaves;
+  const uint64_t g0 = wave * per < G ? wave * per : G;
+  const uint64_t g1 = g0 + per < G ? g0 + per : G;
+  if (g0 >= g1) return;  // no barrier below
+  const uint32_t ng = (uint32_t)(g1 - g0);
+  const uint64_t b0 = g0 * GB, b1 = g1 * GB < a.count * N ? g1 * GB : a.count * N;
+  const __amdgpu_buffer_rsrc_t rs = make_rsrc(a.base + b0, (uint32_t)(b1 - b0));
+  const uint32_t vo = (lane >> 3) * N + 16u * s;
+
+  // Line k (0 <= k < L + D) of local group q; k >= L is the next group's.
+  auto load = [&](uint32_t q, int k) -> u32x4 {
+    if (ABL & 8) return u32x4{q * 977u + (uint32_t)k, lane, q, 5u};
+    return __builtin_bit_cast(
+        u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 128u * (uint32_t)(k % L), (q + (uint32_t)(k / L)) * GB, 2));
+  };
+
+  struct Fin {
+    uint32_t r[4];    // chain registers
+    uint32_t tr;      // trailer word (lane s = 7), for verify
+    uint32_t acc[4];  // multiply accumulators
+    uint32_t u;       // Horner value
+  };
+  auto mul_half = [&](Fin &f, const uint32_t(&B)[32], int h) {
+#pragma unroll
+    for (int j = 16 * h; j < 16 * h + 16; ++j)
+      f.acc[j & 3] = and_xor((uint32_t)(((int32_t)(f.u << (31 - j))) >> 31), B[j], f.acc[j & 3]);
+  };
+  auto take = [](Fin &f) -> uint32_t {
+    const uint32_t v = xor3(f.acc[0], f.acc[1], f.acc[2] ^ f.acc[3]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) f.acc[k] = 0u;
+    return v;
+  };
+  // Slice sl (0..7): u = ((r3 X ^ r2) X ^ r1) X ^ r0, then u * Q.
+  auto fin_slice = [&](Fin &f, int sl) {
+    if (ABL & 2) return;
+    if (sl == 0) {
+      f.u = f.r[3];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) f.acc[k] = 0u;
+    }
+    if (sl < 6) mul_half(f, a.XB, sl & 1);
+    else mul_half(f, Q, sl & 1);
+    if (sl == 1) f.u = take(f) ^ f.r[2];
+    if (sl == 3) f.u = take(f) ^ f.r[1];
+    if (sl == 5) f.u = take(f) ^ f.r[0];
+    if (sl == 7) f.u = take(f);
+  };
+  uint32_t res = 0, sink = 0;
+  const uint32_t vmask = __builtin_amdgcn_readfirstlane(a.verify ? 0xFFFFFFFFu : 0u);
+  auto fin_store = [&](Fin &f, uint32_t qf, bool live) {  // live: wave-uniform
+    const uint32_t crc = (ABL & 2) ? (f.r[0] ^ f.r[1] ^ f.r[2] ^ f.r[3]) : f.u;
+    const uint32_t v = group_xor(crc, 3);
+    const uint32_t chk = group_xor(f.tr, 3) == ~v ? 1u : 0u;
+    const uint32_t val = __builtin_amdgcn_bitop3_b32(vmask, chk, ~v, 0xCA);  // vmask ? chk : ~v, bitwise
+    if (ABL & 16) {
+      sink ^= val;
+      return;
+    }
+    res = (s == (qf & 7u)) ? val : res;
+    if (live && ((qf & 7u) == 7u || qf + 1 == ng)) {
+      const uint64_t pb = (g0 + (qf & ~7u)) * 8u;
+      const uint32_t nout = (uint32_t)(a.count - pb < 64u ? a.count - pb : 64u);
+      const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out + pb, 4u * nout);
+      __builtin_amdgcn_raw_buffer_store_b32(res, ro, s <= (qf & 7u) ? 4u * (8u * s + (lane >> 3)) : 0x7FFFFFF0u, 0,
+                                            0);
+    }
+  };
+
+  u32x4 ring[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) {  // in order: the loop's vmcnt waits assume it
+    __builtin_amdgcn_sched_barrier(0);
+    ring[k] = load(0, k);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  Fin pf{};
+  for (uint32_t q = 0; q < ng; ++q) {
+    u32x4 w = ring[0];
+    ring[0] = load(q, D);
+    w[0] = or_xor(w[0], mw0, xw0);
+    w[2] |= mw2;
+    uint32_t x[4] = {w[0], w[1], w[2], w[3]};  // chain register (0) ^ line-0 word
+    uint32_t tr = 0;
+#pragma unroll
+    for (int k = 0; k < L; ++k) {
+      // Fence each step: the scheduler would otherwise hoist the whole
+      // group's ring refills to the top and drain vmcnt to zero there.
+      __builtin_amdgcn_sched_barrier(0);
+      u32x4 wn = {0u, 0u, 0u, 0u};
+      if (k + 1 < L) {
+        wn = ring[(k + 1) % D];
+        ring[(k + 1) % D] = load(q, k + 1 + D);
+        if (k + 1 == L - 1) {
+          tr = keep3 ? 0u : wn[3];
+          wn[3] &= keep3;
+        }
+      }
+      uint32_t t[4][4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (ABL & 1) {
+          t[i][0] = __builtin_amdgcn_perm(x[i], lt.lo0, 0x0C0C0400u);
+          t[i][1] = x[i] >> 7;
+          t[i][2] = x[i] * 3u;
+          t[i][3] = 0u;
+        } else {
+          t[i][0] = lds_at(lds, __builtin_amdgcn_perm(x[i], lt.lo0, 0x0C0C0400u));
+          t[i][1] = lds_at(lds, __builtin_amdgcn_perm(x[i], lt.lo0, 0x0C0C0500u) + 128);
+          t[i][2] = lds_at(lds, __builtin_amdgcn_perm(x[i], lt.lo1, 0x0C020600u));
+          t[i][3] = lds_at(lds, __builtin_amdgcn_perm(x[i], lt.lo1, 0x0C020700u) + 128);
+        }
+      }
+      // The previous group's finish, in the shadow of the reads (for q = 0 it
+      // runs on zeros and stores nothing).
+      if (k < 8) fin_slice(pf, k);
+      if (k == 8) fin_store(pf, q - 1, q > 0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) x[i] = xor3(t[i][0], t[i][1], xor3(t[i][2], t[i][3], wn[i]));
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pf.r[i] = x[i];
+    pf.tr = tr;
+  }
+#pragma unroll
+  for (int sl = 0; sl < 8; ++sl) fin_slice(pf, sl);
+  fin_store(pf, ng - 1, true);
+  if (ABL & 16) a.out[wave * 64 + lane] = sink;
+}
+
+// =======================================================================
 // Byte-level helpers for packets that do not start or end on a word.
 // =======================================================================
 __device__ __forceinline__ uint32_t byte_span_mask(int lo, int hi) {  // bytes [lo,hi) of a word
@@ -1117,6 +1313,14 @@ hipError_t launch_stream(const StreamArgs &a, int cpl, int grid, hipStream_t st)
 hipError_t launch_tsk(const TskArgs &a, int grid, hipStream_t st) {
   if (a.log2C == 7) hipLaunchKernelGGL((icrc_tsk_kernel<true, 0>), dim3(grid), dim3(kBlock), 0, st, a);
   else hipLaunchKernelGGL((icrc_tsk_kernel<false, 0>), dim3(grid), dim3(kBlock), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_sck(const SckArgs &a, int grid, hipStream_t st) {
+  if (a.n == 4096) hipLaunchKernelGGL((icrc_sck_kernel<32, 0>), dim3(grid), dim3(kBlock), 0, st, a);
+  else if (a.n == 2048) hipLaunchKernelGGL((icrc_sck_kernel<16, 0>), dim3(grid), dim3(kBlock), 0, st, a);
+  else if (a.n == 1024) hipLaunchKernelGGL((icrc_sck_kernel<8, 0>), dim3(grid), dim3(kBlock), 0, st, a);
+  else return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

@@ -135,3 +135,35 @@ def test_ragged_kernel_decomposition():
                 carry = o.gf_mul(seg, x8n(4096))
     for i, (m, _, _) in enumerate(pkts):
         assert got[i] == zlib.crc32(o.PREFIX + bytes(m)), (i, len(m))
+
+
+def test_strided_chain_decomposition():
+    """The strided-chain kernel's algebra (icrc_kernels.hip icrc_sck_kernel):
+    8 lanes per packet, lane s loads the 16-byte slot s of every 128-byte line,
+    and each of its 4 words is its own chain j = 4 s + i over words
+    j, j + 32, j + 64, ... (one fold step = XOR the word, advance 128 bytes:
+    tables T_124..T_127).  With the trailer word zeroed,
+    register = XOR_j r_j * x^(-32 (j + 1)); the lane combines its four chains
+    by Horner in x^-32 and multiplies once by x^(-32 (4 s + 1))."""
+    rng = random.Random(7)
+    X = _xinv8n_fast(4)
+    for n in (128, 256, 1024, 4096):
+        pkt = bytes(rng.randrange(256) for _ in range(n))
+        body = bytearray(masked(pkt)) + bytes(4)  # trailer word zeroed
+        words = [int.from_bytes(body[4 * t: 4 * t + 4], "little") for t in range(n // 4)]
+        words[0] ^= SEED_REG
+        chains = [0] * 32
+        for t, w in enumerate(words):
+            chains[t % 32] = o.crc_shift(chains[t % 32] ^ w, 128)
+        flat = 0
+        for j in range(32):
+            flat ^= o.gf_mul(chains[j], _xinv8n_fast(4 * (j + 1)))
+        horner = 0
+        for s in range(8):
+            u = chains[4 * s + 3]
+            for i in (2, 1, 0):
+                u = o.gf_mul(u, X) ^ chains[4 * s + i]
+            horner ^= o.gf_mul(u, _xinv8n_fast(16 * s + 4))
+        want = o.icrc(pkt) ^ 0xFFFFFFFF
+        assert flat == want
+        assert horner == want
