@@ -49,18 +49,36 @@ def parse():
     return ap.parse_args()
 
 
+def kernel_source_hash():
+    """sha256 of the kernel source: PMC traffic measured on other code is stale."""
+    import hashlib
+
+    with open(os.path.join(ROOT, "roce-test_amd", "csrc", "icrc_kernels.hip"), "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
 def load_traffic(size, count):
     """HBM bytes per launch measured by a separate rocprofv3 --pmc pass
-    (profiles/*pmc*.json, produced by tools/pmc_traffic.py), or None."""
+    (profiles/pmc_traffic.json, produced by tools/pmc_traffic.py) on this very
+    kernel source, or None."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")  # from tools/pmc_traffic.py
     try:
         with open(p) as f:
             d = json.load(f)
-        if d.get("size") == size and d.get("count") == count:
+        if d.get("size") == size and d.get("count") == count and d.get("kernel_src") == kernel_source_hash():
             return d.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
     return None
+
+
+def kernel_label(size):
+    """The kernel libroceicrc's dispatch picks for back-to-back packets of `size` bytes."""
+    if size in (1024, 2048, 4096):
+        return "strided-chain ICRC kernel (icrc_sck_kernel)"
+    if 64 <= size <= 4096 and size & (size - 1) == 0:
+        return "transposed streaming ICRC kernel (icrc_tsk_kernel)"
+    return "streaming ICRC kernel"
 
 
 def cpu_baseline(sample_host, got_sample, size, budget_s):
@@ -200,7 +218,7 @@ def main():
         "dtype": "u8",
         "data": "synthetic (device-generated RoCEv2 SEND_ONLY packets, seeded; reference P4 header template)",
         "config": {"workload": f"{count} x {size} B RoCEv2 packets per GPU, device-resident, "
-                               f"streaming ICRC kernel" + (" + RCCL all-gather of ICRCs" + (" (overlapped)" if args.overlap_gather else "")
+                               + kernel_label(size) + (" + RCCL all-gather of ICRCs" + (" (overlapped)" if args.overlap_gather else "")
                                                            if do_gather else ""),
                    "packets_per_gpu": count, "packet_bytes": size,
                    "parallelism": f"dp{world}" + (" (all-gather u32 results)" if do_gather else "")},

@@ -194,7 +194,8 @@ int launch_batch(Dev &d, const uint8_t *base, const uint64_t *off, const uint32_
       if (l3_offset == 0 && stride == fixed_len && (fixed_len == 1024 || fixed_len == 2048 || fixed_len == 4096) &&
           ((uintptr_t)base % 16 == 0) && getenv("RICRC_NO_SCK") == nullptr) {
         const uint64_t groups = (count + 7) / 8;
-        const int sgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)d.n_cu, (groups + 15) / 16));
+        int sgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)d.n_cu, (groups + 15) / 16));
+        if (const char *e = getenv("RICRC_SCK_GRID")) sgrid = std::max(1, std::min(sgrid, atoi(e)));  // tests
         const uint64_t waves = 16ull * (uint64_t)sgrid;
         if ((groups + waves - 1) / waves * 8ull * fixed_len < (1ull << 31)) {
           SckArgs k{};

@@ -47,12 +47,22 @@ __device__ __forceinline__ uint32_t or_xor(uint32_t a, uint32_t b, uint32_t c) {
 
 // Build the LDS tables: region 0 = {T3 | T2}, region 1 = {T1 | T0}, 256-byte
 // rows of 32 copies x 4 B per half.
+// One table entry per thread (4 x 256 = 1024 = kBlock): a single global load,
+// then the entry's 32 copies (128 contiguous bytes) in 8 ds_write_b128.
+__device__ __forceinline__ uint32_t table_entry(const SliceTables<4> &tab) {
+  return tab.t[threadIdx.x >> 8][threadIdx.x & 255];
+}
+__device__ __forceinline__ void table_store(uint32_t *lds, uint32_t v) {
+  const uint32_t t = threadIdx.x >> 8, e = threadIdx.x & 255;
+  const uint32_t region = t <= 1 ? 1u : 0u, half = (t == 0 || t == 2) ? 1u : 0u;  // T3 T2 | T1 T0
+  typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+  v4 *dst = reinterpret_cast<v4 *>(lds + ((region << 14) | (e << 6) | (half << 5)));
+#pragma unroll
+  for (int k = 0; k < 8; ++k) dst[k] = v4{v, v, v, v};
+}
 __device__ __forceinline__ void fill_tables(uint32_t *lds, const SliceTables<4> &tab = g_tab) {
-  for (int i = threadIdx.x; i < kLdsWords; i += blockDim.x) {
-    const int region = i >> 14, e = (i >> 6) & 255, half = (i >> 5) & 1;
-    const int t = region ? (half ? 0 : 1) : (half ? 2 : 3);
-    lds[i] = tab.t[t][e];
-  }
+  static_assert(kBlock == 1024, "one table entry per thread");
+  table_store(lds, table_entry(tab));
 }
 
 struct LaneTab {
@@ -652,17 +662,50 @@ __device__ constexpr SliceTables<4> g_tab128 = make_stride_tables(124);  // word
 
 template <int L, int ABL>
 __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
-  __shared__ uint32_t lds[kLdsWords];
-  fill_tables(lds, g_tab128);
-  __syncthreads();
+  // 128 KiB of tables + 2 KiB of result slots per wave (512 packets).
+  constexpr uint32_t kSlots = 512;
+  __shared__ uint32_t lds[kLdsWords + kWaves * kSlots];
 
   constexpr int D = 8;  // lines in flight per wave
   static_assert(L % D == 0, "ring indices must repeat every group");
   constexpr uint32_t N = 128u * L, GB = 8u * N;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const LaneTab lt{(lane & 31) << 2, ((lane & 31) << 2) | 0x10000u};
   const uint32_t s = lane & 7;
+
+  const uint64_t wave = (uint64_t)blockIdx.x * kWaves + wid;
+  const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
+  const uint64_t G = (a.count + 7) >> 3;
+  const uint64_t per = (G + nwaves - 1) / nwaves;
+  const uint64_t g0 = wave * per < G ? wave * per : G;
+  const uint64_t g1 = g0 + per < G ? g0 + per : G;
+  const uint32_t ng = (uint32_t)(g1 - g0);
+  const uint64_t b0 = g0 * GB, b1 = g1 * GB < a.count * N ? g1 * GB : a.count * N;
+  const __amdgpu_buffer_rsrc_t rs = make_rsrc(a.base + (ng ? b0 : 0), ng ? (uint32_t)(b1 - b0) : 0u);
+  const uint32_t vo = (lane >> 3) * N + 16u * s;
+
+  // Line k (0 <= k < L + D) of local group q; k >= L is the next group's.
+  auto load = [&](uint32_t q, int k) -> u32x4 {
+    if (ABL & 8) return u32x4{q * 977u + (uint32_t)k, lane, q, 5u};
+    return __builtin_bit_cast(
+        u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 128u * (uint32_t)(k % L), (q + (uint32_t)(k / L)) * GB, 2));
+  };
+  // The first D lines are in flight while the workgroup builds its tables
+  // (the table load is issued first, so waiting for it leaves them in flight).
+  const uint32_t tab_v = table_entry(g_tab128);
+  u32x4 ring[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) {  // in order: the loop's vmcnt waits assume it
+    __builtin_amdgcn_sched_barrier(0);
+    ring[k] = load(0, k);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  table_store(lds, tab_v);
+  __syncthreads();
+  if (ng == 0) return;  // no barrier below
+
+  uint32_t *slots = lds + kLdsWords + wid * kSlots;
+  const LaneTab lt{(lane & 31) << 2, ((lane & 31) << 2) | 0x10000u};
   const uint32_t mw0 = s == 0 ? kMaskW0 : (s == 2 ? kMaskW8 : 0u);  // bytes 1 / 32
   const uint32_t xw0 = s == 0 ? kSeed : 0u;
   const uint32_t mw2 = s == 0 ? kMaskW2 : (s == 1 ? kMaskW6 : 0u);  // bytes 8, 10-11 / 26-27
@@ -672,25 +715,6 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
   for (int k = 0; k < 8; ++k) qs = s == (uint32_t)k ? a.QS[k] : qs;
   uint32_t Q[32];
   make_basis(qs, Q);
-
-  const uint64_t wave = (uint64_t)blockIdx.x * kWaves + wid;
-  const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
-  const uint64_t G = (a.count + 7) >> 3;
-  const uint64_t per = (G + nwaves - 1) / nwaves;
-  const uint64_t g0 = wave * per < G ? wave * per : G;
-  const uint64_t g1 = g0 + per < G ? g0 + per : G;
-  if (g0 >= g1) return;  // no barrier below
-  const uint32_t ng = (uint32_t)(g1 - g0);
-  const uint64_t b0 = g0 * GB, b1 = g1 * GB < a.count * N ? g1 * GB : a.count * N;
-  const __amdgpu_buffer_rsrc_t rs = make_rsrc(a.base + b0, (uint32_t)(b1 - b0));
-  const uint32_t vo = (lane >> 3) * N + 16u * s;
-
-  // Line k (0 <= k < L + D) of local group q; k >= L is the next group's.
-  auto load = [&](uint32_t q, int k) -> u32x4 {
-    if (ABL & 8) return u32x4{q * 977u + (uint32_t)k, lane, q, 5u};
-    return __builtin_bit_cast(
-        u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 128u * (uint32_t)(k % L), (q + (uint32_t)(k / L)) * GB, 2));
-  };
 
   struct Fin {
     uint32_t r[4];    // chain registers
@@ -724,9 +748,29 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
     if (sl == 5) f.u = take(f) ^ f.r[0];
     if (sl == 7) f.u = take(f);
   };
-  uint32_t res = 0, sink = 0;
   const uint32_t vmask = __builtin_amdgcn_readfirstlane(a.verify ? 0xFFFFFFFFu : 0u);
-  auto fin_store = [&](Fin &f, uint32_t qf, bool live) {  // live: wave-uniform
+  uint32_t sink = 0;
+  // Results go to the wave's LDS slots (all 8 lanes of a packet write the
+  // same value to the same slot: no exec mask) and leave for HBM in
+  // coalesced stores once per 512 packets, so the streaming loop holds no
+  // global store: a store shares vmcnt with the ring and every load queued
+  // behind it would wait for its write acknowledgement.
+  auto flush = [&](uint32_t q_end) {  // the round of groups ending at q_end (at most 64)
+    if (ABL & 16) return;
+    const uint32_t q_lo = (q_end - 1) & ~63u;
+    const uint64_t pb = (g0 + q_lo) * 8u;
+    const uint32_t valid = (q_end - q_lo) * 8u;  // slots written this round
+    const uint32_t nout = (uint32_t)(a.count - pb < valid ? a.count - pb : valid);
+    const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out + pb, 4u * nout);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the slot writes have landed
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const u32x4 v = *reinterpret_cast<const u32x4 *>(slots + 256 * h + 4 * lane);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v), ro,
+                                             1024u * h + 16u * lane, 0, 0);
+    }
+  };
+  auto fin_store = [&](Fin &f, uint32_t qf) {
     const uint32_t crc = (ABL & 2) ? (f.r[0] ^ f.r[1] ^ f.r[2] ^ f.r[3]) : f.u;
     const uint32_t v = group_xor(crc, 3);
     const uint32_t chk = group_xor(f.tr, 3) == ~v ? 1u : 0u;
@@ -735,23 +779,14 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
       sink ^= val;
       return;
     }
-    res = (s == (qf & 7u)) ? val : res;
-    if (live && ((qf & 7u) == 7u || qf + 1 == ng)) {
-      const uint64_t pb = (g0 + (qf & ~7u)) * 8u;
-      const uint32_t nout = (uint32_t)(a.count - pb < 64u ? a.count - pb : 64u);
-      const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out + pb, 4u * nout);
-      __builtin_amdgcn_raw_buffer_store_b32(res, ro, s <= (qf & 7u) ? 4u * (8u * s + (lane >> 3)) : 0x7FFFFFF0u, 0,
-                                            0);
-    }
+    slots[((qf & 63u) << 3) | (lane >> 3)] = val;
   };
 
-  u32x4 ring[D];
-#pragma unroll
-  for (int k = 0; k < D; ++k) {  // in order: the loop's vmcnt waits assume it
-    __builtin_amdgcn_sched_barrier(0);
-    ring[k] = load(0, k);
-  }
-  __builtin_amdgcn_sched_barrier(0);
+  // Finish slices of the previous group ride in steps 0..7 (0..6 for L = 8,
+  // two in step 0), its result is written in the step after.
+  constexpr int kStoreStep = L >= 16 ? 8 : L - 1;
+  auto slice_step = [](int sl) constexpr { return L >= 16 ? sl : sl * (L - 1) / 8; };
+  static_assert(L >= 8, "finish needs 8 fold steps");
   Fin pf{};
   for (uint32_t q = 0; q < ng; ++q) {
     u32x4 w = ring[0];
@@ -790,9 +825,14 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
         }
       }
       // The previous group's finish, in the shadow of the reads (for q = 0 it
-      // runs on zeros and stores nothing).
-      if (k < 8) fin_slice(pf, k);
-      if (k == 8) fin_store(pf, q - 1, q > 0);
+      // runs on zeros; its slot write is overwritten before any flush).
+#pragma unroll
+      for (int sl = 0; sl < 8; ++sl)
+        if (slice_step(sl) == k) fin_slice(pf, sl);
+      if (k == kStoreStep) {
+        fin_store(pf, q - 1);
+        if (q > 0 && ((q - 1) & 63u) == 63u) flush(q);  // wave-uniform: a full round of slots
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i) x[i] = xor3(t[i][0], t[i][1], xor3(t[i][2], t[i][3], wn[i]));
     }
@@ -800,9 +840,11 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
     for (int i = 0; i < 4; ++i) pf.r[i] = x[i];
     pf.tr = tr;
   }
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int sl = 0; sl < 8; ++sl) fin_slice(pf, sl);
-  fin_store(pf, ng - 1, true);
+  fin_store(pf, ng - 1);
+  flush(ng);
   if (ABL & 16) a.out[wave * 64 + lane] = sink;
 }
 

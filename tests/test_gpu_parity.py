@@ -311,3 +311,25 @@ def test_headline_full_size_bit_exact(ctx):
     d.copy_(torch.from_numpy(host))
     ctx.batch_device(d, count, out, stride=n, stream=_stream(), verify=True)
     assert int(_host_u32(out).sum()) == count
+
+
+@pytest.mark.parametrize("n", [1024, 2048, 4096])
+@pytest.mark.parametrize("count,grid", [(1, None), (7, None), (9, None), (8 * 16 * 64 + 3, 1),
+                                         (8 * 16 * 130 + 5, 1), (8 * 16 * 200, 2), (70001, None)])
+def test_strided_chain_kernel(ctx, monkeypatch, n, count, grid):
+    """icrc_sck_kernel (back-to-back 1/2/4 KiB packets): partial 8-packet
+    groups, waves with no groups, and -- with the grid capped -- waves that
+    flush their 512 LDS result slots several times; compared with the oracle
+    and with the transposed kernel on the same bytes."""
+    if grid is not None:
+        monkeypatch.setenv("RICRC_SCK_GRID", str(grid))
+    host = oracle_c.synth_batch(SEED ^ count, 3, count, n)
+    want = oracle_c.icrc_batch(host, stride=n, threads=8)
+    d = _dev(host)
+    out = _out(count)
+    ctx.batch_device(d, count, out, stride=n, stream=_stream())
+    np.testing.assert_array_equal(_host_u32(out), want)
+    monkeypatch.setenv("RICRC_NO_SCK", "1")
+    out2 = _out(count)
+    ctx.batch_device(d, count, out2, stride=n, stream=_stream())
+    np.testing.assert_array_equal(_host_u32(out2), want)

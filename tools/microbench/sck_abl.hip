@@ -1,0 +1,43 @@
+// Ablation timing of the strided-chain kernel (timing only: outputs are
+// meaningless for ABL != 0).  Build:
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 sck_abl.hip -o sck_abl
+#include "../../roce-test_amd/csrc/icrc_kernels.hip"
+#include <stdio.h>
+#include <stdlib.h>
+using namespace ricrc;
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s\n", hipGetErrorString(e)); exit(1); } } while (0)
+template <int L, int ABL> float run(SckArgs a, int grid, int reps) {
+  hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  for (int w = 0; w < 3; ++w) hipLaunchKernelGGL((icrc_sck_kernel<L, ABL>), dim3(grid), dim3(kBlock), 0, 0, a);
+  CK(hipDeviceSynchronize()); CK(hipEventRecord(e0));
+  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL((icrc_sck_kernel<L, ABL>), dim3(grid), dim3(kBlock), 0, 0, a);
+  CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); float ms; CK(hipEventElapsedTime(&ms, e0, e1)); return ms / reps;
+}
+int main(int argc, char **argv) {
+  const uint64_t n = 4096, count = 1 << 20;
+  uint8_t *buf; uint32_t *out; CK(hipMalloc(&buf, n * count)); CK(hipMalloc(&out, 4 * count + (1 << 22)));
+  {  // random bytes (DVFS: constant data runs at a higher clock than real traffic)
+    uint8_t *h = (uint8_t *)malloc(n * count);
+    uint64_t x = 0x9E3779B97F4A7C15ull;
+    for (uint64_t i = 0; i < n * count / 8; ++i) { x ^= x << 13; x ^= x >> 7; x ^= x << 17; ((uint64_t *)h)[i] = x; }
+    CK(hipMemcpy(buf, h, n * count, hipMemcpyHostToDevice));
+    free(h);
+  }
+  hipDeviceProp_t p; CK(hipGetDeviceProperties(&p, 0));
+  SckArgs a{}; a.base = buf; a.count = count; a.out = out; a.n = n;
+  for (int j = 0; j < 32; ++j) a.XB[j] = 0x85EBCA6Bu * (j + 3);
+  for (int s = 0; s < 8; ++s) a.QS[s] = 0x9E3779B9u * (s + 1);
+  const int grid = p.multiProcessorCount;
+  auto rep = [&](const char *nm, float ms) { printf("%-36s %7.3f ms  %7.1f GB/s\n", nm, ms, n * count / (ms * 1e-3) / 1e9); };
+  for (int r = 0; r < 2; ++r) {
+    rep("full", run<32, 0>(a, grid, 20));
+    rep("no fold (VALU stand-in)", run<32, 1>(a, grid, 20));
+    rep("no finish", run<32, 2>(a, grid, 20));
+    rep("no loads", run<32, 8>(a, grid, 20));
+    rep("no stores", run<32, 16>(a, grid, 20));
+    rep("no fold, no finish (memory path)", run<32, 1 | 2>(a, grid, 20));
+    rep("no loads, no finish (fold only)", run<32, 8 | 2>(a, grid, 20));
+    rep("no loads, no fold (finish only)", run<32, 8 | 1>(a, grid, 20));
+  }
+  return 0;
+}
