@@ -650,6 +650,8 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
 //
 // ABL (timing-only ablations for tools/microbench; the product uses 0):
 // 1 no table fold, 2 no finish, 8 no global loads, 16 no stores.
+// D: lines in flight per wave; QLDS: lane bases read from LDS instead of 32
+// VGPRs (frees registers for a deeper ring).
 // =======================================================================
 constexpr SliceTables<4> make_stride_tables(uint64_t gap) {
   SliceTables<4> s = make_tables<4>();
@@ -660,13 +662,14 @@ constexpr SliceTables<4> make_stride_tables(uint64_t gap) {
 }
 __device__ constexpr SliceTables<4> g_tab128 = make_stride_tables(124);  // word + 124 bytes = one line
 
-template <int L, int ABL>
+template <int L, int ABL, int D = 8, bool QLDS = false>
 __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
-  // 128 KiB of tables + 2 KiB of result slots per wave (512 packets).
-  constexpr uint32_t kSlots = 512;
-  __shared__ uint32_t lds[kLdsWords + kWaves * kSlots];
+  // 128 KiB of tables + result slots per wave (+ the 8 lane bases, QLDS).
+  constexpr uint32_t kSlots = QLDS ? 256 : 512;
+  constexpr uint32_t kQStride = 36;  // words per lane-slot basis (padded: conflict-free ds_read_b128)
+  __shared__ uint32_t lds[kLdsWords + kWaves * kSlots + (QLDS ? 8 * kQStride : 0)];
 
-  constexpr int D = 8;  // lines in flight per wave
+  // D: lines in flight per wave
   static_assert(L % D == 0, "ring indices must repeat every group");
   constexpr uint32_t N = 128u * L, GB = 8u * N;
   const uint32_t lane = threadIdx.x & 63;
@@ -701,20 +704,32 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
   }
   __builtin_amdgcn_sched_barrier(0);
   table_store(lds, tab_v);
+  if (QLDS && threadIdx.x < 256) {  // basis word j of lane slot s: x^(-32 (4 s + 1)) * x^(31 - j)
+    const uint32_t bs = threadIdx.x >> 5, j = threadIdx.x & 31;
+    uint32_t v = a.QS[0];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) v = bs == (uint32_t)k ? a.QS[k] : v;
+    for (uint32_t t = j; t < 31; ++t) v = gf_mulx(v);
+    lds[kLdsWords + kWaves * kSlots + bs * kQStride + j] = v;
+  }
   __syncthreads();
   if (ng == 0) return;  // no barrier below
 
   uint32_t *slots = lds + kLdsWords + wid * kSlots;
+  constexpr uint32_t kRoundMask = kSlots / 8 - 1;  // groups per round of slots - 1
   const LaneTab lt{(lane & 31) << 2, ((lane & 31) << 2) | 0x10000u};
   const uint32_t mw0 = s == 0 ? kMaskW0 : (s == 2 ? kMaskW8 : 0u);  // bytes 1 / 32
   const uint32_t xw0 = s == 0 ? kSeed : 0u;
   const uint32_t mw2 = s == 0 ? kMaskW2 : (s == 1 ? kMaskW6 : 0u);  // bytes 8, 10-11 / 26-27
   const uint32_t keep3 = s == 7 ? 0u : 0xFFFFFFFFu;                  // the trailer word
-  uint32_t qs = 0;
+  uint32_t Q[32];  // lane basis in registers (!QLDS)
+  const uint32_t *qlds = lds + kLdsWords + kWaves * kSlots + s * kQStride;
+  if (!QLDS) {
+    uint32_t qs = 0;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) qs = s == (uint32_t)k ? a.QS[k] : qs;
-  uint32_t Q[32];
-  make_basis(qs, Q);
+    for (int k = 0; k < 8; ++k) qs = s == (uint32_t)k ? a.QS[k] : qs;
+    make_basis(qs, Q);
+  }
 
   struct Fin {
     uint32_t r[4];    // chain registers
@@ -742,7 +757,19 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
       for (int k = 0; k < 4; ++k) f.acc[k] = 0u;
     }
     if (sl < 6) mul_half(f, a.XB, sl & 1);
-    else mul_half(f, Q, sl & 1);
+    else if (!QLDS) mul_half(f, Q, sl & 1);
+    else {
+      const int h = sl & 1;
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) {
+        const u32x4 b = *reinterpret_cast<const u32x4 *>(qlds + 16 * h + 4 * q4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int j = 16 * h + 4 * q4 + i;
+          f.acc[i] = and_xor((uint32_t)(((int32_t)(f.u << (31 - j))) >> 31), b[i], f.acc[i]);
+        }
+      }
+    }
     if (sl == 1) f.u = take(f) ^ f.r[2];
     if (sl == 3) f.u = take(f) ^ f.r[1];
     if (sl == 5) f.u = take(f) ^ f.r[0];
@@ -757,14 +784,14 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
   // behind it would wait for its write acknowledgement.
   auto flush = [&](uint32_t q_end) {  // the round of groups ending at q_end (at most 64)
     if (ABL & 16) return;
-    const uint32_t q_lo = (q_end - 1) & ~63u;
+    const uint32_t q_lo = (q_end - 1) & ~kRoundMask;
     const uint64_t pb = (g0 + q_lo) * 8u;
     const uint32_t valid = (q_end - q_lo) * 8u;  // slots written this round
     const uint32_t nout = (uint32_t)(a.count - pb < valid ? a.count - pb : valid);
     const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out + pb, 4u * nout);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the slot writes have landed
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < (int)kSlots / 256; ++h) {
       const u32x4 v = *reinterpret_cast<const u32x4 *>(slots + 256 * h + 4 * lane);
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v), ro,
                                              1024u * h + 16u * lane, 0, 0);
@@ -779,7 +806,7 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
       sink ^= val;
       return;
     }
-    slots[((qf & 63u) << 3) | (lane >> 3)] = val;
+    slots[((qf & kRoundMask) << 3) | (lane >> 3)] = val;
   };
 
   // Finish slices of the previous group ride in steps 0..7 (0..6 for L = 8,
@@ -831,7 +858,7 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
         if (slice_step(sl) == k) fin_slice(pf, sl);
       if (k == kStoreStep) {
         fin_store(pf, q - 1);
-        if (q > 0 && ((q - 1) & 63u) == 63u) flush(q);  // wave-uniform: a full round of slots
+        if (q > 0 && ((q - 1) & kRoundMask) == kRoundMask) flush(q);  // wave-uniform: a full round of slots
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) x[i] = xor3(t[i][0], t[i][1], xor3(t[i][2], t[i][3], wn[i]));

@@ -1,16 +1,16 @@
-// Ablation timing of the strided-chain kernel (timing only: outputs are
-// meaningless for ABL != 0).  Build:
+// Ablation / variant timing of the strided-chain kernel (timing only: outputs
+// are meaningless for ABL != 0).  Build:
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 sck_abl.hip -o sck_abl
 #include "../../roce-test_amd/csrc/icrc_kernels.hip"
 #include <stdio.h>
 #include <stdlib.h>
 using namespace ricrc;
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s\n", hipGetErrorString(e)); exit(1); } } while (0)
-template <int L, int ABL> float run(SckArgs a, int grid, int reps) {
+template <int L, int ABL, int D = 8, bool QL = false> float run(SckArgs a, int grid, int reps) {
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-  for (int w = 0; w < 3; ++w) hipLaunchKernelGGL((icrc_sck_kernel<L, ABL>), dim3(grid), dim3(kBlock), 0, 0, a);
+  for (int w = 0; w < 3; ++w) hipLaunchKernelGGL((icrc_sck_kernel<L, ABL, D, QL>), dim3(grid), dim3(kBlock), 0, 0, a);
   CK(hipDeviceSynchronize()); CK(hipEventRecord(e0));
-  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL((icrc_sck_kernel<L, ABL>), dim3(grid), dim3(kBlock), 0, 0, a);
+  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL((icrc_sck_kernel<L, ABL, D, QL>), dim3(grid), dim3(kBlock), 0, 0, a);
   CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); float ms; CK(hipEventElapsedTime(&ms, e0, e1)); return ms / reps;
 }
 int main(int argc, char **argv) {
@@ -30,12 +30,17 @@ int main(int argc, char **argv) {
   const int grid = p.multiProcessorCount;
   auto rep = [&](const char *nm, float ms) { printf("%-36s %7.3f ms  %7.1f GB/s\n", nm, ms, n * count / (ms * 1e-3) / 1e9); };
   for (int r = 0; r < 2; ++r) {
-    rep("full", run<32, 0>(a, grid, 20));
+    rep("full D8", run<32, 0>(a, grid, 20));
+    rep("full D8 qlds", run<32, 0, 8, true>(a, grid, 20));
+    rep("full D16 qlds", run<32, 0, 16, true>(a, grid, 20));
+    rep("full D4", run<32, 0, 4>(a, grid, 20));
+    rep("no stores", run<32, 16>(a, grid, 20));
+    rep("full D8 again", run<32, 0>(a, grid, 20));
     rep("no fold (VALU stand-in)", run<32, 1>(a, grid, 20));
     rep("no finish", run<32, 2>(a, grid, 20));
     rep("no loads", run<32, 8>(a, grid, 20));
-    rep("no stores", run<32, 16>(a, grid, 20));
     rep("no fold, no finish (memory path)", run<32, 1 | 2>(a, grid, 20));
+    rep("memory path D16", run<32, 1 | 2, 16, true>(a, grid, 20));
     rep("no loads, no finish (fold only)", run<32, 8 | 2>(a, grid, 20));
     rep("no loads, no fold (finish only)", run<32, 8 | 1>(a, grid, 20));
   }
