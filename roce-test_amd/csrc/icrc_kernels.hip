@@ -23,109 +23,13 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "icrc_device.h"
 #include "icrc_kernels.h"
 #include "icrc_math.h"
 
 namespace ricrc {
 
-__device__ constexpr SliceTables<4> g_tab = make_tables<4>();
-
-static constexpr int kWaves = 16;       // waves per workgroup
-static constexpr int kBlock = 64 * kWaves;
-static constexpr int kLdsWords = 32768;  // 128 KiB
-
-// ---------------------------------------------------------------- helpers
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
-}
-__device__ __forceinline__ uint32_t and_xor(uint32_t a, uint32_t b, uint32_t c) {  // (a & b) ^ c
-  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x6A);
-}
-__device__ __forceinline__ uint32_t or_xor(uint32_t a, uint32_t b, uint32_t c) {  // (a | b) ^ c
-  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x56);
-}
-
-// Build the LDS tables: region 0 = {T3 | T2}, region 1 = {T1 | T0}, 256-byte
-// rows of 32 copies x 4 B per half.
-// One table entry per thread (4 x 256 = 1024 = kBlock): a single global load,
-// then the entry's 32 copies (128 contiguous bytes) in 8 ds_write_b128.
-__device__ __forceinline__ uint32_t table_entry(const SliceTables<4> &tab) {
-  return tab.t[threadIdx.x >> 8][threadIdx.x & 255];
-}
-__device__ __forceinline__ void table_store(uint32_t *lds, uint32_t v) {
-  const uint32_t t = threadIdx.x >> 8, e = threadIdx.x & 255;
-  const uint32_t region = t <= 1 ? 1u : 0u, half = (t == 0 || t == 2) ? 1u : 0u;  // T3 T2 | T1 T0
-  typedef uint32_t v4 __attribute__((ext_vector_type(4)));
-  v4 *dst = reinterpret_cast<v4 *>(lds + ((region << 14) | (e << 6) | (half << 5)));
-#pragma unroll
-  for (int k = 0; k < 8; ++k) dst[k] = v4{v, v, v, v};
-}
-__device__ __forceinline__ void fill_tables(uint32_t *lds, const SliceTables<4> &tab = g_tab) {
-  static_assert(kBlock == 1024, "one table entry per thread");
-  table_store(lds, table_entry(tab));
-}
-
-struct LaneTab {
-  uint32_t lo0, lo1;  // copy offsets for region 0 / region 1
-};
-
-__device__ __forceinline__ uint32_t lds_at(const uint32_t *lds, uint32_t byte_addr) {
-  return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(lds) + byte_addr);
-}
-
-// One slice-by-4 step: register after folding word w into register r.
-__device__ __forceinline__ uint32_t step4(const uint32_t *lds, LaneTab lt, uint32_t r, uint32_t w) {
-  const uint32_t x = r ^ w;
-  const uint32_t t3 = lds_at(lds, __builtin_amdgcn_perm(x, lt.lo0, 0x0C0C0400u));
-  const uint32_t t2 = lds_at(lds, __builtin_amdgcn_perm(x, lt.lo0, 0x0C0C0500u) + 128);
-  const uint32_t t1 = lds_at(lds, __builtin_amdgcn_perm(x, lt.lo1, 0x0C020600u));
-  const uint32_t t0 = lds_at(lds, __builtin_amdgcn_perm(x, lt.lo1, 0x0C020700u) + 128);
-  return xor3(t3, t2, t1 ^ t0);
-}
-
-// Same step, but returns (register ^ next word) directly: the word XOR rides
-// in the second v_bitop3, so a step is 4 v_perm + 2 v_bitop3 + 4 ds_read_b32.
-__device__ __forceinline__ uint32_t step4x(const uint32_t *lds, LaneTab lt, uint32_t x, uint32_t wnext) {
-  const uint32_t t3 = lds_at(lds, __builtin_amdgcn_perm(x, lt.lo0, 0x0C0C0400u));
-  const uint32_t t2 = lds_at(lds, __builtin_amdgcn_perm(x, lt.lo0, 0x0C0C0500u) + 128);
-  const uint32_t t1 = lds_at(lds, __builtin_amdgcn_perm(x, lt.lo1, 0x0C020600u));
-  const uint32_t t0 = lds_at(lds, __builtin_amdgcn_perm(x, lt.lo1, 0x0C020700u) + 128);
-  return xor3(t3, t2, xor3(t1, t0, wnext));
-}
-
-// r * K where Q[j] = K * x^(31-j) (bit j of r is the x^(31-j) coefficient).
-// Four independent accumulators keep the 32-term XOR off one dependency chain.
-__device__ __forceinline__ uint32_t mul_basis(uint32_t r, const uint32_t (&Q)[32]) {
-  uint32_t acc[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-  for (int j = 0; j < 32; ++j) {
-    const uint32_t m = (uint32_t)(((int32_t)(r << (31 - j))) >> 31);
-    acc[j & 3] = and_xor(m, Q[j], acc[j & 3]);
-  }
-  return xor3(acc[0], acc[1], acc[2] ^ acc[3]);
-}
-
-__device__ __forceinline__ void make_basis(uint32_t K, uint32_t (&Q)[32]) {
-  Q[31] = K;
-#pragma unroll
-  for (int j = 30; j >= 0; --j) Q[j] = gf_mulx(Q[j + 1]);
-}
-
-__device__ __forceinline__ uint32_t gf_mul_dev(uint32_t a, uint32_t b) {
-  uint32_t p = 0;
-#pragma unroll 8
-  for (int i = 31; i >= 0; --i) {
-    const uint32_t m = (uint32_t)(((int32_t)(a << (31 - i))) >> 31);
-    p = and_xor(m, b, p);
-    b = gf_mulx(b);
-  }
-  return p;
-}
-
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ uint32_t word_of(const u32x4 &v, int i) { return v[i]; }
-
+static constexpr int kStageBytes = 2048;  // TSK: per-wave LDS staging
 // =======================================================================
 // Streaming kernel: fixed length, 16-byte aligned packet starts.
 // Lanes 0..P-1 of each group of P2 = 2^log2P2 lanes take consecutive
@@ -259,49 +163,6 @@ __global__ __launch_bounds__(kBlock) void icrc_stream_kernel(StreamArgs a) {
 // zeros and out-of-batch stores are dropped by the buffer range check, so
 // the loop has no exec-masked memory op and prefetches one step ahead.
 // =======================================================================
-static constexpr int kStageBytes = 2048;  // per wave
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, uint32_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, (int)bytes, 0x00020000);
-}
-
-// Swizzled 16-byte slot of piece p in a 2 KiB round: the 8-lane groups of
-// ds_write_b128 stay in one 128-byte row, and the 32-byte chunk reads of each
-// 16-lane ds_read_b128 group hit 16 distinct bank quads.
-__device__ __forceinline__ uint32_t stage_slot(uint32_t p) { return p ^ ((p >> 4) & 1u); }
-
-// XOR of v over aligned groups of 2^levels lanes, result in every lane.
-__device__ __forceinline__ uint32_t group_xor(uint32_t v, uint32_t levels) {
-  if (levels > 0) v ^= __builtin_amdgcn_update_dpp(0u, v, 0xB1, 0xF, 0xF, true);   // quad_perm [1,0,3,2]
-  if (levels > 1) v ^= __builtin_amdgcn_update_dpp(0u, v, 0x4E, 0xF, 0xF, true);   // quad_perm [2,3,0,1]
-  if (levels > 2) v ^= __builtin_amdgcn_update_dpp(0u, v, 0x141, 0xF, 0xF, true);  // row_half_mirror
-  if (levels > 3) v ^= __builtin_amdgcn_update_dpp(0u, v, 0x140, 0xF, 0xF, true);  // row_mirror
-  if (levels > 4) {
-    const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
-    v = p[0] ^ p[1];
-  }
-  if (levels > 5) {
-    const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-    v = p[0] ^ p[1];
-  }
-  return v;
-}
-
-// Branch-free variant for a run-time group size: level k is applied through
-// a wave-uniform all-ones / zero mask, so the code stays one basic block and
-// the scheduler can interleave it with the next step's table lookups.
-__device__ __forceinline__ uint32_t group_xor_masked(uint32_t v, const uint32_t (&lm)[6]) {
-  v = and_xor(__builtin_amdgcn_update_dpp(0u, v, 0xB1, 0xF, 0xF, true), lm[0], v);
-  v = and_xor(__builtin_amdgcn_update_dpp(0u, v, 0x4E, 0xF, 0xF, true), lm[1], v);
-  v = and_xor(__builtin_amdgcn_update_dpp(0u, v, 0x141, 0xF, 0xF, true), lm[2], v);
-  v = and_xor(__builtin_amdgcn_update_dpp(0u, v, 0x140, 0xF, 0xF, true), lm[3], v);
-  const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
-  v = and_xor(p[0] ^ p[1] ^ v, lm[4], v);
-  const auto q = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-  v = and_xor(q[0] ^ q[1] ^ v, lm[5], v);
-  return v;
-}
-
 // Per-lane word constants for one chain at packet chunk position pos.
 struct ChunkMask {
   uint32_t mw0, xw0, m2, m6, keep7;
@@ -653,15 +514,6 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
 // D: lines in flight per wave; QLDS: lane bases read from LDS instead of 32
 // VGPRs (frees registers for a deeper ring).
 // =======================================================================
-constexpr SliceTables<4> make_stride_tables(uint64_t gap) {
-  SliceTables<4> s = make_tables<4>();
-  const uint32_t g = gf_x8n(gap);
-  for (int k = 0; k < 4; ++k)
-    for (int b = 0; b < 256; ++b) s.t[k][b] = gf_mul(s.t[k][b], g);
-  return s;
-}
-__device__ constexpr SliceTables<4> g_tab128 = make_stride_tables(124);  // word + 124 bytes = one line
-
 template <int L, int ABL, int D = 8, bool QLDS = false>
 __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
   // 128 KiB of tables + result slots per wave (+ the 8 lane bases, QLDS).
@@ -876,23 +728,6 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
 }
 
 // =======================================================================
-// Byte-level helpers for packets that do not start or end on a word.
-// =======================================================================
-__device__ __forceinline__ uint32_t byte_span_mask(int lo, int hi) {  // bytes [lo,hi) of a word
-  // Branch-free: 64-bit shifts of 0xFFFFFFFF handle the 0- and 32-bit ends.
-  const uint32_t l = (uint32_t)(lo < 0 ? 0 : lo > 4 ? 4 : lo);
-  const uint32_t h = (uint32_t)(hi < 0 ? 0 : hi > 4 ? 4 : hi);
-  const uint32_t keep_hi = (uint32_t)(0xFFFFFFFFull >> (32u - 8u * h));
-  const uint32_t keep_lo = (uint32_t)(0xFFFFFFFFull << (8u * l));
-  return keep_hi & keep_lo;
-}
-
-__device__ __forceinline__ uint32_t expand_nibble(uint32_t b) {
-  return ((b & 1u) ? 0x000000FFu : 0u) | ((b & 2u) ? 0x0000FF00u : 0u) | ((b & 4u) ? 0x00FF0000u : 0u) |
-         ((b & 8u) ? 0xFF000000u : 0u);
-}
-
-// =======================================================================
 // Ragged kernel: any alignment, per-packet offsets and/or lengths, any mix
 // of sizes.  The batch is a sequence of 64-byte pieces (packet i owns pieces
 // [ps[i], ps[i+1]), laid from its L3 start rounded down to 16 B, so every
@@ -918,17 +753,6 @@ __device__ __forceinline__ uint32_t expand_nibble(uint32_t b) {
 // shifted by x^(8*4096).  Waves own contiguous piece ranges cut at packet
 // boundaries, so no packet is split between waves.
 // =======================================================================
-// Loads through explicit global (address space 1) pointers: an address
-// built from an integer is otherwise a flat access, and flat loads may retire
-// out of order with global ones, which forces vmcnt(0) after each of them.
-typedef const u32x4 __attribute__((address_space(1))) *gptr_u32x4;
-typedef uint32_t __attribute__((aligned(1))) u32_unaligned;
-typedef const u32_unaligned __attribute__((address_space(1))) *gptr_u32_unaligned;
-__device__ __forceinline__ u32x4 gload16(uintptr_t addr) { return *reinterpret_cast<gptr_u32x4>(addr); }
-__device__ __forceinline__ uint32_t gload4_unaligned(uintptr_t addr) {
-  return *reinterpret_cast<gptr_u32_unaligned>(addr);
-}
-
 __device__ constexpr Basis g_x4096 = make_const_basis(gf_x8n(4096));
 
 // r * K for a wave-uniform r and a constant basis: scalar ALU code.

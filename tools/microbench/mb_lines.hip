@@ -24,6 +24,42 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, ui
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, (int)bytes, 0x00020000);
 }
 
+// Gathered variant: packet slot g of group q is packet perm[8 q + g] (random
+// order, as after bucketing a ragged batch by size), lines offset by SHIFT bytes
+// from 128-byte alignment; global loads with 64-bit addresses.
+template <int SHIFT, int D, bool NT>
+__global__ __launch_bounds__(1024) void gather_lines(const uint8_t *buf, const uint32_t *perm, uint64_t npkt,
+                                                     uint32_t *sink) {
+  constexpr uint32_t PKT = 4096, STEPS = PKT / 128;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t wave = (uint64_t)blockIdx.x * 16 + (threadIdx.x >> 6);
+  const uint64_t nw = (uint64_t)gridDim.x * 16;
+  const uint64_t ngroups = npkt / 8 - 1;  // the shifted last packet would run past the buffer
+  const uint64_t per = (ngroups + nw - 1) / nw;
+  const uint64_t g0 = wave * per < ngroups ? wave * per : ngroups;
+  const uint64_t g1 = g0 + per < ngroups ? g0 + per : ngroups;
+  const uint64_t nsteps = (g1 - g0) * STEPS;
+  auto addr = [&](uint64_t t) -> const u32x4 * {
+    uint64_t g = g0 + t / STEPS;
+    if (g >= g1) g = g0;
+    const uint32_t k = (uint32_t)(t % STEPS);
+    const uint64_t pk = perm[8 * g + (lane >> 3)];
+    return (const u32x4 *)(buf + pk * PKT + SHIFT + 128 * k + 16 * (lane & 7));
+  };
+  u32x4 acc = {0, 0, 0, 0};
+  u32x4 v[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) v[d] = NT ? __builtin_nontemporal_load(addr(d)) : *addr(d);
+  for (uint64_t t = 0; t < nsteps; t += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      acc ^= v[d];
+      v[d] = NT ? __builtin_nontemporal_load(addr(t + D + d)) : *addr(t + D + d);
+    }
+  }
+  sink[blockIdx.x * blockDim.x + threadIdx.x] = acc.x ^ acc.y ^ acc.z ^ acc.w;
+}
+
 template <int LPP, int D, int AUX, int WAVES>
 __global__ __launch_bounds__(64 * WAVES) void read_lines(const uint8_t *buf, uint64_t npkt, uint32_t *sink) {
   constexpr uint32_t PKT = 4096, PPG = 64 / LPP, LINE = 16 * LPP, STEPS = PKT / LINE, GB = PPG * PKT;
@@ -97,7 +133,32 @@ int main() {
 #define RUN(LPP, D, AUX, W)                                                                          \
   rep("LPP " #LPP " D " #D " aux " #AUX " w" #W,                                                      \
       timeit([&] { hipLaunchKernelGGL((read_lines<LPP, D, AUX, W>), dim3(ncu * 16 / W), dim3(64 * W), 0, 0, buf, npkt, sink); }, 20))
+  uint32_t *perm_id, *perm_rnd;
+  {
+    uint32_t *h = (uint32_t *)malloc(4 * npkt);
+    for (uint64_t i = 0; i < npkt; ++i) h[i] = (uint32_t)i;
+    CK(hipMalloc(&perm_id, 4 * npkt));
+    CK(hipMemcpy(perm_id, h, 4 * npkt, hipMemcpyHostToDevice));
+    uint64_t x = 12345;
+    for (uint64_t i = npkt - 1; i > 0; --i) {
+      x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+      const uint64_t j = x % (i + 1);
+      const uint32_t t = h[i]; h[i] = h[j]; h[j] = t;
+    }
+    CK(hipMalloc(&perm_rnd, 4 * npkt));
+    CK(hipMemcpy(perm_rnd, h, 4 * npkt, hipMemcpyHostToDevice));
+    free(h);
+  }
+#define GRUN(NAME, SHIFT, D, NT, PERM)                                                                  \
+  rep(NAME, timeit([&] { hipLaunchKernelGGL((gather_lines<SHIFT, D, NT>), dim3(ncu), dim3(1024), 0, 0, buf, PERM, npkt, sink); }, 20))
   for (int rep2 = 0; rep2 < 2; ++rep2) {
+    GRUN("gather id  shift0  D8 nt", 0, 8, true, perm_id);
+    GRUN("gather id  shift64 D8 nt", 64, 8, true, perm_id);
+    GRUN("gather id  shift16 D8 nt", 16, 8, true, perm_id);
+    GRUN("gather rnd shift0  D8 nt", 0, 8, true, perm_rnd);
+    GRUN("gather rnd shift64 D8 nt", 64, 8, true, perm_rnd);
+    GRUN("gather rnd shift0  D8", 0, 8, false, perm_rnd);
+    GRUN("gather rnd shift64 D8", 64, 8, false, perm_rnd);
     RUN(64, 2, 2, 16);
     RUN(64, 4, 2, 16);
     RUN(64, 4, 0, 16);

@@ -3,8 +3,9 @@
 
 Device-resident (HIP-event kernel time, inputs already in HBM):
   * fixed-size batches at the BASELINE configs' MTUs (C1 64 B, 256 B, C2 1024 B,
-    headline 4096 B) through the default dispatch (TSK kernel) and, for
-    comparison, with RICRC_NO_TSK=1 (the stride/offset streaming kernel);
+    headline 4096 B) through the default dispatch (SCK for 1/2/4 KiB, TSK for
+    smaller powers of two) and, for comparison, with RICRC_NO_SCK=1 (TSK) and
+    with RICRC_NO_SCK=1 RICRC_NO_TSK=1 (the stride/offset streaming kernel);
   * the C4 ragged mix (N uniform over {64,256,1024,4096}, packed, uint64
     offsets + uint32 lengths) through the ragged kernel.
 Host-resident (ricrc_batch_host: host in, host out; PCIe-inclusive):
@@ -79,14 +80,18 @@ def main():
         pk = torch.empty(count * n, dtype=torch.uint8, device=dev)
         out = torch.empty(count, dtype=torch.int32, device=dev)
         ctx.synth_device(pk, SEED, 0, count, n, stream=torch.cuda.current_stream())
-        for mode in ("default", "stream"):
-            if mode == "stream":
-                os.environ["RICRC_NO_TSK"] = "1"
+        for mode in ("default", "tsk", "stream"):
+            knobs = {"default": [], "tsk": ["RICRC_NO_SCK"], "stream": ["RICRC_NO_SCK", "RICRC_NO_TSK"]}[mode]
+            if mode == "tsk" and n not in (1024, 2048, 4096):
+                continue  # TSK is already the default there
+            for k in knobs:
+                os.environ[k] = "1"
             try:
                 ms = time_device(torch, ctx, lambda s: ctx.batch_device(pk, count, out, stride=n, stream=s),
                                  reps, warm)
             finally:
-                os.environ.pop("RICRC_NO_TSK", None)
+                for k in knobs:
+                    os.environ.pop(k, None)
             ns = min(count, 8192)
             check_sample(np, oracle_c, pk[: ns * n].cpu().numpy(), None, None,
                          out[:ns].cpu().numpy().view(np.uint32), f"{n}B/{mode}", stride=n)
