@@ -47,11 +47,15 @@ struct Dev {
   hipStream_t stream = nullptr;
   uint32_t *d_inv = nullptr;   // x^(-8 z), z <= 4096
   uint32_t *d_inv4 = nullptr;  // t: x^(8 (k - t)), k = 0..3, t <= 4096
+  uint32_t *d_tzb = nullptr;   // [128][8]: basis words 4q of x^(-8 tz) (ragged strided-chain path)
   Slot slot[2];
   bool staged = false;
 };
 
-int hip_err(hipError_t e) { return e == hipSuccess ? 0 : (e == hipErrorOutOfMemory ? -ENOMEM : -EIO); }
+int hip_err(hipError_t e) {
+  if (e != hipSuccess && getenv("RICRC_DEBUG")) fprintf(stderr, "libroceicrc: HIP error %d: %s\n", (int)e, hipGetErrorString(e));
+  return e == hipSuccess ? 0 : (e == hipErrorOutOfMemory ? -ENOMEM : -EIO);
+}
 
 #define HIP_TRY(x)                          \
   do {                                      \
@@ -113,6 +117,13 @@ int init_dev(Dev &d) {
     for (int k = 0; k < 4; ++k) inv4[4 * t + k] = k >= t ? gf_x8n((uint64_t)(k - t)) : gf_xinv8n((uint64_t)(t - k));
   HIP_TRY(hipMalloc(&d.d_inv4, inv4.size() * sizeof(uint32_t)));
   HIP_TRY(hipMemcpy(d.d_inv4, inv4.data(), inv4.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  std::vector<uint32_t> tzb(128 * 8);  // basis words 4q of x^(-8 tz): the kernel derives 4q+1..4q+3 by x^-1
+  for (int tz = 0; tz < 128; ++tz) {
+    const uint32_t c = gf_xinv8n((uint64_t)tz);
+    for (int q = 0; q < 8; ++q) tzb[8 * tz + q] = gf_mul(c, 1u << (4 * q));
+  }
+  HIP_TRY(hipMalloc(&d.d_tzb, tzb.size() * sizeof(uint32_t)));
+  HIP_TRY(hipMemcpy(d.d_tzb, tzb.data(), tzb.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
   return 0;
 }
 
@@ -145,6 +156,7 @@ void free_dev(Dev &d) {
   }
   (void)hipFree(d.d_inv);
   (void)hipFree(d.d_inv4);
+  (void)hipFree(d.d_tzb);
   if (d.stream) (void)hipStreamDestroy(d.stream);
 }
 
@@ -234,8 +246,34 @@ int launch_batch(Dev &d, const uint8_t *base, const uint64_t *off, const uint32_
       return hip_err(launch_stream(a, cpl, grid, st));
     }
   }
-  // Everything else: the ragged kernel.  Pieces from a device-side scan of
-  // the descriptors, or arithmetic when every packet has the same length and
+  // Everything else (offsets, lengths, any alignment, Ethernet framing): the
+  // ragged strided-chain pipeline (icrc_rsck.hip), packets bucketed on the
+  // device by line count.  RICRC_NO_RSCK=1 selects the older piece-based
+  // ragged kernel below (kept for comparison and as a second implementation).
+  if (getenv("RICRC_NO_RSCK") == nullptr && count < (1ull << 31)) {
+    RsckArgs k{};
+    k.base = base;
+    k.off = off;
+    k.len = len;
+    k.stride = stride;
+    k.count = count;
+    k.fixed_len = fixed_len;
+    k.l3_offset = l3_offset;
+    k.verify = verify ? 1u : 0u;
+    k.out = out;
+    k.tzb = d.d_tzb;
+    const uint32_t xi = gf_xinv8n(4);
+    for (int j = 0; j < 32; ++j) k.XB[j] = gf_mul(xi, 1u << j);
+    for (int s = 0; s < 8; ++s) k.QS[s] = gf_xinv8n(16ull * s);
+    void *ws = nullptr;
+    HIP_TRY(hipMallocAsync(&ws, rs_workspace_bytes(count), st));
+    rs_bind_workspace(k, ws);
+    const hipError_t e = launch_rsck(k, d.n_cu, st);
+    const hipError_t e2 = hipFreeAsync(ws, st);
+    return hip_err(e != hipSuccess ? e : e2);
+  }
+  // The piece-based ragged kernel.  Pieces from a device-side scan of the
+  // descriptors, or arithmetic when every packet has the same length and
   // 16-byte phase.
   RaggedArgs r{};
   r.base = base;

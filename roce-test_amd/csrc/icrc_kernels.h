@@ -84,6 +84,53 @@ __host__ __device__ inline uint32_t ragged_pieces(uintptr_t start, uint32_t n) {
   return p ? p : 1u;
 }
 
+// Ragged strided-chain path (icrc_rsck.hip): any packet addresses and
+// lengths, packets bucketed by their number of 128-byte lines on the device,
+// 8 packets of equal line count per group, folded as in the SCK.
+constexpr int kRsClasses = 514;  // lines per packet 1..513 (n <= 65535, any start offset)
+// 8-byte descriptor in class order: lo = address bits 0..31, hi = address
+// bits 32..47 | n << 16 (device addresses are 48-bit, n <= 65535).  Padding
+// entries of a class's last group repeat the class's last packet.
+struct RsDesc {
+  uint32_t lo, hi;
+};
+struct RsPlan {
+  uint32_t nc;        // non-empty classes
+  uint32_t ngroups;   // 8-packet groups over all classes
+  uint64_t nsteps;    // weighted work over all groups: lines + a per-group finish cost
+  uint32_t L[kRsClasses];   // compact, ascending
+  uint32_t g0[kRsClasses];  // first group of the class
+  uint64_t s0[kRsClasses];  // weighted work before the class's first group
+};
+struct RsckArgs {
+  const uint8_t *base;
+  const uint64_t *off;  // may be null (then p * stride)
+  const uint32_t *len;  // may be null (then fixed_len)
+  uint64_t stride;
+  uint64_t count;
+  uint32_t fixed_len;
+  uint32_t l3_offset;
+  uint32_t verify;
+  uint32_t *out;
+  // device workspace (icrc_api.cpp sizes it: rs_workspace_bytes)
+  uint32_t *counts;   // [kRsClasses], zeroed before the count pass
+  uint32_t *cursor;   // [kRsClasses], zeroed by the plan pass
+  uint32_t *bucket;   // [kRsClasses] first position of each class
+  RsPlan *plan;
+  RsDesc *desc;       // [count + 8 kRsClasses] in class order
+  uint32_t *pos_of;   // [count] position of packet i, or ~0 (written by the scatter pass)
+  uint32_t *res;      // [count + 8 kRsClasses] results in class order
+  uint32_t *hist;     // [pass blocks][kRsClasses] per-block class counts
+  const uint32_t *tzb;  // [128][8]: words 0, 4, ..., 28 of the basis of x^(-8 tz)
+  uint32_t XB[32];      // basis of x^-32
+  uint32_t QS[8];       // x^(-8*16 s): lane slot s -> line start
+};
+uint64_t rs_workspace_bytes(uint64_t count);
+// Carves the workspace (rs_workspace_bytes(count) bytes at ws) into a.
+void rs_bind_workspace(RsckArgs &a, void *ws);
+// The whole ragged pipeline on `st`: count/classify, plan, scatter, fold, gather.
+hipError_t launch_rsck(RsckArgs &a, int grid, hipStream_t st);
+
 struct SynthArgs {
   uint8_t *buf;
   uint64_t seed, first, count;

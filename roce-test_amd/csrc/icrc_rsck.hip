@@ -1,0 +1,504 @@
+// Ragged strided-chain path of libroceicrc (gfx950): batches with per-packet
+// offsets and/or lengths, any alignment, any mix of sizes -- the C4 mixed-MTU
+// configuration and NIC rings with Ethernet framing.
+//
+// The fixed-size strided-chain kernel (icrc_kernels.hip, icrc_sck_kernel)
+// streams at the HBM read ceiling because a wave reads whole 128-byte lines
+// of 8 packets per load and folds them without any transpose.  This path
+// gives ragged batches the same inner loop:
+//
+//  1. rsck_count    classify every packet by its number of 128-byte lines on
+//                   the ABSOLUTE line grid, L = ceil(((addr & 127) + n - 4) /
+//                   128), histogram the classes; packets too short for a
+//                   RoCEv2 header (4 <= n < 44) are computed right there by a
+//                   scalar loop, invalid lengths yield 0 (as the ragged kernel
+//                   always did);
+//  2. rsck_plan     one workgroup scans the 513 class counts: each class gets
+//                   a bucket padded to whole 8-packet groups, a first group and
+//                   a first step (line);
+//  3. rsck_scatter  writes each packet's descriptor {addr, n, idx} into its
+//                   class bucket (block-aggregated atomics) and its position;
+//  4. icrc_rsck_kernel  folds groups of 8 equal-L packets exactly like the
+//                   SCK -- lane 8g+s owns slot s of every line of packet g,
+//                   four chains per lane, T_124..T_127 tables in LDS -- with
+//                   a load cursor running 8 lines ahead of the fold cursor
+//                   across group boundaries (groups of 64-byte packets are
+//                   one line long), descriptors read 64 at a time;
+//  5. rsck_gather   out[i] = res[pos(i)] (verify mode: the trailer compared
+//                   with it).
+//
+// Lines are 128-byte aligned in memory (misaligned line grids measured 20 %
+// slower, tools/microbench/mb_lines.hip), so a packet's first and last line
+// generally hold bytes of its neighbours: bytes outside the covered range
+// [addr, addr + n - 4) are zeroed (leading zeros do not change a register
+// folded from 0), the seed and the invariant masks are applied by
+// packet-relative byte offset on the packet's head lines, and the zero tail
+// tz = 128 L - a - M of the last line is removed at the end by x^(-8 tz)
+// (tests/test_kernel_algebra.py::test_ragged_line_grid_decomposition).
+// Every load is a 16-byte slot of a line that holds packet bytes, i.e. in a
+// page the packet occupies.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "icrc_device.h"
+#include "icrc_kernels.h"
+#include "icrc_math.h"
+
+namespace ricrc {
+namespace {
+
+typedef const u32x4 __attribute__((address_space(1))) *gptr_u32x4_t;
+__device__ __forceinline__ u32x4 gload16_nt(uint64_t addr) {
+  return __builtin_nontemporal_load(reinterpret_cast<gptr_u32x4_t>((uintptr_t)addr));
+}
+
+__device__ __forceinline__ void rs_packet(const RsckArgs &a, uint64_t i, uint64_t &addr, uint32_t &n) {
+  addr = (uint64_t)(uintptr_t)a.base + (a.off ? a.off[i] : i * a.stride) + a.l3_offset;
+  n = a.len ? a.len[i] : a.fixed_len;
+}
+
+// Lines of the absolute grid a packet's covered bytes span; 0 = not folded here.
+__device__ __forceinline__ uint32_t rs_class(uint64_t addr, uint32_t n) {
+  if (n < kMinLen || n > kMaxLen) return 0u;
+  return (uint32_t)(((addr & 127u) + (n - 4u) + 127u) >> 7);
+}
+
+// ICRC of a packet shorter than a RoCEv2 header (4 <= n < 44): Sarwate loop.
+__device__ uint32_t icrc_small(uint64_t addr, uint32_t n) {
+  const uint8_t *p = reinterpret_cast<const uint8_t *>((uintptr_t)addr);
+  uint32_t r = kSeed;
+  for (uint32_t i = 0; i < n - 4u; ++i) {
+    const uint32_t b = p[i] | mask_byte(kFamV4, i);
+    r = g_tab.t[0][(r ^ b) & 0xFFu] ^ (r >> 8);
+  }
+  return ~r;
+}
+
+// Pass blocks own contiguous packet ranges (the same in the count and the
+// scatter pass), so each block reserves its bucket ranges with ONE global
+// atomic per class (per-chunk reservations serialised on the few hot class
+// counters: 50 us per million packets).
+constexpr int kPassBlock = 1024;
+// Work of a group in line-steps: its L lines plus the per-group finish
+// (4 GF(2) multiplies, reductions, descriptor and slot traffic), measured on
+// MI355X as ~5-6 memory-bound line-steps.  Waves split the total weighted
+// work, not the lines: split by lines, a wave that drew 64-byte packets (one
+// line per group) ran ~8x longer than one that drew 4 KiB packets.
+constexpr uint32_t kGroupCost = 6;
+constexpr int kPassBlocks = 512;  // pass grid cap (per-block class histograms: 1 MiB)
+__device__ __forceinline__ void pass_range(uint64_t count, uint64_t &lo, uint64_t &hi) {
+  const uint64_t per = ((count + gridDim.x - 1) / gridDim.x + kPassBlock - 1) / kPassBlock * kPassBlock;
+  lo = (uint64_t)blockIdx.x * per;
+  lo = lo < count ? lo : count;
+  hi = lo + per < count ? lo + per : count;
+}
+
+__global__ __launch_bounds__(kPassBlock) void rsck_count(RsckArgs a) {
+  __shared__ uint32_t h[kRsClasses];
+  for (int t = threadIdx.x; t < kRsClasses; t += blockDim.x) h[t] = 0;
+  __syncthreads();
+  uint64_t lo, hi;
+  pass_range(a.count, lo, hi);
+  for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    uint64_t addr;
+    uint32_t n;
+    rs_packet(a, i, addr, n);
+    const uint32_t c = rs_class(addr, n);
+    if (c) {
+      atomicAdd(&h[c], 1u);
+    } else {
+      uint32_t v = 0u;
+      if (n >= 4u && n <= kMaxLen) {
+        v = icrc_small(addr, n);
+        if (a.verify) v = gload4_unaligned((uintptr_t)(addr + n - 4u)) == v ? 1u : 0u;
+      }
+      a.out[i] = v;
+    }
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < kRsClasses; t += blockDim.x) {
+    a.hist[(uint64_t)blockIdx.x * kRsClasses + t] = h[t];
+    if (h[t]) atomicAdd(&a.counts[t], h[t]);
+  }
+}
+
+// One workgroup: exclusive scans of groups, steps and non-empty classes.
+__global__ __launch_bounds__(1024) void rsck_plan(RsckArgs a) {
+  __shared__ uint32_t sg[1024], sf[1024];
+  __shared__ uint64_t ss[1024];
+  const uint32_t t = threadIdx.x;
+  const uint32_t cnt = (t >= 1 && t < (uint32_t)kRsClasses) ? a.counts[t] : 0u;
+  const uint32_t G = (cnt + 7u) >> 3, f = cnt ? 1u : 0u;
+  const uint64_t S = (uint64_t)G * (t + kGroupCost);
+  sg[t] = G;
+  sf[t] = f;
+  ss[t] = S;
+  __syncthreads();
+  for (uint32_t d = 1; d < 1024; d <<= 1) {
+    const uint32_t g2 = t >= d ? sg[t - d] : 0u, f2 = t >= d ? sf[t - d] : 0u;
+    const uint64_t s2 = t >= d ? ss[t - d] : 0u;
+    __syncthreads();
+    sg[t] += g2;
+    sf[t] += f2;
+    ss[t] += s2;
+    __syncthreads();
+  }
+  const uint32_t g0 = sg[t] - G, ci = sf[t] - f;
+  const uint64_t s0 = ss[t] - S;
+  RsPlan *P = a.plan;
+  if (f) {
+    P->L[ci] = t;
+    P->g0[ci] = g0;
+    P->s0[ci] = s0;
+  }
+  if (t < (uint32_t)kRsClasses) {
+    a.bucket[t] = 8u * g0;
+    a.cursor[t] = 0u;
+  }
+  if (t == 1023) {
+    P->nc = sf[t];
+    P->ngroups = sg[t];
+    P->nsteps = ss[t];
+  }
+}
+
+__global__ __launch_bounds__(kPassBlock) void rsck_scatter(RsckArgs a) {
+  __shared__ uint32_t lc[kRsClasses], base[kRsClasses];
+  for (int t = threadIdx.x; t < kRsClasses; t += blockDim.x) {
+    const uint32_t hb = a.hist[(uint64_t)blockIdx.x * kRsClasses + t];
+    base[t] = hb ? a.bucket[t] + atomicAdd(&a.cursor[t], hb) : 0u;
+  }
+  uint64_t lo, hi;
+  pass_range(a.count, lo, hi);
+  for (uint64_t b0 = lo; b0 < hi; b0 += blockDim.x) {
+    for (int t = threadIdx.x; t < kRsClasses; t += blockDim.x) lc[t] = 0;
+    __syncthreads();
+    const uint64_t i = b0 + threadIdx.x;
+    uint64_t addr = 0;
+    uint32_t n = 0, c = 0, r = 0;
+    if (i < hi) {
+      rs_packet(a, i, addr, n);
+      c = rs_class(addr, n);
+      if (c) r = atomicAdd(&lc[c], 1u);
+    }
+    __syncthreads();
+    if (i < hi) {
+      if (c) {
+        const uint32_t pos = base[c] + r;
+        const RsDesc d{(uint32_t)addr, (uint32_t)(addr >> 32) | (n << 16)};
+        a.desc[pos] = d;
+        a.pos_of[i] = pos;
+        const uint32_t end = a.bucket[c] + a.counts[c];
+        if (pos + 1 == end)  // the class's last packet pads its group with copies of itself
+          for (uint32_t p = end; (p - a.bucket[c]) & 7u; ++p) a.desc[p] = d;
+      } else {
+        a.pos_of[i] = 0xFFFFFFFFu;
+      }
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < kRsClasses; t += blockDim.x) base[t] += lc[t];
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void rsck_gather(RsckArgs a) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.count;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t p = a.pos_of[i];
+    if (p == 0xFFFFFFFFu) continue;  // done by the count pass
+    uint32_t v = a.res[p];
+    if (a.verify) {  // out = trailer holds the ICRC
+      uint64_t addr;
+      uint32_t n;
+      rs_packet(a, i, addr, n);
+      v = gload4_unaligned((uintptr_t)(addr + n - 4u)) == v ? 1u : 0u;
+    }
+    a.out[i] = v;
+  }
+}
+
+// Bytes [0, M) of the packet kept, invariant masks, seed: word i of a slot whose
+// first byte is packet-relative offset rel (any sign, any alignment).  Branch
+// free (one-direction 64-bit shifts + selects): a divergent branch here made
+// the compiler drain vmcnt(0) at its join, stalling the whole load ring.
+__device__ __forceinline__ uint32_t edge_word(uint32_t w, int rel, int M) {
+  const uint32_t keep = byte_span_mask(-rel, M - rel);
+  const uint32_t sh = (uint32_t)(rel + 3 < 0 ? 0 : rel + 3 > 63 ? 63 : rel + 3);  // byte b <-> bit/byte rel + b
+  const uint32_t bits = (uint32_t)(((kMaskBits << 3) >> sh) & 0xFu);
+  const uint32_t orm = (rel > -4 && rel < 40) ? (expand_nibble(bits) & keep) : 0u;
+  const uint64_t s64 = (uint64_t)kSeed << 24;  // seed byte k at byte k + 3
+  const uint32_t sx = (rel > -4 && rel < 4) ? (uint32_t)(s64 >> (8u * (sh & 7u))) : 0u;
+  return ((w & keep) | orm) ^ sx;
+}
+
+}  // namespace
+
+// ABL (timing-only ablations, tools/microbench): 1 no table fold, 2 no finish.
+template <int ABL>
+__global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
+  constexpr uint32_t kSlots = 64, kRound = kSlots / 8;   // result slots per wave, groups per round
+  constexpr uint32_t kQStride = 36;                       // padded lane-basis rows: conflict-free ds_read_b128
+  constexpr uint32_t kBlk = 128;                          // words per descriptor block (8 groups x 8 x 8 B)
+  constexpr uint32_t kWaveWords = kSlots + 2 * kBlk + 64;  // slots | 2-block ring | 8-group info FIFO
+  constexpr int D = 8;                                    // lines in flight per wave
+  // 128 KiB tables | 4 KiB tz bases | 8 lane bases | 1.5 KiB per wave = 157 KiB
+  __shared__ uint32_t lds[kLdsWords + 128 * 8 + 8 * kQStride + kWaves * kWaveWords];
+  uint32_t *tzl = lds + kLdsWords;
+  uint32_t *qsl = tzl + 128 * 8;
+
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t s = lane & 7, g = lane >> 3;
+
+  const uint32_t tab_v = table_entry(g_tab128);
+  const uint32_t tz_v = a.tzb[threadIdx.x];
+  table_store(lds, tab_v);
+  tzl[threadIdx.x] = tz_v;
+  if (threadIdx.x < 256) {  // word j of lane slot s's basis: x^(-128 s) x^(31 - j)
+    const uint32_t bs = threadIdx.x >> 5, j = threadIdx.x & 31;
+    uint32_t v = a.QS[0];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) v = bs == (uint32_t)k ? a.QS[k] : v;
+    for (uint32_t t = j; t < 31; ++t) v = gf_mulx(v);
+    qsl[bs * kQStride + j] = v;
+  }
+  __syncthreads();
+
+  // This wave's groups: those whose first line lies in its share of steps.
+  const RsPlan *P = a.plan;
+  const uint32_t nc = P->nc, NG = P->ngroups;
+  const uint64_t S = P->nsteps;
+  const uint64_t wave = (uint64_t)blockIdx.x * kWaves + wid;
+  const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
+  const uint64_t share = (S + nwaves - 1) / nwaves;
+  auto first_group_at = [&](uint64_t x) -> uint32_t {
+    if (x >= S) return NG;
+    uint32_t cnt = 0;
+    for (uint32_t b = 0; b < nc; b += 64) {
+      const uint32_t c = b + lane;
+      cnt += (uint32_t)__builtin_popcountll(__ballot(c < nc && P->s0[c < nc ? c : 0] <= x));
+    }
+    const uint32_t c = __builtin_amdgcn_readfirstlane(cnt - 1u);  // s0[0] = 0 <= x
+    const uint32_t L = P->L[c], g0 = P->g0[c], gend = c + 1 < nc ? P->g0[c + 1] : NG;
+    const uint64_t w = L + kGroupCost;
+    const uint64_t q = g0 + (x - P->s0[c] + w - 1) / w;
+    return q < gend ? (uint32_t)q : gend;
+  };
+  const uint64_t x0 = wave * share < S ? wave * share : S;
+  const uint32_t q_begin = first_group_at(x0), q_end = first_group_at(x0 + share);
+  if (q_begin >= q_end) return;  // no barrier below
+
+  const LaneTab lt{(lane & 31) << 2, ((lane & 31) << 2) | 0x10000u};
+  const uint32_t *qrow = qsl + s * kQStride;
+  uint32_t *slots = qsl + 8 * kQStride + wid * kWaveWords;
+  uint32_t *dring = slots + kSlots;
+  uint32_t *fifo = dring + 2 * kBlk;
+  const uint64_t npos = 8ull * NG;
+
+  // Descriptor blocks (8 groups = 64 descriptors of 8 B, lane l holding
+  // descriptor l) go through a 2-slot LDS ring, block b in slot b & 1; only
+  // the load cursor reads them.  Entering block b it stores block b + 1
+  // (loaded into NB when it entered block b - 1, >= 8 lines ago) into the
+  // slot block b - 1 used, and requests block b + 2 into NB.  (LDS-DMA would
+  // skip the register, but the compiler then waits for it before every LDS
+  // read -- the table lookups included.)  The fold cursor gets (a, M) of each
+  // group through an 8-entry LDS FIFO the load cursor fills (the fold lags
+  // at most 8 lines = 8 groups; each step folds before it loads, so an entry
+  // is read before it is reused).
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  auto load_block = [&](uint32_t b) -> u32x2 {
+    uint64_t e = (uint64_t)b * 64u + lane;
+    e = e < npos ? e : npos - 1;
+    return *reinterpret_cast<const u32x2 __attribute__((address_space(1))) *>(
+        (uintptr_t)reinterpret_cast<const uint32_t *>(a.desc + e));
+  };
+  auto put_block = [&](uint32_t b, const u32x2 &v) {
+    *reinterpret_cast<u32x2 *>(dring + (b & 1u) * kBlk + 2u * lane) = v;
+  };
+  u32x2 NB;
+  {
+    const uint32_t b = q_begin >> 3;
+    put_block(b, load_block(b));
+    put_block(b + 1, load_block(b + 1));
+    NB = load_block(b + 2);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+  }
+
+  struct LInfo {
+    uint64_t line0;  // lane's slot in the packet's first line
+  };
+  // Load cursor enters group q: line base, L, and (a, M) into the FIFO.
+  auto ld_enter = [&](uint32_t q, LInfo &li) -> uint32_t {
+    const u32x2 d = *reinterpret_cast<const u32x2 *>(dring + ((q >> 3) & 1u) * kBlk + 2u * (8u * (q & 7u) + g));
+    const uint64_t addr = ((uint64_t)(d[1] & 0xFFFFu) << 32) | d[0];
+    const uint32_t ga = d[0] & 127u, gM = (d[1] >> 16) - 4u;
+    li.line0 = (addr & ~127ull) + 16u * s;
+    fifo[((q & 7u) << 3) | g] = (gM << 7) | ga;
+    return __builtin_amdgcn_readfirstlane((ga + gM + 127u) >> 7);  // equal within a group
+  };
+
+  LInfo ld;
+  uint32_t ld_q = q_begin, ld_k = 0, ld_L = ld_enter(ld_q, ld);
+  uint32_t fd_q = q_begin, fd_k = 0, fd_L = ld_L, fd_a, fd_M;
+  auto fd_enter = [&](uint32_t q) {
+    const uint32_t v = fifo[((q & 7u) << 3) | g];
+    fd_a = v & 127u;
+    fd_M = v >> 7;
+    fd_L = __builtin_amdgcn_readfirstlane((fd_a + fd_M + 127u) >> 7);
+  };
+  fd_enter(fd_q);
+  bool fd_head2 = __ballot(fd_a > 88u) != 0;  // the header runs into line 1
+
+  auto ld_advance = [&]() {
+    if (++ld_k == ld_L) {  // wave-uniform
+      ld_k = 0;
+      if (ld_q + 1 < q_end) {
+        ++ld_q;
+        if ((ld_q & 7u) == 0) {
+          put_block((ld_q >> 3) + 1, NB);
+          NB = load_block((ld_q >> 3) + 2);
+        }
+        ld_L = ld_enter(ld_q, ld);
+      } else {
+        ld_L = 1;  // done: re-read line 0 of the last group (ld_k wraps to 0 every step)
+      }
+    }
+  };
+  auto ld_issue = [&]() -> u32x4 { return gload16_nt(ld.line0 + 128ull * ld_k); };
+
+  u32x4 ring[D];
+#pragma unroll
+  for (int u = 0; u < D; ++u) {
+    __builtin_amdgcn_sched_barrier(0);
+    ring[u] = ld_issue();
+    ld_advance();
+  }
+  __builtin_amdgcn_sched_barrier(0);
+
+  uint32_t r[4] = {0u, 0u, 0u, 0u};
+  uint32_t round_q0 = q_begin;  // first group of the current round of result slots
+  auto flush = [&](uint32_t q_stop) {  // groups [round_q0, q_stop) of the round
+    const uint32_t valid = 8u * (q_stop - round_q0);
+    const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.res + 8ull * round_q0, 4u * valid);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the slot writes have landed
+    __builtin_amdgcn_raw_buffer_store_b32(slots[lane], ro, 4u * lane, 0, 0);
+  };
+  auto finish = [&]() {
+    uint32_t R;
+    if (ABL & 2) {
+      R = group_xor(r[0] ^ r[1] ^ r[2] ^ r[3], 3);
+    } else {
+      uint32_t u = r[3];
+#pragma unroll
+      for (int i = 2; i >= 0; --i) u = mul_basis(u, a.XB) ^ r[i];
+      uint32_t acc[4] = {0u, 0u, 0u, 0u};  // u * x^(-128 s), basis rows from LDS
+#pragma unroll
+      for (int q4 = 0; q4 < 8; ++q4) {
+        const u32x4 b = *reinterpret_cast<const u32x4 *>(qrow + 4 * q4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[i] = and_xor((uint32_t)(((int32_t)(u << (31 - (4 * q4 + i)))) >> 31), b[i], acc[i]);
+      }
+      R = group_xor(xor3(acc[0], acc[1], acc[2] ^ acc[3]), 3);
+      // x^(-8 tz), distributed: lane s takes bits 4s..4s+3 of R; basis word
+      // 4s from LDS, 4s+1..4s+3 by successive x^-1.
+      const uint32_t tz = 128u * fd_L - fd_a - fd_M;
+      uint32_t bw = tzl[8u * tz + s], p = 0;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)R, (int)(4u * s + t), 1);
+        p = and_xor(m, bw, p);
+        bw = and_xor((uint32_t)((int32_t)bw >> 31), kXInv, bw << 1);
+      }
+      R = group_xor(p, 3);
+    }
+    slots[((fd_q - round_q0) << 3) | g] = ~R;
+    if (fd_q + 1 - round_q0 == kRound) {  // wave-uniform
+      flush(fd_q + 1);
+      round_q0 = fd_q + 1;
+    }
+  };
+
+  bool done = false;
+  while (!done) {
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      __builtin_amdgcn_sched_barrier(0);
+      u32x4 w = ring[u];
+      if (fd_k == 0 || (fd_k == 1 && fd_head2) || fd_k + 1 == fd_L) {  // wave-uniform
+        const int rel0 = (int)(128u * fd_k + 16u * s) - (int)fd_a;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) w[i] = edge_word(w[i], rel0 + 4 * i, (int)fd_M);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t x = r[i] ^ w[i];
+        if (ABL & 1) {
+          r[i] = __builtin_amdgcn_perm(x, lt.lo0, 0x0C0C0400u) ^ (x >> 7);
+        } else {
+          const uint32_t t3 = lds_at(lds, __builtin_amdgcn_perm(x, lt.lo0, 0x0C0C0400u));
+          const uint32_t t2 = lds_at(lds, __builtin_amdgcn_perm(x, lt.lo0, 0x0C0C0500u) + 128);
+          const uint32_t t1 = lds_at(lds, __builtin_amdgcn_perm(x, lt.lo1, 0x0C020600u));
+          const uint32_t t0 = lds_at(lds, __builtin_amdgcn_perm(x, lt.lo1, 0x0C020700u) + 128);
+          r[i] = xor3(t3, t2, t1 ^ t0);
+        }
+      }
+      if (++fd_k == fd_L) {  // wave-uniform: group fd_q folded
+        finish();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) r[i] = 0u;
+        fd_k = 0;
+        if (fd_q + 1 < q_end) {
+          ++fd_q;
+          fd_enter(fd_q);
+          fd_head2 = __ballot(fd_a > 88u) != 0;
+        } else {
+          done = true;
+          fd_L = 0xFFFFFFFFu;
+        }
+      }
+      // Refill after folding: the FIFO entry the fold just read may be
+      // rewritten by this step's load-cursor advance.
+      ring[u] = ld_issue();
+      ld_advance();
+    }
+  }
+  if (q_end != round_q0) flush(q_end);
+}
+
+uint64_t rs_workspace_bytes(uint64_t count) {
+  const uint64_t npos = count + 8ull * kRsClasses;
+  auto al = [](uint64_t b) { return (b + 255) & ~255ull; };
+  return 3 * al(4ull * kRsClasses) + al(sizeof(RsPlan)) + al(sizeof(RsDesc) * npos) + al(4 * count) + al(4 * npos) +
+         al(4ull * kRsClasses * kPassBlocks);
+}
+
+void rs_bind_workspace(RsckArgs &a, void *ws) {
+  const uint64_t npos = a.count + 8ull * kRsClasses;
+  auto al = [](uint64_t b) { return (b + 255) & ~255ull; };
+  char *p = static_cast<char *>(ws);
+  a.counts = reinterpret_cast<uint32_t *>(p), p += al(4ull * kRsClasses);
+  a.cursor = reinterpret_cast<uint32_t *>(p), p += al(4ull * kRsClasses);
+  a.bucket = reinterpret_cast<uint32_t *>(p), p += al(4ull * kRsClasses);
+  a.plan = reinterpret_cast<RsPlan *>(p), p += al(sizeof(RsPlan));
+  a.desc = reinterpret_cast<RsDesc *>(p), p += al(sizeof(RsDesc) * npos);
+  a.pos_of = reinterpret_cast<uint32_t *>(p), p += al(4 * a.count);
+  a.res = reinterpret_cast<uint32_t *>(p), p += al(4 * npos);
+  a.hist = reinterpret_cast<uint32_t *>(p);
+}
+
+hipError_t launch_rsck(RsckArgs &a, int grid, hipStream_t st) {
+  if (a.count == 0) return hipSuccess;
+  hipError_t e = hipMemsetAsync(a.counts, 0, 4ull * kRsClasses, st);
+  if (e != hipSuccess) return e;
+  const uint64_t want = (a.count + kPassBlock - 1) / kPassBlock;
+  const int pgrid = (int)(want < kPassBlocks ? want : kPassBlocks);
+  hipLaunchKernelGGL(rsck_count, dim3(pgrid), dim3(kPassBlock), 0, st, a);
+  hipLaunchKernelGGL(rsck_plan, dim3(1), dim3(1024), 0, st, a);
+  hipLaunchKernelGGL(rsck_scatter, dim3(pgrid), dim3(kPassBlock), 0, st, a);
+  hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, st, a);
+  hipLaunchKernelGGL(rsck_gather, dim3(pgrid), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace ricrc

@@ -167,3 +167,41 @@ def test_strided_chain_decomposition():
         want = o.icrc(pkt) ^ 0xFFFFFFFF
         assert flat == want
         assert horner == want
+
+
+def test_ragged_line_grid_decomposition():
+    """The ragged strided-chain kernel's algebra (icrc_rsck.hip): a packet at
+    any byte address is folded on the absolute 128-byte line grid -- lines
+    [A, A + 128 L), A = addr & ~127 -- with bytes outside the covered range
+    zeroed, the seed XORed into covered bytes 0..3 and the masks applied by
+    packet-relative offset.  Chains j = t mod 32 as in the fixed-size kernel;
+    lane s combines its 4 chains by Horner in x^-32 and multiplies by
+    x^(-128 s); the packet register is the XOR over lanes times x^(-8 tz),
+    tz = 128 L - a - M the zero tail of the last line."""
+    rng = random.Random(11)
+    X = _xinv8n_fast(4)
+    for _ in range(40):
+        n = rng.choice([44, 45, 60, 64, 100, 127, 128, 129, 256, 1000, 1500, 4096])
+        a = rng.randrange(128)
+        pkt = bytes(rng.randrange(256) for _ in range(n))
+        M = n - 4
+        L = (a + M + 127) // 128
+        body = masked(pkt)
+        stream = bytearray(128 * L)
+        stream[a:a + M] = body
+        for k in range(4):
+            stream[a + k] ^= (SEED_REG >> (8 * k)) & 0xFF
+        words = [int.from_bytes(stream[4 * t: 4 * t + 4], "little") for t in range(32 * L)]
+        chains = [0] * 32
+        for t, w in enumerate(words):
+            chains[t % 32] = o.crc_shift(chains[t % 32] ^ w, 128)
+        reg = 0
+        for s in range(8):
+            u = chains[4 * s + 3]
+            for i in (2, 1, 0):
+                u = o.gf_mul(u, X) ^ chains[4 * s + i]
+            reg ^= o.gf_mul(u, _xinv8n_fast(16 * s))
+        tz = 128 * L - a - M
+        assert 0 <= tz < 128
+        reg = o.gf_mul(reg, _xinv8n_fast(tz))
+        assert reg ^ 0xFFFFFFFF == o.icrc(pkt), (n, a)

@@ -129,15 +129,22 @@ def main():
             buf[ix] = rows[c:c + step].reshape(-1)
         del tmp, rows, starts
     out = torch.empty(count, dtype=torch.int32, device=dev)
-    ms = time_device(torch, ctx, lambda s: ctx.batch_device(buf, count, out, offsets=d_offs, lengths=d_lens,
-                                                             stream=s), reps, warm)
-    ns = 8192
-    span = int(offs[ns - 1] + lens[ns - 1])
-    check_sample(np, oracle_c, buf[:span].cpu().numpy(), offs[:ns], lens[:ns],
-                 out[:ns].cpu().numpy().view(np.uint32), "C4 ragged")
-    alg = nbytes + 16 * count
-    emit(path="device", kernel="ragged (C4 mix)", packets=count, bytes=nbytes, kernel_ms=round(ms, 4),
-         gib_s=round(nbytes / (ms * 1e-3) / 2**30, 1), hbm_frac=round(alg / (ms * 1e-3) / 8e12, 4))
+    for label, knob in (("ragged strided-chain (C4 mix)", None), ("ragged piece kernel (C4 mix)", "RICRC_NO_RSCK")):
+        if knob:
+            os.environ[knob] = "1"
+        try:
+            ms = time_device(torch, ctx, lambda s: ctx.batch_device(buf, count, out, offsets=d_offs,
+                                                                     lengths=d_lens, stream=s), reps, warm)
+        finally:
+            if knob:
+                os.environ.pop(knob, None)
+        ns = 8192
+        span = int(offs[ns - 1] + lens[ns - 1])
+        check_sample(np, oracle_c, buf[:span].cpu().numpy(), offs[:ns], lens[:ns],
+                     out[:ns].cpu().numpy().view(np.uint32), label)
+        alg = nbytes + 16 * count
+        emit(path="device", kernel=label, packets=count, bytes=nbytes, kernel_ms=round(ms, 4),
+             gib_s=round(nbytes / (ms * 1e-3) / 2**30, 1), hbm_frac=round(alg / (ms * 1e-3) / 8e12, 4))
     host_ragged = (buf.cpu().numpy(), offs, lens, out.cpu().numpy().view(np.uint32).copy())
     del buf, out, d_offs, d_lens
     torch.cuda.empty_cache()
