@@ -265,10 +265,16 @@ int launch_batch(Dev &d, const uint8_t *base, const uint64_t *off, const uint32_
     const uint32_t xi = gf_xinv8n(4);
     for (int j = 0; j < 32; ++j) k.XB[j] = gf_mul(xi, 1u << j);
     for (int s = 0; s < 8; ++s) k.QS[s] = gf_xinv8n(16ull * s);
+    RaggedArgs small{};
+    small.inv_tab = d.d_inv;
+    small.inv4 = reinterpret_cast<const u32x4_t *>(d.d_inv4);
+    for (uint32_t l = 0; l < 64; ++l) small.K[l] = x8n_host(64ull * (63 - l));
     void *ws = nullptr;
     HIP_TRY(hipMallocAsync(&ws, rs_workspace_bytes(count), st));
     rs_bind_workspace(k, ws);
-    const hipError_t e = launch_rsck(k, d.n_cu, st);
+    int rgrid = d.n_cu;
+    if (const char *e = getenv("RICRC_RSCK_GRID")) rgrid = std::max(1, std::min(rgrid, atoi(e)));  // tests
+    const hipError_t e = launch_rsck(k, small, rgrid, st);
     const hipError_t e2 = hipFreeAsync(ws, st);
     return hip_err(e != hipSuccess ? e : e2);
   }

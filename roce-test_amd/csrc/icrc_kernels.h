@@ -53,6 +53,13 @@ struct SckArgs {
   uint64_t *stamps;  // diagnostic builds only (tools/microbench); null in the product
 };
 
+// 8-byte descriptor in class order: lo = address bits 0..31, hi = address
+// bits 32..47 | n << 16 (device addresses are 48-bit, n <= 65535).  Padding
+// entries of a class's last group repeat the class's last packet.
+struct RsDesc {
+  uint32_t lo, hi;
+};
+
 // Ragged batches (any alignment, per-packet offsets and/or lengths): the
 // batch is cut into 64-byte pieces, packet by packet -- packet i covers
 // pieces [ps[i], ps[i+1]) laid from its start rounded down to 16 B -- and a
@@ -73,6 +80,10 @@ struct RaggedArgs {
   uint32_t verify;
   uint32_t P;              // pieces per packet when ps == null
   uint32_t K[64];          // x^(8*64*(63-lane)): lane piece end -> step end
+  // Descriptor mode (the small packets of the ragged strided-chain path):
+  // packet i is desc[i], the count is *dev_count (device memory).
+  const RsDesc *desc;
+  const uint32_t *dev_count;
 };
 
 // Pieces of a packet of n bytes whose L3 header starts at address `start`:
@@ -87,20 +98,21 @@ __host__ __device__ inline uint32_t ragged_pieces(uintptr_t start, uint32_t n) {
 // Ragged strided-chain path (icrc_rsck.hip): any packet addresses and
 // lengths, packets bucketed by their number of 128-byte lines on the device,
 // 8 packets of equal line count per group, folded as in the SCK.
-constexpr int kRsClasses = 514;  // lines per packet 1..513 (n <= 65535, any start offset)
-// 8-byte descriptor in class order: lo = address bits 0..31, hi = address
-// bits 32..47 | n << 16 (device addresses are 48-bit, n <= 65535).  Padding
-// entries of a class's last group repeat the class's last packet.
-struct RsDesc {
-  uint32_t lo, hi;
-};
+// Classes: 0 = not bucketed (n < 44 or n > 65535: done in the count pass);
+// 1 + P for packets spanning <= kRsSmallL lines, by their 64-byte piece count P
+// (they go to the piece kernel: 8 lanes per packet is too coarse for them);
+// kRsBigBase + L for the rest, by line count L (the strided-chain fold).
+constexpr int kRsSmallL = 3;
+constexpr int kRsBigBase = 8;                  // small classes 2..8 (P <= 7 for L <= 3)
+constexpr int kRsClasses = kRsBigBase + 514;   // L <= 513 (n <= 65535, any start offset)
 struct RsPlan {
-  uint32_t nc;        // non-empty classes
+  uint32_t nc;        // non-empty big classes
   uint32_t ngroups;   // 8-packet groups over all classes
   uint64_t nsteps;    // weighted work over all groups: lines + a per-group finish cost
   uint32_t L[kRsClasses];   // compact, ascending
   uint32_t g0[kRsClasses];  // first group of the class
   uint64_t s0[kRsClasses];  // weighted work before the class's first group
+  uint64_t ps0[kRsClasses]; // small classes: first piece of the class (by class index)
 };
 struct RsckArgs {
   const uint8_t *base;
@@ -121,6 +133,8 @@ struct RsckArgs {
   uint32_t *pos_of;   // [count] position of packet i, or ~0 (written by the scatter pass)
   uint32_t *res;      // [count + 8 kRsClasses] results in class order
   uint32_t *hist;     // [pass blocks][kRsClasses] per-block class counts
+  uint64_t *ps;       // [count + 8 kRsClasses + 1] piece prefix of the small region
+  uint32_t *small_pos;  // positions of the small region (device count for the piece kernel)
   const uint32_t *tzb;  // [128][8]: words 0, 4, ..., 28 of the basis of x^(-8 tz)
   uint32_t XB[32];      // basis of x^-32
   uint32_t QS[8];       // x^(-8*16 s): lane slot s -> line start
@@ -129,7 +143,8 @@ uint64_t rs_workspace_bytes(uint64_t count);
 // Carves the workspace (rs_workspace_bytes(count) bytes at ws) into a.
 void rs_bind_workspace(RsckArgs &a, void *ws);
 // The whole ragged pipeline on `st`: count/classify, plan, scatter, fold, gather.
-hipError_t launch_rsck(RsckArgs &a, int grid, hipStream_t st);
+// `small` carries the piece kernel's tables (inv_tab, inv4, K) for the small packets.
+hipError_t launch_rsck(RsckArgs &a, const RaggedArgs &small, int grid, hipStream_t st);
 
 struct SynthArgs {
   uint8_t *buf;

@@ -781,7 +781,8 @@ __device__ __forceinline__ uint32_t wave_prefix_xor(uint32_t v, uint32_t lane) {
 // descriptor loads, then folds step i -- every global load has one step of
 // slack.  Loads are unconditional (lanes without a unit read a device table
 // the kernel owns) so the compiler counts vmcnt instead of draining at a
-// branch join.  MODE: 0 uniform (no descriptors), 1 offsets + lengths,
+// branch join.  MODE: 4 RsDesc descriptors + device-side count (the small
+// packets of the ragged strided-chain path), 0 uniform (no descriptors), 1 offsets + lengths,
 // 2 offsets only, 3 lengths only.
 // ABL: timing-only ablation mask for tools/microbench/ragged_abl.hip (the
 // product instantiates 0): 1 no table fold, 2 no finish slices, 4 no piece
@@ -790,6 +791,7 @@ __device__ __forceinline__ uint32_t wave_prefix_xor(uint32_t v, uint32_t lane) {
 template <int MODE, int kRaggedBlock, int ABL = 0>
 __global__ __launch_bounds__(kRaggedBlock) void icrc_ragged_kernel(RaggedArgs a) {
   constexpr bool UNI = MODE == 0, HAS_OFF = MODE == 1 || MODE == 2, HAS_LEN = MODE == 1 || MODE == 3;
+  constexpr bool DESC = MODE == 4;
   // 128 KiB slice tables + the lanes' alignment bases (8 KiB, shared by all
   // waves: word 4q+i of lane l's basis at 16-byte slot q*64 + l, so the
   // eight ds_read_b128 of a multiply are conflict-free).
@@ -823,14 +825,15 @@ __global__ __launch_bounds__(kRaggedBlock) void icrc_ragged_kernel(RaggedArgs a)
   const uint64_t wave = (uint64_t)blockIdx.x * (kRaggedBlock / 64) + (threadIdx.x >> 6);
   const uint64_t nwaves = (uint64_t)gridDim.x * (kRaggedBlock / 64);
   auto PS = [&](uint64_t i) -> uint64_t { return UNI ? i * (uint64_t)a.P : a.ps[i]; };
+  const uint64_t count = DESC ? (uint64_t)*a.dev_count : a.count;
 
   // This wave's packets: those whose first piece lies in its share.
-  const uint64_t total = PS(a.count);
+  const uint64_t total = PS(count);
   const uint64_t share = (total + nwaves - 1) / nwaves;
   const uint64_t q_lo = min(wave * share, total), q_hi = min(q_lo + share, total);
   auto lower_bound = [&](uint64_t x) -> uint64_t {  // first packet p with PS(p) >= x
     if (UNI) return (x + a.P - 1) / a.P;
-    uint64_t lo = 0, hi = a.count;  // PS(count) = total >= x
+    uint64_t lo = 0, hi = count;  // PS(count) = total >= x
     while (hi - lo > 64) {  // 64-ary search, one probe per lane
       const uint64_t step = (hi - lo + 63) / 64;
       const uint64_t probe = min(lo + step * (lane + 1), hi);
@@ -862,8 +865,14 @@ __global__ __launch_bounds__(kRaggedBlock) void icrc_ragged_kernel(RaggedArgs a)
     Desc d;
     const int64_t r64 = (int64_t)((in ? PS(pjc) : g_end) - gstep);
     d.rel = r64 > 64 ? 64 : (int32_t)r64;
-    d.start = (uintptr_t)a.base + (HAS_OFF ? a.off[pjc] : pjc * a.stride) + a.l3_offset;
-    d.n = HAS_LEN ? a.len[pjc] : a.fixed_len;
+    if (DESC) {
+      const RsDesc dd = a.desc[pjc];
+      d.start = (uintptr_t)(((uint64_t)(dd.hi & 0xFFFFu) << 32) | dd.lo);
+      d.n = dd.hi >> 16;
+    } else {
+      d.start = (uintptr_t)a.base + (HAS_OFF ? a.off[pjc] : pjc * a.stride) + a.l3_offset;
+      d.n = HAS_LEN ? a.len[pjc] : a.fixed_len;
+    }
     return d;
   };
 
@@ -1041,7 +1050,7 @@ __global__ __launch_bounds__(kRaggedBlock) void icrc_ragged_kernel(RaggedArgs a)
           sink ^= o;
         } else {
           const __amdgpu_buffer_rsrc_t out_rsrc =
-              make_rsrc(a.out, a.count < (1ull << 30) ? (uint32_t)a.count * 4u : 0xFFFFFFF0u);
+              make_rsrc(a.out, count < (1ull << 30) ? (uint32_t)count * 4u : 0xFFFFFFF0u);
           __builtin_amdgcn_raw_buffer_store_b32(o, out_rsrc, (int)ooff, 0, 0);
         }
         break;
@@ -1115,7 +1124,7 @@ __global__ __launch_bounds__(kRaggedBlock) void icrc_ragged_kernel(RaggedArgs a)
   }
 #pragma unroll
   for (int sl = 0; sl < 8; ++sl) fin_slice(prev, sl);
-  if (ABL & 32) a.out[wave % a.count] = sink;
+  if (ABL & 32) a.out[wave % count] = sink;
 }
 
 // =======================================================================
@@ -1219,7 +1228,8 @@ hipError_t launch_sck(const SckArgs &a, int grid, hipStream_t st) {
 
 hipError_t launch_ragged(const RaggedArgs &a, int grid, hipStream_t st) {
   const dim3 b(1024);
-  if (!a.ps) hipLaunchKernelGGL((icrc_ragged_kernel<0, 1024>), dim3(grid), b, 0, st, a);
+  if (a.desc) hipLaunchKernelGGL((icrc_ragged_kernel<4, 1024>), dim3(grid), b, 0, st, a);
+  else if (!a.ps) hipLaunchKernelGGL((icrc_ragged_kernel<0, 1024>), dim3(grid), b, 0, st, a);
   else if (a.off && a.len) hipLaunchKernelGGL((icrc_ragged_kernel<1, 1024>), dim3(grid), b, 0, st, a);
   else if (a.off) hipLaunchKernelGGL((icrc_ragged_kernel<2, 1024>), dim3(grid), b, 0, st, a);
   else hipLaunchKernelGGL((icrc_ragged_kernel<3, 1024>), dim3(grid), b, 0, st, a);

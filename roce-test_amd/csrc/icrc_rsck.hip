@@ -18,12 +18,16 @@
 //                   a first step (line);
 //  3. rsck_scatter  writes each packet's descriptor {addr, n, idx} into its
 //                   class bucket (block-aggregated atomics) and its position;
-//  4. icrc_rsck_kernel  folds groups of 8 equal-L packets exactly like the
+//  4. icrc_rsck_kernel  folds groups of 8 equal-L packets (L > kRsSmallL)
+//                   exactly like the
 //                   SCK -- lane 8g+s owns slot s of every line of packet g,
 //                   four chains per lane, T_124..T_127 tables in LDS -- with
 //                   a load cursor running 8 lines ahead of the fold cursor
 //                   across group boundaries (groups of 64-byte packets are
 //                   one line long), descriptors read 64 at a time;
+//     icrc_ragged_kernel<4> folds the small packets (<= kRsSmallL lines; 8
+//                   lanes per packet is too coarse for them), bucketed by
+//                   64-byte piece count so their piece prefix is arithmetic;
 //  5. rsck_gather   out[i] = res[pos(i)] (verify mode: the trailer compared
 //                   with it).
 //
@@ -57,10 +61,15 @@ __device__ __forceinline__ void rs_packet(const RsckArgs &a, uint64_t i, uint64_
   n = a.len ? a.len[i] : a.fixed_len;
 }
 
-// Lines of the absolute grid a packet's covered bytes span; 0 = not folded here.
+// Class of a packet (icrc_kernels.h): by 128-byte lines of the absolute grid
+// its covered bytes span, or, for packets of <= kRsSmallL lines, by 64-byte
+// pieces; 0 = not bucketed.
 __device__ __forceinline__ uint32_t rs_class(uint64_t addr, uint32_t n) {
   if (n < kMinLen || n > kMaxLen) return 0u;
-  return (uint32_t)(((addr & 127u) + (n - 4u) + 127u) >> 7);
+  const uint32_t M = n - 4u;
+  const uint32_t L = (uint32_t)(((addr & 127u) + M + 127u) >> 7);
+  if (L <= (uint32_t)kRsSmallL) return 1u + (uint32_t)(((addr & 15u) + M + 63u) >> 6);
+  return (uint32_t)kRsBigBase + L;
 }
 
 // ICRC of a packet shorter than a RoCEv2 header (4 <= n < 44): Sarwate loop.
@@ -122,38 +131,50 @@ __global__ __launch_bounds__(kPassBlock) void rsck_count(RsckArgs a) {
   }
 }
 
-// One workgroup: exclusive scans of groups, steps and non-empty classes.
+// One workgroup: exclusive scans over the classes of groups (bucket
+// positions), of weighted work and of the non-empty big classes (the fold's
+// class table), and of pieces of the small classes (the piece kernel's prefix).
 __global__ __launch_bounds__(1024) void rsck_plan(RsckArgs a) {
   __shared__ uint32_t sg[1024], sf[1024];
-  __shared__ uint64_t ss[1024];
+  __shared__ uint64_t ss[1024], sp[1024];
   const uint32_t t = threadIdx.x;
   const uint32_t cnt = (t >= 1 && t < (uint32_t)kRsClasses) ? a.counts[t] : 0u;
-  const uint32_t G = (cnt + 7u) >> 3, f = cnt ? 1u : 0u;
-  const uint64_t S = (uint64_t)G * (t + kGroupCost);
+  const bool big = t > (uint32_t)kRsBigBase;
+  const uint32_t G = (cnt + 7u) >> 3, f = (big && cnt) ? 1u : 0u;
+  const uint32_t L = big ? t - (uint32_t)kRsBigBase : 0u;
+  const uint64_t S = big ? (uint64_t)G * (L + kGroupCost) : 0u;
+  const uint64_t PC = big ? 0u : 8ull * G * (t >= 1 ? t - 1 : 0);  // small class t: pieces of t - 1 each
   sg[t] = G;
   sf[t] = f;
   ss[t] = S;
+  sp[t] = PC;
   __syncthreads();
   for (uint32_t d = 1; d < 1024; d <<= 1) {
     const uint32_t g2 = t >= d ? sg[t - d] : 0u, f2 = t >= d ? sf[t - d] : 0u;
-    const uint64_t s2 = t >= d ? ss[t - d] : 0u;
+    const uint64_t s2 = t >= d ? ss[t - d] : 0u, p2 = t >= d ? sp[t - d] : 0u;
     __syncthreads();
     sg[t] += g2;
     sf[t] += f2;
     ss[t] += s2;
+    sp[t] += p2;
     __syncthreads();
   }
   const uint32_t g0 = sg[t] - G, ci = sf[t] - f;
-  const uint64_t s0 = ss[t] - S;
+  const uint64_t s0 = ss[t] - S, p0 = sp[t] - PC;
   RsPlan *P = a.plan;
   if (f) {
-    P->L[ci] = t;
+    P->L[ci] = L;
     P->g0[ci] = g0;
     P->s0[ci] = s0;
   }
   if (t < (uint32_t)kRsClasses) {
     a.bucket[t] = 8u * g0;
     a.cursor[t] = 0u;
+    P->ps0[t] = p0;
+  }
+  if (t == (uint32_t)kRsBigBase + 1) {  // end of the small region (all small classes come first)
+    *a.small_pos = 8u * g0;
+    a.ps[8u * g0] = p0;
   }
   if (t == 1023) {
     P->nc = sf[t];
@@ -186,11 +207,18 @@ __global__ __launch_bounds__(kPassBlock) void rsck_scatter(RsckArgs a) {
       if (c) {
         const uint32_t pos = base[c] + r;
         const RsDesc d{(uint32_t)addr, (uint32_t)(addr >> 32) | (n << 16)};
+        const bool small = c <= (uint32_t)kRsBigBase;
+        const uint64_t psb = small ? a.plan->ps0[c] : 0u;
+        const uint32_t bk = a.bucket[c];
         a.desc[pos] = d;
         a.pos_of[i] = pos;
-        const uint32_t end = a.bucket[c] + a.counts[c];
+        if (small) a.ps[pos] = psb + (uint64_t)(pos - bk) * (c - 1u);
+        const uint32_t end = bk + a.counts[c];
         if (pos + 1 == end)  // the class's last packet pads its group with copies of itself
-          for (uint32_t p = end; (p - a.bucket[c]) & 7u; ++p) a.desc[p] = d;
+          for (uint32_t p = end; (p - bk) & 7u; ++p) {
+            a.desc[p] = d;
+            if (small) a.ps[p] = psb + (uint64_t)(p - bk) * (c - 1u);
+          }
       } else {
         a.pos_of[i] = 0xFFFFFFFFu;
       }
@@ -470,7 +498,7 @@ uint64_t rs_workspace_bytes(uint64_t count) {
   const uint64_t npos = count + 8ull * kRsClasses;
   auto al = [](uint64_t b) { return (b + 255) & ~255ull; };
   return 3 * al(4ull * kRsClasses) + al(sizeof(RsPlan)) + al(sizeof(RsDesc) * npos) + al(4 * count) + al(4 * npos) +
-         al(4ull * kRsClasses * kPassBlocks);
+         al(4ull * kRsClasses * kPassBlocks) + al(8 * (npos + 1)) + al(4);
 }
 
 void rs_bind_workspace(RsckArgs &a, void *ws) {
@@ -484,10 +512,12 @@ void rs_bind_workspace(RsckArgs &a, void *ws) {
   a.desc = reinterpret_cast<RsDesc *>(p), p += al(sizeof(RsDesc) * npos);
   a.pos_of = reinterpret_cast<uint32_t *>(p), p += al(4 * a.count);
   a.res = reinterpret_cast<uint32_t *>(p), p += al(4 * npos);
-  a.hist = reinterpret_cast<uint32_t *>(p);
+  a.hist = reinterpret_cast<uint32_t *>(p), p += al(4ull * kRsClasses * kPassBlocks);
+  a.ps = reinterpret_cast<uint64_t *>(p), p += al(8 * (npos + 1));
+  a.small_pos = reinterpret_cast<uint32_t *>(p);
 }
 
-hipError_t launch_rsck(RsckArgs &a, int grid, hipStream_t st) {
+hipError_t launch_rsck(RsckArgs &a, const RaggedArgs &small, int grid, hipStream_t st) {
   if (a.count == 0) return hipSuccess;
   hipError_t e = hipMemsetAsync(a.counts, 0, 4ull * kRsClasses, st);
   if (e != hipSuccess) return e;
@@ -497,6 +527,20 @@ hipError_t launch_rsck(RsckArgs &a, int grid, hipStream_t st) {
   hipLaunchKernelGGL(rsck_plan, dim3(1), dim3(1024), 0, st, a);
   hipLaunchKernelGGL(rsck_scatter, dim3(pgrid), dim3(kPassBlock), 0, st, a);
   hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, st, a);
+  RaggedArgs r = small;  // the small region [0, *small_pos) of the buckets: piece kernel, ICRCs into res
+  r.base = nullptr;
+  r.off = nullptr;
+  r.len = nullptr;
+  r.ps = a.ps;
+  r.desc = a.desc;
+  r.dev_count = a.small_pos;
+  r.count = 0;
+  r.out = a.res;
+  r.verify = 0;  // verify mode is applied by the gather pass
+  r.fixed_len = 0;
+  r.l3_offset = 0;
+  e = launch_ragged(r, grid, st);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(rsck_gather, dim3(pgrid), dim3(256), 0, st, a);
   return hipGetLastError();
 }

@@ -333,3 +333,43 @@ def test_strided_chain_kernel(ctx, monkeypatch, n, count, grid):
     out2 = _out(count)
     ctx.batch_device(d, count, out2, stride=n, stream=_stream())
     np.testing.assert_array_equal(_host_u32(out2), want)
+
+
+@pytest.mark.parametrize("grid", [None, 1])
+def test_ragged_strided_chain_mixed(ctx, monkeypatch, grid):
+    """Ragged strided-chain path: lengths from 44 B to 9 KiB, start offsets of
+    any alignment (bytes before the first packet and between packets), so every
+    line-count class, the small-packet classes (piece kernel) and byte-granular
+    head/tail masks occur; with the fold grid capped to one workgroup each wave
+    crosses many descriptor blocks and result rounds.  Verify mode on the same
+    batch with a few corrupted packets."""
+    if grid is not None:
+        monkeypatch.setenv("RICRC_RSCK_GRID", str(grid))
+    rng = np.random.default_rng(7)
+    count = 6000
+    lens = rng.integers(44, 9001, size=count).astype(np.uint32)
+    pick = rng.random(count) < 0.3  # a share of the BASELINE mix sizes
+    lens[pick] = rng.choice(np.array([64, 256, 1024, 4096], np.uint32), size=int(pick.sum()))
+    gaps = rng.integers(0, 200, size=count).astype(np.uint64)
+    offs = np.zeros(count, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + gaps[:-1])
+    offs += 37
+    total = int(offs[-1] + lens[-1]) + 64
+    buf = rng.integers(0, 256, size=total, dtype=np.uint8)
+    want = oracle_c.icrc_batch(buf, offsets=offs, lengths=lens, threads=8)
+    d, d_off, d_len = _dev(buf), _dev(offs.view(np.int64)), _dev(lens.view(np.int32))
+    out = _out(count)
+    ctx.batch_device(d, count, out, offsets=d_off, lengths=d_len, stream=_stream())
+    np.testing.assert_array_equal(_host_u32(out), want)
+    # verify: stamp every packet, corrupt every 11th in an unmasked covered byte
+    stamped = buf.copy()
+    for i in range(count):
+        o, n = int(offs[i]), int(lens[i])
+        stamped[o + n - 4:o + n] = np.frombuffer(int(want[i]).to_bytes(4, "little"), np.uint8)
+    bad = np.arange(0, count, 11)
+    for i in bad:
+        stamped[int(offs[i]) + 41] ^= 0x01
+    ctx.batch_device(_dev(stamped), count, out, offsets=d_off, lengths=d_len, stream=_stream(), verify=True)
+    exp = np.ones(count, np.uint32)
+    exp[bad] = 0
+    np.testing.assert_array_equal(_host_u32(out), exp)
