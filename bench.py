@@ -50,11 +50,14 @@ def parse():
 
 
 def kernel_source_hash():
-    """sha256 of the kernel source: PMC traffic measured on other code is stale."""
+    """sha256 of the headline kernel's sources: PMC traffic measured on other code is stale."""
     import hashlib
 
-    with open(os.path.join(ROOT, "roce-test_amd", "csrc", "icrc_kernels.hip"), "rb") as f:
-        return hashlib.sha256(f.read()).hexdigest()[:16]
+    h = hashlib.sha256()
+    for name in ("icrc_kernels.hip", "icrc_device.h", "icrc_math.h", "icrc_kernels.h"):
+        with open(os.path.join(ROOT, "roce-test_amd", "csrc", name), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
 
 
 def load_traffic(size, count):
