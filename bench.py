@@ -42,8 +42,9 @@ def parse():
     ap.add_argument("--count", type=int, default=1 << 20, help="packets per GPU")
     ap.add_argument("--size", type=int, default=4096, help="L3 packet bytes (IPv4 total_len)")
     ap.add_argument("--no-gather", action="store_true", help="skip the RCCL all-gather at N>1")
-    ap.add_argument("--overlap-gather", action="store_true",
-                    help="run step i's all-gather async, overlapping step i+1's kernel (default: in-stream)")
+    ap.add_argument("--in-stream-gather", dest="overlap_gather", action="store_false",
+                    help="order step i's all-gather after its kernel on the compute stream "
+                         "(default: async on RCCL's stream, overlapping step i+1's kernel)")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="wall budget of the CPU baseline")
     ap.add_argument("--no-cpu", action="store_true")
     return ap.parse_args()
@@ -139,12 +140,13 @@ def main():
     # world*count): generated on its own device from the global index.
     ctx.synth_device(pk, SEED, rank * count, count, size, stream=stream)
     do_gather = distributed and not args.no_gather
-    # Double-buffered results.  Default: the all-gather is ordered after the
-    # kernel on the compute stream.  --overlap-gather: step i's all-gather
-    # runs async on RCCL's stream, overlapping step i+1's kernel, and a buffer
-    # is reused only after the gather that read it has been waited for.  (Each
-    # ICRC block fills a whole CU's LDS, so RCCL blocks compete for whole CUs;
-    # measured in DESIGN.md.)
+    # Double-buffered results.  Default: step i's all-gather runs async on
+    # RCCL's stream, overlapping step i+1's kernel, and a buffer is reused only
+    # after the gather that read it has been waited for.  --in-stream-gather:
+    # the gather is ordered after the kernel on the compute stream.  (Each ICRC
+    # workgroup fills a whole CU, so the kernel's blocks on CUs that RCCL holds
+    # start late: measured +3-6 % kernel time with 16-32 CUs held for
+    # 100-150 us, against a fully exposed gather in-stream)
     outs = [torch.empty(count, dtype=torch.int32, device=dev) for _ in range(2)]
     gathered = [torch.empty(world * count, dtype=torch.int32, device=dev) for _ in range(2)] if do_gather else None
     pending = [None, None]

@@ -27,6 +27,7 @@ namespace {
 
 constexpr uint64_t kStageBytes = 256ull << 20;  // per staging slot (bytes of packets)
 constexpr uint64_t kStagePkts = 1ull << 20;     // per staging slot (packets)
+constexpr uint32_t kWorkSlots = 64;
 
 struct Slot {
   uint8_t *d_buf = nullptr;
@@ -48,6 +49,8 @@ struct Dev {
   uint32_t *d_inv = nullptr;   // x^(-8 z), z <= 4096
   uint32_t *d_inv4 = nullptr;  // t: x^(8 (k - t)), k = 0..3, t <= 4096
   uint32_t *d_tzb = nullptr;   // [128][8]: basis words 4q of x^(-8 tz) (ragged strided-chain path)
+  uint32_t *d_work = nullptr;  // kWorkSlots x {group counter, finished waves} (dynamic SCK schedule)
+  uint32_t work_next = 0;      // round-robin slot: launches in flight on different streams never share one
   Slot slot[2];
   bool staged = false;
 };
@@ -124,6 +127,8 @@ int init_dev(Dev &d) {
   }
   HIP_TRY(hipMalloc(&d.d_tzb, tzb.size() * sizeof(uint32_t)));
   HIP_TRY(hipMemcpy(d.d_tzb, tzb.data(), tzb.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  HIP_TRY(hipMalloc(&d.d_work, kWorkSlots * 2 * sizeof(uint32_t)));
+  HIP_TRY(hipMemset(d.d_work, 0, kWorkSlots * 2 * sizeof(uint32_t)));
   return 0;
 }
 
@@ -157,6 +162,7 @@ void free_dev(Dev &d) {
   (void)hipFree(d.d_inv);
   (void)hipFree(d.d_inv4);
   (void)hipFree(d.d_tzb);
+  (void)hipFree(d.d_work);
   if (d.stream) (void)hipStreamDestroy(d.stream);
 }
 
@@ -219,6 +225,11 @@ int launch_batch(Dev &d, const uint8_t *base, const uint64_t *off, const uint32_
           const uint32_t xi = gf_xinv8n(4);
           for (int j = 0; j < 32; ++j) k.XB[j] = gf_mul(xi, 1u << j);
           for (int s = 0; s < 8; ++s) k.QS[s] = gf_xinv8n(16ull * s + 4);
+          // Dynamic schedule (groups from a device counter): robust when other
+          // kernels (RCCL) hold CUs while this one starts.  RICRC_SCK_STATIC=1:
+          // contiguous per-wave blocks.
+          k.dynamic = getenv("RICRC_SCK_DYNAMIC") != nullptr ? 1u : 0u;
+          k.work = d.d_work + 2 * (d.work_next++ % kWorkSlots);
           return hip_err(launch_sck(k, sgrid, st));
         }
       }

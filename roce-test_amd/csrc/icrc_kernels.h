@@ -50,6 +50,8 @@ struct SckArgs {
   uint32_t verify;
   uint32_t XB[32];   // basis of x^-32 (Horner step between a lane's chains)
   uint32_t QS[8];    // x^(-32 (4 s + 1)): lane slot s's chain 0 -> packet end
+  uint32_t *work;    // dynamic schedule: {group counter, finished waves}, zero between launches
+  uint32_t dynamic;  // 1: groups from the counter (see icrc_sck_kernel), 0: static blocks
   uint64_t *stamps;  // diagnostic builds only (tools/microbench); null in the product
 };
 

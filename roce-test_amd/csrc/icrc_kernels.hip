@@ -514,15 +514,18 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
 // D: lines in flight per wave; QLDS: lane bases read from LDS instead of 32
 // VGPRs (frees registers for a deeper ring).
 // =======================================================================
-template <int L, int ABL, int D = 8, bool QLDS = false>
+template <int L, int ABL, int D = 8, bool QLDS = false, bool DYN = false>
 __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
-  // 128 KiB of tables + result slots per wave (+ the 8 lane bases, QLDS).
-  constexpr uint32_t kSlots = QLDS ? 256 : 512;
+  // 128 KiB of tables + result slots per wave (+ DYN: the slots' group
+  // indices; QLDS: the 8 lane bases).
+  constexpr uint32_t kSlots = (QLDS || DYN) ? 256 : 512;
+  constexpr uint32_t kRoundMask = kSlots / 8 - 1;  // groups per round of slots - 1
+  constexpr uint32_t kWaveWords = kSlots + (DYN ? kSlots / 8 : 0);
   constexpr uint32_t kQStride = 36;  // words per lane-slot basis (padded: conflict-free ds_read_b128)
-  __shared__ uint32_t lds[kLdsWords + kWaves * kSlots + (QLDS ? 8 * kQStride : 0)];
+  __shared__ uint32_t lds[kLdsWords + kWaves * kWaveWords + (QLDS ? 8 * kQStride : 0)];
 
   // D: lines in flight per wave
-  static_assert(L % D == 0, "ring indices must repeat every group");
+  static_assert(L % D == 0 || D == L, "ring indices must repeat every group");
   constexpr uint32_t N = 128u * L, GB = 8u * N;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -530,20 +533,47 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
 
   const uint64_t wave = (uint64_t)blockIdx.x * kWaves + wid;
   const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
-  const uint64_t G = (a.count + 7) >> 3;
-  const uint64_t per = (G + nwaves - 1) / nwaves;
-  const uint64_t g0 = wave * per < G ? wave * per : G;
-  const uint64_t g1 = g0 + per < G ? g0 + per : G;
-  const uint32_t ng = (uint32_t)(g1 - g0);
-  const uint64_t b0 = g0 * GB, b1 = g1 * GB < a.count * N ? g1 * GB : a.count * N;
-  const __amdgpu_buffer_rsrc_t rs = make_rsrc(a.base + (ng ? b0 : 0), ng ? (uint32_t)(b1 - b0) : 0u);
+  const uint32_t G = (uint32_t)((a.count + 7) >> 3);
+  const uint64_t total = a.count * N;
   const uint32_t vo = (lane >> 3) * N + 16u * s;
 
-  // Line k (0 <= k < L + D) of local group q; k >= L is the next group's.
-  auto load = [&](uint32_t q, int k) -> u32x4 {
-    if (ABL & 8) return u32x4{q * 977u + (uint32_t)k, lane, q, 5u};
-    return __builtin_bit_cast(
-        u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 128u * (uint32_t)(k % L), (q + (uint32_t)(k / L)) * GB, 2));
+  // The wave's sequence of groups.  Static: the contiguous block [g0, g1).
+  // DYN: groups taken one at a time from a device counter (a.work[0]) with
+  // two grabs in flight, so a workgroup that starts late -- its CU held by
+  // RCCL's all-gather of the previous step -- simply takes fewer groups; the
+  // last wave to finish resets the counter for the next launch.  A buffer
+  // atomic whose other 63 lanes fall outside the range-checked record keeps
+  // the grab free of exec masking.
+  const __amdgpu_buffer_rsrc_t wrs = make_rsrc(a.work, 8u);
+  // grab(): the raw per-lane result (lane 0 holds the value); it is made
+  // wave-uniform only one group later, when it is needed -- reading it at
+  // once would drain vmcnt(0) at every group end.
+  auto grab = [&]() -> uint32_t {
+    return (uint32_t)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, wrs, lane == 0 ? 0u : 0x7FFFFFF0u, 0, 0);
+  };
+  auto uni = [](uint32_t v) -> uint32_t { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
+  uint32_t g0 = 0, g1 = 0, qcur, qnext, qpend = 0;
+  if (DYN) {
+    qcur = grab();
+    qnext = grab();
+    qpend = grab();
+    qcur = uni(qcur);
+    qnext = uni(qnext);
+  } else {
+    const uint64_t per = (G + nwaves - 1) / nwaves;
+    g0 = (uint32_t)(wave * per < G ? wave * per : G);
+    g1 = (uint32_t)(g0 + per < G ? g0 + per : G);
+    qcur = g0 < g1 ? g0 : G;
+    qnext = g0 + 1 < g1 ? g0 + 1 : G;
+  }
+
+  // Line `line` of absolute group q (q >= G: no group, the range check reads zeros).
+  auto load = [&](uint32_t q, uint32_t line) -> u32x4 {
+    if (ABL & 8) return u32x4{q * 977u + line, lane, q, 5u};
+    const uint64_t b = (uint64_t)q * GB;
+    const uint32_t rem = q < G ? (uint32_t)(total - b < GB ? total - b : GB) : 0u;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(a.base + (q < G ? b : 0), rem);
+    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 128u * line, 0, 2));
   };
   // The first D lines are in flight while the workgroup builds its tables
   // (the table load is issued first, so waiting for it leaves them in flight).
@@ -552,7 +582,7 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
 #pragma unroll
   for (int k = 0; k < D; ++k) {  // in order: the loop's vmcnt waits assume it
     __builtin_amdgcn_sched_barrier(0);
-    ring[k] = load(0, k);
+    ring[k] = load(k < L ? qcur : qnext, (uint32_t)(k % L));
   }
   __builtin_amdgcn_sched_barrier(0);
   table_store(lds, tab_v);
@@ -562,20 +592,19 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
 #pragma unroll
     for (int k = 1; k < 8; ++k) v = bs == (uint32_t)k ? a.QS[k] : v;
     for (uint32_t t = j; t < 31; ++t) v = gf_mulx(v);
-    lds[kLdsWords + kWaves * kSlots + bs * kQStride + j] = v;
+    lds[kLdsWords + kWaves * kWaveWords + bs * kQStride + j] = v;
   }
   __syncthreads();
-  if (ng == 0) return;  // no barrier below
 
-  uint32_t *slots = lds + kLdsWords + wid * kSlots;
-  constexpr uint32_t kRoundMask = kSlots / 8 - 1;  // groups per round of slots - 1
+  uint32_t *slots = lds + kLdsWords + wid * kWaveWords;
+  uint32_t *gtab = slots + kSlots;  // DYN: absolute group of each slot row
   const LaneTab lt{(lane & 31) << 2, ((lane & 31) << 2) | 0x10000u};
   const uint32_t mw0 = s == 0 ? kMaskW0 : (s == 2 ? kMaskW8 : 0u);  // bytes 1 / 32
   const uint32_t xw0 = s == 0 ? kSeed : 0u;
   const uint32_t mw2 = s == 0 ? kMaskW2 : (s == 1 ? kMaskW6 : 0u);  // bytes 8, 10-11 / 26-27
   const uint32_t keep3 = s == 7 ? 0u : 0xFFFFFFFFu;                  // the trailer word
   uint32_t Q[32];  // lane basis in registers (!QLDS)
-  const uint32_t *qlds = lds + kLdsWords + kWaves * kSlots + s * kQStride;
+  const uint32_t *qlds = lds + kLdsWords + kWaves * kWaveWords + s * kQStride;
   if (!QLDS) {
     uint32_t qs = 0;
 #pragma unroll
@@ -630,26 +659,37 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
   const uint32_t vmask = __builtin_amdgcn_readfirstlane(a.verify ? 0xFFFFFFFFu : 0u);
   uint32_t sink = 0;
   // Results go to the wave's LDS slots (all 8 lanes of a packet write the
-  // same value to the same slot: no exec mask) and leave for HBM in
-  // coalesced stores once per 512 packets, so the streaming loop holds no
-  // global store: a store shares vmcnt with the ring and every load queued
-  // behind it would wait for its write acknowledgement.
-  auto flush = [&](uint32_t q_end) {  // the round of groups ending at q_end (at most 64)
+  // same value to the same slot: no exec mask) and leave for HBM once per
+  // round of slots, so the streaming loop holds no global store: a store
+  // shares vmcnt with the ring and every load queued behind it would wait
+  // for its write acknowledgement.  j counts the wave's finished groups.
+  auto flush = [&](uint32_t j_end) {  // the round of groups ending at local index j_end
     if (ABL & 16) return;
-    const uint32_t q_lo = (q_end - 1) & ~kRoundMask;
-    const uint64_t pb = (g0 + q_lo) * 8u;
-    const uint32_t valid = (q_end - q_lo) * 8u;  // slots written this round
-    const uint32_t nout = (uint32_t)(a.count - pb < valid ? a.count - pb : valid);
-    const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out + pb, 4u * nout);
+    const uint32_t j_lo = (j_end - 1) & ~kRoundMask;
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the slot writes have landed
+    if (DYN) {  // rows of 8 results to scattered groups: 32 B runs
+      const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out, (uint32_t)(a.count < (1ull << 30) ? 4 * a.count : 0xFFFFFFF0u));
 #pragma unroll
-    for (int h = 0; h < (int)kSlots / 256; ++h) {
-      const u32x4 v = *reinterpret_cast<const u32x4 *>(slots + 256 * h + 4 * lane);
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v), ro,
-                                             1024u * h + 16u * lane, 0, 0);
+      for (int h = 0; h < (int)kSlots / 64; ++h) {
+        const uint32_t row = 8u * h + (lane >> 3);  // slot row = local group (mod round)
+        const uint32_t q = gtab[row];
+        const bool live = j_lo + row < j_end;
+        __builtin_amdgcn_raw_buffer_store_b32(slots[64 * h + lane], ro, live ? 4u * (8u * q + s) : 0x7FFFFFF0u, 0, 0);
+      }
+    } else {  // consecutive groups: coalesced
+      const uint64_t pb = ((uint64_t)g0 + j_lo) * 8u;
+      const uint32_t valid = (j_end - j_lo) * 8u;  // slots written this round
+      const uint32_t nout = (uint32_t)(a.count - pb < valid ? a.count - pb : valid);
+      const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out + pb, 4u * nout);
+#pragma unroll
+      for (int h = 0; h < (int)kSlots / 256; ++h) {
+        const u32x4 v = *reinterpret_cast<const u32x4 *>(slots + 256 * h + 4 * lane);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v),
+                                               ro, 1024u * h + 16u * lane, 0, 0);
+      }
     }
   };
-  auto fin_store = [&](Fin &f, uint32_t qf) {
+  auto fin_store = [&](Fin &f, uint32_t jf, uint32_t qf) {
     const uint32_t crc = (ABL & 2) ? (f.r[0] ^ f.r[1] ^ f.r[2] ^ f.r[3]) : f.u;
     const uint32_t v = group_xor(crc, 3);
     const uint32_t chk = group_xor(f.tr, 3) == ~v ? 1u : 0u;
@@ -658,7 +698,8 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
       sink ^= val;
       return;
     }
-    slots[((qf & kRoundMask) << 3) | (lane >> 3)] = val;
+    slots[((jf & kRoundMask) << 3) | (lane >> 3)] = val;
+    if (DYN) gtab[jf & kRoundMask] = qf;
   };
 
   // Finish slices of the previous group ride in steps 0..7 (0..6 for L = 8,
@@ -667,9 +708,11 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
   auto slice_step = [](int sl) constexpr { return L >= 16 ? sl : sl * (L - 1) / 8; };
   static_assert(L >= 8, "finish needs 8 fold steps");
   Fin pf{};
-  for (uint32_t q = 0; q < ng; ++q) {
+  uint32_t qprev = 0;
+  uint32_t j = 0;
+  for (; qcur < G; ++j) {  // qcur: wave-uniform
     u32x4 w = ring[0];
-    ring[0] = load(q, D);
+    ring[0] = load(D < L ? qcur : qnext, (uint32_t)(D % L));
     w[0] = or_xor(w[0], mw0, xw0);
     w[2] |= mw2;
     uint32_t x[4] = {w[0], w[1], w[2], w[3]};  // chain register (0) ^ line-0 word
@@ -682,7 +725,7 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
       u32x4 wn = {0u, 0u, 0u, 0u};
       if (k + 1 < L) {
         wn = ring[(k + 1) % D];
-        ring[(k + 1) % D] = load(q, k + 1 + D);
+        ring[(k + 1) % D] = load(k + 1 + D < L ? qcur : qnext, (uint32_t)((k + 1 + D) % L));
         if (k + 1 == L - 1) {
           tr = keep3 ? 0u : wn[3];
           wn[3] &= keep3;
@@ -703,14 +746,14 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
           t[i][3] = lds_at(lds, __builtin_amdgcn_perm(x[i], lt.lo1, 0x0C020700u) + 128);
         }
       }
-      // The previous group's finish, in the shadow of the reads (for q = 0 it
+      // The previous group's finish, in the shadow of the reads (for j = 0 it
       // runs on zeros; its slot write is overwritten before any flush).
 #pragma unroll
       for (int sl = 0; sl < 8; ++sl)
         if (slice_step(sl) == k) fin_slice(pf, sl);
       if (k == kStoreStep) {
-        fin_store(pf, q - 1);
-        if (q > 0 && ((q - 1) & kRoundMask) == kRoundMask) flush(q);  // wave-uniform: a full round of slots
+        fin_store(pf, j - 1, qprev);
+        if (j > 0 && ((j - 1) & kRoundMask) == kRoundMask) flush(j);  // wave-uniform: a full round of slots
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) x[i] = xor3(t[i][0], t[i][1], xor3(t[i][2], t[i][3], wn[i]));
@@ -718,13 +761,35 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) pf.r[i] = x[i];
     pf.tr = tr;
+    qprev = qcur;
+    qcur = qnext;  // advance the group sequence (wave-uniform)
+    if (DYN) {
+      qnext = uni(qpend);
+      qpend = grab();
+    } else {
+      qnext = qnext + 1 < g1 ? qnext + 1 : G;
+    }
   }
-  __builtin_amdgcn_sched_barrier(0);
+  if (j > 0) {
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-  for (int sl = 0; sl < 8; ++sl) fin_slice(pf, sl);
-  fin_store(pf, ng - 1);
-  flush(ng);
+    for (int sl = 0; sl < 8; ++sl) fin_slice(pf, sl);
+    fin_store(pf, j - 1, qprev);
+    flush(j);
+  }
   if (ABL & 16) a.out[wave * 64 + lane] = sink;
+  if (DYN) {
+    // All of this wave's grabs have returned before it checks in, so when the
+    // last wave checks in nobody touches the counter any more: reset it.
+    const __amdgpu_buffer_rsrc_t drs = make_rsrc(a.work, 8u);
+    const uint32_t mine = lane == 0 ? 4u : 0x7FFFFFF0u;
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): every grab of this wave has returned
+    const uint32_t seen = (uint32_t)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, drs, mine, 0, 0);
+    if (__builtin_amdgcn_readfirstlane((int)seen) == (int)(nwaves - 1)) {
+      __builtin_amdgcn_raw_buffer_store_b32(0u, drs, lane == 0 ? 0u : 0x7FFFFFF0u, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(0u, drs, mine, 0, 0);
+    }
+  }
 }
 
 // =======================================================================
@@ -1219,9 +1284,15 @@ hipError_t launch_tsk(const TskArgs &a, int grid, hipStream_t st) {
 }
 
 hipError_t launch_sck(const SckArgs &a, int grid, hipStream_t st) {
-  if (a.n == 4096) hipLaunchKernelGGL((icrc_sck_kernel<32, 0>), dim3(grid), dim3(kBlock), 0, st, a);
-  else if (a.n == 2048) hipLaunchKernelGGL((icrc_sck_kernel<16, 0>), dim3(grid), dim3(kBlock), 0, st, a);
-  else if (a.n == 1024) hipLaunchKernelGGL((icrc_sck_kernel<8, 0>), dim3(grid), dim3(kBlock), 0, st, a);
+  const dim3 g(grid), b(kBlock);
+  if (a.dynamic) {
+    if (a.n == 4096) hipLaunchKernelGGL((icrc_sck_kernel<32, 0, 8, false, true>), g, b, 0, st, a);
+    else if (a.n == 2048) hipLaunchKernelGGL((icrc_sck_kernel<16, 0, 8, false, true>), g, b, 0, st, a);
+    else if (a.n == 1024) hipLaunchKernelGGL((icrc_sck_kernel<8, 0, 8, false, true>), g, b, 0, st, a);
+    else return hipErrorInvalidValue;
+  } else if (a.n == 4096) hipLaunchKernelGGL((icrc_sck_kernel<32, 0>), g, b, 0, st, a);
+  else if (a.n == 2048) hipLaunchKernelGGL((icrc_sck_kernel<16, 0>), g, b, 0, st, a);
+  else if (a.n == 1024) hipLaunchKernelGGL((icrc_sck_kernel<8, 0>), g, b, 0, st, a);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }

@@ -373,3 +373,18 @@ def test_ragged_strided_chain_mixed(ctx, monkeypatch, grid):
     exp = np.ones(count, np.uint32)
     exp[bad] = 0
     np.testing.assert_array_equal(_host_u32(out), exp)
+
+
+def test_strided_chain_dynamic_schedule(ctx, monkeypatch):
+    """Opt-in dynamic schedule of the strided-chain kernel (groups from a
+    self-resetting device counter): same results as the oracle, launch after
+    launch (a counter left non-zero would skip groups in the next launch)."""
+    monkeypatch.setenv("RICRC_SCK_DYNAMIC", "1")
+    for n, count in ((4096, 20003), (1024, 70001), (2048, 9)):
+        host = oracle_c.synth_batch(SEED ^ n, 11, count, n)
+        want = oracle_c.icrc_batch(host, stride=n, threads=8)
+        d = _dev(host)
+        for _ in range(3):
+            out = _out(count)
+            ctx.batch_device(d, count, out, stride=n, stream=_stream())
+            np.testing.assert_array_equal(_host_u32(out), want)
