@@ -512,17 +512,19 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
 // ABL (timing-only ablations for tools/microbench; the product uses 0):
 // 1 no table fold, 2 no finish, 8 no global loads, 16 no stores.
 // D: lines in flight per wave; QLDS: lane bases read from LDS instead of 32
-// VGPRs (frees registers for a deeper ring).
+// VGPRs (frees registers for a deeper ring); XT: the Horner multiplies by
+// x^-32 through a conflict-free nibble table in LDS.
 // =======================================================================
-template <int L, int ABL, int D = 8, bool QLDS = false, bool DYN = false>
+template <int L, int ABL, int D = 8, bool QLDS = false, bool DYN = false, bool XT = false>
 __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
   // 128 KiB of tables + result slots per wave (+ DYN: the slots' group
-  // indices; QLDS: the 8 lane bases).
-  constexpr uint32_t kSlots = (QLDS || DYN) ? 256 : 512;
+  // indices; QLDS: the 8 lane bases; XT: 16 KiB nibble table of x^-32).
+  constexpr uint32_t kSlots = (DYN && XT) ? 128 : (QLDS || DYN || XT) ? 256 : 512;
   constexpr uint32_t kRoundMask = kSlots / 8 - 1;  // groups per round of slots - 1
   constexpr uint32_t kWaveWords = kSlots + (DYN ? kSlots / 8 : 0);
   constexpr uint32_t kQStride = 36;  // words per lane-slot basis (padded: conflict-free ds_read_b128)
-  __shared__ uint32_t lds[kLdsWords + kWaves * kWaveWords + (QLDS ? 8 * kQStride : 0)];
+  constexpr uint32_t kXtWord = kLdsWords + kWaves * kWaveWords + (QLDS ? 8 * kQStride : 0);
+  __shared__ uint32_t lds[kXtWord + (XT ? 128 * 32 : 0)];
 
   // D: lines in flight per wave
   static_assert(L % D == 0 || D == L, "ring indices must repeat every group");
@@ -586,6 +588,13 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
   }
   __builtin_amdgcn_sched_barrier(0);
   table_store(lds, tab_v);
+  if (XT) {  // entry (w, v) = (nibble v at bits 4w..4w+3) * x^-32, 32 copies: 8 threads x 4 copies each
+    const uint32_t e = threadIdx.x >> 3, w = e >> 4, v = e & 15u;
+    uint32_t t = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) t ^= ((v >> b) & 1u) ? a.XB[4 * w + b] : 0u;
+    *reinterpret_cast<u32x4 *>(lds + kXtWord + 32 * e + 4 * (threadIdx.x & 7)) = u32x4{t, t, t, t};
+  }
   if (QLDS && threadIdx.x < 256) {  // basis word j of lane slot s: x^(-32 (4 s + 1)) * x^(31 - j)
     const uint32_t bs = threadIdx.x >> 5, j = threadIdx.x & 31;
     uint32_t v = a.QS[0];
@@ -597,6 +606,7 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
   __syncthreads();
 
   uint32_t *slots = lds + kLdsWords + wid * kWaveWords;
+  const uint32_t xt_lane = 4u * kXtWord + ((lane & 31u) << 2);  // byte address of the lane's XT copy
   uint32_t *gtab = slots + kSlots;  // DYN: absolute group of each slot row
   const LaneTab lt{(lane & 31) << 2, ((lane & 31) << 2) | 0x10000u};
   const uint32_t mw0 = s == 0 ? kMaskW0 : (s == 2 ? kMaskW8 : 0u);  // bytes 1 / 32
@@ -637,7 +647,13 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) f.acc[k] = 0u;
     }
-    if (sl < 6) mul_half(f, a.XB, sl & 1);
+    if (sl < 6 && XT) {  // 4 nibble lookups: 2 VALU + 1 ds_read_b32 each instead of 8 bfe/bitop3 pairs
+#pragma unroll
+      for (int w = 4 * (sl & 1); w < 4 * (sl & 1) + 4; ++w) {
+        const uint32_t nib = (f.u >> (4 * w)) & 15u;
+        f.acc[w & 3] ^= lds_at(lds, xt_lane + (nib << 7) + 2048u * w);
+      }
+    } else if (sl < 6) mul_half(f, a.XB, sl & 1);
     else if (!QLDS) mul_half(f, Q, sl & 1);
     else {
       const int h = sl & 1;
@@ -1285,14 +1301,15 @@ hipError_t launch_tsk(const TskArgs &a, int grid, hipStream_t st) {
 
 hipError_t launch_sck(const SckArgs &a, int grid, hipStream_t st) {
   const dim3 g(grid), b(kBlock);
+  // XT (x^-32 nibble table): 0.735 -> 0.703 ms on 4 M x 1 KiB, ~1 % on 1 M x 4 KiB (tools/microbench/sck_abl.hip).
   if (a.dynamic) {
-    if (a.n == 4096) hipLaunchKernelGGL((icrc_sck_kernel<32, 0, 8, false, true>), g, b, 0, st, a);
-    else if (a.n == 2048) hipLaunchKernelGGL((icrc_sck_kernel<16, 0, 8, false, true>), g, b, 0, st, a);
-    else if (a.n == 1024) hipLaunchKernelGGL((icrc_sck_kernel<8, 0, 8, false, true>), g, b, 0, st, a);
+    if (a.n == 4096) hipLaunchKernelGGL((icrc_sck_kernel<32, 0, 8, false, true, true>), g, b, 0, st, a);
+    else if (a.n == 2048) hipLaunchKernelGGL((icrc_sck_kernel<16, 0, 8, false, true, true>), g, b, 0, st, a);
+    else if (a.n == 1024) hipLaunchKernelGGL((icrc_sck_kernel<8, 0, 8, false, true, true>), g, b, 0, st, a);
     else return hipErrorInvalidValue;
-  } else if (a.n == 4096) hipLaunchKernelGGL((icrc_sck_kernel<32, 0>), g, b, 0, st, a);
-  else if (a.n == 2048) hipLaunchKernelGGL((icrc_sck_kernel<16, 0>), g, b, 0, st, a);
-  else if (a.n == 1024) hipLaunchKernelGGL((icrc_sck_kernel<8, 0>), g, b, 0, st, a);
+  } else if (a.n == 4096) hipLaunchKernelGGL((icrc_sck_kernel<32, 0, 8, false, false, true>), g, b, 0, st, a);
+  else if (a.n == 2048) hipLaunchKernelGGL((icrc_sck_kernel<16, 0, 8, false, false, true>), g, b, 0, st, a);
+  else if (a.n == 1024) hipLaunchKernelGGL((icrc_sck_kernel<8, 0, 8, false, false, true>), g, b, 0, st, a);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }

@@ -6,16 +6,16 @@
 #include <stdlib.h>
 using namespace ricrc;
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s\n", hipGetErrorString(e)); exit(1); } } while (0)
-template <int L, int ABL, int D = 8, bool QL = false> float run(SckArgs a, int grid, int reps) {
+template <int L, int ABL, int D = 8, bool QL = false, bool XT = false> float run(SckArgs a, int grid, int reps) {
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-  for (int w = 0; w < 3; ++w) hipLaunchKernelGGL((icrc_sck_kernel<L, ABL, D, QL>), dim3(grid), dim3(kBlock), 0, 0, a);
+  for (int w = 0; w < 3; ++w) hipLaunchKernelGGL((icrc_sck_kernel<L, ABL, D, QL, false, XT>), dim3(grid), dim3(kBlock), 0, 0, a);
   CK(hipDeviceSynchronize()); CK(hipEventRecord(e0));
-  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL((icrc_sck_kernel<L, ABL, D, QL>), dim3(grid), dim3(kBlock), 0, 0, a);
+  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL((icrc_sck_kernel<L, ABL, D, QL, false, XT>), dim3(grid), dim3(kBlock), 0, 0, a);
   CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); float ms; CK(hipEventElapsedTime(&ms, e0, e1)); return ms / reps;
 }
 int main(int argc, char **argv) {
   const uint64_t n = 4096, count = 1 << 20;
-  uint8_t *buf; uint32_t *out; CK(hipMalloc(&buf, n * count)); CK(hipMalloc(&out, 4 * count + (1 << 22)));
+  uint8_t *buf; uint32_t *out; CK(hipMalloc(&buf, n * count)); CK(hipMalloc(&out, 4 * (4ull << 20) + (1 << 22)));  // room for the L = 8 run (4 M packets) + ABL sink
   {  // random bytes (DVFS: constant data runs at a higher clock than real traffic)
     uint8_t *h = (uint8_t *)malloc(n * count);
     uint64_t x = 0x9E3779B97F4A7C15ull;
@@ -28,21 +28,29 @@ int main(int argc, char **argv) {
   for (int j = 0; j < 32; ++j) a.XB[j] = 0x85EBCA6Bu * (j + 3);
   for (int s = 0; s < 8; ++s) a.QS[s] = 0x9E3779B9u * (s + 1);
   const int grid = p.multiProcessorCount;
-  auto rep = [&](const char *nm, float ms) { printf("%-36s %7.3f ms  %7.1f GB/s\n", nm, ms, n * count / (ms * 1e-3) / 1e9); };
+  auto rep = [&](const char *nm, float ms) { printf("%-36s %7.3f ms  %7.1f GB/s\n", nm, ms, 4294967296.0 / (ms * 1e-3) / 1e9); };
   for (int r = 0; r < 2; ++r) {
     rep("full D8", run<32, 0>(a, grid, 20));
-    rep("full D8 qlds", run<32, 0, 8, true>(a, grid, 20));
-    rep("full D16 qlds", run<32, 0, 16, true>(a, grid, 20));
-    rep("full D4", run<32, 0, 4>(a, grid, 20));
+    rep("full D8 XT", run<32, 0, 8, false, true>(a, grid, 20));
+    rep("no loads XT", run<32, 8, 8, false, true>(a, grid, 20));
     rep("no stores", run<32, 16>(a, grid, 20));
-    rep("full D8 again", run<32, 0>(a, grid, 20));
     rep("no fold (VALU stand-in)", run<32, 1>(a, grid, 20));
     rep("no finish", run<32, 2>(a, grid, 20));
     rep("no loads", run<32, 8>(a, grid, 20));
     rep("no fold, no finish (memory path)", run<32, 1 | 2>(a, grid, 20));
-    rep("memory path D16", run<32, 1 | 2, 16, true>(a, grid, 20));
     rep("no loads, no finish (fold only)", run<32, 8 | 2>(a, grid, 20));
     rep("no loads, no fold (finish only)", run<32, 8 | 1>(a, grid, 20));
+  }
+  // 1 KiB packets (C2): L = 8, the ring spans exactly one group
+  SckArgs b = a; b.n = 1024; b.count = 4ull << 20;
+  for (int r = 0; r < 2; ++r) {
+    rep("L8 full", run<8, 0>(b, grid, 20));
+    rep("L8 full XT", run<8, 0, 8, false, true>(b, grid, 20));
+    rep("L8 no loads XT", run<8, 8, 8, false, true>(b, grid, 20));
+    rep("L8 no finish", run<8, 2>(b, grid, 20));
+    rep("L8 no fold", run<8, 1>(b, grid, 20));
+    rep("L8 memory path", run<8, 1 | 2>(b, grid, 20));
+    rep("L8 no loads", run<8, 8>(b, grid, 20));
   }
   return 0;
 }
