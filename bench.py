@@ -80,7 +80,7 @@ def kernel_label(size):
     """The kernel libroceicrc's dispatch picks for back-to-back packets of `size` bytes."""
     if size in (1024, 2048, 4096):
         return "strided-chain ICRC kernel (icrc_sck_kernel)"
-    if 64 <= size <= 4096 and size & (size - 1) == 0:
+    if 128 <= size <= 4096 and size & (size - 1) == 0:
         return "transposed streaming ICRC kernel (icrc_tsk_kernel)"
     return "streaming ICRC kernel"
 

@@ -234,7 +234,8 @@ int launch_batch(Dev &d, const uint8_t *base, const uint64_t *off, const uint32_
         }
       }
       // Back-to-back packets of 32 * 2^j bytes: coalesced + LDS-transposed kernel.
-      if (l3_offset == 0 && stride == fixed_len && fixed_len >= 64 && fixed_len <= 4096 &&
+      // (64-byte packets: the direct streaming kernel is faster, 20.1 vs 23.8 us on 1 M x 64 B.)
+      if (l3_offset == 0 && stride == fixed_len && fixed_len >= 128 && fixed_len <= 4096 &&
           (fixed_len & (fixed_len - 1)) == 0 && ((uintptr_t)base % 16 == 0) && getenv("RICRC_NO_TSK") == nullptr) {
         TskArgs t{};
         t.base = base;
