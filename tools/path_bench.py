@@ -60,6 +60,7 @@ def main():
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--skip-host", action="store_true")
     ap.add_argument("--only-ragged", action="store_true", help="only the C4 ragged device measurement")
+    ap.add_argument("--ragged-paths", default="rsck,piece", help="which ragged paths to time (rsck, piece)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -129,7 +130,10 @@ def main():
             buf[ix] = rows[c:c + step].reshape(-1)
         del tmp, rows, starts
     out = torch.empty(count, dtype=torch.int32, device=dev)
-    for label, knob in (("ragged strided-chain (C4 mix)", None), ("ragged piece kernel (C4 mix)", "RICRC_NO_RSCK")):
+    paths = [(lbl, knob) for key, lbl, knob in (("rsck", "ragged strided-chain (C4 mix)", None),
+                                                ("piece", "ragged piece kernel (C4 mix)", "RICRC_NO_RSCK"))
+             if key in args.ragged_paths.split(",")]
+    for label, knob in paths:
         if knob:
             os.environ[knob] = "1"
         try:
