@@ -127,7 +127,7 @@ struct RsckArgs {
   uint32_t verify;
   uint32_t *out;
   // device workspace (icrc_api.cpp sizes it: rs_workspace_bytes)
-  uint32_t *counts;   // [kRsClasses], zeroed before the count pass
+  uint32_t *counts;   // [kRsClasses + 1], zeroed before the count pass; the last: "misaligned" flag
   uint32_t *cursor;   // [kRsClasses], zeroed by the plan pass
   uint32_t *bucket;   // [kRsClasses] first position of each class
   RsPlan *plan;

@@ -44,6 +44,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "icrc_device.h"
 #include "icrc_kernels.h"
 #include "icrc_math.h"
@@ -108,6 +110,7 @@ __global__ __launch_bounds__(kPassBlock) void rsck_count(RsckArgs a) {
   __syncthreads();
   uint64_t lo, hi;
   pass_range(a.count, lo, hi);
+  int odd = 0;  // a strided-chain packet not starting or ending on a 4-byte word
   for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
     uint64_t addr;
     uint32_t n;
@@ -115,6 +118,7 @@ __global__ __launch_bounds__(kPassBlock) void rsck_count(RsckArgs a) {
     const uint32_t c = rs_class(addr, n);
     if (c) {
       atomicAdd(&h[c], 1u);
+      odd |= (c >= (uint32_t)kRsBigBase && ((addr | n) & 3u)) ? 1 : 0;
     } else {
       uint32_t v = 0u;
       if (n >= 4u && n <= kMaxLen) {
@@ -124,7 +128,7 @@ __global__ __launch_bounds__(kPassBlock) void rsck_count(RsckArgs a) {
       a.out[i] = v;
     }
   }
-  __syncthreads();
+  if (__syncthreads_or(odd) && threadIdx.x == 0) atomicOr(&a.counts[kRsClasses], 1u);
   for (int t = threadIdx.x; t < kRsClasses; t += blockDim.x) {
     a.hist[(uint64_t)blockIdx.x * kRsClasses + t] = h[t];
     if (h[t]) atomicAdd(&a.counts[t], h[t]);
@@ -257,6 +261,18 @@ __device__ __forceinline__ uint32_t edge_word(uint32_t w, int rel, int M) {
   const uint64_t s64 = (uint64_t)kSeed << 24;  // seed byte k at byte k + 3
   const uint32_t sx = (rel > -4 && rel < 4) ? (uint32_t)(s64 >> (8u * (sh & 7u))) : 0u;
   return ((w & keep) | orm) ^ sx;
+}
+
+// The same for a word-aligned packet start and length (rel and M multiples
+// of 4): whole-word keep, the mask words of offsets 0, 8, 24, 32, the seed at 0.
+__device__ __forceinline__ uint32_t edge_word_aligned(uint32_t w, int rel, int M) {
+  // Arithmetic masks, not ternaries: a select chain on rel lowers to a
+  // divergent switch (and a vmcnt(0) drain at the loop head).
+  const uint32_t keep = (uint32_t)((unsigned)rel < (unsigned)M) * 0xFFFFFFFFu;
+  const uint32_t z0 = (uint32_t)(rel == 0) * 0xFFFFFFFFu;
+  const uint32_t orm = (z0 & kMaskW0) | ((uint32_t)(rel == 8) * kMaskW2) | ((uint32_t)(rel == 24) * kMaskW6) |
+                       ((uint32_t)(rel == 32) * kMaskW8);
+  return ((w & keep) | orm) ^ (z0 & kSeed);  // M >= 40: the mask words are always kept
 }
 
 }  // namespace
@@ -447,6 +463,11 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
     }
   };
 
+  // Two copies of the fold loop: one with whole-word edges when the count
+  // pass found every strided-chain packet word-aligned in start and length
+  // (a per-group choice inside the loop made the compiler rotate the load
+  // ring through copies and drain vmcnt(0) at the loop head).
+  auto fold_loop = [&](auto words) {
   bool done = false;
   while (!done) {
 #pragma unroll
@@ -455,8 +476,13 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
       u32x4 w = ring[u];
       if (fd_k == 0 || (fd_k == 1 && fd_head2) || fd_k + 1 == fd_L) {  // wave-uniform
         const int rel0 = (int)(128u * fd_k + 16u * s) - (int)fd_a;
+        if constexpr (decltype(words)::value) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) w[i] = edge_word(w[i], rel0 + 4 * i, (int)fd_M);
+          for (int i = 0; i < 4; ++i) w[i] = edge_word_aligned(w[i], rel0 + 4 * i, (int)fd_M);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) w[i] = edge_word(w[i], rel0 + 4 * i, (int)fd_M);
+        }
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -491,6 +517,11 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
       ld_advance();
     }
   }
+  };
+  if (a.counts[kRsClasses] == 0)
+    fold_loop(std::true_type{});
+  else
+    fold_loop(std::false_type{});
   if (q_end != round_q0) flush(q_end);
 }
 
@@ -519,7 +550,7 @@ void rs_bind_workspace(RsckArgs &a, void *ws) {
 
 hipError_t launch_rsck(RsckArgs &a, const RaggedArgs &small, int grid, hipStream_t st) {
   if (a.count == 0) return hipSuccess;
-  hipError_t e = hipMemsetAsync(a.counts, 0, 4ull * kRsClasses, st);
+  hipError_t e = hipMemsetAsync(a.counts, 0, 4ull * (kRsClasses + 1), st);  // + the misaligned flag
   if (e != hipSuccess) return e;
   const uint64_t want = (a.count + kPassBlock - 1) / kPassBlock;
   const int pgrid = (int)(want < kPassBlocks ? want : kPassBlocks);

@@ -375,6 +375,37 @@ def test_ragged_strided_chain_mixed(ctx, monkeypatch, grid):
     np.testing.assert_array_equal(_host_u32(out), exp)
 
 
+@pytest.mark.gpu
+def test_ragged_strided_chain_word_aligned(ctx):
+    """Word-aligned ragged batches take the fold loop with whole-word edges
+    (the count pass raises a device flag for any misaligned strided-chain
+    packet): starts at every multiple of 4 inside a 128-byte line (headers
+    running into line 1 included), lengths multiple of 4.  Then the same batch
+    with ONE packet moved off the word grid (the flag must switch the launch to
+    byte-granular edges), then the aligned batch again (the flag must not
+    leak from the previous launch)."""
+    rng = np.random.default_rng(11)
+    count = 5000
+    lens = (rng.integers(11, 2300, size=count) * 4).astype(np.uint32)
+    gaps = (rng.integers(0, 50, size=count) * 4).astype(np.uint64)
+    offs = np.zeros(count, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + gaps[:-1])
+    offs += 4
+    total = int(offs[-1] + lens[-1]) + 128
+    buf = rng.integers(0, 256, size=total, dtype=np.uint8)
+    d = _dev(buf)
+    odd_offs = offs.copy()
+    odd_offs[count // 2] += 1  # one byte later and 4 shorter: stays inside its slot
+    odd_lens = lens.copy()
+    odd_lens[count // 2] -= 4
+    for o, l in ((offs, lens), (odd_offs, odd_lens), (offs, lens)):
+        want = oracle_c.icrc_batch(buf, offsets=o, lengths=l, threads=8)
+        out = _out(count)
+        ctx.batch_device(d, count, out, offsets=_dev(o.view(np.int64)), lengths=_dev(l.view(np.int32)),
+                         stream=_stream())
+        np.testing.assert_array_equal(_host_u32(out), want)
+
+
 def test_strided_chain_dynamic_schedule(ctx, monkeypatch):
     """Opt-in dynamic schedule of the strided-chain kernel (groups from a
     self-resetting device counter): same results as the oracle, launch after
