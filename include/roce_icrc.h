@@ -140,6 +140,28 @@ int ricrc_verify_device(ricrc_ctx *ctx, int dev, const void *d_base, const uint6
                         const uint32_t *d_len, uint32_t stride, uint64_t count, uint32_t l3_offset,
                         uint32_t *d_out, void *stream);
 
+/* Batch incremental repair on the device, after a header rewrite of packets
+ * that were already stamped -- the switch egress's PSN/MSN/opcode patches
+ * (shuffle_egress.p4:635-671), the reason the reference disables NIC ICRC
+ * checking (scripts/icrc/disable-icrc.sh:13,30).  Packet i is addressed as in
+ * ricrc_batch_device (d_base is writable); its bytes [off, off+len) held
+ * d_old_bytes + i*old_stride before the rewrite and its trailer still holds
+ * the old packet's ICRC.  d_out[i] (d_out may be NULL when stamp != 0) = the
+ * rewritten packet's ICRC, computed from 2*len + 4 bytes of the packet
+ * instead of n (ricrc_repair_one's identity); stamp != 0 also writes it
+ * LE32 into the trailer.  flags as the *_ex calls.  Per packet, a length
+ * outside [4, RICRC_MAX_LEN], a range past n-4, or an AUTO rewrite that
+ * changes the IP version nibble gives d_out[i] = 0 and leaves the trailer
+ * alone.  A wrong old trailer stays wrong (repair is incremental, not a
+ * check: verify first where that matters).  0, -EINVAL (NULL pointers,
+ * len > RICRC_REPAIR_MAX, off + len > RICRC_MAX_LEN - 4, old_stride < len,
+ * bad flags), -ENODEV, -EIO.  Asynchronous on `stream`. */
+#define RICRC_REPAIR_MAX 256u
+int ricrc_repair_device(ricrc_ctx *ctx, int dev, void *d_base, const uint64_t *d_off, const uint32_t *d_len,
+                        uint32_t stride, uint64_t count, uint32_t l3_offset, uint32_t off, uint32_t len,
+                        const uint8_t *d_old_bytes, uint32_t old_stride, uint32_t flags, uint32_t stamp,
+                        uint32_t *d_out, void *stream);
+
 /* Pinned host memory for NIC-ring style buffers (the role of huge_malloc in
  * common/huge_malloc.h:12-22).  NULL on failure.  ricrc_batch_host DMAs
  * straight out of such memory (no CPU copy) whenever a chunk's packets form

@@ -49,6 +49,7 @@ struct Dev {
   uint32_t *d_inv = nullptr;   // x^(-8 z), z <= 4096
   uint32_t *d_inv4 = nullptr;  // t: x^(8 (k - t)), k = 0..3, t <= 4096
   uint32_t *d_tzb = nullptr;   // [128][8]: basis words 4q of x^(-8 tz) (ragged strided-chain path)
+  uint32_t *d_x8n = nullptr;   // x^(8 k), k < 65536 (incremental repair)
   uint32_t *d_work = nullptr;  // kWorkSlots x {group counter, finished waves} (dynamic SCK schedule)
   uint32_t work_next = 0;      // round-robin slot: launches in flight on different streams never share one
   Slot slot[2];
@@ -127,6 +128,14 @@ int init_dev(Dev &d) {
   }
   HIP_TRY(hipMalloc(&d.d_tzb, tzb.size() * sizeof(uint32_t)));
   HIP_TRY(hipMemcpy(d.d_tzb, tzb.data(), tzb.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  std::vector<uint32_t> x8n(65536);  // x^(8 k): a repair's shift over the bytes after the rewrite
+  uint32_t w = kOne;
+  for (size_t k = 0; k < x8n.size(); ++k) {
+    x8n[k] = w;
+    for (int b = 0; b < 8; ++b) w = gf_mulx(w);
+  }
+  HIP_TRY(hipMalloc(&d.d_x8n, x8n.size() * sizeof(uint32_t)));
+  HIP_TRY(hipMemcpy(d.d_x8n, x8n.data(), x8n.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
   HIP_TRY(hipMalloc(&d.d_work, kWorkSlots * 2 * sizeof(uint32_t)));
   HIP_TRY(hipMemset(d.d_work, 0, kWorkSlots * 2 * sizeof(uint32_t)));
   return 0;
@@ -162,6 +171,7 @@ void free_dev(Dev &d) {
   (void)hipFree(d.d_inv);
   (void)hipFree(d.d_inv4);
   (void)hipFree(d.d_tzb);
+  (void)hipFree(d.d_x8n);
   (void)hipFree(d.d_work);
   if (d.stream) (void)hipStreamDestroy(d.stream);
 }
@@ -412,6 +422,40 @@ int ricrc_verify_device(ricrc_ctx *ctx, int dev, const void *d_base, const uint6
                         const uint32_t *d_len, uint32_t stride, uint64_t count, uint32_t l3_offset,
                         uint32_t *d_out, void *stream) {
   return batch_device_impl(ctx, dev, d_base, d_off, d_len, stride, count, l3_offset, d_out, stream, true);
+}
+
+int ricrc_repair_device(ricrc_ctx *ctx, int dev, void *d_base, const uint64_t *d_off, const uint32_t *d_len,
+                        uint32_t stride, uint64_t count, uint32_t l3_offset, uint32_t off, uint32_t len,
+                        const uint8_t *d_old_bytes, uint32_t old_stride, uint32_t flags, uint32_t stamp,
+                        uint32_t *d_out, void *stream) {
+  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size()) return -EINVAL;
+  if (flags > RICRC_F_AUTO) return -EINVAL;
+  if (len > RICRC_REPAIR_MAX || (uint64_t)off + len > kMaxLen - 4) return -EINVAL;
+  if (count == 0) return 0;
+  if (!d_base || (len && !d_old_bytes) || (!d_out && !stamp)) return -EINVAL;
+  if (count > 1 && old_stride < len) return -EINVAL;
+  if (!d_off && stride == 0) return -EINVAL;
+  if (!d_len && stride <= l3_offset) return -EINVAL;
+  Dev &d = ctx->devs[dev];
+  DeviceGuard g(d.id);
+  if (!g.ok()) return -ENODEV;
+  RepairArgs a{};
+  a.base = (uint8_t *)d_base;
+  a.off = d_off;
+  a.len = d_len;
+  a.old_bytes = d_old_bytes;
+  a.x8n = d.d_x8n;
+  a.out = d_out;
+  a.stride = stride;
+  a.old_stride = old_stride;
+  a.count = count;
+  a.fixed_len = stride > l3_offset ? (uint32_t)std::min<uint64_t>(stride - l3_offset, 0xFFFFFFFFu) : 0u;
+  a.l3_offset = l3_offset;
+  a.roff = off;
+  a.rlen = len;
+  a.family = flags;
+  a.stamp = stamp ? 1u : 0u;
+  return hip_err(launch_repair(a, 16 * d.n_cu, (hipStream_t)stream));
 }
 
 int ricrc_synth_device(ricrc_ctx *ctx, int dev, uint64_t seed, uint64_t first, uint64_t count, uint32_t n,

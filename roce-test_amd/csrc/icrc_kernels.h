@@ -154,6 +154,24 @@ struct SynthArgs {
   uint32_t n, stride;  // stride % 8 == 0, n <= stride
 };
 
+// Incremental repair (icrc_repair.hip): packet i's bytes [roff, roff+rlen)
+// were old_bytes + i*old_stride when its trailer was stamped.
+struct RepairArgs {
+  uint8_t *base;
+  const uint64_t *off;  // may be null (then i * stride)
+  const uint32_t *len;  // may be null (then fixed_len)
+  const uint8_t *old_bytes;
+  const uint32_t *x8n;  // x^(8 k), k in [0, 65536)
+  uint32_t *out;        // may be null (stamp only)
+  uint64_t stride, old_stride, count;
+  uint32_t fixed_len, l3_offset;
+  uint32_t roff, rlen;
+  uint32_t family;      // kFamV4 / kFamV6 / kFamAuto
+  uint32_t stamp;
+  uint32_t mask4[4], mask6[4];  // set by launch_repair: byte k = mask bits of range byte k (k < 16)
+};
+hipError_t launch_repair(const RepairArgs &a, int grid, hipStream_t st);
+
 hipError_t launch_stream(const StreamArgs &a, int cpl, int grid, hipStream_t st);
 hipError_t launch_tsk(const TskArgs &a, int grid, hipStream_t st);
 // Returns hipErrorInvalidValue for an n it has no instantiation for.

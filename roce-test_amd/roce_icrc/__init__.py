@@ -35,7 +35,7 @@ EXPORTED = (
     "ricrc_one", "ricrc_verify_one", "ricrc_stamp_one", "ricrc_is_rocev2", "ricrc_shift",
     "ricrc_one_ex", "ricrc_verify_one_ex", "ricrc_stamp_one_ex", "ricrc_classify", "ricrc_repair_one",
     "ricrc_combine", "ricrc_create", "ricrc_create_devices", "ricrc_destroy", "ricrc_device_count", "ricrc_batch_host",
-    "ricrc_batch_device", "ricrc_verify_device", "ricrc_host_alloc", "ricrc_host_free",
+    "ricrc_batch_device", "ricrc_verify_device", "ricrc_repair_device", "ricrc_host_alloc", "ricrc_host_free",
     "ricrc_host_register", "ricrc_host_unregister", "ricrc_synth_device", "ricrc_stream", "ricrc_strerror",
 )
 
@@ -82,6 +82,7 @@ def _load():
         "ricrc_batch_host": ([vp, u8p, vp, vp, u32, u64, u32, vp], i32),
         "ricrc_batch_device": ([vp, i32, vp, vp, vp, u32, u64, u32, vp, vp], i32),
         "ricrc_verify_device": ([vp, i32, vp, vp, vp, u32, u64, u32, vp, vp], i32),
+        "ricrc_repair_device": ([vp, i32, vp, vp, vp, u32, u64, u32, u32, u32, vp, u32, u32, u32, vp, vp], i32),
         "ricrc_host_alloc": ([vp, u64], vp),
         "ricrc_host_free": ([vp, vp], None),
         "ricrc_host_register": ([vp, vp, u64], i32),
@@ -285,6 +286,22 @@ class Context:
                 _ptr(out), _stream_ptr(stream))
         if rc:
             raise ICRCError(rc, "ricrc_verify_device" if verify else "ricrc_batch_device")
+
+    def repair_device(self, base, count: int, off: int, old_bytes, out=None, stride: int = 0,
+                      offsets=None, lengths=None, l3_offset: int = 0, old_stride: int | None = None,
+                      family: str = "v4", stamp: bool = True, dev: int = 0, stream=None) -> None:
+        """Incremental ICRC repair after a header rewrite (``ricrc_repair_device``):
+        bytes ``[off, off + L)`` of packet i held ``old_bytes[i]`` (a ``count x L``
+        uint8 device tensor) when its trailer was stamped.  ``out[i]`` = the new
+        ICRC; with ``stamp`` the trailer is rewritten too."""
+        ln = int(old_bytes.shape[-1]) if getattr(old_bytes, "ndim", 1) > 1 else int(old_bytes.numel() // max(count, 1))
+        if old_stride is None:
+            old_stride = ln
+        rc = lib.ricrc_repair_device(self._h, dev, _ptr(base), _ptr(offsets), _ptr(lengths), stride, count,
+                                     l3_offset, off, ln, _ptr(old_bytes), old_stride, _fam(family),
+                                     1 if stamp else 0, _ptr(out), _stream_ptr(stream))
+        if rc:
+            raise ICRCError(rc, "ricrc_repair_device")
 
     def synth_device(self, buf, seed: int, first: int, count: int, n: int, stride: int | None = None,
                      dev: int = 0, stream=None) -> None:
