@@ -140,6 +140,22 @@ int ricrc_verify_device(ricrc_ctx *ctx, int dev, const void *d_base, const uint6
                         const uint32_t *d_len, uint32_t stride, uint64_t count, uint32_t l3_offset,
                         uint32_t *d_out, void *stream);
 
+/* Address-family variants of the batch calls (flags as the *_ex per-packet
+ * calls: RICRC_F_IPV4 / RICRC_F_IPV6 / RICRC_F_AUTO by each packet's version
+ * nibble).  The batch kernels apply the IPv4 masks; for IPV6 / AUTO one more
+ * pass per packet corrects the result from the first min(56, n-4) header
+ * bytes (the families' masks differ only there; the register is linear), and
+ * does the verify compare.  Bad flags: -EINVAL.  Otherwise as the plain calls,
+ * which are these with RICRC_F_IPV4. */
+int ricrc_batch_host_ex(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *off, const uint32_t *len,
+                        uint32_t stride, uint64_t count, uint32_t l3_offset, uint32_t *out, uint32_t flags);
+int ricrc_batch_device_ex(ricrc_ctx *ctx, int dev, const void *d_base, const uint64_t *d_off,
+                          const uint32_t *d_len, uint32_t stride, uint64_t count, uint32_t l3_offset,
+                          uint32_t *d_out, void *stream, uint32_t flags);
+int ricrc_verify_device_ex(ricrc_ctx *ctx, int dev, const void *d_base, const uint64_t *d_off,
+                           const uint32_t *d_len, uint32_t stride, uint64_t count, uint32_t l3_offset,
+                           uint32_t *d_out, void *stream, uint32_t flags);
+
 /* Batch incremental repair on the device, after a header rewrite of packets
  * that were already stamped -- the switch egress's PSN/MSN/opcode patches
  * (shuffle_egress.p4:635-671), the reason the reference disables NIC ICRC

@@ -183,8 +183,8 @@ int ilog2_ceil(uint32_t v) {
 }
 
 // Kernel selection + launch for one device-resident batch.
-int launch_batch(Dev &d, const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
-                 uint64_t count, uint32_t l3_offset, uint32_t *out, hipStream_t st, bool verify) {
+int launch_batch_v4(Dev &d, const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
+                    uint64_t count, uint32_t l3_offset, uint32_t *out, hipStream_t st, bool verify) {
   if (count == 0) return 0;
   const uint8_t *first = base + l3_offset;
   const uint32_t fixed_len = stride > l3_offset ? (uint32_t)std::min<uint64_t>(stride - l3_offset, 0xFFFFFFFFu) : 0u;
@@ -330,6 +330,30 @@ int launch_batch(Dev &d, const uint8_t *base, const uint64_t *off, const uint32_
   return hip_err(e != hipSuccess ? e : e2);
 }
 
+// Any address family: the IPv4-mask kernels, then (IPv6 / AUTO) the linear
+// header fix-up, which also does the verify compare in that case.
+int launch_batch(Dev &d, const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
+                 uint64_t count, uint32_t l3_offset, uint32_t *out, hipStream_t st, bool verify,
+                 uint32_t family = kFamV4) {
+  if (family == kFamV4 || count == 0)
+    return launch_batch_v4(d, base, off, len, stride, count, l3_offset, out, st, verify);
+  const int rc = launch_batch_v4(d, base, off, len, stride, count, l3_offset, out, st, false);
+  if (rc) return rc;
+  FamilyFixArgs f{};
+  f.base = base;
+  f.off = off;
+  f.len = len;
+  f.x8n = d.d_x8n;
+  f.out = out;
+  f.stride = stride;
+  f.count = count;
+  f.fixed_len = stride > l3_offset ? (uint32_t)std::min<uint64_t>(stride - l3_offset, 0xFFFFFFFFu) : 0u;
+  f.l3_offset = l3_offset;
+  f.family = family;
+  f.verify = verify ? 1u : 0u;
+  return hip_err(launch_family_fix(f, 16 * d.n_cu, st));
+}
+
 }  // namespace
 
 extern "C" {
@@ -399,8 +423,9 @@ void *ricrc_stream(ricrc_ctx *ctx, int dev) {
 
 static int batch_device_impl(ricrc_ctx *ctx, int dev, const void *d_base, const uint64_t *d_off,
                              const uint32_t *d_len, uint32_t stride, uint64_t count, uint32_t l3_offset,
-                             uint32_t *d_out, void *stream, bool verify) {
+                             uint32_t *d_out, void *stream, bool verify, uint32_t flags = RICRC_F_IPV4) {
   if (!ctx || dev < 0 || dev >= (int)ctx->devs.size()) return -EINVAL;
+  if (flags > RICRC_F_AUTO) return -EINVAL;
   if (count == 0) return 0;
   if (!d_base || !d_out) return -EINVAL;
   if (!d_off && stride == 0) return -EINVAL;
@@ -409,7 +434,7 @@ static int batch_device_impl(ricrc_ctx *ctx, int dev, const void *d_base, const 
   DeviceGuard g(d.id);
   if (!g.ok()) return -ENODEV;
   hipStream_t st = (hipStream_t)stream;  // NULL = the HIP null stream, like any HIP API
-  return launch_batch(d, (const uint8_t *)d_base, d_off, d_len, stride, count, l3_offset, d_out, st, verify);
+  return launch_batch(d, (const uint8_t *)d_base, d_off, d_len, stride, count, l3_offset, d_out, st, verify, flags);
 }
 
 int ricrc_batch_device(ricrc_ctx *ctx, int dev, const void *d_base, const uint64_t *d_off,
@@ -422,6 +447,18 @@ int ricrc_verify_device(ricrc_ctx *ctx, int dev, const void *d_base, const uint6
                         const uint32_t *d_len, uint32_t stride, uint64_t count, uint32_t l3_offset,
                         uint32_t *d_out, void *stream) {
   return batch_device_impl(ctx, dev, d_base, d_off, d_len, stride, count, l3_offset, d_out, stream, true);
+}
+
+int ricrc_batch_device_ex(ricrc_ctx *ctx, int dev, const void *d_base, const uint64_t *d_off,
+                          const uint32_t *d_len, uint32_t stride, uint64_t count, uint32_t l3_offset,
+                          uint32_t *d_out, void *stream, uint32_t flags) {
+  return batch_device_impl(ctx, dev, d_base, d_off, d_len, stride, count, l3_offset, d_out, stream, false, flags);
+}
+
+int ricrc_verify_device_ex(ricrc_ctx *ctx, int dev, const void *d_base, const uint64_t *d_off,
+                           const uint32_t *d_len, uint32_t stride, uint64_t count, uint32_t l3_offset,
+                           uint32_t *d_out, void *stream, uint32_t flags) {
+  return batch_device_impl(ctx, dev, d_base, d_off, d_len, stride, count, l3_offset, d_out, stream, true, flags);
 }
 
 int ricrc_repair_device(ricrc_ctx *ctx, int dev, void *d_base, const uint64_t *d_off, const uint32_t *d_len,
@@ -576,7 +613,12 @@ extern "C" {
 //              the pinned slot, 16-byte aligned, with new offsets.
 int ricrc_batch_host(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *off, const uint32_t *len,
                      uint32_t stride, uint64_t count, uint32_t l3_offset, uint32_t *out) {
-  if (!ctx || ctx->devs.empty()) return -EINVAL;
+  return ricrc_batch_host_ex(ctx, base, off, len, stride, count, l3_offset, out, RICRC_F_IPV4);
+}
+
+int ricrc_batch_host_ex(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *off, const uint32_t *len,
+                        uint32_t stride, uint64_t count, uint32_t l3_offset, uint32_t *out, uint32_t flags) {
+  if (!ctx || ctx->devs.empty() || flags > RICRC_F_AUTO) return -EINVAL;
   if (count == 0) return 0;
   if (!base || !out) return -EINVAL;
   if (!off && stride == 0) return -EINVAL;
@@ -690,12 +732,12 @@ int ricrc_batch_host(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *off, c
       }
       const bool fixed = span && !off && !len;  // frames at i*stride from d_buf + pad
       if (fixed) {
-        rc = launch_batch(d, sl.d_buf + pad, nullptr, nullptr, stride, m, kl3, sl.d_out, sl.st, false);
+        rc = launch_batch(d, sl.d_buf + pad, nullptr, nullptr, stride, m, kl3, sl.d_out, sl.st, false, flags);
       } else {
         HIP_TRY(hipMemcpyAsync(sl.d_off, sl.h_off, m * sizeof(uint64_t), hipMemcpyHostToDevice, sl.st));
         for (uint64_t i = 0; i < m; ++i) sl.h_len[i] = (uint32_t)pkt_len(lo + i);
         HIP_TRY(hipMemcpyAsync(sl.d_len, sl.h_len, m * sizeof(uint32_t), hipMemcpyHostToDevice, sl.st));
-        rc = launch_batch(d, sl.d_buf, sl.d_off, sl.d_len, 0, m, kl3, sl.d_out, sl.st, false);
+        rc = launch_batch(d, sl.d_buf, sl.d_off, sl.d_len, 0, m, kl3, sl.d_out, sl.st, false, flags);
       }
       if (rc) return rc;
       HIP_TRY(hipMemcpyAsync(sl.h_out, sl.d_out, m * sizeof(uint32_t), hipMemcpyDeviceToHost, sl.st));

@@ -172,6 +172,22 @@ struct RepairArgs {
 };
 hipError_t launch_repair(const RepairArgs &a, int grid, hipStream_t st);
 
+// Address-family fix-up after a batch kernel ran with the IPv4 masks
+// (icrc_repair.hip): out[i] (the IPv4-mask ICRC) becomes the family's ICRC,
+// or, with verify, 1/0 = trailer matches it.
+struct FamilyFixArgs {
+  const uint8_t *base;
+  const uint64_t *off;  // may be null (then i * stride)
+  const uint32_t *len;  // may be null (then fixed_len)
+  const uint32_t *x8n;  // x^(8 k), k in [0, 65536)
+  uint32_t *out;
+  uint64_t stride, count;
+  uint32_t fixed_len, l3_offset;
+  uint32_t family;      // kFamV6 / kFamAuto
+  uint32_t verify;
+};
+hipError_t launch_family_fix(const FamilyFixArgs &a, int grid, hipStream_t st);
+
 hipError_t launch_stream(const StreamArgs &a, int cpl, int grid, hipStream_t st);
 hipError_t launch_tsk(const TskArgs &a, int grid, hipStream_t st);
 // Returns hipErrorInvalidValue for an n it has no instantiation for.

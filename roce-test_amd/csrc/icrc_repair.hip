@@ -109,7 +109,68 @@ __global__ __launch_bounds__(256) void repair_kernel(RepairArgs a) {
   }
 }
 
+// Address-family fix-up (ricrc_batch_device_ex & co.).  The batch kernels
+// apply the reference's IPv4 masks.  A packet's register is linear in its
+// bytes and the two families' masks differ only in L3 [0, 56), so
+//   icrc_v6(P) = icrc_v4(P) ^ crc0(D) * x^(8 (n - 4 - h)),
+//   D = (P|m4) ^ (P|m6) over the h = min(56, n-4) header bytes,
+// byte k of D being (m4[k] ^ m6[k]) & ~P[k].  One lane per packet reads the
+// header (aligned dwords, never outside the packet), folds D with the Sarwate
+// chain in LDS and applies the shift; verify mode compares with the trailer
+// here (the batch kernel ran in compute mode).
+__global__ __launch_bounds__(256) void family_fix_kernel(FamilyFixArgs a) {
+  __shared__ uint32_t tab[256];
+  tab[threadIdx.x] = g_tab.t[0][threadIdx.x];
+  __syncthreads();
+  constexpr uint32_t kH = kMaskSpan;  // 56
+  const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.count; i += nthreads) {
+    const uint32_t n = a.len ? a.len[i] : a.fixed_len;
+    if (n < 4 || n > kMaxLen) {
+      a.out[i] = 0;  // the batch kernel's value for an invalid length, in both modes
+      continue;
+    }
+    const uint8_t *p = a.base + (a.off ? a.off[i] : i * a.stride) + a.l3_offset;
+    uint32_t r = a.out[i];
+    const bool v6 = a.family == kFamV6 || (a.family == kFamAuto && (p[0] >> 4) == 6);
+    if (v6) {
+      const uint32_t h = n - 4 < kH ? n - 4 : kH;
+      const uintptr_t q = (uintptr_t)p;
+      const uint32_t *qw = reinterpret_cast<const uint32_t *>(q & ~(uintptr_t)3);
+      const uint32_t sh = (uint32_t)(q & 3u);
+      uint32_t hw[kH / 4 + 1];
+#pragma unroll
+      for (uint32_t j = 0; j <= kH / 4; ++j) hw[j] = 4 * j < sh + h ? qw[j] : 0u;
+      uint32_t c = 0;
+#pragma unroll
+      for (uint32_t j = 0; j < kH / 4; ++j) {
+        const uint32_t w = __builtin_amdgcn_alignbyte(hw[j + 1], hw[j], sh);
+        const uint32_t dm = mask_word(kFamV4, j) ^ mask_word(kFamV6, j);  // compile-time per j
+#pragma unroll
+        for (uint32_t b = 0; b < 4; ++b) {
+          const uint32_t k = 4 * j + b;
+          if (k < h) {
+            const uint32_t d = (dm >> (8 * b)) & ~(w >> (8 * b)) & 0xFFu;
+            c = tab[(c ^ d) & 0xFFu] ^ (c >> 8);
+          }
+        }
+      }
+      r ^= gf_mul_dev(c, a.x8n[n - 4 - h]);
+    }
+    if (a.verify) r = load_le32(p + (n - 4)) == r ? 1u : 0u;
+    a.out[i] = r;
+  }
+}
+
 }  // namespace
+
+hipError_t launch_family_fix(const FamilyFixArgs &a, int grid, hipStream_t st) {
+  if (a.count == 0) return hipSuccess;
+  const uint64_t need = (a.count + 255) / 256;
+  const unsigned blocks = (unsigned)std::min<uint64_t>(need, (uint64_t)grid);
+  hipLaunchKernelGGL(family_fix_kernel, dim3(blocks), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
 
 hipError_t launch_repair(const RepairArgs &a, int grid, hipStream_t st) {
   if (a.count == 0) return hipSuccess;

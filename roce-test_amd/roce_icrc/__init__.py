@@ -35,7 +35,8 @@ EXPORTED = (
     "ricrc_one", "ricrc_verify_one", "ricrc_stamp_one", "ricrc_is_rocev2", "ricrc_shift",
     "ricrc_one_ex", "ricrc_verify_one_ex", "ricrc_stamp_one_ex", "ricrc_classify", "ricrc_repair_one",
     "ricrc_combine", "ricrc_create", "ricrc_create_devices", "ricrc_destroy", "ricrc_device_count", "ricrc_batch_host",
-    "ricrc_batch_device", "ricrc_verify_device", "ricrc_repair_device", "ricrc_host_alloc", "ricrc_host_free",
+    "ricrc_batch_device", "ricrc_verify_device", "ricrc_repair_device", "ricrc_batch_host_ex",
+    "ricrc_batch_device_ex", "ricrc_verify_device_ex", "ricrc_host_alloc", "ricrc_host_free",
     "ricrc_host_register", "ricrc_host_unregister", "ricrc_synth_device", "ricrc_stream", "ricrc_strerror",
 )
 
@@ -82,6 +83,9 @@ def _load():
         "ricrc_batch_host": ([vp, u8p, vp, vp, u32, u64, u32, vp], i32),
         "ricrc_batch_device": ([vp, i32, vp, vp, vp, u32, u64, u32, vp, vp], i32),
         "ricrc_verify_device": ([vp, i32, vp, vp, vp, u32, u64, u32, vp, vp], i32),
+        "ricrc_batch_host_ex": ([vp, u8p, vp, vp, u32, u64, u32, vp, u32], i32),
+        "ricrc_batch_device_ex": ([vp, i32, vp, vp, vp, u32, u64, u32, vp, vp, u32], i32),
+        "ricrc_verify_device_ex": ([vp, i32, vp, vp, vp, u32, u64, u32, vp, vp, u32], i32),
         "ricrc_repair_device": ([vp, i32, vp, vp, vp, u32, u64, u32, u32, u32, vp, u32, u32, u32, vp, vp], i32),
         "ricrc_host_alloc": ([vp, u64], vp),
         "ricrc_host_free": ([vp, vp], None),
@@ -265,25 +269,26 @@ class Context:
 
     # -- host in, host out ------------------------------------------------
     def batch_host(self, buf, offsets=None, lengths=None, stride: int = 0, l3_offset: int = 0,
-                   count: int | None = None) -> np.ndarray:
+                   count: int | None = None, family: str = "v4") -> np.ndarray:
         buf = np.ascontiguousarray(buf).reshape(-1).view(np.uint8)
         off = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint64)
         ln = None if lengths is None else np.ascontiguousarray(lengths, dtype=np.uint32)
         if count is None:
             count = len(off) if off is not None else (len(ln) if ln is not None else buf.size // stride)
         out = np.empty(count, dtype=np.uint32)
-        rc = lib.ricrc_batch_host(self._h, buf.ctypes.data, _ptr(off), _ptr(ln), stride, count,
-                                  l3_offset, out.ctypes.data)
+        rc = lib.ricrc_batch_host_ex(self._h, buf.ctypes.data, _ptr(off), _ptr(ln), stride, count,
+                                     l3_offset, out.ctypes.data, _fam(family))
         if rc:
             raise ICRCError(rc, "ricrc_batch_host")
         return out
 
     # -- device resident --------------------------------------------------
     def batch_device(self, base, count: int, out, stride: int = 0, offsets=None, lengths=None,
-                     l3_offset: int = 0, dev: int = 0, stream=None, verify: bool = False) -> None:
-        fn = lib.ricrc_verify_device if verify else lib.ricrc_batch_device
+                     l3_offset: int = 0, dev: int = 0, stream=None, verify: bool = False,
+                     family: str = "v4") -> None:
+        fn = lib.ricrc_verify_device_ex if verify else lib.ricrc_batch_device_ex
         rc = fn(self._h, dev, _ptr(base), _ptr(offsets), _ptr(lengths), stride, count, l3_offset,
-                _ptr(out), _stream_ptr(stream))
+                _ptr(out), _stream_ptr(stream), _fam(family))
         if rc:
             raise ICRCError(rc, "ricrc_verify_device" if verify else "ricrc_batch_device")
 
