@@ -38,8 +38,10 @@ static constexpr int kStageBytes = 2048;  // TSK: per-wave LDS staging
 template <int CPL, bool PIPE>
 __global__ __launch_bounds__(kBlock) void icrc_stream_kernel(StreamArgs a) {
   __shared__ uint32_t lds[kLdsWords];
-  fill_tables(lds);
-  __syncthreads();
+  // The table entry's load goes first; with PIPE the wave's first packets are
+  // requested before the tables are built (waiting for the table load leaves
+  // them in flight), so the fill no longer sits in front of the first loads.
+  const uint32_t tab_v = table_entry(g_tab);
 
   constexpr int NP = 4 * CPL;   // 16-byte pieces per lane
   constexpr int NW = 16 * CPL;  // words per lane
@@ -124,20 +126,32 @@ __global__ __launch_bounds__(kBlock) void icrc_stream_kernel(StreamArgs a) {
   };
 
   if (PIPE) {
-    u32x4 cur[NP], nxt[NP];
+    // Two steps in flight ahead of the fold (a wave does only a few steps on
+    // small batches, so the first two loads overlap the table fill).
+    u32x4 cur[NP], nxt[NP], nx2[NP];
     uint64_t it = wave;
-    if (it < a.n_iters) load(it, cur);
+    const uint64_t last = a.n_iters - 1;  // n_iters >= 1
+    load(it < last ? it : last, cur);      // unconditional: no branch join
+    load(it + nwaves < last ? it + nwaves : last, nxt);
+    __builtin_amdgcn_sched_barrier(0);
+    table_store(lds, tab_v);
+    __syncthreads();
     for (; it < a.n_iters; it += nwaves) {
-      // Unconditional prefetch (the last step re-loads itself) so the compiler
-      // counts vmcnt exactly instead of draining at a branch join.
-      const uint64_t itn = it + nwaves < a.n_iters ? it + nwaves : it;
-      load(itn, nxt);
+      // Unconditional prefetch (past the end it re-loads the last step) so the
+      // compiler counts vmcnt exactly instead of draining at a branch join.
+      const uint64_t it2 = it + 2 * nwaves < last ? it + 2 * nwaves : last;
+      load(it2, nx2);
       __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the fold
       fold(it, cur);
 #pragma unroll
-      for (int k = 0; k < NP; ++k) cur[k] = nxt[k];
+      for (int k = 0; k < NP; ++k) {
+        cur[k] = nxt[k];
+        nxt[k] = nx2[k];
+      }
     }
   } else {
+    table_store(lds, tab_v);
+    __syncthreads();
     for (uint64_t it = wave; it < a.n_iters; it += nwaves) {
       u32x4 v[NP];
       load(it, v);
