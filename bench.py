@@ -9,6 +9,12 @@ north_star's multi-GPU design asks).
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+    python bench.py --mix        # BASELINE configs[4]: 4 M mixed-MTU packets per GPU
+
+--mix runs the C4 workload instead of the headline: 4,194,304 packets per GPU
+with lengths uniform over {64, 256, 1024, 4096}, packed back to back and
+addressed by uint64 offsets + uint32 lengths (the ragged path: bucketing
+passes + strided-chain fold + piece kernel + gather), its own metric name.
 
 Prints ONE JSON line on rank 0 (the task's bench contract) with a
 ``roofline`` block (kernel bytes / HIP-event kernel time vs 8 TB/s HBM) and,
@@ -28,6 +34,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "roce-test_amd"))
 
 METRIC = "device-resident ICRC GiB/s on 1M×4096B RoCE packets; bit-exact vs reference"
+MIX_METRIC = "device-resident ICRC GiB/s on mixed-MTU (64/256/1024/4096 B) RoCE packets; bit-exact vs reference"
+MIX_SIZES = (64, 256, 1024, 4096)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 SEED = 0x1CEC0DE
 
@@ -39,15 +47,21 @@ def parse():
     # The first ~20 launches of a fresh process run ~10 % slower (clock / TLB
     # ramp measured in tools/microbench/abl.hip); 40 untimed steps cover it.
     ap.add_argument("--warmup", type=int, default=40)
-    ap.add_argument("--count", type=int, default=1 << 20, help="packets per GPU")
-    ap.add_argument("--size", type=int, default=4096, help="L3 packet bytes (IPv4 total_len)")
+    ap.add_argument("--count", type=int, default=None, help="packets per GPU (default 1 M; 4 M with --mix)")
+    ap.add_argument("--size", "--mtu", dest="size", type=int, default=4096, help="L3 packet bytes (IPv4 total_len)")
+    ap.add_argument("--mix", action="store_true",
+                    help="C4: lengths uniform over 64/256/1024/4096 B, offsets + lengths (ragged path)")
+    ap.add_argument("--seed", type=int, default=SEED)
     ap.add_argument("--no-gather", action="store_true", help="skip the RCCL all-gather at N>1")
     ap.add_argument("--in-stream-gather", dest="overlap_gather", action="store_false",
                     help="order step i's all-gather after its kernel on the compute stream "
                          "(default: async on RCCL's stream, overlapping step i+1's kernel)")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="wall budget of the CPU baseline")
     ap.add_argument("--no-cpu", action="store_true")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.count is None:
+        a.count = (4 << 20) if a.mix else (1 << 20)
+    return a
 
 
 def kernel_source_hash():
@@ -85,7 +99,7 @@ def kernel_label(size):
     return "streaming ICRC kernel"
 
 
-def cpu_baseline(sample_host, got_sample, size, budget_s):
+def cpu_baseline(sample_host, got_sample, size, budget_s, offsets=None, lengths=None):
     """Time the C oracle (slice-by-8, pthreads over the host's cores)."""
     import numpy as np
 
@@ -93,25 +107,58 @@ def cpu_baseline(sample_host, got_sample, size, budget_s):
     import oracle_c
 
     threads = max(1, min(16, len(os.sched_getaffinity(0))))
-    want = oracle_c.icrc_batch(sample_host, stride=size, threads=threads)
+    kw = dict(offsets=offsets, lengths=lengths) if offsets is not None else dict(stride=size)
+    want = oracle_c.icrc_batch(sample_host, threads=threads, **kw)
     if not np.array_equal(want, got_sample):
         raise SystemExit("bench: GPU ICRCs differ from the oracle on the CPU-baseline sample")
     reps, t0 = 0, time.perf_counter()
     while True:
-        oracle_c.icrc_batch(sample_host, stride=size, threads=threads)
+        oracle_c.icrc_batch(sample_host, threads=threads, **kw)
         reps += 1
         dt = time.perf_counter() - t0
         if dt >= budget_s:
             break
-    nbytes = sample_host.size * reps
+    nbytes = (int(lengths.sum(dtype=np.uint64)) if lengths is not None else sample_host.size) * reps
+    what = (f"{len(lengths)} mixed-MTU packets ({int(lengths.sum(dtype=np.uint64))} B)" if lengths is not None
+            else f"{sample_host.shape[0]} x {size} B packets")
     return {
         "value": nbytes / dt / 2**30,
         "unit": "GiB/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{sample_host.shape[0]} x {size} B packets of the same synthetic batch, "
+        "sample": f"{what} of the same synthetic batch, "
                   f"{reps} passes in {dt:.1f} s; oracle/icrc_oracle.c slice-by-8, {threads} threads",
     }
+
+
+def build_mix(torch, np, ctx, dev, stream, seed, rank, count):
+    """C4 batch on `dev`: lengths uniform over MIX_SIZES (numpy PCG64 keyed on
+    (seed, rank), so every rank holds its own shard), packets packed back to
+    back; packet contents from the device generator of its size class,
+    scattered into place.  Returns (buf, offsets, lengths, d_offsets, d_lengths)."""
+    rng = np.random.default_rng([seed, rank])
+    lens = rng.choice(np.array(MIX_SIZES, np.uint32), size=count)
+    offs = np.zeros(count, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    nbytes = int(lens.sum(dtype=np.uint64))
+    buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    for n in MIX_SIZES:
+        idx = np.flatnonzero(lens == n)
+        if len(idx) == 0:
+            continue
+        tmp = torch.empty(len(idx) * n, dtype=torch.uint8, device=dev)
+        ctx.synth_device(tmp, seed, rank * count, len(idx), n, stream=stream)
+        rows = tmp.view(len(idx), n)
+        starts = torch.from_numpy(offs[idx].view(np.int64)).to(dev)
+        cols = torch.arange(n, device=dev)
+        step = max(1, (64 << 20) // n)
+        for c in range(0, len(idx), step):
+            ix = (starts[c:c + step, None] + cols[None, :]).reshape(-1)
+            buf[ix] = rows[c:c + step].reshape(-1)
+        del tmp, rows, starts
+    d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
+    d_lens = torch.from_numpy(lens.view(np.int32)).to(dev)
+    return buf, offs, lens, d_offs, d_lens
 
 
 def main():
@@ -135,10 +182,16 @@ def main():
 
     count, size = args.count, args.size
     stream = torch.cuda.current_stream()
-    pk = torch.empty(count * size, dtype=torch.uint8, device=dev)
-    # Rank r owns global packets [r*count, (r+1)*count) (dist.shard_range of
-    # world*count): generated on its own device from the global index.
-    ctx.synth_device(pk, SEED, rank * count, count, size, stream=stream)
+    if args.mix:
+        pk, h_offs, h_lens, d_offs, d_lens = build_mix(torch, np, ctx, dev, stream, args.seed, rank, count)
+        rank_bytes = int(h_lens.sum(dtype=np.uint64))
+    else:
+        pk = torch.empty(count * size, dtype=torch.uint8, device=dev)
+        # Rank r owns global packets [r*count, (r+1)*count) (dist.shard_range of
+        # world*count): generated on its own device from the global index.
+        ctx.synth_device(pk, args.seed, rank * count, count, size, stream=stream)
+        d_offs = d_lens = None
+        rank_bytes = count * size
     do_gather = distributed and not args.no_gather
     # Double-buffered results.  Default: step i's all-gather runs async on
     # RCCL's stream, overlapping step i+1's kernel, and a buffer is reused only
@@ -158,7 +211,10 @@ def main():
             pending[b] = None
         if ev is not None:
             ev[0].record(stream)
-        ctx.batch_device(pk, count, outs[b], stride=size, stream=stream)
+        if args.mix:
+            ctx.batch_device(pk, count, outs[b], offsets=d_offs, lengths=d_lens, stream=stream)
+        else:
+            ctx.batch_device(pk, count, outs[b], stride=size, stream=stream)
         if ev is not None:
             ev[1].record(stream)
         if do_gather:
@@ -198,19 +254,32 @@ def main():
         if not torch.equal(g[rank * count:(rank + 1) * count], out):
             raise SystemExit("bench: all-gathered ICRCs do not contain this rank's shard")
 
+    all_bytes = rank_bytes
     if distributed:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
+        nb = torch.tensor([rank_bytes], dtype=torch.int64, device=dev)
+        dist.all_reduce(nb, op=dist.ReduceOp.SUM)
+        all_bytes = int(nb[0])
 
-    total_bytes = world * count * size * args.steps
+    total_bytes = all_bytes * args.steps
     value = total_bytes / elapsed / 2**30
-    alg_bytes = count * size + 4 * count  # per launch: packets read + ICRCs written
+    # per launch: packets read + ICRCs written (+ 12 B of offset/length descriptors per packet, ragged)
+    alg_bytes = rank_bytes + 4 * count + (12 * count if args.mix else 0)
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-    traffic = load_traffic(size, count)
+    traffic = None if args.mix else load_traffic(size, count)
 
+    if args.mix:
+        workload = (f"{count} RoCEv2 packets per GPU, lengths uniform over 64/256/1024/4096 B "
+                    f"({rank_bytes} B on rank 0), packed, uint64 offsets + uint32 lengths, device-resident, "
+                    "ragged strided-chain path (bucketing passes + icrc_rsck_kernel + piece kernel + gather)")
+    else:
+        workload = f"{count} x {size} B RoCEv2 packets per GPU, device-resident, " + kernel_label(size)
+    if do_gather:
+        workload += " + RCCL all-gather of ICRCs" + (" (overlapped)" if args.overlap_gather else "")
     result = {
-        "metric": METRIC,
+        "metric": MIX_METRIC if args.mix else METRIC,
         "value": round(value, 2),
         "unit": "GiB/s",
         "n_gpus": world,
@@ -222,10 +291,8 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (device-generated RoCEv2 SEND_ONLY packets, seeded; reference P4 header template)",
-        "config": {"workload": f"{count} x {size} B RoCEv2 packets per GPU, device-resident, "
-                               + kernel_label(size) + (" + RCCL all-gather of ICRCs" + (" (overlapped)" if args.overlap_gather else "")
-                                                           if do_gather else ""),
-                   "packets_per_gpu": count, "packet_bytes": size,
+        "config": {"workload": workload,
+                   "packets_per_gpu": count, "packet_bytes": "mix 64/256/1024/4096" if args.mix else size,
                    "parallelism": f"dp{world}" + (" (all-gather u32 results)" if do_gather else "")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -235,9 +302,15 @@ def main():
     if world == 1 and not args.no_cpu:
         ns = min(count, 32768)
         torch.cuda.synchronize()
-        sample = pk[: ns * size].cpu().numpy().reshape(ns, size)
         got = out[:ns].cpu().numpy().view(np.uint32)
-        result["cpu_baseline"] = cpu_baseline(sample, got, size, args.cpu_seconds)
+        if args.mix:
+            span = int(h_offs[ns - 1]) + int(h_lens[ns - 1])
+            sample = pk[:span].cpu().numpy()
+            result["cpu_baseline"] = cpu_baseline(sample, got, size, args.cpu_seconds,
+                                                  offsets=h_offs[:ns].copy(), lengths=h_lens[:ns].copy())
+        else:
+            sample = pk[: ns * size].cpu().numpy().reshape(ns, size)
+            result["cpu_baseline"] = cpu_baseline(sample, got, size, args.cpu_seconds)
 
     if rank == 0:
         print(json.dumps(result), flush=True)

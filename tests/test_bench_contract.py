@@ -29,6 +29,16 @@ def test_driver_flags_parse(monkeypatch):
     assert (a.gpus, a.steps, a.warmup, a.overlap_gather) == (8, 7, 3, False)
 
 
+def test_mix_and_aliases_parse(monkeypatch):
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--mix"])
+    a = bench.parse()
+    assert a.mix and a.count == 4 << 20  # BASELINE configs[4]: 4 M mixed-MTU packets
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--mtu", "1024", "--count", "5", "--seed", "7"])
+    a = bench.parse()
+    assert (a.size, a.count, a.seed, a.mix) == (1024, 5, 7, False)
+    assert bench.MIX_METRIC != bench.METRIC and bench.MIX_SIZES == (64, 256, 1024, 4096)
+
+
 def test_metric_matches_baseline_json():
     with open(os.path.join(ROOT, "BASELINE.json")) as f:
         assert json.load(f)["metric"] == bench.METRIC
