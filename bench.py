@@ -1,32 +1,42 @@
 #!/usr/bin/env python3
 """Headline benchmark: device-resident RoCEv2 ICRC GiB/s (BASELINE.json metric).
 
-One step = one pass of the ICRC hot path (libroceicrc's streaming kernel on
-gfx950) over one resident batch of synthetic RoCEv2 SEND_ONLY packets:
-1,048,576 x 4096 B per GPU (BASELINE headline config; weak scaling at N > 1,
-where every rank also all-gathers the 4-byte results over RCCL, as the
-north_star's multi-GPU design asks).
+One step = one pass of the ICRC hot path (libroceicrc's gfx950 kernels) over
+one resident batch of synthetic RoCEv2 SEND_ONLY packets, plus, at N > 1, the
+RCCL all-gather of the 4-byte results over xGMI (the north_star's multi-GPU
+design; overlapped with the next step's kernel by default).
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W]     N > 1: self-launches torchrun
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
-    python bench.py --mix        # BASELINE configs[4]: 4 M mixed-MTU packets per GPU
+    python bench.py --global-count 4194304               C3: a fixed 4 M x 4 KiB batch
+    python bench.py --mix                                C4: mixed-MTU ragged batch
 
---mix runs the C4 workload instead of the headline: 4,194,304 packets per GPU
-with lengths uniform over {64, 256, 1024, 4096}, packed back to back and
-addressed by uint64 offsets + uint32 lengths (the ragged path: bucketing
-passes + strided-chain fold + piece kernel + gather), its own metric name.
+Workloads (the packet batch is one global batch of T packets,
+cut into contiguous per-rank shards by roce_icrc.dist, each rank generating
+its shard on its own device from the global packet index):
+  default       T = 1,048,576 x 4096 B per GPU (BASELINE headline; weak scaling)
+  --global-count T   T packets in all, shard_range split (strong scaling; C3)
+  --mix         lengths uniform over {64, 256, 1024, 4096}, packed back to
+                back, uint64 offsets + uint32 lengths (the ragged path); T =
+                4 M per GPU (weak) or --global-count; shards cut at equal bytes
+                (byte_balanced_cuts), so shard sizes differ and the gather is
+                the unequal-shard IcrcGather (one all_gather_into_tensor).
 
 Prints ONE JSON line on rank 0 (the task's bench contract) with a
-``roofline`` block (kernel bytes / HIP-event kernel time vs 8 TB/s HBM) and,
-at N = 1, a ``cpu_baseline`` block (the C oracle port timed on this host's
-cores over a bounded sample of the same packets; the sample's GPU results are
-also checked bit-exact against it).
+``roofline`` block (rank 0's kernel bytes / HIP-event kernel time vs 8 TB/s)
+and, at N = 1, a ``cpu_baseline`` block (the C oracle port on this host's CPU
+share over a bounded sample of the same packets) plus the C0 per-packet CPU
+latency of the product's ricrc_one.  Every rank checks a sample of EVERY
+rank's gathered ICRCs against the oracle restatement of the generator (after
+the timed region), so "bit-exact" holds at every N.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -38,16 +48,19 @@ MIX_METRIC = "device-resident ICRC GiB/s on mixed-MTU (64/256/1024/4096 B) RoCE 
 MIX_SIZES = (64, 256, 1024, 4096)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 SEED = 0x1CEC0DE
+# Headline kernel's sources: PMC traffic (profiles/pmc_traffic.json) is only
+# reported for the exact sources it was measured on.
+SCK_SOURCES = ("icrc_sck.hip", "icrc_sck.h", "icrc_device.h", "icrc_math.h")
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
-    # The first ~20 launches of a fresh process run ~10 % slower (clock / TLB
-    # ramp measured in tools/microbench/abl.hip); 40 untimed steps cover it.
     ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--count", type=int, default=None, help="packets per GPU (default 1 M; 4 M with --mix)")
+    ap.add_argument("--global-count", type=int, default=None,
+                    help="packets in the whole batch, split over the ranks (strong scaling; C3 = 4194304)")
     ap.add_argument("--size", "--mtu", dest="size", type=int, default=4096, help="L3 packet bytes (IPv4 total_len)")
     ap.add_argument("--mix", action="store_true",
                     help="C4: lengths uniform over 64/256/1024/4096 B, offsets + lengths (ragged path)")
@@ -56,30 +69,60 @@ def parse():
     ap.add_argument("--in-stream-gather", dest="overlap_gather", action="store_false",
                     help="order step i's all-gather after its kernel on the compute stream "
                          "(default: async on RCCL's stream, overlapping step i+1's kernel)")
-    ap.add_argument("--cpu-seconds", type=float, default=6.0, help="wall budget of the CPU baseline")
+    # After >= 20 ms of GPU idle the first ~12 launches run up to 15 % slower
+    # (profiles/r02/ramp_probe.jsonl); ricrc_prime keeps the device busy this
+    # long right before the warmup (untimed).
+    ap.add_argument("--prime-ms", type=float, default=25.0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="wall budget of the CPU baseline")
     ap.add_argument("--no-cpu", action="store_true")
-    a = ap.parse_args()
+    a = ap.parse_args(argv)
     if a.count is None:
         a.count = (4 << 20) if a.mix else (1 << 20)
     return a
 
 
+def launcher_argv(argv, gpus, port):
+    """The torch.distributed.run command that re-runs this script on `gpus` ranks."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def check_world(args, env=os.environ):
+    """None when this process runs the bench as it is; (0, "relaunch") for
+    --gpus N > 1 outside torchrun (re-run on N ranks); (2, message) when
+    WORLD_SIZE disagrees with --gpus (never report a mislabelled run)."""
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return None if args.gpus == 1 else (0, "relaunch")
+    if int(ws) != args.gpus:
+        return (2, f"bench: --gpus {args.gpus} but WORLD_SIZE={ws}; refusing to report a mislabelled run")
+    return None
+
+
 def kernel_source_hash():
-    """sha256 of the headline kernel's sources: PMC traffic measured on other code is stale."""
+    """sha256 of the headline kernel's sources (SCK_SOURCES)."""
     import hashlib
 
     h = hashlib.sha256()
-    for name in ("icrc_kernels.hip", "icrc_device.h", "icrc_math.h", "icrc_kernels.h"):
+    for name in SCK_SOURCES:
         with open(os.path.join(ROOT, "roce-test_amd", "csrc", name), "rb") as f:
             h.update(f.read())
     return h.hexdigest()[:16]
 
 
 def load_traffic(size, count):
-    """HBM bytes per launch measured by a separate rocprofv3 --pmc pass
-    (profiles/pmc_traffic.json, produced by tools/pmc_traffic.py) on this very
-    kernel source, or None."""
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")  # from tools/pmc_traffic.py
+    """HBM bytes per launch measured by separate rocprofv3 --pmc passes
+    (profiles/pmc_traffic.json, from tools/pmc_traffic.py) on this very kernel
+    source, or None."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
             d = json.load(f)
@@ -99,14 +142,71 @@ def kernel_label(size):
     return "streaming ICRC kernel"
 
 
-def cpu_baseline(sample_host, got_sample, size, budget_s, offsets=None, lengths=None):
-    """Time the C oracle (slice-by-8, pthreads over the host's cores)."""
-    import numpy as np
+def cpu_share():
+    """Host threads this process may use: its affinity, capped by the CPU share
+    the box grants one GPU (OMP_NUM_THREADS, 16 on the GPU pool)."""
+    n = len(os.sched_getaffinity(0))
+    share = os.environ.get("OMP_NUM_THREADS")
+    if share and share.isdigit() and int(share) > 0:
+        n = min(n, int(share))
+    return max(1, n)
 
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+# ----------------------------------------------------- cpu_baseline leg (oracle)
+def _oracle():
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import icrc_oracle
     import oracle_c
 
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    return oracle_c, icrc_oracle
+
+
+def oracle_check(gathered, sizes, cuts, args, lens_global=None, per_rank=256):
+    """Checker (untimed): regenerate a sample of every rank's packets on the
+    host from the generator's restatement and compare the gathered ICRCs."""
+    import numpy as np
+
+    oracle_c, _ = _oracle()
+    bad = 0
+    for r in range(len(sizes)):
+        lo, n = cuts[r], sizes[r]
+        if n == 0:
+            continue
+        idx = np.unique(np.concatenate([np.arange(min(per_rank, n)),
+                                        np.linspace(0, n - 1, num=min(per_rank, n)).astype(np.int64)]))
+        if lens_global is None:
+            pk = np.concatenate([oracle_c.synth_batch(args.seed, lo + int(k), 1, args.size) for k in idx])
+            want = oracle_c.icrc_batch(pk.reshape(-1), stride=args.size)
+        else:
+            lens = lens_global[lo + idx]
+            bufs = [oracle_c.synth_ragged(args.seed, lo + int(k), lens[j:j + 1])[0] for j, k in enumerate(idx)]
+            offs = np.zeros(len(idx), np.uint64)
+            offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+            want = oracle_c.icrc_batch(np.concatenate(bufs), offsets=offs, lengths=lens)
+        got = gathered[lo + idx]
+        bad += int((got != want).sum())
+    return bad
+
+
+def cpu_baseline(sample_host, got_sample, size, budget_s, offsets=None, lengths=None):
+    """Time the C oracle (slice-by-8, pthreads over this host's CPU share) on a
+    sample of the batch, check the GPU's ICRCs on it, and add a 1-core zlib
+    figure (the Python oracle, zlib.crc32 per packet)."""
+    import numpy as np
+
+    oracle_c, icrc_oracle = _oracle()
+    threads = cpu_share()
     kw = dict(offsets=offsets, lengths=lengths) if offsets is not None else dict(stride=size)
     want = oracle_c.icrc_batch(sample_host, threads=threads, **kw)
     if not np.array_equal(want, got_sample):
@@ -118,51 +218,112 @@ def cpu_baseline(sample_host, got_sample, size, budget_s, offsets=None, lengths=
         dt = time.perf_counter() - t0
         if dt >= budget_s:
             break
-    nbytes = (int(lengths.sum(dtype=np.uint64)) if lengths is not None else sample_host.size) * reps
-    what = (f"{len(lengths)} mixed-MTU packets ({int(lengths.sum(dtype=np.uint64))} B)" if lengths is not None
+    sample_bytes = int(lengths.sum(dtype=np.uint64)) if lengths is not None else sample_host.size
+    what = (f"{len(lengths)} mixed-MTU packets ({sample_bytes} B)" if lengths is not None
             else f"{sample_host.shape[0]} x {size} B packets")
+    # 1 core, zlib.crc32 per packet (icrc_oracle.icrc), ~2 s
+    flat = sample_host.reshape(-1)
+    pk = ([bytes(flat[int(o): int(o) + int(n)]) for o, n in zip(offsets, lengths)] if offsets is not None
+          else [bytes(r) for r in sample_host])
+    zb, zt0 = 0, time.perf_counter()
+    while time.perf_counter() - zt0 < 2.0:
+        for p in pk[:2048]:
+            icrc_oracle.icrc(p)
+            zb += len(p)
+    zdt = time.perf_counter() - zt0
     return {
-        "value": nbytes / dt / 2**30,
+        "value": sample_bytes * reps / dt / 2**30,
         "unit": "GiB/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{what} of the same synthetic batch, "
-                  f"{reps} passes in {dt:.1f} s; oracle/icrc_oracle.c slice-by-8, {threads} threads",
+        "sample": f"{what} of the same synthetic batch, {reps} passes in {dt:.1f} s; oracle/icrc_oracle.c "
+                  f"slice-by-8 on {threads} threads (this GPU's CPU share of {os.cpu_count()} visible host CPUs)",
+        "cpu_model": cpu_model(),
+        "zlib_1core_GiBs": round(zb / zdt / 2**30, 3),
     }
 
 
-def build_mix(torch, np, ctx, dev, stream, seed, rank, count):
-    """C4 batch on `dev`: lengths uniform over MIX_SIZES (numpy PCG64 keyed on
-    (seed, rank), so every rank holds its own shard), packets packed back to
-    back; packet contents from the device generator of its size class,
-    scattered into place.  Returns (buf, offsets, lengths, d_offsets, d_lengths)."""
-    rng = np.random.default_rng([seed, rank])
-    lens = rng.choice(np.array(MIX_SIZES, np.uint32), size=count)
-    offs = np.zeros(count, np.uint64)
-    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
-    nbytes = int(lens.sum(dtype=np.uint64))
-    buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-    for n in MIX_SIZES:
-        idx = np.flatnonzero(lens == n)
-        if len(idx) == 0:
-            continue
-        tmp = torch.empty(len(idx) * n, dtype=torch.uint8, device=dev)
-        ctx.synth_device(tmp, seed, rank * count, len(idx), n, stream=stream)
-        rows = tmp.view(len(idx), n)
-        starts = torch.from_numpy(offs[idx].view(np.int64)).to(dev)
-        cols = torch.arange(n, device=dev)
-        step = max(1, (64 << 20) // n)
-        for c in range(0, len(idx), step):
-            ix = (starts[c:c + step, None] + cols[None, :]).reshape(-1)
-            buf[ix] = rows[c:c + step].reshape(-1)
-        del tmp, rows, starts
-    d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
-    d_lens = torch.from_numpy(lens.view(np.int32)).to(dev)
-    return buf, offs, lens, d_offs, d_lens
+def c0_latency():
+    """BASELINE configs[0]: ICRC of one 1 KiB RoCE packet on the CPU through the
+    product's per-packet entry point (libroceicrc_cpu.so via ctypes, the way
+    python/simulator.py's crossings would call it)."""
+    import roce_icrc
+
+    pkt = bytearray(os.urandom(1024))
+    pkt[0], pkt[9], pkt[2], pkt[3], pkt[22], pkt[23] = 0x45, 17, 4, 0, 0x12, 0xB7
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < 0.5:
+        for _ in range(1000):
+            roce_icrc.icrc(pkt)
+        n += 1000
+    dt = time.perf_counter() - t0
+    # the C call alone (no Python argument marshalling): ctypes with a raw pointer
+    import ctypes
+
+    buf = (ctypes.c_uint8 * 1024).from_buffer(pkt)
+    f = roce_icrc.cpu.ricrc_one
+    addr = ctypes.addressof(buf)
+    m, t1 = 0, time.perf_counter()
+    while time.perf_counter() - t1 < 0.5:
+        for _ in range(1000):
+            f(addr, 1024)
+        m += 1000
+    dt1 = time.perf_counter() - t1
+    return {"config": "1 x 1024 B RoCEv2 packet, CPU, libroceicrc_cpu.so (BASELINE configs[0])",
+            "us_per_packet_python_api": round(dt / n * 1e6, 3),
+            "us_per_packet_ctypes_call": round(dt1 / m * 1e6, 3)}
 
 
-def main():
-    args = parse()
+def build_batch(torch, np, ctx, dev, stream, args, world, rank):
+    """This rank's shard of the global batch, generated on `dev`.  Returns a
+    dict: buf, d_offs, d_lens, h_offs, h_lens (ragged), cuts, sizes,
+    lens_global (ragged), rank_bytes."""
+    from roce_icrc.dist import byte_balanced_cuts, cuts_to_sizes, shard_range
+
+    T = args.global_count if args.global_count is not None else args.count * world
+    b = {}
+    if args.mix:
+        rng = np.random.default_rng(args.seed)
+        lens_g = rng.choice(np.array(MIX_SIZES, np.uint32), size=T)
+        cuts = byte_balanced_cuts(lens_g, world)
+        lo, hi = cuts[rank], cuts[rank + 1]
+        lens = np.ascontiguousarray(lens_g[lo:hi])
+        offs = np.zeros(len(lens), np.uint64)
+        if len(lens) > 1:
+            offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+        nbytes = int(lens.sum(dtype=np.uint64))
+        buf = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
+        d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
+        d_lens = torch.from_numpy(lens.view(np.int32)).to(dev)
+        ctx.synth_ragged_device(buf, args.seed, lo, len(lens), d_offs, d_lens, stream=stream)
+        b.update(buf=buf, d_offs=d_offs, d_lens=d_lens, h_offs=offs, h_lens=lens, lens_global=lens_g,
+                 rank_bytes=nbytes)
+    else:
+        cuts = [shard_range(T, world, r)[0] for r in range(world)] + [T]
+        lo, hi = cuts[rank], cuts[rank + 1]
+        buf = torch.empty(max((hi - lo) * args.size, 1), dtype=torch.uint8, device=dev)
+        ctx.synth_device(buf, args.seed, lo, hi - lo, args.size, stream=stream)
+        b.update(buf=buf, d_offs=None, d_lens=None, lens_global=None, rank_bytes=(hi - lo) * args.size)
+    b.update(cuts=cuts, sizes=cuts_to_sizes(cuts), T=T)
+    return b
+
+
+def relaunch(args, argv):
+    cmd = launcher_argv(argv, args.gpus, _free_port())
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.call(cmd, env=env)
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    chk = check_world(args)
+    if chk is not None:
+        code, msg = chk
+        if msg == "relaunch":  # --gpus N > 1 outside torchrun: N ranks, before any GPU call
+            return relaunch(args, argv)
+        print(msg, file=sys.stderr)
+        return code
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -172,63 +333,56 @@ def main():
     import torch.distributed as dist
 
     import roce_icrc
+    from roce_icrc.dist import IcrcGather
 
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    distributed = "MASTER_ADDR" in os.environ  # launched by torch.distributed.run
+    distributed = world > 1 or "MASTER_ADDR" in os.environ
     if distributed:
         dist.init_process_group("nccl", device_id=dev)
     ctx = roce_icrc.Context(devices=[local])
 
-    count, size = args.count, args.size
     stream = torch.cuda.current_stream()
-    if args.mix:
-        pk, h_offs, h_lens, d_offs, d_lens = build_mix(torch, np, ctx, dev, stream, args.seed, rank, count)
-        rank_bytes = int(h_lens.sum(dtype=np.uint64))
-    else:
-        pk = torch.empty(count * size, dtype=torch.uint8, device=dev)
-        # Rank r owns global packets [r*count, (r+1)*count) (dist.shard_range of
-        # world*count): generated on its own device from the global index.
-        ctx.synth_device(pk, args.seed, rank * count, count, size, stream=stream)
-        d_offs = d_lens = None
-        rank_bytes = count * size
+    b = build_batch(torch, np, ctx, dev, stream, args, world, rank)
+    count, sizes = b["sizes"][rank], b["sizes"]
+    pk, d_offs, d_lens, rank_bytes = b["buf"], b["d_offs"], b["d_lens"], b["rank_bytes"]
     do_gather = distributed and not args.no_gather
-    # Double-buffered results.  Default: step i's all-gather runs async on
-    # RCCL's stream, overlapping step i+1's kernel, and a buffer is reused only
-    # after the gather that read it has been waited for.  --in-stream-gather:
-    # the gather is ordered after the kernel on the compute stream.  (Each ICRC
-    # workgroup fills a whole CU, so the kernel's blocks on CUs that RCCL holds
-    # start late: measured +3-6 % kernel time with 16-32 CUs held for
-    # 100-150 us, against a fully exposed gather in-stream)
-    outs = [torch.empty(count, dtype=torch.int32, device=dev) for _ in range(2)]
-    gathered = [torch.empty(world * count, dtype=torch.int32, device=dev) for _ in range(2)] if do_gather else None
+    g = IcrcGather(sizes)
+    # Double-buffered results (padded to the longest shard).  Default: step
+    # i's all-gather runs async on RCCL's stream, overlapping step i+1's
+    # kernel, and a buffer is reused only after the gather that read it has
+    # been waited for.  --in-stream-gather: the gather is ordered after the
+    # kernel on the compute stream.
+    outs = [g.local_buffer(dev) for _ in range(2)]
+    gathered = [g.gathered_buffer(dev) for _ in range(2)] if do_gather else None
     pending = [None, None]
 
     def step(i, ev=None):
-        b = i & 1
-        if pending[b] is not None:
-            pending[b].wait()  # the current stream waits for the gather that read outs[b]
-            pending[b] = None
+        j = i & 1
+        if pending[j] is not None:
+            pending[j].wait()  # the current stream waits for the gather that read outs[j]
+            pending[j] = None
         if ev is not None:
             ev[0].record(stream)
-        if args.mix:
-            ctx.batch_device(pk, count, outs[b], offsets=d_offs, lengths=d_lens, stream=stream)
-        else:
-            ctx.batch_device(pk, count, outs[b], stride=size, stream=stream)
+        if count:
+            if args.mix:
+                ctx.batch_device(pk, count, outs[j], offsets=d_offs, lengths=d_lens, stream=stream)
+            else:
+                ctx.batch_device(pk, count, outs[j], stride=args.size, stream=stream)
         if ev is not None:
             ev[1].record(stream)
         if do_gather:
-            if args.overlap_gather:
-                pending[b] = dist.all_gather_into_tensor(gathered[b], outs[b], async_op=True)
-            else:
-                dist.all_gather_into_tensor(gathered[b], outs[b])
+            pending[j] = g.start(outs[j], gathered[j], async_op=args.overlap_gather)
 
     def drain():
-        for b in range(2):
-            if pending[b] is not None:
-                pending[b].wait()
-                pending[b] = None
+        for j in range(2):
+            if pending[j] is not None:
+                pending[j].wait()
+                pending[j] = None
 
+    torch.cuda.synchronize()
+    if args.prime_ms > 0:
+        ctx.prime(int(args.prime_ms * 1000))
     for i in range(args.warmup):
         step(i)
     drain()
@@ -247,12 +401,27 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
-    out = outs[(args.steps - 1) & 1]
-    if do_gather:  # every rank holds all world*count ICRCs in packet order
-        g = gathered[(args.steps - 1) & 1]
-        if not torch.equal(g[rank * count:(rank + 1) * count], out):
+    kern_ms = sum(a.elapsed_time(c) for a, c in evs) / max(args.steps, 1)
+
+    # ---- after the timed region: correctness on every rank
+    last = (args.steps - 1) & 1
+    out = outs[last][:count]
+    if do_gather:
+        gv = gathered[last]
+        if not torch.equal(g.shard_of(gv, rank), out):
             raise SystemExit("bench: all-gathered ICRCs do not contain this rank's shard")
+        full = g.compact(gv)
+    else:
+        full = out
+    full_h = full.cpu().numpy().view(np.uint32)
+    if do_gather or world == 1:
+        bad = oracle_check(full_h, sizes if do_gather else [count], b["cuts"] if do_gather else [0],
+                           args, lens_global=b["lens_global"])
+    else:  # --no-gather at N > 1: only this rank's own shard is here
+        bad = oracle_check(np.concatenate([np.zeros(b["cuts"][rank], np.uint32), full_h]),
+                           [0] * rank + [count], b["cuts"], args, lens_global=b["lens_global"])
+    if bad:
+        raise SystemExit(f"bench: rank {rank}: {bad} sampled ICRCs differ from the oracle")
 
     all_bytes = rank_bytes
     if distributed:
@@ -263,21 +432,24 @@ def main():
         dist.all_reduce(nb, op=dist.ReduceOp.SUM)
         all_bytes = int(nb[0])
 
-    total_bytes = all_bytes * args.steps
-    value = total_bytes / elapsed / 2**30
+    value = all_bytes * args.steps / elapsed / 2**30
     # per launch: packets read + ICRCs written (+ 12 B of offset/length descriptors per packet, ragged)
     alg_bytes = rank_bytes + 4 * count + (12 * count if args.mix else 0)
-    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-    traffic = None if args.mix else load_traffic(size, count)
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
+    traffic = None if args.mix else load_traffic(args.size, count)
 
+    strong = args.global_count is not None
     if args.mix:
-        workload = (f"{count} RoCEv2 packets per GPU, lengths uniform over 64/256/1024/4096 B "
-                    f"({rank_bytes} B on rank 0), packed, uint64 offsets + uint32 lengths, device-resident, "
-                    "ragged strided-chain path (bucketing passes + icrc_rsck_kernel + piece kernel + gather)")
+        workload = (f"{b['T']} RoCEv2 packets in all ({'fixed total' if strong else f'{args.count} per GPU'}), "
+                    "lengths uniform over 64/256/1024/4096 B, packed, uint64 offsets + uint32 lengths, "
+                    f"shards cut at equal bytes; rank 0: {sizes[0]} packets, {rank_bytes if rank == 0 else '?'} B; "
+                    "device-resident, ragged strided-chain path (bucketing passes + icrc_rsck_kernel + piece "
+                    "kernel + gather)")
     else:
-        workload = f"{count} x {size} B RoCEv2 packets per GPU, device-resident, " + kernel_label(size)
+        workload = (f"{b['T']} x {args.size} B RoCEv2 packets in all ({count} on rank 0), device-resident, "
+                    + kernel_label(args.size))
     if do_gather:
-        workload += " + RCCL all-gather of ICRCs" + (" (overlapped)" if args.overlap_gather else "")
+        workload += " + RCCL all-gather of the u32 ICRCs" + (" (overlapped)" if args.overlap_gather else "")
     result = {
         "metric": MIX_METRIC if args.mix else METRIC,
         "value": round(value, 2),
@@ -287,37 +459,40 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (device-generated RoCEv2 SEND_ONLY packets, seeded; reference P4 header template)",
-        "config": {"workload": workload,
-                   "packets_per_gpu": count, "packet_bytes": "mix 64/256/1024/4096" if args.mix else size,
+        "config": {"workload": workload, "packets_total": b["T"], "packets_rank0": sizes[0],
+                   "packet_bytes": "mix 64/256/1024/4096" if args.mix else args.size,
                    "parallelism": f"dp{world}" + (" (all-gather u32 results)" if do_gather else "")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": alg_bytes},
+        "oracle_sampled_all_ranks": True,
     }
 
     if world == 1 and not args.no_cpu:
         ns = min(count, 32768)
-        torch.cuda.synchronize()
-        got = out[:ns].cpu().numpy().view(np.uint32)
+        got = full_h[:ns]
         if args.mix:
+            h_offs, h_lens = b["h_offs"], b["h_lens"]
             span = int(h_offs[ns - 1]) + int(h_lens[ns - 1])
             sample = pk[:span].cpu().numpy()
-            result["cpu_baseline"] = cpu_baseline(sample, got, size, args.cpu_seconds,
+            result["cpu_baseline"] = cpu_baseline(sample, got, args.size, args.cpu_seconds,
                                                   offsets=h_offs[:ns].copy(), lengths=h_lens[:ns].copy())
         else:
-            sample = pk[: ns * size].cpu().numpy().reshape(ns, size)
-            result["cpu_baseline"] = cpu_baseline(sample, got, size, args.cpu_seconds)
+            sample = pk[: ns * args.size].cpu().numpy().reshape(ns, args.size)
+            result["cpu_baseline"] = cpu_baseline(sample, got, args.size, args.cpu_seconds)
+        result["c0"] = c0_latency()
 
     if rank == 0:
         print(json.dumps(result), flush=True)
     ctx.close()
     if distributed:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

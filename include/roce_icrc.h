@@ -22,7 +22,15 @@
  * (shuffle_egress.p4:493), i.e. trailer bytes = v & 0xff, v >> 8, ...
  *
  * Errors: 0 = success, negative errno: -EINVAL (bad length / NULL / alignment),
- * -ENODEV (no GPU), -ENOMEM, -EIO (HIP / RCCL failure).  Nothing aborts.
+ * -ENODEV (no GPU), -ENOMEM, -EIO (HIP / RCCL failure), -EPROTO (not RoCEv2,
+ * strict mode).  Nothing aborts.
+ *
+ * Two shared libraries implement this header:
+ *   libroceicrc.so      everything (gfx950 kernels + host runtime + RCCL);
+ *   libroceicrc_cpu.so  the per-packet CPU section only (ricrc_one .. ricrc_combine,
+ *                       ricrc_icrc, ricrc_strerror), built by g++ with no HIP,
+ *                       RCCL or torch dependency: the simulator drop-in
+ *                       (python/simulator.py:49-55) loads it on any host.
  */
 #ifndef ROCE_ICRC_H
 #define ROCE_ICRC_H
@@ -44,6 +52,14 @@ typedef struct ricrc_ctx ricrc_ctx;
  * Replaces calc_icrc() (shuffle_egress.p4:463-494) for the simulator's
  * one-packet-at-a-time crossings, where a GPU launch would be pure overhead. */
 uint32_t ricrc_one(const uint8_t *l3, uint32_t n);
+
+/* Checked per-packet call with the SURVEY §8(b) length contract: *out = the
+ * ICRC, return 0; -EINVAL for NULL, n outside [RICRC_MIN_LEN, RICRC_MAX_LEN]
+ * or bad flags.  flags = a family (RICRC_F_IPV4/IPV6/AUTO, below), optionally
+ * | RICRC_F_STRICT: the packet must also classify as RoCEv2 of that family
+ * (ricrc_classify: the ingress parser's accept path,
+ * shuffle_ingress_parser.p4:12-36), else -EPROTO and *out is untouched. */
+int ricrc_icrc(const uint8_t *l3, uint32_t n, uint32_t flags, uint32_t *out);
 
 /* 1 if the trailer holds the right ICRC, 0 if not, -EINVAL if n < 4 / NULL.
  * The check NICs perform and scripts/icrc/disable-icrc.sh:27-33 turns off. */
@@ -71,6 +87,7 @@ int ricrc_is_rocev2(const uint8_t *l3, uint32_t n);
 #define RICRC_F_IPV4 0u
 #define RICRC_F_IPV6 1u
 #define RICRC_F_AUTO 2u
+#define RICRC_F_STRICT 0x100u /* ricrc_icrc only: reject packets that do not classify */
 
 uint32_t ricrc_one_ex(const uint8_t *l3, uint32_t n, uint32_t flags);
 int ricrc_verify_one_ex(const uint8_t *l3, uint32_t n, uint32_t flags);
@@ -178,6 +195,36 @@ int ricrc_repair_device(ricrc_ctx *ctx, int dev, void *d_base, const uint64_t *d
                         const uint8_t *d_old_bytes, uint32_t old_stride, uint32_t flags, uint32_t stamp,
                         uint32_t *d_out, void *stream);
 
+/* ----------------------------------------------- multi-GPU, one process
+ * The reference's only scale-out is N endpoints behind one switch
+ * (switchd/vswitchd.hpp:150-154); here a batch is sharded over the
+ * context's GPUs and the 4-byte results are all-gathered over xGMI with RCCL
+ * (the multi-process form is torch.distributed in bench.py).
+ *
+ * ricrc_comm_init: one RCCL communicator per context device, ncclCommInitAll
+ * over the context's device list.  RCCL is resolved at run time (dlopen of
+ * librccl.so.1, sharing one already loaded in the process).  Idempotent;
+ * freed by ricrc_destroy.  0, -EINVAL, -ENODEV (no RCCL), -EIO.
+ *
+ * ricrc_batch_device_all: shard k lives on context device k: counts[k]
+ * packets at d_base[k], addressed as in ricrc_batch_device (d_off / d_len
+ * may be NULL, or arrays of per-device pointers, entries NULL too).  d_out[k]
+ * is a buffer on device k of sum(counts) uint32; shard j's ICRCs go to
+ * offset counts[0] + ... + counts[j-1] of every d_out[k].  Equal counts: one
+ * in-place ncclAllGather; unequal counts (byte-balanced ragged cuts):
+ * ncclSend/ncclRecv pairs in one group.  Asynchronous on each device's
+ * context stream (ricrc_stream); ricrc_sync waits for all of them.  flags as
+ * the *_ex calls.  0, -EINVAL (also: ricrc_comm_init not called), -EIO.
+ *
+ * ricrc_allgather: only the exchange, for shards computed by the caller into
+ * d_out[k] + counts[0] + ... + counts[k-1] (on ricrc_stream(ctx, k)). */
+int ricrc_comm_init(ricrc_ctx *ctx);
+int ricrc_batch_device_all(ricrc_ctx *ctx, const void *const *d_base, const uint64_t *const *d_off,
+                           const uint32_t *const *d_len, uint32_t stride, const uint64_t *counts,
+                           uint32_t l3_offset, uint32_t *const *d_out, uint32_t flags);
+int ricrc_allgather(ricrc_ctx *ctx, const uint64_t *counts, uint32_t *const *d_out);
+int ricrc_sync(ricrc_ctx *ctx);
+
 /* Pinned host memory for NIC-ring style buffers (the role of huge_malloc in
  * common/huge_malloc.h:12-22).  NULL on failure.  ricrc_batch_host DMAs
  * straight out of such memory (no CPU copy) whenever a chunk's packets form
@@ -199,6 +246,20 @@ int ricrc_host_unregister(ricrc_ctx *ctx, void *p);
  * masked fields and payload seeded-random.  Asynchronous on `stream`. */
 int ricrc_synth_device(ricrc_ctx *ctx, int dev, uint64_t seed, uint64_t first, uint64_t count,
                        uint32_t n, uint32_t stride, void *d_buf, void *stream);
+
+/* Ragged variant: packet k is global packet first+k (same bytes as
+ * ricrc_synth_device makes for that index and length), len[k] bytes at
+ * d_buf + off[k] (device arrays).  Bytes between packets are left alone. */
+int ricrc_synth_ragged_device(ricrc_ctx *ctx, int dev, uint64_t seed, uint64_t first, uint64_t count,
+                              const uint64_t *d_off, const uint32_t *d_len, void *d_buf, void *stream);
+
+/* Bring context device dev out of its idle power state: runs the headline
+ * kernel over a 256 MiB scratch batch back to back for usec microseconds
+ * (synchronous; ~20000 is enough on MI355X).  After >= 20 ms of idle, the
+ * first ~12 launches of a burst otherwise run up to 15 % slower (DESIGN.md §4
+ * "Power ramp").  A NIC-ring service calls it when traffic resumes; bench.py
+ * calls it once before its warmup.  0, -EINVAL, -ENODEV, -ENOMEM, -EIO. */
+int ricrc_prime(ricrc_ctx *ctx, int dev, uint32_t usec);
 
 /* The context's own stream (a hipStream_t) for context device dev. */
 void *ricrc_stream(ricrc_ctx *ctx, int dev);

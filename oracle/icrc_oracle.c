@@ -236,3 +236,10 @@ void oracle_synth_batch(uint64_t seed, uint64_t first, uint64_t count, uint32_t 
                         uint8_t *buf) {
   for (uint64_t k = 0; k < count; ++k) oracle_synth_packet(seed, first + k, n, stride, buf + k * stride);
 }
+
+/* Ragged restatement (ricrc_synth_ragged_device): packet k is global packet
+ * first + k, len[k] bytes at buf + off[k]; bytes between packets untouched. */
+void oracle_synth_ragged(uint64_t seed, uint64_t first, uint64_t count, const uint64_t *off,
+                         const uint32_t *len, uint8_t *buf) {
+  for (uint64_t k = 0; k < count; ++k) oracle_synth_packet(seed, first + k, len[k], len[k], buf + off[k]);
+}

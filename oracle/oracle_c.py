@@ -39,6 +39,8 @@ def lib():
         L.oracle_synth_batch.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                          ctypes.c_uint32, ctypes.c_uint32, u8p]
         L.oracle_synth_batch.restype = None
+        L.oracle_synth_ragged.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, u64p, u32p, u8p]
+        L.oracle_synth_ragged.restype = None
         _lib = L
     return _lib
 
@@ -79,3 +81,20 @@ def synth_batch(seed: int, first: int, count: int, n: int, stride: int | None = 
     buf = np.empty((count, stride), dtype=np.uint8)
     lib().oracle_synth_batch(seed, first, count, n, stride, buf.ctypes.data)
     return buf
+
+
+def synth_ragged(seed: int, first: int, lengths, offsets=None, size: int | None = None) -> tuple:
+    """Host restatement of ricrc_synth_ragged_device: packet k = global packet
+    first + k with lengths[k] bytes, at offsets[k] (default: packed back to
+    back).  Returns (buf, offsets)."""
+    lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
+    if offsets is None:
+        offsets = np.zeros(len(lengths), np.uint64)
+        if len(lengths) > 1:
+            offsets[1:] = np.cumsum(lengths[:-1], dtype=np.uint64)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    if size is None:
+        size = int(offsets[-1]) + int(lengths[-1]) if len(lengths) else 0
+    buf = np.zeros(size, np.uint8)
+    lib().oracle_synth_ragged(seed, first, len(lengths), offsets.ctypes.data, lengths.ctypes.data, buf.ctypes.data)
+    return buf, offsets

@@ -6,14 +6,18 @@
 // errno returns (endpoint/shuffle_endpoint.hpp:364-389), no aborts
 // (common/logger.hpp:190 logassert only logs), caller-owned buffers
 // (common/huge_malloc.h:12-22).
+#include <dlfcn.h>
 #include <errno.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <new>
+#include <type_traits>
 #include <thread>
 #include <vector>
 
@@ -96,6 +100,7 @@ struct ricrc_ctx {
   std::vector<Dev> devs;
   std::vector<HostRange> pinned;  // host ranges the DMA engines may read directly
   int host_threads = 1;           // CPU copy threads for pageable host batches
+  std::vector<ncclComm_t> comms;  // ricrc_comm_init: one RCCL communicator per device
 };
 
 namespace {
@@ -354,6 +359,91 @@ int launch_batch(Dev &d, const uint8_t *base, const uint64_t *off, const uint32_
   return hip_err(launch_family_fix(f, 16 * d.n_cu, st));
 }
 
+// ------------------------------------------------------------------- RCCL
+// Resolved at run time (dlopen), so libroceicrc carries no link-time RCCL
+// dependency and shares the process's RCCL when one is already loaded (e.g.
+// torch's, same SONAME librccl.so.1).  Single process, N devices:
+// ncclCommInitAll; the one collective is the all-gather of
+// the 4-byte results.
+struct Rccl {
+  bool tried = false, ok = false;
+  ncclResult_t (*init_all)(ncclComm_t *, int, const int *) = nullptr;
+  ncclResult_t (*destroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*all_gather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*send)(const void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*recv)(void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*group_start)() = nullptr;
+  ncclResult_t (*group_end)() = nullptr;
+  const char *(*err_str)(ncclResult_t) = nullptr;
+};
+
+Rccl &rccl() {
+  static Rccl r;
+  if (r.tried) return r;
+  r.tried = true;
+  void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+  if (!h) h = dlopen("librccl.so.1", RTLD_NOW);
+  if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW);
+  if (!h) return r;
+  auto sym = [&](auto &fp, const char *name) {
+    fp = reinterpret_cast<std::remove_reference_t<decltype(fp)>>(dlsym(h, name));
+    return fp != nullptr;
+  };
+  r.ok = sym(r.init_all, "ncclCommInitAll") && sym(r.destroy, "ncclCommDestroy") &&
+         sym(r.all_gather, "ncclAllGather") && sym(r.send, "ncclSend") && sym(r.recv, "ncclRecv") &&
+         sym(r.group_start, "ncclGroupStart") && sym(r.group_end, "ncclGroupEnd") &&
+         sym(r.err_str, "ncclGetErrorString");
+  return r;
+}
+
+int nccl_err(ncclResult_t e) {
+  if (e == ncclSuccess) return 0;
+  if (getenv("RICRC_DEBUG")) fprintf(stderr, "libroceicrc: RCCL error %d: %s\n", (int)e, rccl().err_str(e));
+  return -EIO;
+}
+
+void comm_destroy(ricrc_ctx *ctx) {
+  if (ctx->comms.empty()) return;
+  for (size_t k = 0; k < ctx->comms.size(); ++k) {
+    DeviceGuard g(ctx->devs[k].id);
+    (void)hipStreamSynchronize(ctx->devs[k].stream);
+    if (ctx->comms[k]) (void)rccl().destroy(ctx->comms[k]);
+  }
+  ctx->comms.clear();
+}
+
+// All-gather of per-device result vectors in place: device k's d_out[k]
+// holds its shard's counts[k] results at offset sum(counts[<k]) and ends with
+// all of them.  Equal shards: one in-place ncclAllGather per device; unequal
+// shards: ncclSend / ncclRecv pairs, every device's calls in one group.
+int comm_allgather(ricrc_ctx *ctx, const uint64_t *counts, uint32_t *const *d_out) {
+  Rccl &r = rccl();
+  const int n = (int)ctx->devs.size();
+  std::vector<uint64_t> at(n + 1, 0);
+  bool equal = true;
+  for (int k = 0; k < n; ++k) {
+    at[k + 1] = at[k] + counts[k];
+    equal = equal && counts[k] == counts[0];
+  }
+  if (n == 1) return 0;  // already in place
+  int rc = nccl_err(r.group_start());
+  if (rc) return rc;
+  for (int k = 0; k < n && !rc; ++k) {
+    Dev &d = ctx->devs[k];
+    if (equal) {
+      rc = nccl_err(r.all_gather(d_out[k] + at[k], d_out[k], (size_t)counts[k], ncclUint32, ctx->comms[k], d.stream));
+      continue;
+    }
+    for (int p = 0; p < n && !rc; ++p) {
+      if (p == k) continue;
+      if (counts[k]) rc = nccl_err(r.send(d_out[k] + at[k], (size_t)counts[k], ncclUint32, p, ctx->comms[k], d.stream));
+      if (!rc && counts[p]) rc = nccl_err(r.recv(d_out[k] + at[p], (size_t)counts[p], ncclUint32, p, ctx->comms[k], d.stream));
+    }
+  }
+  const int rc2 = nccl_err(r.group_end());
+  return rc ? rc : rc2;
+}
+
 }  // namespace
 
 extern "C" {
@@ -406,6 +496,7 @@ int ricrc_create(ricrc_ctx **ctx, int n_gpus) {
 
 void ricrc_destroy(ricrc_ctx *ctx) {
   if (!ctx) return;
+  comm_destroy(ctx);
   for (Dev &d : ctx->devs) free_dev(d);
   for (const HostRange &r : ctx->pinned) {
     if (r.owned) (void)hipHostFree((void *)r.lo);
@@ -502,8 +593,52 @@ int ricrc_synth_device(ricrc_ctx *ctx, int dev, uint64_t seed, uint64_t first, u
   Dev &d = ctx->devs[dev];
   DeviceGuard g(d.id);
   if (!g.ok()) return -ENODEV;
-  SynthArgs a{(uint8_t *)d_buf, seed, first, count, n, stride};
+  SynthArgs a{(uint8_t *)d_buf, seed, first, count, n, stride, nullptr, nullptr};
   return hip_err(launch_synth(a, (hipStream_t)stream));
+}
+
+int ricrc_synth_ragged_device(ricrc_ctx *ctx, int dev, uint64_t seed, uint64_t first, uint64_t count,
+                              const uint64_t *d_off, const uint32_t *d_len, void *d_buf, void *stream) {
+  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size()) return -EINVAL;
+  if (count == 0) return 0;
+  if (!d_buf || !d_off || !d_len) return -EINVAL;
+  Dev &d = ctx->devs[dev];
+  DeviceGuard g(d.id);
+  if (!g.ok()) return -ENODEV;
+  SynthArgs a{(uint8_t *)d_buf, seed, first, count, 0u, 0u, d_off, d_len};
+  return hip_err(launch_synth_ragged(a, (hipStream_t)stream));
+}
+
+// Bring a device out of its idle power state before a latency-sensitive
+// burst: the headline kernel over a 256 MiB scratch batch, back to back, for
+// `usec` microseconds.  Measured (tools/ramp_probe.py, profiles/r02/
+// ramp_probe.jsonl): after >= 20 ms of GPU idle the 5th-12th launches of the
+// 1 M x 4 KiB batch run 700-750 us instead of 645-650 us; 20 ms of busy work
+// first removes that transient.
+int ricrc_prime(ricrc_ctx *ctx, int dev, uint32_t usec) {
+  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size()) return -EINVAL;
+  if (usec == 0) return 0;
+  Dev &d = ctx->devs[dev];
+  DeviceGuard g(d.id);
+  if (!g.ok()) return -ENODEV;
+  constexpr uint64_t kPkts = 65536, kN = 4096;
+  uint8_t *buf = nullptr;
+  uint32_t *out = nullptr;
+  HIP_TRY(hipMalloc(&buf, kPkts * kN));
+  int rc = hip_err(hipMalloc(&out, kPkts * sizeof(uint32_t)));
+  if (!rc) rc = hip_err(hipMemsetAsync(buf, 0, kPkts * kN, d.stream));
+  const auto t0 = std::chrono::steady_clock::now();
+  while (!rc) {
+    for (int k = 0; k < 16 && !rc; ++k)
+      rc = launch_batch_v4(d, buf, nullptr, nullptr, kN, kPkts, 0, out, d.stream, false);
+    if (!rc) rc = hip_err(hipStreamSynchronize(d.stream));
+    const auto us = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0);
+    if (us.count() >= (long long)usec) break;
+  }
+  (void)hipStreamSynchronize(d.stream);
+  (void)hipFree(out);
+  (void)hipFree(buf);
+  return rc;
 }
 
 void *ricrc_host_alloc(ricrc_ctx *ctx, uint64_t bytes) {
@@ -549,6 +684,65 @@ int ricrc_host_unregister(ricrc_ctx *ctx, void *p) {
       return hipHostUnregister(p) == hipSuccess ? 0 : ((void)hipGetLastError(), -EIO);
     }
   return -EINVAL;
+}
+
+int ricrc_comm_init(ricrc_ctx *ctx) {
+  if (!ctx || ctx->devs.empty()) return -EINVAL;
+  if (!ctx->comms.empty()) return 0;
+  Rccl &r = rccl();
+  if (!r.ok) return -ENODEV;
+  std::vector<int> ids;
+  for (const Dev &d : ctx->devs) ids.push_back(d.id);
+  std::vector<ncclComm_t> comms(ids.size(), nullptr);
+  const int rc = nccl_err(r.init_all(comms.data(), (int)ids.size(), ids.data()));
+  if (rc) return rc;
+  ctx->comms = comms;
+  return 0;
+}
+
+int ricrc_allgather(ricrc_ctx *ctx, const uint64_t *counts, uint32_t *const *d_out) {
+  if (!ctx || !counts || !d_out) return -EINVAL;
+  if (ctx->comms.empty()) return -EINVAL;  // ricrc_comm_init first
+  for (size_t k = 0; k < ctx->devs.size(); ++k)
+    if (!d_out[k]) return -EINVAL;
+  return comm_allgather(ctx, counts, d_out);
+}
+
+int ricrc_batch_device_all(ricrc_ctx *ctx, const void *const *d_base, const uint64_t *const *d_off,
+                           const uint32_t *const *d_len, uint32_t stride, const uint64_t *counts,
+                           uint32_t l3_offset, uint32_t *const *d_out, uint32_t flags) {
+  if (!ctx || !d_base || !counts || !d_out || flags > RICRC_F_AUTO) return -EINVAL;
+  if (ctx->comms.empty()) return -EINVAL;  // ricrc_comm_init first
+  const int n = (int)ctx->devs.size();
+  uint64_t at = 0;
+  for (int k = 0; k < n; ++k) {
+    if (!d_out[k] || (counts[k] && !d_base[k])) return -EINVAL;
+    const uint64_t *off = d_off ? d_off[k] : nullptr;
+    const uint32_t *len = d_len ? d_len[k] : nullptr;
+    if (counts[k] && ((!off && stride == 0) || (!len && stride <= l3_offset))) return -EINVAL;
+  }
+  for (int k = 0; k < n; ++k) {
+    Dev &d = ctx->devs[k];
+    DeviceGuard g(d.id);
+    if (!g.ok()) return -ENODEV;
+    if (counts[k]) {
+      const int rc = launch_batch(d, (const uint8_t *)d_base[k], d_off ? d_off[k] : nullptr, d_len ? d_len[k] : nullptr,
+                                  stride, counts[k], l3_offset, d_out[k] + at, d.stream, false, flags);
+      if (rc) return rc;
+    }
+    at += counts[k];
+  }
+  return comm_allgather(ctx, counts, d_out);
+}
+
+int ricrc_sync(ricrc_ctx *ctx) {
+  if (!ctx) return -EINVAL;
+  for (Dev &d : ctx->devs) {
+    DeviceGuard g(d.id);
+    if (!g.ok()) return -ENODEV;
+    HIP_TRY(hipStreamSynchronize(d.stream));
+  }
+  return 0;
 }
 
 }  // extern "C"
@@ -665,95 +859,119 @@ int ricrc_batch_host_ex(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *off
     return 0;
   };
 
-  bool busy = true;
-  while (busy) {
-    busy = false;
-    for (int k = 0; k < ndev; ++k) {
-      Dev &d = ctx->devs[k];
-      Cur &c = cur[k];
-      if (c.next >= c.end) continue;
-      busy = true;
-      DeviceGuard g(d.id);
-      if (!g.ok()) return -ENODEV;
-      const int s = c.slot;
-      int rc = drain(d, c, s);
-      if (rc) return rc;
-      Slot &sl = d.slot[s];
-      const uint64_t lo = c.next;
-      // Span plan: the largest [lo, hi) whose frames ascend without overlap
-      // and whose byte span [frame(lo), end of hi-1) fits the slot with at
-      // most 25 % slack.  The span lands at d_buf + pad so that packet lo's
-      // L3 header is 16-byte aligned on the device (so are the others when
-      // the frames are 16 apart, e.g. a fixed stride).
-      const uint64_t s_lo = frame(lo);
-      const uint64_t pad = (16u - (l3_offset & 15u)) & 15u;
-      uint64_t hi = lo, s_hi = s_lo, used = 0;
-      while (hi < c.end && hi - lo < kStagePkts) {
-        const uint64_t fs = frame(hi), fe = fs + l3_offset + pkt_len(hi);
-        if (fs < s_hi && hi > lo) break;  // not ascending / overlapping
-        if (fe - s_lo > kStageBytes) break;
-        s_hi = fe;
-        used += pkt_len(hi);
-        ++hi;
-      }
-      const bool span = hi > lo && (s_hi - s_lo) <= used + used / 4 + 64;
-      uint64_t m, bytes;
-      uint32_t kl3 = l3_offset;
-      if (span) {
-        m = hi - lo;
-        bytes = s_hi - s_lo;
-        const uint8_t *src = base + s_lo;
-        if (dma_readable(ctx, src, bytes)) {
-          HIP_TRY(hipMemcpyAsync(sl.d_buf + pad, src, bytes, hipMemcpyHostToDevice, sl.st));
-        } else {
-          par_for(bytes, T, 4u << 20, [&](uint64_t a, uint64_t b) { memcpy(sl.h_buf + a, src + a, b - a); });
-          HIP_TRY(hipMemcpyAsync(sl.d_buf + pad, sl.h_buf, bytes, hipMemcpyHostToDevice, sl.st));
-        }
-        if (off || len)
-          for (uint64_t i = lo; i < hi; ++i) sl.h_off[i - lo] = frame(i) - s_lo + pad;
-      } else {
-        // Gather: packed L3 packets, 16-byte aligned each.
-        hi = lo;
-        bytes = 0;
+  // Debug knob (tests): RICRC_FAIL_CHUNK=k fails the call with -EIO right
+  // after chunk k (0-based, counted over devices) has been queued.
+  long fail_chunk = -1;
+  if (const char *e = getenv("RICRC_FAIL_CHUNK")) fail_chunk = atol(e);
+  long chunk_no = 0;
+
+  auto run = [&]() -> int {
+    bool busy = true;
+    while (busy) {
+      busy = false;
+      for (int k = 0; k < ndev; ++k) {
+        Dev &d = ctx->devs[k];
+        Cur &c = cur[k];
+        if (c.next >= c.end) continue;
+        busy = true;
+        DeviceGuard g(d.id);
+        if (!g.ok()) return -ENODEV;
+        const int s = c.slot;
+        int rc = drain(d, c, s);
+        if (rc) return rc;
+        Slot &sl = d.slot[s];
+        const uint64_t lo = c.next;
+        // Span plan: the largest [lo, hi) whose frames ascend without overlap
+        // and whose byte span [frame(lo), end of hi-1) fits the slot with at
+        // most 25 % slack.  The span lands at d_buf + pad so that packet lo's
+        // L3 header is 16-byte aligned on the device (so are the others when
+        // the frames are 16 apart, e.g. a fixed stride).
+        const uint64_t s_lo = frame(lo);
+        const uint64_t pad = (16u - (l3_offset & 15u)) & 15u;
+        uint64_t hi = lo, s_hi = s_lo, used = 0;
         while (hi < c.end && hi - lo < kStagePkts) {
-          const uint64_t padded = (pkt_len(hi) + 15) & ~15ull;
-          if (bytes + padded > kStageBytes) break;
-          sl.h_off[hi - lo] = bytes;
-          bytes += padded;
+          const uint64_t fs = frame(hi), fe = fs + l3_offset + pkt_len(hi);
+          if (fs < s_hi && hi > lo) break;  // not ascending / overlapping
+          if (fe - s_lo > kStageBytes) break;
+          s_hi = fe;
+          used += pkt_len(hi);
           ++hi;
         }
-        m = hi - lo;
-        par_for(m, T, 4096, [&](uint64_t a, uint64_t b) {
-          for (uint64_t i = a; i < b; ++i)
-            memcpy(sl.h_buf + sl.h_off[i], base + frame(lo + i) + l3_offset, pkt_len(lo + i));
-        });
-        HIP_TRY(hipMemcpyAsync(sl.d_buf, sl.h_buf, bytes, hipMemcpyHostToDevice, sl.st));
-        kl3 = 0;
+        const bool span = hi > lo && (s_hi - s_lo) <= used + used / 4 + 64;
+        uint64_t m, bytes;
+        uint32_t kl3 = l3_offset;
+        if (span) {
+          m = hi - lo;
+          bytes = s_hi - s_lo;
+          const uint8_t *src = base + s_lo;
+          if (dma_readable(ctx, src, bytes)) {
+            HIP_TRY(hipMemcpyAsync(sl.d_buf + pad, src, bytes, hipMemcpyHostToDevice, sl.st));
+          } else {
+            par_for(bytes, T, 4u << 20, [&](uint64_t a, uint64_t b) { memcpy(sl.h_buf + a, src + a, b - a); });
+            HIP_TRY(hipMemcpyAsync(sl.d_buf + pad, sl.h_buf, bytes, hipMemcpyHostToDevice, sl.st));
+          }
+          if (off || len)
+            for (uint64_t i = lo; i < hi; ++i) sl.h_off[i - lo] = frame(i) - s_lo + pad;
+        } else {
+          // Gather: packed L3 packets, 16-byte aligned each.
+          hi = lo;
+          bytes = 0;
+          while (hi < c.end && hi - lo < kStagePkts) {
+            const uint64_t padded = (pkt_len(hi) + 15) & ~15ull;
+            if (bytes + padded > kStageBytes) break;
+            sl.h_off[hi - lo] = bytes;
+            bytes += padded;
+            ++hi;
+          }
+          m = hi - lo;
+          par_for(m, T, 4096, [&](uint64_t a, uint64_t b) {
+            for (uint64_t i = a; i < b; ++i)
+              memcpy(sl.h_buf + sl.h_off[i], base + frame(lo + i) + l3_offset, pkt_len(lo + i));
+          });
+          HIP_TRY(hipMemcpyAsync(sl.d_buf, sl.h_buf, bytes, hipMemcpyHostToDevice, sl.st));
+          kl3 = 0;
+        }
+        const bool fixed = span && !off && !len;  // frames at i*stride from d_buf + pad
+        if (fixed) {
+          rc = launch_batch(d, sl.d_buf + pad, nullptr, nullptr, stride, m, kl3, sl.d_out, sl.st, false, flags);
+        } else {
+          HIP_TRY(hipMemcpyAsync(sl.d_off, sl.h_off, m * sizeof(uint64_t), hipMemcpyHostToDevice, sl.st));
+          for (uint64_t i = 0; i < m; ++i) sl.h_len[i] = (uint32_t)pkt_len(lo + i);
+          HIP_TRY(hipMemcpyAsync(sl.d_len, sl.h_len, m * sizeof(uint32_t), hipMemcpyHostToDevice, sl.st));
+          rc = launch_batch(d, sl.d_buf, sl.d_off, sl.d_len, 0, m, kl3, sl.d_out, sl.st, false, flags);
+        }
+        if (rc) return rc;
+        HIP_TRY(hipMemcpyAsync(sl.h_out, sl.d_out, m * sizeof(uint32_t), hipMemcpyDeviceToHost, sl.st));
+        HIP_TRY(hipEventRecord(sl.done, sl.st));
+        c.pend[s] = true;
+        c.pend_lo[s] = lo;
+        c.pend_hi[s] = hi;
+        c.next = hi;
+        c.slot ^= 1;
+        if (chunk_no++ == fail_chunk) return -EIO;
       }
-      const bool fixed = span && !off && !len;  // frames at i*stride from d_buf + pad
-      if (fixed) {
-        rc = launch_batch(d, sl.d_buf + pad, nullptr, nullptr, stride, m, kl3, sl.d_out, sl.st, false, flags);
-      } else {
-        HIP_TRY(hipMemcpyAsync(sl.d_off, sl.h_off, m * sizeof(uint64_t), hipMemcpyHostToDevice, sl.st));
-        for (uint64_t i = 0; i < m; ++i) sl.h_len[i] = (uint32_t)pkt_len(lo + i);
-        HIP_TRY(hipMemcpyAsync(sl.d_len, sl.h_len, m * sizeof(uint32_t), hipMemcpyHostToDevice, sl.st));
-        rc = launch_batch(d, sl.d_buf, sl.d_off, sl.d_len, 0, m, kl3, sl.d_out, sl.st, false, flags);
-      }
-      if (rc) return rc;
-      HIP_TRY(hipMemcpyAsync(sl.h_out, sl.d_out, m * sizeof(uint32_t), hipMemcpyDeviceToHost, sl.st));
-      HIP_TRY(hipEventRecord(sl.done, sl.st));
-      c.pend[s] = true;
-      c.pend_lo[s] = lo;
-      c.pend_hi[s] = hi;
-      c.next = hi;
-      c.slot ^= 1;
     }
+    for (int k = 0; k < ndev; ++k)
+      for (int s = 0; s < 2; ++s) {
+        const int rc = drain(ctx->devs[k], cur[k], s);
+        if (rc) return rc;
+      }
+    return 0;
+  };
+  const int rc = run();
+  if (rc) {
+    // Leave nothing in flight: earlier chunks may still be reading the
+    // caller's buffer or the pinned slots and writing h_out; the next call
+    // reuses the slots.  Every staged slot stream of every device is drained
+    // (best effort: the first error is what the caller gets).
+    for (Dev &d : ctx->devs) {
+      DeviceGuard g(d.id);
+      for (Slot &sl : d.slot)
+        if (sl.st) (void)hipStreamSynchronize(sl.st);
+    }
+    (void)hipGetLastError();
+    return rc;
   }
-  for (int k = 0; k < ndev; ++k)
-    for (int s = 0; s < 2; ++s) {
-      const int rc = drain(ctx->devs[k], cur[k], s);
-      if (rc) return rc;
-    }
   return 0;
 }
 

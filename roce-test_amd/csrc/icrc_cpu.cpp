@@ -68,6 +68,18 @@ uint32_t ricrc_one_ex(const uint8_t *l3, uint32_t n, uint32_t flags) {
 
 uint32_t ricrc_one(const uint8_t *l3, uint32_t n) { return ricrc_one_ex(l3, n, RICRC_F_IPV4); }
 
+int ricrc_icrc(const uint8_t *l3, uint32_t n, uint32_t flags, uint32_t *out) {
+  const uint32_t fam = flags & ~RICRC_F_STRICT;
+  if (!l3 || !out || !flags_ok(fam) || n < RICRC_MIN_LEN || n > RICRC_MAX_LEN) return -EINVAL;
+  if (flags & RICRC_F_STRICT) {
+    const int c = ricrc_classify(l3, n);
+    const uint32_t want = fam == RICRC_F_AUTO ? 0u : (fam == RICRC_F_IPV6 ? 6u : 4u);
+    if (c == 0 || (want && (uint32_t)c != want)) return -EPROTO;
+  }
+  *out = ~icrc_register(l3, n, family_of(l3, n, fam));
+  return 0;
+}
+
 int ricrc_verify_one_ex(const uint8_t *l3, uint32_t n, uint32_t flags) {
   if (!l3 || n < 4 || !flags_ok(flags)) return -EINVAL;
   return ricrc_one_ex(l3, n, flags) == load_le32(l3 + n - 4) ? 1 : 0;
@@ -135,6 +147,7 @@ const char *ricrc_strerror(int err) {
     case -ENODEV: return "no usable GPU device";
     case -ENOMEM: return "out of memory";
     case -EIO: return "HIP/RCCL runtime error";
+    case -EPROTO: return "not a RoCEv2 packet of the requested address family (RICRC_F_STRICT)";
     default: return "unknown error";
   }
 }

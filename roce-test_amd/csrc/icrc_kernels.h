@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "icrc_sck.h"  // SckArgs / launch_sck (the headline kernel)
+
 namespace ricrc {
 
 struct u32x4_t {
@@ -37,21 +39,6 @@ struct TskArgs {
   uint32_t verify;
   uint32_t K[128];   // per chunk position: x^(8 (n - 4 - 32 (pos + 1)))
   uint32_t YB[32];   // x^(8*2048) * x^(31-j): uniform basis for 4 KiB packets
-  uint64_t *stamps;  // diagnostic builds only (tools/microbench); null in the product
-};
-
-// Back-to-back packets of n = 128 * L bytes (L = 8, 16, 32), 16-byte aligned:
-// the strided-chain kernel.  8 lanes per packet, 8 packets per wave group.
-struct SckArgs {
-  const uint8_t *base;
-  uint64_t count;
-  uint32_t *out;
-  uint32_t n;        // == stride
-  uint32_t verify;
-  uint32_t XB[32];   // basis of x^-32 (Horner step between a lane's chains)
-  uint32_t QS[8];    // x^(-32 (4 s + 1)): lane slot s's chain 0 -> packet end
-  uint32_t *work;    // dynamic schedule: {group counter, finished waves}, zero between launches
-  uint32_t dynamic;  // 1: groups from the counter (see icrc_sck_kernel), 0: static blocks
   uint64_t *stamps;  // diagnostic builds only (tools/microbench); null in the product
 };
 
@@ -151,7 +138,9 @@ hipError_t launch_rsck(RsckArgs &a, const RaggedArgs &small, int grid, hipStream
 struct SynthArgs {
   uint8_t *buf;
   uint64_t seed, first, count;
-  uint32_t n, stride;  // stride % 8 == 0, n <= stride
+  uint32_t n, stride;    // stride % 8 == 0, n <= stride (fixed-size batches)
+  const uint64_t *off;   // ragged batches (launch_synth_ragged): packet k at buf + off[k],
+  const uint32_t *len;   //   len[k] bytes
 };
 
 // Incremental repair (icrc_repair.hip): packet i's bytes [roff, roff+rlen)
@@ -190,12 +179,11 @@ hipError_t launch_family_fix(const FamilyFixArgs &a, int grid, hipStream_t st);
 
 hipError_t launch_stream(const StreamArgs &a, int cpl, int grid, hipStream_t st);
 hipError_t launch_tsk(const TskArgs &a, int grid, hipStream_t st);
-// Returns hipErrorInvalidValue for an n it has no instantiation for.
-hipError_t launch_sck(const SckArgs &a, int grid, hipStream_t st);
 hipError_t launch_ragged(const RaggedArgs &a, int grid, hipStream_t st);
 // ps[0..count] = exclusive prefix of ragged_pieces over the batch (stream
 // ordered; temporary storage from the stream-ordered allocator).
 hipError_t ragged_piece_scan(const RaggedArgs &a, uint64_t *ps, hipStream_t st);
 hipError_t launch_synth(const SynthArgs &a, hipStream_t st);
+hipError_t launch_synth_ragged(const SynthArgs &a, hipStream_t st);
 
 }  // namespace ricrc

@@ -496,333 +496,6 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
 }
 
 // =======================================================================
-// Strided-chain kernel (SCK): the headline path, packets of n = 128 L bytes
-// back to back (L = 8, 16, 32: 1, 2, 4 KiB).
-//
-// A wave takes 8 packets at a time (a "group", 8 n bytes); lane 8 g + s
-// belongs to packet g of the group and owns the 16-byte slot s of every
-// 128-byte line of it.  Load k of a group is one buffer_load_dwordx4 that
-// reads line k of all 8 packets -- whole 128-byte lines, which streams as
-// fast as 1 KiB-contiguous loads on MI355X (tools/microbench/mb_lines.hip)
-// -- and lands, with no LDS transpose, as one fold step for each of the
-// lane's 4 chains: chain j = 4 s + i folds words j, j + 32, j + 64, ... of
-// its packet, one word per line, so a fold step is "XOR the word, advance
-// the register 128 bytes" with the slice-by-4 tables T_124..T_127 in LDS
-// (same conflict-free layout as above).  Four independent chains per lane
-// and no cross-lane traffic while folding.
-//
-// Algebra (tests/test_kernel_algebra.py::test_strided_chain_decomposition):
-// with the trailer word zeroed, register = XOR_j r_j x^-32(j+1).  A lane
-// combines its chains by Horner in x^-32 (uniform basis, SGPRs), multiplies
-// once by x^-32(4 s + 1) (lane basis) and the 8 lanes of a packet XOR-reduce
-// with three DPP steps.  That finish (4 GF(2) multiplies per lane per group,
-// 4 per 8 packets instead of the transposed kernel's 2 per packet) runs in 8
-// VALU slices inside the first fold steps of the next group.  Loads run D
-// lines ahead through a rotating register ring; past the wave's span the
-// buffer range check returns zeros, so no load is ever exec-masked.
-// Results: lane l keeps packet 8 (l & 7) + (l >> 3) of each block of 8
-// groups and the block leaves in one coalesced 64-dword store.
-//
-// ABL (timing-only ablations for tools/microbench; the product uses 0):
-// 1 no table fold, 2 no finish, 8 no global loads, 16 no stores.
-// D: lines in flight per wave; QLDS: lane bases read from LDS instead of 32
-// VGPRs (frees registers for a deeper ring); XT: the Horner multiplies by
-// x^-32 through a conflict-free nibble table in LDS.
-// =======================================================================
-template <int L, int ABL, int D = 8, bool QLDS = false, bool DYN = false, bool XT = false>
-__global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
-  // 128 KiB of tables + result slots per wave (+ DYN: the slots' group
-  // indices; QLDS: the 8 lane bases; XT: 16 KiB nibble table of x^-32).
-  constexpr uint32_t kSlots = (DYN && XT) ? 128 : (QLDS || DYN || XT) ? 256 : 512;
-  constexpr uint32_t kRoundMask = kSlots / 8 - 1;  // groups per round of slots - 1
-  constexpr uint32_t kWaveWords = kSlots + (DYN ? kSlots / 8 : 0);
-  constexpr uint32_t kQStride = 36;  // words per lane-slot basis (padded: conflict-free ds_read_b128)
-  constexpr uint32_t kXtWord = kLdsWords + kWaves * kWaveWords + (QLDS ? 8 * kQStride : 0);
-  __shared__ uint32_t lds[kXtWord + (XT ? 128 * 32 : 0)];
-
-  // D: lines in flight per wave
-  static_assert(L % D == 0 || D == L, "ring indices must repeat every group");
-  constexpr uint32_t N = 128u * L, GB = 8u * N;
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t s = lane & 7;
-
-  const uint64_t wave = (uint64_t)blockIdx.x * kWaves + wid;
-  const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
-  const uint32_t G = (uint32_t)((a.count + 7) >> 3);
-  const uint64_t total = a.count * N;
-  const uint32_t vo = (lane >> 3) * N + 16u * s;
-
-  // The wave's sequence of groups.  Static: the contiguous block [g0, g1).
-  // DYN: groups taken one at a time from a device counter (a.work[0]) with
-  // two grabs in flight, so a workgroup that starts late -- its CU held by
-  // RCCL's all-gather of the previous step -- simply takes fewer groups; the
-  // last wave to finish resets the counter for the next launch.  A buffer
-  // atomic whose other 63 lanes fall outside the range-checked record keeps
-  // the grab free of exec masking.
-  const __amdgpu_buffer_rsrc_t wrs = make_rsrc(a.work, 8u);
-  // grab(): the raw per-lane result (lane 0 holds the value); it is made
-  // wave-uniform only one group later, when it is needed -- reading it at
-  // once would drain vmcnt(0) at every group end.
-  auto grab = [&]() -> uint32_t {
-    return (uint32_t)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, wrs, lane == 0 ? 0u : 0x7FFFFFF0u, 0, 0);
-  };
-  auto uni = [](uint32_t v) -> uint32_t { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
-  uint32_t g0 = 0, g1 = 0, qcur, qnext, qpend = 0;
-  if (DYN) {
-    qcur = grab();
-    qnext = grab();
-    qpend = grab();
-    qcur = uni(qcur);
-    qnext = uni(qnext);
-  } else {
-    const uint64_t per = (G + nwaves - 1) / nwaves;
-    g0 = (uint32_t)(wave * per < G ? wave * per : G);
-    g1 = (uint32_t)(g0 + per < G ? g0 + per : G);
-    qcur = g0 < g1 ? g0 : G;
-    qnext = g0 + 1 < g1 ? g0 + 1 : G;
-  }
-
-  // Line `line` of absolute group q (q >= G: no group, the range check reads zeros).
-  auto load = [&](uint32_t q, uint32_t line) -> u32x4 {
-    if (ABL & 8) return u32x4{q * 977u + line, lane, q, 5u};
-    const uint64_t b = (uint64_t)q * GB;
-    const uint32_t rem = q < G ? (uint32_t)(total - b < GB ? total - b : GB) : 0u;
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(a.base + (q < G ? b : 0), rem);
-    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 128u * line, 0, 2));
-  };
-  // The first D lines are in flight while the workgroup builds its tables
-  // (the table load is issued first, so waiting for it leaves them in flight).
-  const uint32_t tab_v = table_entry(g_tab128);
-  u32x4 ring[D];
-#pragma unroll
-  for (int k = 0; k < D; ++k) {  // in order: the loop's vmcnt waits assume it
-    __builtin_amdgcn_sched_barrier(0);
-    ring[k] = load(k < L ? qcur : qnext, (uint32_t)(k % L));
-  }
-  __builtin_amdgcn_sched_barrier(0);
-  table_store(lds, tab_v);
-  if (XT) {  // entry (w, v) = (nibble v at bits 4w..4w+3) * x^-32, 32 copies: 8 threads x 4 copies each
-    const uint32_t e = threadIdx.x >> 3, w = e >> 4, v = e & 15u;
-    uint32_t t = 0;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) t ^= ((v >> b) & 1u) ? a.XB[4 * w + b] : 0u;
-    *reinterpret_cast<u32x4 *>(lds + kXtWord + 32 * e + 4 * (threadIdx.x & 7)) = u32x4{t, t, t, t};
-  }
-  if (QLDS && threadIdx.x < 256) {  // basis word j of lane slot s: x^(-32 (4 s + 1)) * x^(31 - j)
-    const uint32_t bs = threadIdx.x >> 5, j = threadIdx.x & 31;
-    uint32_t v = a.QS[0];
-#pragma unroll
-    for (int k = 1; k < 8; ++k) v = bs == (uint32_t)k ? a.QS[k] : v;
-    for (uint32_t t = j; t < 31; ++t) v = gf_mulx(v);
-    lds[kLdsWords + kWaves * kWaveWords + bs * kQStride + j] = v;
-  }
-  __syncthreads();
-
-  uint32_t *slots = lds + kLdsWords + wid * kWaveWords;
-  const uint32_t xt_lane = 4u * kXtWord + ((lane & 31u) << 2);  // byte address of the lane's XT copy
-  uint32_t *gtab = slots + kSlots;  // DYN: absolute group of each slot row
-  const LaneTab lt{(lane & 31) << 2, ((lane & 31) << 2) | 0x10000u};
-  const uint32_t mw0 = s == 0 ? kMaskW0 : (s == 2 ? kMaskW8 : 0u);  // bytes 1 / 32
-  const uint32_t xw0 = s == 0 ? kSeed : 0u;
-  const uint32_t mw2 = s == 0 ? kMaskW2 : (s == 1 ? kMaskW6 : 0u);  // bytes 8, 10-11 / 26-27
-  const uint32_t keep3 = s == 7 ? 0u : 0xFFFFFFFFu;                  // the trailer word
-  uint32_t Q[32];  // lane basis in registers (!QLDS)
-  const uint32_t *qlds = lds + kLdsWords + kWaves * kWaveWords + s * kQStride;
-  if (!QLDS) {
-    uint32_t qs = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) qs = s == (uint32_t)k ? a.QS[k] : qs;
-    make_basis(qs, Q);
-  }
-
-  struct Fin {
-    uint32_t r[4];    // chain registers
-    uint32_t tr;      // trailer word (lane s = 7), for verify
-    uint32_t acc[4];  // multiply accumulators
-    uint32_t u;       // Horner value
-  };
-  auto mul_half = [&](Fin &f, const uint32_t(&B)[32], int h) {
-#pragma unroll
-    for (int j = 16 * h; j < 16 * h + 16; ++j)
-      f.acc[j & 3] = and_xor((uint32_t)(((int32_t)(f.u << (31 - j))) >> 31), B[j], f.acc[j & 3]);
-  };
-  auto take = [](Fin &f) -> uint32_t {
-    const uint32_t v = xor3(f.acc[0], f.acc[1], f.acc[2] ^ f.acc[3]);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) f.acc[k] = 0u;
-    return v;
-  };
-  // Slice sl (0..7): u = ((r3 X ^ r2) X ^ r1) X ^ r0, then u * Q.
-  auto fin_slice = [&](Fin &f, int sl) {
-    if (ABL & 2) return;
-    if (sl == 0) {
-      f.u = f.r[3];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) f.acc[k] = 0u;
-    }
-    if (sl < 6 && XT) {  // 4 nibble lookups: 2 VALU + 1 ds_read_b32 each instead of 8 bfe/bitop3 pairs
-#pragma unroll
-      for (int w = 4 * (sl & 1); w < 4 * (sl & 1) + 4; ++w) {
-        const uint32_t nib = (f.u >> (4 * w)) & 15u;
-        f.acc[w & 3] ^= lds_at(lds, xt_lane + (nib << 7) + 2048u * w);
-      }
-    } else if (sl < 6) mul_half(f, a.XB, sl & 1);
-    else if (!QLDS) mul_half(f, Q, sl & 1);
-    else {
-      const int h = sl & 1;
-#pragma unroll
-      for (int q4 = 0; q4 < 4; ++q4) {
-        const u32x4 b = *reinterpret_cast<const u32x4 *>(qlds + 16 * h + 4 * q4);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int j = 16 * h + 4 * q4 + i;
-          f.acc[i] = and_xor((uint32_t)(((int32_t)(f.u << (31 - j))) >> 31), b[i], f.acc[i]);
-        }
-      }
-    }
-    if (sl == 1) f.u = take(f) ^ f.r[2];
-    if (sl == 3) f.u = take(f) ^ f.r[1];
-    if (sl == 5) f.u = take(f) ^ f.r[0];
-    if (sl == 7) f.u = take(f);
-  };
-  const uint32_t vmask = __builtin_amdgcn_readfirstlane(a.verify ? 0xFFFFFFFFu : 0u);
-  uint32_t sink = 0;
-  // Results go to the wave's LDS slots (all 8 lanes of a packet write the
-  // same value to the same slot: no exec mask) and leave for HBM once per
-  // round of slots, so the streaming loop holds no global store: a store
-  // shares vmcnt with the ring and every load queued behind it would wait
-  // for its write acknowledgement.  j counts the wave's finished groups.
-  auto flush = [&](uint32_t j_end) {  // the round of groups ending at local index j_end
-    if (ABL & 16) return;
-    const uint32_t j_lo = (j_end - 1) & ~kRoundMask;
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the slot writes have landed
-    if (DYN) {  // rows of 8 results to scattered groups: 32 B runs
-      const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out, (uint32_t)(a.count < (1ull << 30) ? 4 * a.count : 0xFFFFFFF0u));
-#pragma unroll
-      for (int h = 0; h < (int)kSlots / 64; ++h) {
-        const uint32_t row = 8u * h + (lane >> 3);  // slot row = local group (mod round)
-        const uint32_t q = gtab[row];
-        const bool live = j_lo + row < j_end;
-        __builtin_amdgcn_raw_buffer_store_b32(slots[64 * h + lane], ro, live ? 4u * (8u * q + s) : 0x7FFFFFF0u, 0, 0);
-      }
-    } else {  // consecutive groups: coalesced
-      const uint64_t pb = ((uint64_t)g0 + j_lo) * 8u;
-      const uint32_t valid = (j_end - j_lo) * 8u;  // slots written this round
-      const uint32_t nout = (uint32_t)(a.count - pb < valid ? a.count - pb : valid);
-      const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out + pb, 4u * nout);
-#pragma unroll
-      for (int h = 0; h < (int)kSlots / 256; ++h) {
-        const u32x4 v = *reinterpret_cast<const u32x4 *>(slots + 256 * h + 4 * lane);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v),
-                                               ro, 1024u * h + 16u * lane, 0, 0);
-      }
-    }
-  };
-  auto fin_store = [&](Fin &f, uint32_t jf, uint32_t qf) {
-    const uint32_t crc = (ABL & 2) ? (f.r[0] ^ f.r[1] ^ f.r[2] ^ f.r[3]) : f.u;
-    const uint32_t v = group_xor(crc, 3);
-    const uint32_t chk = group_xor(f.tr, 3) == ~v ? 1u : 0u;
-    const uint32_t val = __builtin_amdgcn_bitop3_b32(vmask, chk, ~v, 0xCA);  // vmask ? chk : ~v, bitwise
-    if (ABL & 16) {
-      sink ^= val;
-      return;
-    }
-    slots[((jf & kRoundMask) << 3) | (lane >> 3)] = val;
-    if (DYN) gtab[jf & kRoundMask] = qf;
-  };
-
-  // Finish slices of the previous group ride in steps 0..7 (0..6 for L = 8,
-  // two in step 0), its result is written in the step after.
-  constexpr int kStoreStep = L >= 16 ? 8 : L - 1;
-  auto slice_step = [](int sl) constexpr { return L >= 16 ? sl : sl * (L - 1) / 8; };
-  static_assert(L >= 8, "finish needs 8 fold steps");
-  Fin pf{};
-  uint32_t qprev = 0;
-  uint32_t j = 0;
-  for (; qcur < G; ++j) {  // qcur: wave-uniform
-    u32x4 w = ring[0];
-    ring[0] = load(D < L ? qcur : qnext, (uint32_t)(D % L));
-    w[0] = or_xor(w[0], mw0, xw0);
-    w[2] |= mw2;
-    uint32_t x[4] = {w[0], w[1], w[2], w[3]};  // chain register (0) ^ line-0 word
-    uint32_t tr = 0;
-#pragma unroll
-    for (int k = 0; k < L; ++k) {
-      // Fence each step: the scheduler would otherwise hoist the whole
-      // group's ring refills to the top and drain vmcnt to zero there.
-      __builtin_amdgcn_sched_barrier(0);
-      u32x4 wn = {0u, 0u, 0u, 0u};
-      if (k + 1 < L) {
-        wn = ring[(k + 1) % D];
-        ring[(k + 1) % D] = load(k + 1 + D < L ? qcur : qnext, (uint32_t)((k + 1 + D) % L));
-        if (k + 1 == L - 1) {
-          tr = keep3 ? 0u : wn[3];
-          wn[3] &= keep3;
-        }
-      }
-      uint32_t t[4][4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if (ABL & 1) {
-          t[i][0] = __builtin_amdgcn_perm(x[i], lt.lo0, 0x0C0C0400u);
-          t[i][1] = x[i] >> 7;
-          t[i][2] = x[i] * 3u;
-          t[i][3] = 0u;
-        } else {
-          t[i][0] = lds_at(lds, __builtin_amdgcn_perm(x[i], lt.lo0, 0x0C0C0400u));
-          t[i][1] = lds_at(lds, __builtin_amdgcn_perm(x[i], lt.lo0, 0x0C0C0500u) + 128);
-          t[i][2] = lds_at(lds, __builtin_amdgcn_perm(x[i], lt.lo1, 0x0C020600u));
-          t[i][3] = lds_at(lds, __builtin_amdgcn_perm(x[i], lt.lo1, 0x0C020700u) + 128);
-        }
-      }
-      // The previous group's finish, in the shadow of the reads (for j = 0 it
-      // runs on zeros; its slot write is overwritten before any flush).
-#pragma unroll
-      for (int sl = 0; sl < 8; ++sl)
-        if (slice_step(sl) == k) fin_slice(pf, sl);
-      if (k == kStoreStep) {
-        fin_store(pf, j - 1, qprev);
-        if (j > 0 && ((j - 1) & kRoundMask) == kRoundMask) flush(j);  // wave-uniform: a full round of slots
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) x[i] = xor3(t[i][0], t[i][1], xor3(t[i][2], t[i][3], wn[i]));
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) pf.r[i] = x[i];
-    pf.tr = tr;
-    qprev = qcur;
-    qcur = qnext;  // advance the group sequence (wave-uniform)
-    if (DYN) {
-      qnext = uni(qpend);
-      qpend = grab();
-    } else {
-      qnext = qnext + 1 < g1 ? qnext + 1 : G;
-    }
-  }
-  if (j > 0) {
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int sl = 0; sl < 8; ++sl) fin_slice(pf, sl);
-    fin_store(pf, j - 1, qprev);
-    flush(j);
-  }
-  if (ABL & 16) a.out[wave * 64 + lane] = sink;
-  if (DYN) {
-    // All of this wave's grabs have returned before it checks in, so when the
-    // last wave checks in nobody touches the counter any more: reset it.
-    const __amdgpu_buffer_rsrc_t drs = make_rsrc(a.work, 8u);
-    const uint32_t mine = lane == 0 ? 4u : 0x7FFFFFF0u;
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): every grab of this wave has returned
-    const uint32_t seen = (uint32_t)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, drs, mine, 0, 0);
-    if (__builtin_amdgcn_readfirstlane((int)seen) == (int)(nwaves - 1)) {
-      __builtin_amdgcn_raw_buffer_store_b32(0u, drs, lane == 0 ? 0u : 0x7FFFFFF0u, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b32(0u, drs, mine, 0, 0);
-    }
-  }
-}
-
-// =======================================================================
 // Ragged kernel: any alignment, per-packet offsets and/or lengths, any mix
 // of sizes.  The batch is a sequence of 64-byte pieces (packet i owns pieces
 // [ps[i], ps[i+1]), laid from its L3 start rounded down to 16 B, so every
@@ -1233,67 +906,94 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   return z ^ (z >> 31);
 }
 
+// 8-byte block j of synthetic packet i (n bytes): header template of the
+// reference (shuffle_ingress.p4:717-724,734-735), everything else seeded.
+__device__ __forceinline__ uint64_t synth_block(uint64_t seed, uint64_t i, uint32_t n, uint64_t j) {
+  uint64_t r = mix64(mix64(seed + i) + j);
+  const uint32_t b0 = (uint32_t)(j * 8);
+  if (b0 + 8 > n) {
+    const uint32_t keep = n > b0 ? n - b0 : 0u;
+    r = keep ? (r & (~0ull >> (64 - 8 * keep))) : 0ull;
+  }
+  if (b0 < 40 && n >= 40) {
+    uint8_t b[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) b[q] = (uint8_t)(r >> (8 * q));
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const uint32_t o = b0 + q;
+      uint8_t x = b[q];
+      switch (o) {
+        case 0: x = 0x45; break;
+        case 2: x = (uint8_t)(n >> 8); break;
+        case 3: x = (uint8_t)n; break;
+        case 4: x = 0x12; break;
+        case 5: x = 0x34; break;
+        case 6: x = 0x40; break;
+        case 7: x = 0x00; break;
+        case 9: x = 17; break;
+        case 12: x = 192; break;
+        case 13: x = 168; break;
+        case 14: x = 1; break;
+        case 15: x = 100; break;
+        case 16: x = 192; break;
+        case 17: x = 168; break;
+        case 18: x = 1; break;
+        case 19: x = (uint8_t)(1 + (i & 3)); break;
+        case 20: x = 0x45; break;
+        case 21: x = 0x7b; break;
+        case 22: x = 0x12; break;
+        case 23: x = 0xb7; break;
+        case 24: x = (uint8_t)((n - 20) >> 8); break;
+        case 25: x = (uint8_t)(n - 20); break;
+        case 28: x = 0x04; break;
+        case 29: x = 0x40; break;
+        case 30: x = 0xff; break;
+        case 31: x = 0xff; break;
+        case 36: x = 0; break;
+        case 37: x = (uint8_t)(i >> 16); break;
+        case 38: x = (uint8_t)(i >> 8); break;
+        case 39: x = (uint8_t)i; break;
+        default: break;
+      }
+      b[q] = x;
+    }
+    r = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) r |= (uint64_t)b[q] << (8 * q);
+  }
+  return r;
+}
+
 __global__ void synth_kernel(SynthArgs a) {
   const uint64_t bpp = a.stride >> 3;  // 8-byte blocks per packet slot
   const uint64_t total = a.count * bpp;
   for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
        t += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t k = t / bpp, j = t - k * bpp, i = a.first + k;
-    uint64_t r = mix64(mix64(a.seed + i) + j);
-    const uint32_t b0 = (uint32_t)(j * 8);
-    if (b0 + 8 > a.n) {
-      const uint32_t keep = a.n > b0 ? a.n - b0 : 0u;
-      r = keep ? (r & (~0ull >> (64 - 8 * keep))) : 0ull;
-    }
-    if (b0 < 40 && a.n >= 40) {
-      uint8_t b[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) b[q] = (uint8_t)(r >> (8 * q));
-      const uint32_t n = a.n;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const uint32_t o = b0 + q;
-        uint8_t x = b[q];
-        switch (o) {
-          case 0: x = 0x45; break;
-          case 2: x = (uint8_t)(n >> 8); break;
-          case 3: x = (uint8_t)n; break;
-          case 4: x = 0x12; break;
-          case 5: x = 0x34; break;
-          case 6: x = 0x40; break;
-          case 7: x = 0x00; break;
-          case 9: x = 17; break;
-          case 12: x = 192; break;
-          case 13: x = 168; break;
-          case 14: x = 1; break;
-          case 15: x = 100; break;
-          case 16: x = 192; break;
-          case 17: x = 168; break;
-          case 18: x = 1; break;
-          case 19: x = (uint8_t)(1 + (i & 3)); break;
-          case 20: x = 0x45; break;
-          case 21: x = 0x7b; break;
-          case 22: x = 0x12; break;
-          case 23: x = 0xb7; break;
-          case 24: x = (uint8_t)((n - 20) >> 8); break;
-          case 25: x = (uint8_t)(n - 20); break;
-          case 28: x = 0x04; break;
-          case 29: x = 0x40; break;
-          case 30: x = 0xff; break;
-          case 31: x = 0xff; break;
-          case 36: x = 0; break;
-          case 37: x = (uint8_t)(i >> 16); break;
-          case 38: x = (uint8_t)(i >> 8); break;
-          case 39: x = (uint8_t)i; break;
-          default: break;
-        }
-        b[q] = x;
+    const uint64_t k = t / bpp, j = t - k * bpp;
+    *reinterpret_cast<uint64_t *>(a.buf + k * a.stride + j * 8) = synth_block(a.seed, a.first + k, a.n, j);
+  }
+}
+
+// Ragged variant: packet k (global index first + k) of len[k] bytes at
+// buf + off[k], one wave per packet (coalesced 8-byte blocks; byte stores for
+// a misaligned start or the tail block).  Bytes between packets are untouched.
+__global__ void synth_ragged_kernel(SynthArgs a) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  for (uint64_t k = w0; k < a.count; k += nw) {
+    const uint32_t n = a.len[k];
+    uint8_t *p = a.buf + a.off[k];
+    const bool al = ((uintptr_t)p & 7u) == 0;
+    for (uint32_t j = lane; 8 * j < n; j += 64) {
+      const uint64_t r = synth_block(a.seed, a.first + k, n, j);
+      if (al && 8 * j + 8 <= n) {
+        *reinterpret_cast<uint64_t *>(p + 8 * j) = r;
+      } else {
+        for (uint32_t q = 0; q < 8 && 8 * j + q < n; ++q) p[8 * j + q] = (uint8_t)(r >> (8 * q));
       }
-      r = 0;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) r |= (uint64_t)b[q] << (8 * q);
     }
-    *reinterpret_cast<uint64_t *>(a.buf + k * a.stride + j * 8) = r;
   }
 }
 
@@ -1313,21 +1013,6 @@ hipError_t launch_tsk(const TskArgs &a, int grid, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_sck(const SckArgs &a, int grid, hipStream_t st) {
-  const dim3 g(grid), b(kBlock);
-  // XT (x^-32 nibble table): 0.735 -> 0.703 ms on 4 M x 1 KiB, ~1 % on 1 M x 4 KiB (tools/microbench/sck_abl.hip).
-  if (a.dynamic) {
-    if (a.n == 4096) hipLaunchKernelGGL((icrc_sck_kernel<32, 0, 8, false, true, true>), g, b, 0, st, a);
-    else if (a.n == 2048) hipLaunchKernelGGL((icrc_sck_kernel<16, 0, 8, false, true, true>), g, b, 0, st, a);
-    else if (a.n == 1024) hipLaunchKernelGGL((icrc_sck_kernel<8, 0, 8, false, true, true>), g, b, 0, st, a);
-    else return hipErrorInvalidValue;
-  } else if (a.n == 4096) hipLaunchKernelGGL((icrc_sck_kernel<32, 0, 8, false, false, true>), g, b, 0, st, a);
-  else if (a.n == 2048) hipLaunchKernelGGL((icrc_sck_kernel<16, 0, 8, false, false, true>), g, b, 0, st, a);
-  else if (a.n == 1024) hipLaunchKernelGGL((icrc_sck_kernel<8, 0, 8, false, false, true>), g, b, 0, st, a);
-  else return hipErrorInvalidValue;
-  return hipGetLastError();
-}
-
 hipError_t launch_ragged(const RaggedArgs &a, int grid, hipStream_t st) {
   const dim3 b(1024);
   if (a.desc) hipLaunchKernelGGL((icrc_ragged_kernel<4, 1024>), dim3(grid), b, 0, st, a);
@@ -1344,6 +1029,14 @@ hipError_t launch_synth(const SynthArgs &a, hipStream_t st) {
   if (blocks > 65536) blocks = 65536;
   if (blocks == 0) return hipSuccess;
   hipLaunchKernelGGL(synth_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_synth_ragged(const SynthArgs &a, hipStream_t st) {
+  if (a.count == 0) return hipSuccess;
+  uint64_t blocks = (a.count + 3) / 4;  // 4 waves per block, one packet per wave
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(synth_ragged_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 

@@ -1,0 +1,28 @@
+// Kernel arguments + launcher of the strided-chain kernel (icrc_sck.hip), the
+// headline path.  Kept apart from icrc_kernels.h so the headline kernel's
+// sources are exactly icrc_sck.{h,hip} + icrc_device.h + icrc_math.h.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ricrc {
+
+// Back-to-back packets of n = 128 * L bytes (L = 8, 16, 32), 16-byte aligned:
+// the strided-chain kernel.  8 lanes per packet, 8 packets per wave group.
+struct SckArgs {
+  const uint8_t *base;
+  uint64_t count;
+  uint32_t *out;
+  uint32_t n;        // == stride
+  uint32_t verify;
+  uint32_t XB[32];   // basis of x^-32 (Horner step between a lane's chains)
+  uint32_t QS[8];    // x^(-32 (4 s + 1)): lane slot s's chain 0 -> packet end
+  uint32_t *work;    // dynamic schedule: {group counter, finished waves}, zero between launches
+  uint32_t dynamic;  // 1: groups from the counter (see icrc_sck_kernel), 0: static blocks
+  uint64_t *stamps;  // diagnostic builds only (tools/microbench); null in the product
+};
+
+// Returns hipErrorInvalidValue for an n it has no instantiation for.
+hipError_t launch_sck(const SckArgs &a, int grid, hipStream_t st);
+
+}  // namespace ricrc

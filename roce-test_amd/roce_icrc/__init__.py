@@ -6,14 +6,19 @@ own for this path; see include/roce_icrc.h and INTEGRATION.md):
 
 * :func:`icrc` / :func:`verify` / :func:`stamp` -- one packet at a time
   (the simulator's wire crossings, simulator.py:49-55 and 59-82); CPU,
-  re-entrant, no GPU launch per 60-byte packet.
-* :class:`Context` -- batches on the GPUs: host buffers in/out
-  (``batch_host``), device-resident buffers (``batch_device`` /
-  ``verify_device``, torch tensors or raw pointers, async on a stream) and the
-  synthetic batch generator used by bench.py and the tests.
+  re-entrant, no GPU launch per 60-byte packet.  These bind
+  ``libroceicrc_cpu.so``, the HIP-free build of the per-packet entry points:
+  importing this package needs neither ROCm nor torch.
+* :class:`Context` -- batches on the GPUs through ``libroceicrc.so`` (gfx950
+  kernels + RCCL): host buffers in/out (``batch_host``), device-resident
+  buffers (``batch_device`` / ``verify_device``, torch tensors or raw
+  pointers, async on a stream), single-process multi-GPU sharding with an
+  RCCL all-gather (``batch_device_all``) and the synthetic batch generators
+  used by bench.py and the tests.
 
-Every batch call runs the gfx950 kernels; there is no CPU fallback.  If the
-shared library is missing, importing this package raises.
+Every batch call runs the gfx950 kernels; there is no CPU fallback: if the
+HIP library is missing, creating a :class:`Context` (or touching
+``roce_icrc.lib``) raises.
 """
 from __future__ import annotations
 
@@ -27,18 +32,67 @@ from . import wire  # noqa: F401  (Packet <-> bytes adapter)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libroceicrc.so")
+CPU_LIB_PATH = os.path.join(_HERE, "libroceicrc_cpu.so")
 
 MIN_LEN = 44
 MAX_LEN = 65535
 
-EXPORTED = (
+# Per-packet CPU section of include/roce_icrc.h: in both libraries.
+CPU_EXPORTED = (
     "ricrc_one", "ricrc_verify_one", "ricrc_stamp_one", "ricrc_is_rocev2", "ricrc_shift",
     "ricrc_one_ex", "ricrc_verify_one_ex", "ricrc_stamp_one_ex", "ricrc_classify", "ricrc_repair_one",
-    "ricrc_combine", "ricrc_create", "ricrc_create_devices", "ricrc_destroy", "ricrc_device_count", "ricrc_batch_host",
+    "ricrc_combine", "ricrc_icrc", "ricrc_strerror",
+)
+EXPORTED = CPU_EXPORTED + (
+    "ricrc_create", "ricrc_create_devices", "ricrc_destroy", "ricrc_device_count", "ricrc_batch_host",
     "ricrc_batch_device", "ricrc_verify_device", "ricrc_repair_device", "ricrc_batch_host_ex",
     "ricrc_batch_device_ex", "ricrc_verify_device_ex", "ricrc_host_alloc", "ricrc_host_free",
-    "ricrc_host_register", "ricrc_host_unregister", "ricrc_synth_device", "ricrc_stream", "ricrc_strerror",
+    "ricrc_host_register", "ricrc_host_unregister", "ricrc_synth_device", "ricrc_synth_ragged_device",
+    "ricrc_prime", "ricrc_stream", "ricrc_comm_init", "ricrc_batch_device_all", "ricrc_allgather", "ricrc_sync",
 )
+
+_vp = ctypes.c_void_p
+_u32, _u64, _i32 = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+_PP = ctypes.POINTER(ctypes.c_void_p)
+_SIG = {
+    "ricrc_one": ([_vp, _u32], _u32),
+    "ricrc_verify_one": ([_vp, _u32], _i32),
+    "ricrc_stamp_one": ([_vp, _u32], _i32),
+    "ricrc_is_rocev2": ([_vp, _u32], _i32),
+    "ricrc_one_ex": ([_vp, _u32, _u32], _u32),
+    "ricrc_verify_one_ex": ([_vp, _u32, _u32], _i32),
+    "ricrc_stamp_one_ex": ([_vp, _u32, _u32], _i32),
+    "ricrc_classify": ([_vp, _u32], _i32),
+    "ricrc_repair_one": ([_vp, _u32, _u32, _vp, _u32, _u32, _u32, ctypes.POINTER(_u32)], _i32),
+    "ricrc_icrc": ([_vp, _u32, _u32, ctypes.POINTER(_u32)], _i32),
+    "ricrc_shift": ([_u32, _u64], _u32),
+    "ricrc_combine": ([_u32, _u32, _u64], _u32),
+    "ricrc_strerror": ([_i32], ctypes.c_char_p),
+    "ricrc_create": ([ctypes.POINTER(_vp), _i32], _i32),
+    "ricrc_create_devices": ([ctypes.POINTER(_vp), ctypes.POINTER(_i32), _i32], _i32),
+    "ricrc_destroy": ([_vp], None),
+    "ricrc_device_count": ([_vp], _i32),
+    "ricrc_batch_host": ([_vp, _vp, _vp, _vp, _u32, _u64, _u32, _vp], _i32),
+    "ricrc_batch_device": ([_vp, _i32, _vp, _vp, _vp, _u32, _u64, _u32, _vp, _vp], _i32),
+    "ricrc_verify_device": ([_vp, _i32, _vp, _vp, _vp, _u32, _u64, _u32, _vp, _vp], _i32),
+    "ricrc_batch_host_ex": ([_vp, _vp, _vp, _vp, _u32, _u64, _u32, _vp, _u32], _i32),
+    "ricrc_batch_device_ex": ([_vp, _i32, _vp, _vp, _vp, _u32, _u64, _u32, _vp, _vp, _u32], _i32),
+    "ricrc_verify_device_ex": ([_vp, _i32, _vp, _vp, _vp, _u32, _u64, _u32, _vp, _vp, _u32], _i32),
+    "ricrc_repair_device": ([_vp, _i32, _vp, _vp, _vp, _u32, _u64, _u32, _u32, _u32, _vp, _u32, _u32, _u32, _vp, _vp],
+                            _i32),
+    "ricrc_host_alloc": ([_vp, _u64], _vp),
+    "ricrc_host_free": ([_vp, _vp], None),
+    "ricrc_host_register": ([_vp, _vp, _u64], _i32),
+    "ricrc_host_unregister": ([_vp, _vp], _i32),
+    "ricrc_synth_device": ([_vp, _i32, _u64, _u64, _u64, _u32, _u32, _vp, _vp], _i32),
+    "ricrc_synth_ragged_device": ([_vp, _i32, _u64, _u64, _u64, _vp, _vp, _vp, _vp], _i32),
+    "ricrc_prime": ([_vp, _i32, _u32], _i32),
+    "ricrc_stream": ([_vp, _i32], _vp),
+    "ricrc_comm_init": ([_vp], _i32),
+    "ricrc_batch_device_all": ([_vp, _PP, _PP, _PP, _u32, ctypes.POINTER(_u64), _u32, _PP, _u32], _i32),
+    "ricrc_allgather": ([_vp, ctypes.POINTER(_u64), _PP], _i32),
+    "ricrc_sync": ([_vp], _i32),
+}
 
 
 class ICRCError(RuntimeError):
@@ -47,7 +101,24 @@ class ICRCError(RuntimeError):
         super().__init__(f"{what}: {rc} ({_strerror(rc)})")
 
 
-def _load():
+def _bind(L, names):
+    for name in names:
+        args, res = _SIG[name]
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    return L
+
+
+def _load_cpu():
+    if not os.path.exists(CPU_LIB_PATH):
+        raise ImportError(
+            f"libroceicrc_cpu.so not found at {CPU_LIB_PATH}; build it with "
+            "`make -C roce-test_amd/csrc` or `python -c 'import __graft_entry__ as g; g.build()'`")
+    return _bind(ctypes.CDLL(CPU_LIB_PATH), CPU_EXPORTED)
+
+
+def _load_hip():
     # libroceicrc and PyTorch-ROCm each need a libamdhip64.so.7 (ROCm 7.2 from
     # /opt/rocm, resp. torch's bundled copy) under the same SONAME: whichever
     # is loaded first serves the whole process.  Load torch's first when it is
@@ -61,52 +132,29 @@ def _load():
         raise ImportError(
             f"libroceicrc.so not found at {LIB_PATH}; build it with "
             "`make -C roce-test_amd/csrc` or `python -c 'import __graft_entry__ as g; g.build()'`")
-    L = ctypes.CDLL(LIB_PATH)
-    vp, u8p = ctypes.c_void_p, ctypes.c_void_p
-    u32, u64, i32 = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
-    sig = {
-        "ricrc_one": ([u8p, u32], u32),
-        "ricrc_verify_one": ([u8p, u32], i32),
-        "ricrc_stamp_one": ([u8p, u32], i32),
-        "ricrc_is_rocev2": ([u8p, u32], i32),
-        "ricrc_one_ex": ([u8p, u32, u32], u32),
-        "ricrc_verify_one_ex": ([u8p, u32, u32], i32),
-        "ricrc_stamp_one_ex": ([u8p, u32, u32], i32),
-        "ricrc_classify": ([u8p, u32], i32),
-        "ricrc_repair_one": ([u8p, u32, u32, u8p, u32, u32, u32, ctypes.POINTER(u32)], i32),
-        "ricrc_shift": ([u32, u64], u32),
-        "ricrc_combine": ([u32, u32, u64], u32),
-        "ricrc_create": ([ctypes.POINTER(vp), i32], i32),
-        "ricrc_create_devices": ([ctypes.POINTER(vp), ctypes.POINTER(i32), i32], i32),
-        "ricrc_destroy": ([vp], None),
-        "ricrc_device_count": ([vp], i32),
-        "ricrc_batch_host": ([vp, u8p, vp, vp, u32, u64, u32, vp], i32),
-        "ricrc_batch_device": ([vp, i32, vp, vp, vp, u32, u64, u32, vp, vp], i32),
-        "ricrc_verify_device": ([vp, i32, vp, vp, vp, u32, u64, u32, vp, vp], i32),
-        "ricrc_batch_host_ex": ([vp, u8p, vp, vp, u32, u64, u32, vp, u32], i32),
-        "ricrc_batch_device_ex": ([vp, i32, vp, vp, vp, u32, u64, u32, vp, vp, u32], i32),
-        "ricrc_verify_device_ex": ([vp, i32, vp, vp, vp, u32, u64, u32, vp, vp, u32], i32),
-        "ricrc_repair_device": ([vp, i32, vp, vp, vp, u32, u64, u32, u32, u32, vp, u32, u32, u32, vp, vp], i32),
-        "ricrc_host_alloc": ([vp, u64], vp),
-        "ricrc_host_free": ([vp, vp], None),
-        "ricrc_host_register": ([vp, vp, u64], i32),
-        "ricrc_host_unregister": ([vp, vp], i32),
-        "ricrc_synth_device": ([vp, i32, u64, u64, u64, u32, u32, vp, vp], i32),
-        "ricrc_stream": ([vp, i32], vp),
-        "ricrc_strerror": ([i32], ctypes.c_char_p),
-    }
-    for name, (args, res) in sig.items():
-        f = getattr(L, name)
-        f.argtypes = args
-        f.restype = res
-    return L
+    return _bind(ctypes.CDLL(LIB_PATH), EXPORTED)
 
 
-lib = _load()
+cpu = _load_cpu()
+_hip = None
+
+
+def hip_lib():
+    """libroceicrc.so (gfx950 kernels + runtime), loaded on first use."""
+    global _hip
+    if _hip is None:
+        _hip = _load_hip()
+    return _hip
+
+
+def __getattr__(name):  # roce_icrc.lib: the full HIP library, loaded lazily
+    if name == "lib":
+        return hip_lib()
+    raise AttributeError(name)
 
 
 def _strerror(rc: int) -> str:
-    return lib.ricrc_strerror(rc).decode()
+    return cpu.ricrc_strerror(rc).decode()
 
 
 def _buf(pkt):
@@ -143,13 +191,13 @@ def icrc(pkt, family: str = "v4") -> int:
     p, n, _keep = _buf(pkt)
     if n < 4:
         raise ValueError("packet shorter than the 4-byte ICRC trailer")
-    return int(lib.ricrc_one_ex(p, n, _fam(family)))
+    return int(cpu.ricrc_one_ex(p, n, _fam(family)))
 
 
 def verify(pkt, family: str = "v4") -> bool:
     """True iff the packet's trailer carries its ICRC (what a NIC checks)."""
     p, n, _keep = _buf(pkt)
-    rc = lib.ricrc_verify_one_ex(p, n, _fam(family))
+    rc = cpu.ricrc_verify_one_ex(p, n, _fam(family))
     if rc < 0:
         raise ICRCError(rc, "ricrc_verify_one_ex")
     return rc == 1
@@ -160,7 +208,7 @@ def stamp(pkt: bytearray, family: str = "v4") -> bytearray:
     if not isinstance(pkt, (bytearray, memoryview, np.ndarray)):
         raise TypeError("stamp() needs a mutable buffer (bytearray / memoryview / uint8 array)")
     p, n, _keep = _buf(pkt)
-    rc = lib.ricrc_stamp_one_ex(p, n, _fam(family))
+    rc = cpu.ricrc_stamp_one_ex(p, n, _fam(family))
     if rc < 0:
         raise ICRCError(rc, "ricrc_stamp_one_ex")
     return pkt
@@ -169,7 +217,7 @@ def stamp(pkt: bytearray, family: str = "v4") -> bytearray:
 def classify(pkt) -> int:
     """4 (RoCEv2 over IPv4), 6 (RoCEv2 over IPv6) or 0."""
     p, n, _keep = _buf(pkt)
-    return int(lib.ricrc_classify(p, n))
+    return int(cpu.ricrc_classify(p, n))
 
 
 def repair(pkt, off: int, old_bytes, old_icrc: int, family: str = "v4") -> int:
@@ -178,25 +226,37 @@ def repair(pkt, off: int, old_bytes, old_icrc: int, family: str = "v4") -> int:
     p, n, _keep = _buf(pkt)
     q, m, _keep2 = _buf(bytes(old_bytes))
     out = ctypes.c_uint32()
-    rc = lib.ricrc_repair_one(p, n, off, q, m, old_icrc & 0xFFFFFFFF, _fam(family), ctypes.byref(out))
+    rc = cpu.ricrc_repair_one(p, n, off, q, m, old_icrc & 0xFFFFFFFF, _fam(family), ctypes.byref(out))
     if rc < 0:
         raise ICRCError(rc, "ricrc_repair_one")
     return int(out.value)
 
 
+def icrc_checked(pkt, family: str = "v4", strict: bool = False) -> int:
+    """``ricrc_icrc``: like :func:`icrc` but with the length contract
+    (MIN_LEN..MAX_LEN, else ValueError) and, with ``strict``, the RoCEv2
+    classifier (not RoCEv2 of that family -> ValueError)."""
+    p, n, _keep = _buf(pkt)
+    out = ctypes.c_uint32()
+    rc = cpu.ricrc_icrc(p, n, _fam(family) | (0x100 if strict else 0), ctypes.byref(out))
+    if rc < 0:
+        raise ValueError(f"ricrc_icrc: {rc} ({_strerror(rc)})")
+    return int(out.value)
+
+
 def is_rocev2(pkt) -> bool:
     p, n, _keep = _buf(pkt)
-    return lib.ricrc_is_rocev2(p, n) == 1
+    return cpu.ricrc_is_rocev2(p, n) == 1
 
 
 def shift(reg: int, nbytes: int) -> int:
     """CRC register advanced over ``nbytes`` zero bytes (GF(2) x^(8n))."""
-    return int(lib.ricrc_shift(reg & 0xFFFFFFFF, nbytes))
+    return int(cpu.ricrc_shift(reg & 0xFFFFFFFF, nbytes))
 
 
 def combine(crc1: int, crc2: int, len2: int) -> int:
     """crc32(A || B) from crc32(A), crc32(B), len(B)."""
-    return int(lib.ricrc_combine(crc1 & 0xFFFFFFFF, crc2 & 0xFFFFFFFF, len2))
+    return int(cpu.ricrc_combine(crc1 & 0xFFFFFFFF, crc2 & 0xFFFFFFFF, len2))
 
 
 # ------------------------------------------------------------------- batches
@@ -230,6 +290,7 @@ class Context:
 
     def __init__(self, n_gpus: int = -1, devices=None):
         h = ctypes.c_void_p()
+        self._lib = lib = hip_lib()
         if devices is not None:
             ids = (ctypes.c_int * len(devices))(*devices)
             rc = lib.ricrc_create_devices(ctypes.byref(h), ids, len(devices))
@@ -245,7 +306,7 @@ class Context:
 
     def close(self):
         if getattr(self, "_h", None):
-            lib.ricrc_destroy(self._h)
+            hip_lib().ricrc_destroy(self._h)
             self._h = None
 
     def __enter__(self):
@@ -262,10 +323,10 @@ class Context:
 
     @property
     def device_count(self) -> int:
-        return lib.ricrc_device_count(self._h)
+        return self._lib.ricrc_device_count(self._h)
 
     def stream(self, dev: int = 0) -> int:
-        return lib.ricrc_stream(self._h, dev)
+        return self._lib.ricrc_stream(self._h, dev)
 
     # -- host in, host out ------------------------------------------------
     def batch_host(self, buf, offsets=None, lengths=None, stride: int = 0, l3_offset: int = 0,
@@ -276,7 +337,7 @@ class Context:
         if count is None:
             count = len(off) if off is not None else (len(ln) if ln is not None else buf.size // stride)
         out = np.empty(count, dtype=np.uint32)
-        rc = lib.ricrc_batch_host_ex(self._h, buf.ctypes.data, _ptr(off), _ptr(ln), stride, count,
+        rc = self._lib.ricrc_batch_host_ex(self._h, buf.ctypes.data, _ptr(off), _ptr(ln), stride, count,
                                      l3_offset, out.ctypes.data, _fam(family))
         if rc:
             raise ICRCError(rc, "ricrc_batch_host")
@@ -286,7 +347,7 @@ class Context:
     def batch_device(self, base, count: int, out, stride: int = 0, offsets=None, lengths=None,
                      l3_offset: int = 0, dev: int = 0, stream=None, verify: bool = False,
                      family: str = "v4") -> None:
-        fn = lib.ricrc_verify_device_ex if verify else lib.ricrc_batch_device_ex
+        fn = self._lib.ricrc_verify_device_ex if verify else self._lib.ricrc_batch_device_ex
         rc = fn(self._h, dev, _ptr(base), _ptr(offsets), _ptr(lengths), stride, count, l3_offset,
                 _ptr(out), _stream_ptr(stream), _fam(family))
         if rc:
@@ -302,7 +363,7 @@ class Context:
         ln = int(old_bytes.shape[-1]) if getattr(old_bytes, "ndim", 1) > 1 else int(old_bytes.numel() // max(count, 1))
         if old_stride is None:
             old_stride = ln
-        rc = lib.ricrc_repair_device(self._h, dev, _ptr(base), _ptr(offsets), _ptr(lengths), stride, count,
+        rc = self._lib.ricrc_repair_device(self._h, dev, _ptr(base), _ptr(offsets), _ptr(lengths), stride, count,
                                      l3_offset, off, ln, _ptr(old_bytes), old_stride, _fam(family),
                                      1 if stamp else 0, _ptr(out), _stream_ptr(stream))
         if rc:
@@ -310,33 +371,79 @@ class Context:
 
     def synth_device(self, buf, seed: int, first: int, count: int, n: int, stride: int | None = None,
                      dev: int = 0, stream=None) -> None:
-        rc = lib.ricrc_synth_device(self._h, dev, seed, first, count, n, stride or n, _ptr(buf),
+        rc = self._lib.ricrc_synth_device(self._h, dev, seed, first, count, n, stride or n, _ptr(buf),
                                     _stream_ptr(stream))
         if rc:
             raise ICRCError(rc, "ricrc_synth_device")
 
+    def synth_ragged_device(self, buf, seed: int, first: int, count: int, offsets, lengths,
+                            dev: int = 0, stream=None) -> None:
+        """Packet k = global packet ``first + k`` (the bytes :meth:`synth_device`
+        makes for that index and length) at ``buf + offsets[k]`` (device arrays)."""
+        rc = self._lib.ricrc_synth_ragged_device(self._h, dev, seed, first, count, _ptr(offsets), _ptr(lengths),
+                                                 _ptr(buf), _stream_ptr(stream))
+        if rc:
+            raise ICRCError(rc, "ricrc_synth_ragged_device")
+
+    def prime(self, usec: int = 20000, dev: int = 0) -> None:
+        """``ricrc_prime``: bring the device out of its idle power state."""
+        rc = self._lib.ricrc_prime(self._h, dev, usec)
+        if rc:
+            raise ICRCError(rc, "ricrc_prime")
+
+    # -- one process, all context devices, RCCL ---------------------------
+    def comm_init(self) -> None:
+        rc = self._lib.ricrc_comm_init(self._h)
+        if rc:
+            raise ICRCError(rc, "ricrc_comm_init")
+
+    def batch_device_all(self, bases, counts, outs, stride: int = 0, offsets=None, lengths=None,
+                         l3_offset: int = 0, family: str = "v4") -> None:
+        """``ricrc_batch_device_all``: shard k on context device k, every
+        ``outs[k]`` (``sum(counts)`` int32 on device k) ends with all ICRCs in
+        shard order.  Asynchronous on the context streams: :meth:`sync`."""
+        n = len(bases)
+        arr = lambda xs: None if xs is None else (ctypes.c_void_p * n)(*[_ptr(x) for x in xs])  # noqa: E731
+        cnt = (ctypes.c_uint64 * n)(*[int(c) for c in counts])
+        rc = self._lib.ricrc_batch_device_all(self._h, arr(bases), arr(offsets), arr(lengths), stride, cnt,
+                                              l3_offset, arr(outs), _fam(family))
+        if rc:
+            raise ICRCError(rc, "ricrc_batch_device_all")
+
+    def allgather(self, counts, outs) -> None:
+        n = len(outs)
+        cnt = (ctypes.c_uint64 * n)(*[int(c) for c in counts])
+        rc = self._lib.ricrc_allgather(self._h, cnt, (ctypes.c_void_p * n)(*[_ptr(x) for x in outs]))
+        if rc:
+            raise ICRCError(rc, "ricrc_allgather")
+
+    def sync(self) -> None:
+        rc = self._lib.ricrc_sync(self._h)
+        if rc:
+            raise ICRCError(rc, "ricrc_sync")
+
     def host_alloc(self, nbytes: int) -> np.ndarray:
         """Pinned host buffer (uint8 array); freed with :meth:`host_free`."""
-        p = lib.ricrc_host_alloc(self._h, nbytes)
+        p = self._lib.ricrc_host_alloc(self._h, nbytes)
         if not p:
             raise ICRCError(-errno.ENOMEM, "ricrc_host_alloc")
         arr = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(p))
         return arr
 
     def host_free(self, arr: np.ndarray) -> None:
-        lib.ricrc_host_free(self._h, arr.ctypes.data)
+        self._lib.ricrc_host_free(self._h, arr.ctypes.data)
 
     def host_register(self, arr: np.ndarray) -> None:
         """Pin an existing contiguous host array (a NIC ring) so host batches
         read it by DMA; undo with :meth:`host_unregister`."""
         if not arr.flags["C_CONTIGUOUS"]:
             raise ValueError("host_register needs a contiguous array")
-        rc = lib.ricrc_host_register(self._h, arr.ctypes.data, arr.nbytes)
+        rc = self._lib.ricrc_host_register(self._h, arr.ctypes.data, arr.nbytes)
         if rc:
             raise ICRCError(rc, "ricrc_host_register")
 
     def host_unregister(self, arr: np.ndarray) -> None:
-        rc = lib.ricrc_host_unregister(self._h, arr.ctypes.data)
+        rc = self._lib.ricrc_host_unregister(self._h, arr.ctypes.data)
         if rc:
             raise ICRCError(rc, "ricrc_host_unregister")
 

@@ -39,6 +39,72 @@ def test_mix_and_aliases_parse(monkeypatch):
     assert bench.MIX_METRIC != bench.METRIC and bench.MIX_SIZES == (64, 256, 1024, 4096)
 
 
+def test_gpus_n_relaunches_under_torchrun(monkeypatch):
+    """--gpus N > 1 outside torchrun re-runs the script on N ranks (before any
+    GPU call); inside torchrun WORLD_SIZE must equal --gpus."""
+    a = bench.parse(["--gpus", "2", "--steps", "3"])
+    assert bench.check_world(a, env={}) == (0, "relaunch")
+    argv = bench.launcher_argv(["--gpus", "2", "--steps", "3"], 2, 29511)
+    assert argv[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=2" in argv and "--nnodes=1" in argv and "--master-addr=127.0.0.1" in argv
+    assert "--master-port=29511" in argv
+    assert argv[-4:] == ["--gpus", "2", "--steps", "3"] and argv[-5].endswith("bench.py")
+    assert bench.check_world(a, env={"WORLD_SIZE": "2"}) is None
+    assert bench.check_world(bench.parse([]), env={}) is None
+
+
+def test_world_size_mismatch_exits_nonzero():
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr and r.stdout == ""
+    env["WORLD_SIZE"] = "8"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and r.stdout == ""
+
+
+def test_global_count_is_strong_scaling(monkeypatch):
+    a = bench.parse(["--global-count", "4194304"])
+    assert a.global_count == 4 << 20 and a.count == 1 << 20
+    a = bench.parse(["--mix", "--global-count", "1000"])
+    assert a.mix and a.global_count == 1000
+
+
+def test_cpu_share_respects_the_box_share(monkeypatch):
+    monkeypatch.setenv("OMP_NUM_THREADS", "3")
+    assert bench.cpu_share() == min(3, len(os.sched_getaffinity(0)))
+    monkeypatch.delenv("OMP_NUM_THREADS")
+    assert bench.cpu_share() == len(os.sched_getaffinity(0))
+    assert isinstance(bench.cpu_model(), str)
+
+
+def test_oracle_check_catches_a_wrong_shard():
+    """The post-run checker regenerates every rank's sampled packets from the
+    generator restatement: a correct gathered vector passes, a corrupted one
+    (here: rank 1's shard of a 3-rank fixed batch, and one ragged packet) fails."""
+    import numpy as np
+    import oracle_c
+    from roce_icrc.dist import byte_balanced_cuts, cuts_to_sizes, shard_range
+
+    a = bench.parse(["--size", "256"])
+    T, world = 3001, 3
+    cuts = [shard_range(T, world, r)[0] for r in range(world)] + [T]
+    full = oracle_c.icrc_batch(oracle_c.synth_batch(a.seed, 0, T, 256), stride=256)
+    assert bench.oracle_check(full, cuts_to_sizes(cuts), cuts, a, per_rank=64) == 0
+    bad = full.copy()
+    bad[cuts[1] + 5] ^= 1
+    assert bench.oracle_check(bad, cuts_to_sizes(cuts), cuts, a, per_rank=64) > 0
+    a = bench.parse(["--mix"])
+    lens = np.random.default_rng(a.seed).choice(np.array(bench.MIX_SIZES, np.uint32), size=2000)
+    cuts = byte_balanced_cuts(lens, world)
+    buf, offs = oracle_c.synth_ragged(a.seed, 0, lens)
+    full = oracle_c.icrc_batch(buf, offsets=offs, lengths=lens)
+    assert bench.oracle_check(full, cuts_to_sizes(cuts), cuts, a, lens_global=lens, per_rank=64) == 0
+    full[cuts[2]] ^= 0x80
+    assert bench.oracle_check(full, cuts_to_sizes(cuts), cuts, a, lens_global=lens, per_rank=64) > 0
+
+
 def test_metric_matches_baseline_json():
     with open(os.path.join(ROOT, "BASELINE.json")) as f:
         assert json.load(f)["metric"] == bench.METRIC
@@ -52,6 +118,9 @@ def test_kernel_labels_follow_the_dispatch():
 
 
 def test_traffic_is_tied_to_the_kernel_source(tmp_path):
+    # only the headline kernel's own sources count (an edit of another kernel
+    # must not null roofline.traffic)
+    assert bench.SCK_SOURCES[0] == "icrc_sck.hip"
     h = bench.kernel_source_hash()
     assert len(h) == 16 and h == bench.kernel_source_hash()
     # profiles/pmc_traffic.json is only reported for the source it was measured on

@@ -9,6 +9,7 @@ import random
 import re
 import struct
 import subprocess
+import sys
 import zlib
 
 import numpy as np
@@ -143,3 +144,48 @@ def test_no_cpu_fallback_without_gpu():
     assert e.value.rc == -errno.ENODEV
     with pytest.raises(roce_icrc.ICRCError):
         roce_icrc.icrc_batch(np.zeros(4096, np.uint8), stride=4096)
+
+
+def test_cpu_library_is_hip_free_and_exports_the_per_packet_section():
+    """libroceicrc_cpu.so (the simulator drop-in) links nothing from ROCm, and
+    importing roce_icrc for per-packet calls pulls in neither torch nor HIP."""
+    out = subprocess.run(["ldd", roce_icrc.CPU_LIB_PATH], capture_output=True, text=True).stdout
+    assert "amdhip" not in out and "rccl" not in out and "torch" not in out, out
+    syms = subprocess.run(["nm", "-D", "--defined-only", roce_icrc.CPU_LIB_PATH], capture_output=True,
+                          text=True).stdout
+    for s in roce_icrc.CPU_EXPORTED:
+        assert re.search(rf"\bT {s}\b", syms), s
+    assert set(roce_icrc.CPU_EXPORTED) <= set(declared_symbols())
+    code = ("import sys; sys.modules['torch'] = None; sys.path.insert(0, %r); import roce_icrc; "
+            "p = bytes.fromhex('450200301234400040110000c0a80164c0a80101457b12b7001c00001140ffff"
+            "0000001100000005000000016c1f7922'); assert roce_icrc.icrc(p) == 0x22791F6C; "
+            "assert roce_icrc.verify(p); print('hip' in ' '.join(open('/proc/self/maps').read().split()))"
+            % os.path.join(ROOT, "roce-test_amd"))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip() == "False"  # libamdhip64 never mapped
+
+
+def test_icrc_checked_length_and_classifier_contract():
+    """ricrc_icrc: SURVEY §8(b)'s -EINVAL for n < 44 / n > 65535 / NULL, and
+    with RICRC_F_STRICT -EPROTO for packets the ingress parser would not
+    accept as RoCEv2 (shuffle_ingress_parser.p4:12-36)."""
+    pkt = bytes.fromhex("450200301234400040110000c0a80164c0a80101457b12b7001c00001140ffff"
+                        "0000001100000005000000016c1f7922")
+    assert roce_icrc.icrc_checked(pkt) == 0x22791F6C == roce_icrc.icrc_checked(pkt, strict=True)
+    assert roce_icrc.icrc_checked(pkt, family="auto", strict=True) == 0x22791F6C
+    with pytest.raises(ValueError, match="-22"):
+        roce_icrc.icrc_checked(pkt[:43])
+    with pytest.raises(ValueError, match="-22"):
+        roce_icrc.icrc_checked(bytes(65536))
+    bad = bytearray(pkt)
+    bad[23] ^= 1  # UDP dport != 4791
+    assert roce_icrc.icrc_checked(bytes(bad)) == O.icrc(bytes(bad))  # not strict: any bytes
+    with pytest.raises(ValueError, match="-71"):
+        roce_icrc.icrc_checked(bytes(bad), strict=True)
+    with pytest.raises(ValueError, match="-71"):
+        roce_icrc.icrc_checked(pkt, family="v6", strict=True)  # an IPv4 packet
+    out = ctypes.c_uint32(7)
+    assert roce_icrc.cpu.ricrc_icrc(None, 100, 0, ctypes.byref(out)) == -errno.EINVAL
+    assert roce_icrc.cpu.ricrc_icrc(pkt, len(pkt), 9, ctypes.byref(out)) == -errno.EINVAL
+    assert out.value == 7

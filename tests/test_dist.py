@@ -1,9 +1,11 @@
 """CPU: the N > 1 path (sharding + all-gather of results) with world_size-2 gloo.
 
-Each rank computes the ICRCs of its shard (here with the CPU oracle, the GPU
-being unavailable in this container), all-gathers them with the same helper
-bench.py uses over RCCL, and every rank must end with exactly the
-single-process result vector, for equal and unequal shards."""
+Each rank computes the ICRCs of its shard (here with the CPU oracle: this
+container has no GPU; tests/test_gpu_dist.py runs the same sharding and
+gather with the HIP kernels over an nccl group), all-gathers them with the
+helpers bench.py uses over RCCL (IcrcGather: one all_gather_into_tensor of
+padded shards; all_gather_icrc), and every rank must end with exactly the
+single-process result vector, for equal and unequal (byte-balanced) shards."""
 import os
 import socket
 
@@ -13,7 +15,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from roce_icrc.dist import all_gather_icrc, byte_balanced_cuts, shard_range
+from roce_icrc.dist import IcrcGather, all_gather_icrc, byte_balanced_cuts, cuts_to_sizes, shard_range
 
 
 def _free_port():
@@ -37,6 +39,67 @@ def _worker(rank, world, port, count, n, q):
         q.put((rank, got.numpy().view(np.uint32).copy()))
     finally:
         dist.destroy_process_group()
+
+
+def _mix_worker(rank, world, port, count, q):
+    import oracle_c
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lens_g = np.random.default_rng(11).choice(np.array([64, 256, 1024, 4096], np.uint32), size=count)
+        cuts = byte_balanced_cuts(lens_g, world)
+        g = IcrcGather(cuts_to_sizes(cuts))
+        lo, hi = cuts[rank], cuts[rank + 1]
+        buf, offs = oracle_c.synth_ragged(0x1CEC0DE, lo, lens_g[lo:hi])
+        mine = oracle_c.icrc_batch(buf, offsets=offs, lengths=lens_g[lo:hi])
+        local = g.local_buffer("cpu")
+        local[: hi - lo] = torch.from_numpy(mine.view(np.int32).copy())
+        out = g.gathered_buffer("cpu")
+        g.start(local, out, async_op=True).wait()
+        assert torch.equal(g.shard_of(out, rank), local[: hi - lo])
+        q.put((rank, g.compact(out).numpy().view(np.uint32).copy(), g.equal))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_byte_balanced_mix_unequal_shards():
+    """C4's split: one global mixed-MTU batch cut at equal bytes (unequal packet
+    counts), every rank generates its shard from the global index, one padded
+    all_gather_into_tensor, compacted == the single-process result."""
+    import oracle_c
+
+    world, count = 2, 3001
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mix_worker, args=(r, world, port, count, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, v, eq = q.get(timeout=120)
+        res[r] = v
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    lens_g = np.random.default_rng(11).choice(np.array([64, 256, 1024, 4096], np.uint32), size=count)
+    assert not eq  # the byte cut gives the ranks different packet counts
+    buf, offs = oracle_c.synth_ragged(0x1CEC0DE, 0, lens_g)
+    want = oracle_c.icrc_batch(buf, offsets=offs, lengths=lens_g)
+    for r in range(world):
+        np.testing.assert_array_equal(res[r], want)
+
+
+def test_synth_ragged_restatement_matches_fixed():
+    """Packet contents depend only on (seed, global index, length): the ragged
+    generator agrees with the fixed-size one packet by packet."""
+    import oracle_c
+
+    lens = np.array([64, 1024, 256, 4096, 64], np.uint32)
+    buf, offs = oracle_c.synth_ragged(7, 100, lens)
+    for k, (o, n) in enumerate(zip(offs, lens)):
+        np.testing.assert_array_equal(buf[int(o): int(o) + int(n)], oracle_c.synth_batch(7, 100 + k, 1, int(n))[0])
 
 
 @pytest.mark.parametrize("count,n", [(1000, 1024), (777, 64)])

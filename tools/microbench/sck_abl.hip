@@ -2,6 +2,7 @@
 // are meaningless for ABL != 0).  Build:
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 sck_abl.hip -o sck_abl
 #include "../../roce-test_amd/csrc/icrc_kernels.hip"
+#include "../../roce-test_amd/csrc/icrc_sck.hip"
 #include <stdio.h>
 #include <stdlib.h>
 using namespace ricrc;
