@@ -253,8 +253,8 @@ int ricrc_synth_device(ricrc_ctx *ctx, int dev, uint64_t seed, uint64_t first, u
 int ricrc_synth_ragged_device(ricrc_ctx *ctx, int dev, uint64_t seed, uint64_t first, uint64_t count,
                               const uint64_t *d_off, const uint32_t *d_len, void *d_buf, void *stream);
 
-/* Bring context device dev out of its idle power state: runs the headline
- * kernel over a 256 MiB scratch batch back to back for usec microseconds
+/* Bring context device dev out of its idle power state: streams a 256 MiB
+ * scratch buffer at HBM speed, back to back, for usec microseconds
  * (synchronous; ~20000 is enough on MI355X).  After >= 20 ms of idle, the
  * first ~12 launches of a burst otherwise run up to 15 % slower (DESIGN.md §4
  * "Power ramp").  A NIC-ring service calls it when traffic resumes; bench.py

@@ -610,8 +610,8 @@ int ricrc_synth_ragged_device(ricrc_ctx *ctx, int dev, uint64_t seed, uint64_t f
 }
 
 // Bring a device out of its idle power state before a latency-sensitive
-// burst: the headline kernel over a 256 MiB scratch batch, back to back, for
-// `usec` microseconds.  Measured (tools/ramp_probe.py, profiles/r02/
+// burst: a streaming read of a 256 MiB scratch buffer (icrc_prime_kernel, at
+// HBM speed like the ICRC kernels), back to back, for `usec` microseconds.  Measured (tools/ramp_probe.py, profiles/r02/
 // ramp_probe.jsonl): after >= 20 ms of GPU idle the 5th-12th launches of the
 // 1 M x 4 KiB batch run 700-750 us instead of 645-650 us; 20 ms of busy work
 // first removes that transient.
@@ -625,12 +625,11 @@ int ricrc_prime(ricrc_ctx *ctx, int dev, uint32_t usec) {
   uint8_t *buf = nullptr;
   uint32_t *out = nullptr;
   HIP_TRY(hipMalloc(&buf, kPkts * kN));
-  int rc = hip_err(hipMalloc(&out, kPkts * sizeof(uint32_t)));
+  int rc = hip_err(hipMalloc(&out, 256 * sizeof(uint32_t)));
   if (!rc) rc = hip_err(hipMemsetAsync(buf, 0, kPkts * kN, d.stream));
   const auto t0 = std::chrono::steady_clock::now();
   while (!rc) {
-    for (int k = 0; k < 16 && !rc; ++k)
-      rc = launch_batch_v4(d, buf, nullptr, nullptr, kN, kPkts, 0, out, d.stream, false);
+    for (int k = 0; k < 16 && !rc; ++k) rc = hip_err(launch_prime(buf, kPkts * kN, out, d.n_cu, d.stream));
     if (!rc) rc = hip_err(hipStreamSynchronize(d.stream));
     const auto us = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0);
     if (us.count() >= (long long)usec) break;

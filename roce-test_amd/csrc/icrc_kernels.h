@@ -185,5 +185,7 @@ hipError_t launch_ragged(const RaggedArgs &a, int grid, hipStream_t st);
 hipError_t ragged_piece_scan(const RaggedArgs &a, uint64_t *ps, hipStream_t st);
 hipError_t launch_synth(const SynthArgs &a, hipStream_t st);
 hipError_t launch_synth_ragged(const SynthArgs &a, hipStream_t st);
+// ricrc_prime's streaming read of `bytes` (a multiple of 16) of scratch.
+hipError_t launch_prime(const void *scratch, uint64_t bytes, uint32_t *sink, int n_cu, hipStream_t st);
 
 }  // namespace ricrc

@@ -997,6 +997,19 @@ __global__ void synth_ragged_kernel(SynthArgs a) {
   }
 }
 
+// Power-state primer (ricrc_prime): a plain streaming read of a scratch
+// buffer with 16-byte loads, XOR-folded per thread; one word per thread is
+// written only when the fold hits a value the zeroed scratch never produces
+// (keeps the loads alive).  Its own kernel so profiles of the ICRC kernels
+// never mix primer dispatches into their statistics.
+__global__ __launch_bounds__(256) void icrc_prime_kernel(const u32x4 *src, uint64_t n16, uint32_t *sink) {
+  u32x4 acc = {0u, 0u, 0u, 0u};
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * blockDim.x)
+    acc ^= __builtin_nontemporal_load(src + i);
+  const uint32_t v = acc[0] ^ acc[1] ^ acc[2] ^ acc[3];
+  if (v == 0x9E3779B9u) sink[threadIdx.x] = v;
+}
+
 // ----------------------------------------------------------- host launchers
 hipError_t launch_stream(const StreamArgs &a, int cpl, int grid, hipStream_t st) {
   const bool pipe = cpl == 1;
@@ -1029,6 +1042,12 @@ hipError_t launch_synth(const SynthArgs &a, hipStream_t st) {
   if (blocks > 65536) blocks = 65536;
   if (blocks == 0) return hipSuccess;
   hipLaunchKernelGGL(synth_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_prime(const void *scratch, uint64_t bytes, uint32_t *sink, int n_cu, hipStream_t st) {
+  hipLaunchKernelGGL(icrc_prime_kernel, dim3(8 * n_cu), dim3(256), 0, st, reinterpret_cast<const u32x4 *>(scratch),
+                     bytes / 16, sink);
   return hipGetLastError();
 }
 

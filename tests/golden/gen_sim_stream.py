@@ -4,7 +4,7 @@
 Runs the reference's unchanged python/simulator.py (BASELINE configs[0]:
 per-packet ICRC on the CPU at the simulator's wire crossings) under
 roce_icrc.sim_harness.WireTap for fixed seeds, and records for every packet
-put on a queue its Packet fields (python/rdma.py:5-37), the RoCEv2 bytes the
+transmission (a packet put on a tx queue: the sending NIC) its Packet fields (python/rdma.py:5-37), the RoCEv2 bytes the
 adapter produced (roce_icrc.wire) with the ICRC stamped, and the ICRC as
 computed by the ORACLE (not the product).  The reference itself never leaves
 this container: tests and the GPU box only read the JSON/BIN written here.
@@ -32,14 +32,16 @@ def main(refpy):
            "seeds": {}}
     blob = bytearray()
     for seed in SEEDS:
-        tap = sim_harness.run_simulator(sim, seed)
+        tap, log = sim_harness.run_simulator(sim, seed)
+        assert "Wrong result" not in log and "Too many retries" not in log
         recs = []
         for ev, fields, wire_hex, v in tap.records:
             raw = bytes.fromhex(wire_hex)
             assert O.icrc(raw) == v and O.residue_ok(raw), fields
             recs.append({"fields": fields, "offset": len(blob), "len": len(raw), "icrc": v})
             blob += raw
-        out["seeds"][str(seed)] = {"stamped": tap.stamped, "verified": tap.verified, "packets": recs}
+        out["seeds"][str(seed)] = {"stamped": tap.stamped, "verified": tap.verified,
+                                   "lost_by_simulator": tap.stamped - tap.verified - tap.dropped, "packets": recs}
         print(f"seed {seed}: {tap.stamped} packets stamped, {tap.verified} verified")
     with open(os.path.join(HERE, "sim_stream.bin"), "wb") as f:
         f.write(blob)

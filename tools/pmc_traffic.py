@@ -33,7 +33,7 @@ def run_pass(counter, outdir):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 k = row["Kernel_Name"]
-                if "icrc_" in k and "synth" not in k and row["Counter_Name"] == counter:
+                if "icrc_sck_kernel" in k and row["Counter_Name"] == counter:  # the headline kernel only
                     vals.append(float(row["Counter_Value"]))
                     names.add(k)
     if not vals:
