@@ -44,6 +44,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <stdlib.h>
+
 #include <type_traits>
 
 #include "icrc_device.h"
@@ -525,6 +527,123 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   if (q_end != round_q0) flush(q_end);
 }
 
+
+// =======================================================================
+// Small packets of the ragged path (<= kRsSmallL lines: the 64 / 256-byte
+// share of C4): ONE LANE PER PACKET, descriptors [0, *small_pos) of the
+// buckets.  8 lanes per packet (the fold above) is too coarse for them, and
+// the piece kernel (icrc_kernels.hip, one 64-byte piece per lane) pays a GF(2)
+// re-alignment, prefix XOR and end multiply per packet.  Here a lane folds its
+// packet's whole byte stream from a ZERO register with no multiply at all:
+//
+//   stream = 4 x 0xFF || masked L3[0, M)        (M = n - 4)
+//
+// (the CRC-32 init ~0 folded over the 8-byte 0xFF prefix of calc_icrc,
+// shuffle_egress.p4:465, is the zero register over 00 x 4 || FF x 4, and
+// leading zeros are free; tests/test_kernel_algebra.py::
+// test_small_lane_end_aligned_stream), ICRC = ~register.  The
+// stream is cut into 16-byte blocks that END at the packet's covered end
+// e = addr + M, so no trailing byte is ever folded; leading bytes before the
+// prefix are zeros, which a zero register ignores.  That lets every lane of
+// a wave fold the same number of blocks Kmax (a multiple of 4: lanes with
+// shorter packets start with all-zero blocks), so the loop has no divergence
+// and no exec-masked memory op.  Block j needs the 16-byte native units N and
+// N + 16 (N = e - (e & 15) - 16 (Kmax - j)); loads are clamped to the units
+// that hold packet bytes (never another page) and whatever a clamped unit
+// holds is masked away by packet-relative offset.  A block's words come out
+// of the two units by a 2-level word funnel and v_alignbyte (phase e & 15).
+// =======================================================================
+__device__ __forceinline__ uint32_t small_word(uint32_t w, int r) {  // r = packet-relative offset of byte 0
+  const uint32_t keep = byte_span_mask(-r, 4);            // bytes at r >= 0: packet data
+  const uint32_t pre = byte_span_mask(-4 - r, -r);        // bytes at -4 <= r < 0: the 0xFF prefix
+  // invariant fields -> 0xFF; outside [0, 40) the shifted map is empty, so no
+  // range test (a select on r became a divergent branch)
+  const uint32_t sh = (uint32_t)(r + 3 < 0 ? 0 : r + 3 > 63 ? 63 : r + 3);
+  const uint32_t bits = (uint32_t)(((kMaskBits << 3) >> sh) & 0xFu);
+  return (w & keep) | pre | (expand_nibble(bits) & keep);
+}
+
+__global__ __launch_bounds__(kBlock) void icrc_rsmall_kernel(RsckArgs a) {
+  __shared__ uint32_t lds[kLdsWords];
+  const uint32_t tab_v = table_entry(g_tab);
+  const uint32_t count = *a.small_pos;
+  table_store(lds, tab_v);
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const LaneTab lt{(lane & 31) << 2, ((lane & 31) << 2) | 0x10000u};
+  const uint32_t step = gridDim.x * kWaves * 64u;
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.res, 4u * count);
+  constexpr int D = 4;  // units in the load ring (= the unroll)
+  auto desc_at = [&](uint32_t pos) -> RsDesc { return a.desc[pos < count ? pos : (count ? count - 1u : 0u)]; };
+  uint32_t base = (blockIdx.x * kWaves + wid) * 64u;
+  RsDesc dcur = desc_at(base + lane);
+  for (; base < count; base += step) {
+    const uint32_t pos = base + lane;
+    const RsDesc d = dcur;
+    dcur = desc_at(pos + step);  // the next round's descriptor, in flight meanwhile
+    const uint64_t addr = ((uint64_t)(d.hi & 0xFFFFu) << 32) | d.lo;
+    const uint32_t M = (d.hi >> 16) - 4u;
+    const uint64_t e = addr + M;
+    uint32_t K = (M + 4u + 15u) >> 4;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) K = max(K, (uint32_t)__shfl_xor((int)K, o));
+    const uint32_t Kmax = __builtin_amdgcn_readfirstlane((K + (D - 1)) & ~(uint32_t)(D - 1));
+    const uint32_t t = (uint32_t)(e & 15u), sb = t & 3u;
+    const uint32_t m2 = 0u - ((t >> 3) & 1u), m1 = 0u - ((t >> 2) & 1u);  // all-ones word-shift selects
+    const uint64_t ufirst = addr & ~15ull, ulast = (e - 1u) & ~15ull;
+    const uint64_t N0 = e - t - 16ull * Kmax;  // native unit of block 0
+    auto unit = [&](uint32_t k) -> u32x4 {     // native unit k (block k's first), clamped to the packet's
+      uint64_t u = N0 + 16ull * k;
+      u = u < ufirst ? ufirst : (u > ulast ? ulast : u);
+      return gload16(u);
+    };
+    // Block j folds units j and j + 1, held in a ring of D slots (unit k in
+    // slot k % D); after the fold the slot of unit j -- dead now -- is
+    // refilled with unit j + D, so the load lands in the registers it frees
+    // and the unrolled loop needs no register rotation (an earlier refill
+    // made the compiler rotate the ring with copies and drain vmcnt(0) at
+    // the back edge).  D - 1 units are in flight while a block folds.
+    u32x4 ring[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      __builtin_amdgcn_sched_barrier(0);
+      ring[k] = unit(k);
+    }
+    uint32_t reg = 0u;
+    int rel = (int)M - 16 * (int)Kmax;  // packet-relative offset of the next block
+    for (uint32_t j = 0; j < Kmax; j += D) {  // wave-uniform
+#pragma unroll
+      for (int u = 0; u < D; ++u) {
+        __builtin_amdgcn_sched_barrier(0);
+        const u32x4 c = ring[u], n = ring[(u + 1) % D];
+        // W = c0..c3 n0..n3; X[k] = W[(t >> 2) + k] by bitwise selects
+        // (written as ternaries, the compiler turned the funnel into a
+        // dynamically indexed array in scratch).
+        const uint32_t W[8] = {c[0], c[1], c[2], c[3], n[0], n[1], n[2], n[3]};
+        uint32_t V[6], X[5], w[4];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) V[k] = __builtin_amdgcn_bitop3_b32(m2, W[k + 2], W[k], 0xCA);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) X[k] = __builtin_amdgcn_bitop3_b32(m1, V[k + 1], V[k], 0xCA);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) w[i] = __builtin_amdgcn_alignbyte(X[i + 1], X[i], sb);
+        __builtin_amdgcn_sched_barrier(0);
+        ring[u] = unit(j + u + D);
+        __builtin_amdgcn_sched_barrier(0);
+        if (__builtin_amdgcn_ballot_w64(rel < 40) != 0) {  // wave-uniform: some lane is in its head
+#pragma unroll
+          for (int i = 0; i < 4; ++i) w[i] = small_word(w[i], rel + 4 * i);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) reg = step4(lds, lt, reg, w[i]);
+        rel += 16;
+      }
+    }
+    __builtin_amdgcn_raw_buffer_store_b32(~reg, ro, pos < count ? 4u * pos : 0x7FFFFFF0u, 0, 0);
+  }
+}
+
 uint64_t rs_workspace_bytes(uint64_t count) {
   const uint64_t npos = count + 8ull * kRsClasses;
   auto al = [](uint64_t b) { return (b + 255) & ~255ull; };
@@ -558,6 +677,11 @@ hipError_t launch_rsck(RsckArgs &a, const RaggedArgs &small, int grid, hipStream
   hipLaunchKernelGGL(rsck_plan, dim3(1), dim3(1024), 0, st, a);
   hipLaunchKernelGGL(rsck_scatter, dim3(pgrid), dim3(kPassBlock), 0, st, a);
   hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, st, a);
+  if (getenv("RICRC_RS_PIECE") == nullptr) {  // the small region [0, *small_pos): one lane per packet
+    hipLaunchKernelGGL(icrc_rsmall_kernel, dim3(grid), dim3(kBlock), 0, st, a);
+    hipLaunchKernelGGL(rsck_gather, dim3(pgrid), dim3(256), 0, st, a);
+    return hipGetLastError();
+  }
   RaggedArgs r = small;  // the small region [0, *small_pos) of the buckets: piece kernel, ICRCs into res
   r.base = nullptr;
   r.off = nullptr;

@@ -205,3 +205,57 @@ def test_ragged_line_grid_decomposition():
         assert 0 <= tz < 128
         reg = o.gf_mul(reg, _xinv8n_fast(tz))
         assert reg ^ 0xFFFFFFFF == o.icrc(pkt), (n, a)
+
+
+def _le_words(b: bytes):
+    return [int.from_bytes(b[i:i + 4], "little") for i in range(0, len(b), 4)]
+
+
+def _byte_span(lo, hi):
+    lo, hi = max(0, min(4, lo)), max(0, min(4, hi))
+    return sum(0xFF << (8 * k) for k in range(lo, hi))
+
+
+def _small_word(w, r):  # icrc_rsck.hip small_word()
+    keep = _byte_span(-r, 4)
+    pre = _byte_span(-4 - r, -r)
+    orm = 0
+    for k in range(4):
+        if (r + k) in o.MASK_OFFSETS:
+            orm |= 0xFF << (8 * k)
+    return (w & keep) | pre | orm
+
+
+def test_small_lane_end_aligned_stream():
+    """icrc_rsmall_kernel (one lane per packet): fold 16-byte blocks that END at
+    the covered end e from a ZERO register -- 4 x 0xFF prefix (= init ~0 and the 8 x 0xFF of calc_icrc), masked body,
+    leading zero blocks up to a wave-wide multiple-of-4 block count, units
+    clamped to the packet's own, words by the 2-level funnel + alignbyte --
+    and take ~register.  Restated on a byte image with arbitrary neighbours."""
+    rng = random.Random(5)
+    mem = bytearray(rng.getrandbits(8) for _ in range(1 << 14))
+    for _ in range(400):
+        n = rng.choice([44, 45, 47, 64, 100, 256, 255, 300, 380, rng.randrange(44, 400)])
+        addr = rng.randrange(64, len(mem) - n - 64)
+        M = n - 4
+        e = addr + M
+        K = (M + 4 + 15) >> 4
+        Kmax = ((K + rng.randrange(0, 6)) + 3) & ~3  # the wave's maximum, rounded up
+        t = e & 15
+        ufirst, ulast = addr & ~15, (e - 1) & ~15
+        unit = lambda u: _le_words(bytes(mem[min(max(u, ufirst), ulast):][:16]))  # noqa: E731
+        reg = 0
+        N = e - t - 16 * Kmax
+        rel = M - 16 * Kmax
+        for j in range(Kmax):
+            W = unit(N) + unit(N + 16)
+            X = [W[(t >> 2) + k] for k in range(5)]
+            sb = t & 3
+            for i in range(4):
+                w = ((X[i + 1] << 32 | X[i]) >> (8 * sb)) & 0xFFFFFFFF
+                if rel < 40:
+                    w = _small_word(w, rel + 4 * i)
+                reg = fold(reg, w.to_bytes(4, "little"))
+            rel += 16
+            N += 16
+        assert (~reg) & 0xFFFFFFFF == o.icrc(bytes(mem[addr:addr + n])), (addr, n, Kmax)
