@@ -65,6 +65,8 @@ def parse(argv=None):
     ap.add_argument("--mix", action="store_true",
                     help="C4: lengths uniform over 64/256/1024/4096 B, offsets + lengths (ragged path)")
     ap.add_argument("--seed", type=int, default=SEED)
+    ap.add_argument("--family", choices=("v4", "v6", "auto"), default="v4",
+                    help="address-family masks (v4 = the reference's; v6/auto: SURVEY §8f-3)")
     ap.add_argument("--no-gather", action="store_true", help="skip the RCCL all-gather at N>1")
     ap.add_argument("--in-stream-gather", dest="overlap_gather", action="store_false",
                     help="order step i's all-gather after its kernel on the compute stream "
@@ -187,19 +189,19 @@ def oracle_check(gathered, sizes, cuts, args, lens_global=None, per_rank=256):
                                         np.linspace(0, n - 1, num=min(per_rank, n)).astype(np.int64)]))
         if lens_global is None:
             pk = np.concatenate([oracle_c.synth_batch(args.seed, lo + int(k), 1, args.size) for k in idx])
-            want = oracle_c.icrc_batch(pk.reshape(-1), stride=args.size)
+            want = oracle_c.icrc_batch(pk.reshape(-1), stride=args.size, family=args.family)
         else:
             lens = lens_global[lo + idx]
             bufs = [oracle_c.synth_ragged(args.seed, lo + int(k), lens[j:j + 1])[0] for j, k in enumerate(idx)]
             offs = np.zeros(len(idx), np.uint64)
             offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
-            want = oracle_c.icrc_batch(np.concatenate(bufs), offsets=offs, lengths=lens)
+            want = oracle_c.icrc_batch(np.concatenate(bufs), offsets=offs, lengths=lens, family=args.family)
         got = gathered[lo + idx]
         bad += int((got != want).sum())
     return bad
 
 
-def cpu_baseline(sample_host, got_sample, size, budget_s, offsets=None, lengths=None):
+def cpu_baseline(sample_host, got_sample, size, budget_s, offsets=None, lengths=None, family="v4"):
     """Time the C oracle (slice-by-8, pthreads over this host's CPU share) on a
     sample of the batch, check the GPU's ICRCs on it, and add a 1-core zlib
     figure (the Python oracle, zlib.crc32 per packet)."""
@@ -208,6 +210,7 @@ def cpu_baseline(sample_host, got_sample, size, budget_s, offsets=None, lengths=
     oracle_c, icrc_oracle = _oracle()
     threads = cpu_share()
     kw = dict(offsets=offsets, lengths=lengths) if offsets is not None else dict(stride=size)
+    kw["family"] = family
     want = oracle_c.icrc_batch(sample_host, threads=threads, **kw)
     if not np.array_equal(want, got_sample):
         raise SystemExit("bench: GPU ICRCs differ from the oracle on the CPU-baseline sample")
@@ -228,7 +231,7 @@ def cpu_baseline(sample_host, got_sample, size, budget_s, offsets=None, lengths=
     zb, zt0 = 0, time.perf_counter()
     while time.perf_counter() - zt0 < 2.0:
         for p in pk[:2048]:
-            icrc_oracle.icrc(p)
+            icrc_oracle.icrc(p, family)
             zb += len(p)
     zdt = time.perf_counter() - zt0
     return {
@@ -366,9 +369,10 @@ def main(argv=None):
             ev[0].record(stream)
         if count:
             if args.mix:
-                ctx.batch_device(pk, count, outs[j], offsets=d_offs, lengths=d_lens, stream=stream)
+                ctx.batch_device(pk, count, outs[j], offsets=d_offs, lengths=d_lens, stream=stream,
+                                 family=args.family)
             else:
-                ctx.batch_device(pk, count, outs[j], stride=args.size, stream=stream)
+                ctx.batch_device(pk, count, outs[j], stride=args.size, stream=stream, family=args.family)
         if ev is not None:
             ev[1].record(stream)
         if do_gather:
@@ -436,7 +440,7 @@ def main(argv=None):
     # per launch: packets read + ICRCs written (+ 12 B of offset/length descriptors per packet, ragged)
     alg_bytes = rank_bytes + 4 * count + (12 * count if args.mix else 0)
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
-    traffic = None if args.mix else load_traffic(args.size, count)
+    traffic = None if (args.mix or args.family != "v4") else load_traffic(args.size, count)
 
     strong = args.global_count is not None
     if args.mix:
@@ -463,7 +467,7 @@ def main(argv=None):
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (device-generated RoCEv2 SEND_ONLY packets, seeded; reference P4 header template)",
-        "config": {"workload": workload, "packets_total": b["T"], "packets_rank0": sizes[0],
+        "config": {"workload": workload, "packets_total": b["T"], "packets_rank0": sizes[0], "family": args.family,
                    "packet_bytes": "mix 64/256/1024/4096" if args.mix else args.size,
                    "parallelism": f"dp{world}" + (" (all-gather u32 results)" if do_gather else "")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -480,10 +484,11 @@ def main(argv=None):
             span = int(h_offs[ns - 1]) + int(h_lens[ns - 1])
             sample = pk[:span].cpu().numpy()
             result["cpu_baseline"] = cpu_baseline(sample, got, args.size, args.cpu_seconds,
-                                                  offsets=h_offs[:ns].copy(), lengths=h_lens[:ns].copy())
+                                                  offsets=h_offs[:ns].copy(), lengths=h_lens[:ns].copy(),
+                                                  family=args.family)
         else:
             sample = pk[: ns * args.size].cpu().numpy().reshape(ns, args.size)
-            result["cpu_baseline"] = cpu_baseline(sample, got, args.size, args.cpu_seconds)
+            result["cpu_baseline"] = cpu_baseline(sample, got, args.size, args.cpu_seconds, family=args.family)
         result["c0"] = c0_latency()
 
     if rank == 0:

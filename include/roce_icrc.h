@@ -20,6 +20,11 @@
  * (p4/common/header.p4:42-112).  The ICRC covers 0xFF x 8 || L3[0, n-4) with the
  * invariant fields masked; the returned value v is put on the wire as LE32(v)
  * (shuffle_egress.p4:493), i.e. trailer bytes = v & 0xff, v >> 8, ...
+ * calc_icrc's own field list stops at the AETH: it is written for the
+ * switch's 48-byte write ACKs (IPv4 || UDP || BTH || AETH), for which the two
+ * definitions hash the same bytes; covering every byte after the BTH for
+ * every other packet is IBTA Annex A17's ICRC (as Linux rxe and NICs compute
+ * it), a deliberate generalisation.
  *
  * Errors: 0 = success, negative errno: -EINVAL (bad length / NULL / alignment),
  * -ENODEV (no GPU), -ENOMEM, -EIO (HIP / RCCL failure), -EPROTO (not RoCEv2,

@@ -11,7 +11,11 @@
  *     || L3 bytes [0, n-4) with bytes 1 (tos, :467), 8 (ttl, :471),
  *        10-11 (IPv4 csum, :473), 26-27 (UDP csum, :480) and
  *        32 (BTH FECN/BECN/resv, :485) forced to 0xFF,
- *   all other bytes unmasked (BTH rest :482-487, AETH/ext/payload :489-490).
+ *   all other bytes unmasked (BTH rest :482-487, AETH :489-490).  The P4
+ *   field list ends at the AETH (calc_icrc is written for 48-byte write ACKs);
+ *   bytes after BTH other than an AETH (extension headers, payload, pad) are
+ *   covered unmasked as IBTA Annex A17 / Linux rxe do -- a deliberate
+ *   generalisation that equals calc_icrc on the reference's ACK shape.
  *   Offsets from p4/common/header.p4:42-53 (ipv4_h), :67-72 (udp_h),
  *   :75-85 (bth_h).  The trailer carries the value little-endian (:493).
  *

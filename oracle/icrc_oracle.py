@@ -24,8 +24,16 @@ Spec followed (all citations relative to the reference root):
 * ``shuffle_egress.p4:477-480`` UDP: ports/length kept, checksum -> 0xFFFF.
 * ``shuffle_egress.p4:482-487`` BTH: opcode, se/m/pad/tver, pkey kept,
   FECN/BECN/resv byte -> 0xFF (:485), dqpn and ackreq/psn kept.
-* ``shuffle_egress.p4:489-490`` every byte after BTH (extension headers,
-  payload, pad) is covered unmasked, up to the 4-byte ICRC trailer.
+* ``shuffle_egress.p4:489-490`` the AETH (syndrome, MSN), unmasked.  That is
+  where the reference's field list ENDS: calc_icrc() is written for the
+  switch-generated write ACKs only (its one call site, :669, commented out),
+  whose L3 packet is IPv4 ‖ UDP ‖ BTH ‖ AETH ‖ ICRC (48 bytes,
+  shuffle_ingress.p4:539,550).  DELIBERATE GENERALISATION: for any other
+  packet this oracle covers every byte after BTH up to the trailer
+  (extension headers, payload, pad), unmasked -- IBTA Annex A17's ICRC,
+  which the Linux rxe driver computes the same way and which NICs check.
+  For the reference's ACK shape both definitions are the same bytes
+  (tests/test_oracle.py::test_ack_matches_calc_icrc_field_list).
 * ``shuffle_egress.p4:493`` the 32-bit value is emitted byte-swapped, i.e. the
   trailer holds the CRC little-endian.
 * Header layout offsets: ``p4/common/header.p4:42-53`` (ipv4_h, 20 B),

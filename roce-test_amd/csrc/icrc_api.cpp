@@ -188,8 +188,22 @@ int ilog2_ceil(uint32_t v) {
 }
 
 // Kernel selection + launch for one device-resident batch.
+// True if the batch takes the strided-chain kernel (back-to-back 1, 2 or 4
+// KiB packets, 16-byte aligned), which applies any address family natively.
+bool sck_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride, uint64_t count,
+               uint32_t l3_offset, int n_cu) {
+  if (off || len || l3_offset != 0 || ((uintptr_t)base % 16) != 0 || getenv("RICRC_NO_SCK") != nullptr) return false;
+  if (stride != 1024 && stride != 2048 && stride != 4096) return false;
+  const uint64_t groups = (count + 7) / 8;
+  int sgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)n_cu, (groups + 15) / 16));
+  if (const char *e = getenv("RICRC_SCK_GRID")) sgrid = std::max(1, std::min(sgrid, atoi(e)));  // tests
+  const uint64_t waves = 16ull * (uint64_t)sgrid;
+  return (groups + waves - 1) / waves * 8ull * stride < (1ull << 31);  // each wave's span: a 31-bit buffer offset
+}
+
 int launch_batch_v4(Dev &d, const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
-                    uint64_t count, uint32_t l3_offset, uint32_t *out, hipStream_t st, bool verify) {
+                    uint64_t count, uint32_t l3_offset, uint32_t *out, hipStream_t st, bool verify,
+                    uint32_t family = kFamV4) {
   if (count == 0) return 0;
   const uint8_t *first = base + l3_offset;
   const uint32_t fixed_len = stride > l3_offset ? (uint32_t)std::min<uint64_t>(stride - l3_offset, 0xFFFFFFFFu) : 0u;
@@ -224,14 +238,13 @@ int launch_batch_v4(Dev &d, const uint8_t *base, const uint64_t *off, const uint
       const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)d.n_cu, want));
       // Back-to-back 1, 2 or 4 KiB packets: the strided-chain kernel (no LDS
       // transpose), as long as each wave's span fits a 31-bit buffer offset.
-      if (l3_offset == 0 && stride == fixed_len && (fixed_len == 1024 || fixed_len == 2048 || fixed_len == 4096) &&
-          ((uintptr_t)base % 16 == 0) && getenv("RICRC_NO_SCK") == nullptr) {
+      if (sck_batch(base, off, len, stride, count, l3_offset, d.n_cu)) {
         const uint64_t groups = (count + 7) / 8;
         int sgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)d.n_cu, (groups + 15) / 16));
         if (const char *e = getenv("RICRC_SCK_GRID")) sgrid = std::max(1, std::min(sgrid, atoi(e)));  // tests
-        const uint64_t waves = 16ull * (uint64_t)sgrid;
-        if ((groups + waves - 1) / waves * 8ull * fixed_len < (1ull << 31)) {
+        {
           SckArgs k{};
+          k.family = family;
           k.base = base;
           k.count = count;
           k.out = out;
@@ -342,6 +355,8 @@ int launch_batch(Dev &d, const uint8_t *base, const uint64_t *off, const uint32_
                  uint32_t family = kFamV4) {
   if (family == kFamV4 || count == 0)
     return launch_batch_v4(d, base, off, len, stride, count, l3_offset, out, st, verify);
+  if (sck_batch(base, off, len, stride, count, l3_offset, d.n_cu))  // masks native in the kernel
+    return launch_batch_v4(d, base, off, len, stride, count, l3_offset, out, st, verify, family);
   const int rc = launch_batch_v4(d, base, off, len, stride, count, l3_offset, out, st, false);
   if (rc) return rc;
   FamilyFixArgs f{};

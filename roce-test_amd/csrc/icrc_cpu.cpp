@@ -5,7 +5,9 @@
 // It restates calc_icrc() (p4/shuffle/shuffle_egress.p4:463-494) with a
 // slice-by-16 table fold; the 8 x 0xFF prefix (:465) is folded into the
 // starting register kSeed, the masked fields (:467-485) are applied to a
-// copy of the header, and everything after it (:489-490) is folded straight
+// copy of the header, and everything after it (the AETH of :489-490, and, as
+// IBTA Annex A17 generalises calc_icrc beyond the ACK it was written for,
+// extension headers and payload) is folded straight
 // from the caller's buffer.  The *_ex variants add RoCEv2 over IPv6 (masks of
 // IBTA Annex A17 / Linux rxe) and per-packet family detection.
 #include <errno.h>

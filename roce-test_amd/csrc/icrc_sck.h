@@ -19,6 +19,7 @@ struct SckArgs {
   uint32_t QS[8];    // x^(-32 (4 s + 1)): lane slot s's chain 0 -> packet end
   uint32_t *work;    // dynamic schedule: {group counter, finished waves}, zero between launches
   uint32_t dynamic;  // 1: groups from the counter (see icrc_sck_kernel), 0: static blocks
+  uint32_t family;   // kFamV4 / kFamV6 / kFamAuto: masks applied by the kernel itself
   uint64_t *stamps;  // diagnostic builds only (tools/microbench); null in the product
 };
 

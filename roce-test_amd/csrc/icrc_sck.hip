@@ -46,7 +46,10 @@ namespace ricrc {
 // VGPRs (frees registers for a deeper ring); XT: the Horner multiplies by
 // x^-32 through a conflict-free nibble table in LDS.
 // =======================================================================
-template <int L, int ABL, int D = 8, bool QLDS = false, bool DYN = false, bool XT = false>
+// FAM: the address family's invariant masks, applied natively on line 0
+// (kFamV4 = the reference's IPv4 masks; kFamV6; kFamAuto per packet from the
+// IP version nibble, broadcast from lane 8 g to the packet's 8 lanes).
+template <int L, int ABL, int D = 8, bool QLDS = false, bool DYN = false, bool XT = false, int FAM = kFamV4>
 __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
   // 128 KiB of tables + result slots per wave (+ DYN: the slots' group
   // indices; QLDS: the 8 lane bases; XT: 16 KiB nibble table of x^-32).
@@ -143,6 +146,10 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
   const uint32_t mw0 = s == 0 ? kMaskW0 : (s == 2 ? kMaskW8 : 0u);  // bytes 1 / 32
   const uint32_t xw0 = s == 0 ? kSeed : 0u;
   const uint32_t mw2 = s == 0 ? kMaskW2 : (s == 1 ? kMaskW6 : 0u);  // bytes 8, 10-11 / 26-27
+  // IPv6 (words 4s..4s+3 of line 0): bytes 0-3 / 7 (s = 0), 46-47 (s = 2), 52 (s = 3)
+  const uint32_t m6w0 = s == 0 ? kMaskV6W0 : 0u;
+  const uint32_t m6w1 = s == 0 ? kMaskV6W1 : (s == 3 ? kMaskV6W13 : 0u);
+  const uint32_t m6w3 = s == 2 ? kMaskV6W11 : 0u;
   const uint32_t keep3 = s == 7 ? 0u : 0xFFFFFFFFu;                  // the trailer word
   uint32_t Q[32];  // lane basis in registers (!QLDS)
   const uint32_t *qlds = lds + kLdsWords + kWaves * kWaveWords + s * kQStride;
@@ -260,8 +267,21 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
   for (; qcur < G; ++j) {  // qcur: wave-uniform
     u32x4 w = ring[0];
     ring[0] = load(D < L ? qcur : qnext, (uint32_t)(D % L));
-    w[0] = or_xor(w[0], mw0, xw0);
-    w[2] |= mw2;
+    if constexpr (FAM == kFamV4) {
+      w[0] = or_xor(w[0], mw0, xw0);
+      w[2] |= mw2;
+    } else if constexpr (FAM == kFamV6) {
+      w[0] = or_xor(w[0], m6w0, xw0);
+      w[1] |= m6w1;
+      w[3] |= m6w3;
+    } else {  // per packet: IP version nibble of lane 8 g's first byte (ds_swizzle: lane & 0x18)
+      const uint32_t b0 = (uint32_t)__builtin_amdgcn_ds_swizzle((int)w[0], 0x18);
+      const uint32_t v6 = ((b0 >> 4) & 15u) == 6u ? 0xFFFFFFFFu : 0u;
+      w[0] = or_xor(w[0], __builtin_amdgcn_bitop3_b32(v6, m6w0, mw0, 0xCA), xw0);
+      w[1] |= v6 & m6w1;
+      w[2] |= ~v6 & mw2;
+      w[3] |= v6 & m6w3;
+    }
     uint32_t x[4] = {w[0], w[1], w[2], w[3]};  // chain register (0) ^ line-0 word
     uint32_t tr = 0;
 #pragma unroll
@@ -340,19 +360,27 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
 }
 
 // ----------------------------------------------------------- host launcher
-hipError_t launch_sck(const SckArgs &a, int grid, hipStream_t st) {
+template <int FAM>
+hipError_t launch_sck_fam(const SckArgs &a, int grid, hipStream_t st) {
   const dim3 g(grid), b(kBlock);
   // XT (x^-32 nibble table): 0.735 -> 0.703 ms on 4 M x 1 KiB, ~1 % on 1 M x 4 KiB (tools/microbench/sck_abl.hip).
   if (a.dynamic) {
-    if (a.n == 4096) hipLaunchKernelGGL((icrc_sck_kernel<32, 0, 8, false, true, true>), g, b, 0, st, a);
-    else if (a.n == 2048) hipLaunchKernelGGL((icrc_sck_kernel<16, 0, 8, false, true, true>), g, b, 0, st, a);
-    else if (a.n == 1024) hipLaunchKernelGGL((icrc_sck_kernel<8, 0, 8, false, true, true>), g, b, 0, st, a);
+    if (a.n == 4096) hipLaunchKernelGGL((icrc_sck_kernel<32, 0, 8, false, true, true, FAM>), g, b, 0, st, a);
+    else if (a.n == 2048) hipLaunchKernelGGL((icrc_sck_kernel<16, 0, 8, false, true, true, FAM>), g, b, 0, st, a);
+    else if (a.n == 1024) hipLaunchKernelGGL((icrc_sck_kernel<8, 0, 8, false, true, true, FAM>), g, b, 0, st, a);
     else return hipErrorInvalidValue;
-  } else if (a.n == 4096) hipLaunchKernelGGL((icrc_sck_kernel<32, 0, 8, false, false, true>), g, b, 0, st, a);
-  else if (a.n == 2048) hipLaunchKernelGGL((icrc_sck_kernel<16, 0, 8, false, false, true>), g, b, 0, st, a);
-  else if (a.n == 1024) hipLaunchKernelGGL((icrc_sck_kernel<8, 0, 8, false, false, true>), g, b, 0, st, a);
+  } else if (a.n == 4096) hipLaunchKernelGGL((icrc_sck_kernel<32, 0, 8, false, false, true, FAM>), g, b, 0, st, a);
+  else if (a.n == 2048) hipLaunchKernelGGL((icrc_sck_kernel<16, 0, 8, false, false, true, FAM>), g, b, 0, st, a);
+  else if (a.n == 1024) hipLaunchKernelGGL((icrc_sck_kernel<8, 0, 8, false, false, true, FAM>), g, b, 0, st, a);
   else return hipErrorInvalidValue;
   return hipGetLastError();
+}
+
+hipError_t launch_sck(const SckArgs &a, int grid, hipStream_t st) {
+  if (a.family == kFamV6) return launch_sck_fam<kFamV6>(a, grid, st);
+  if (a.family == kFamAuto) return launch_sck_fam<kFamAuto>(a, grid, st);
+  if (a.family != kFamV4) return hipErrorInvalidValue;
+  return launch_sck_fam<kFamV4>(a, grid, st);
 }
 
 }  // namespace ricrc

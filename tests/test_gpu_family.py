@@ -136,3 +136,47 @@ def test_bad_family_flags(ctx):
     rc = roce_icrc.lib.ricrc_batch_device_ex(ctx.handle, 0, d.data_ptr(), None, None, 64, 1, 0,
                                              out.data_ptr(), None, 7)
     assert rc < 0
+
+
+@pytest.mark.parametrize("n", [1024, 2048, 4096])
+@pytest.mark.parametrize("family", ["v6", "auto"])
+@pytest.mark.parametrize("grid", [None, "1"])
+def test_sck_native_family_compute_and_verify(ctx, monkeypatch, n, family, grid):
+    """The strided-chain kernel applies the IPv6 / per-packet AUTO masks itself
+    (no fix-up pass): every lane slot's mask words, the version nibble
+    broadcast across a packet's 8 lanes, partial last groups, one workgroup
+    walking many groups (RICRC_SCK_GRID=1), verify mode with corruptions."""
+    if grid:
+        monkeypatch.setenv("RICRC_SCK_GRID", grid)
+    count = 8 * 16 * 5 + 3
+    rng = np.random.default_rng(SEED + n)
+    rows = _v6_rows(rng, count, n)
+    if family == "auto":
+        v4 = oracle_c.synth_batch(SEED, 0, count, n)
+        pick = rng.random(count) < 0.5
+        rows[pick] = v4[pick]
+    want = _want(rows, family, stride=n)
+    out = _out(count)
+    ctx.batch_device(_dev(rows), count, out, stride=n, family=family)
+    np.testing.assert_array_equal(_u32(out), want)
+    rows[:, n - 4:] = want.view(np.uint8).reshape(count, 4)
+    bad = np.arange(2, count, 7)
+    rows[bad, 40 + bad % (n - 48)] ^= 0x10
+    ok6 = np.flatnonzero((rows[:, 0] >> 4 == 6) & (np.arange(count) % 7 != 2))
+    rows[ok6, 1] ^= 0xA5   # flow label / traffic class: masked for IPv6
+    rows[ok6, 7] ^= 0x3C   # hop limit
+    rows[ok6, 52] ^= 0xFF  # BTH byte 4
+    ctx.batch_device(_dev(rows), count, out, stride=n, verify=True, family=family)
+    w = np.ones(count, np.uint32)
+    w[bad] = 0
+    np.testing.assert_array_equal(_u32(out), w)
+
+
+@pytest.mark.slow
+def test_headline_ipv6_native(ctx):
+    """1 M x 4096 B IPv6 packets through the native-mask SCK, bit-exact."""
+    count, n = 1 << 20, 4096
+    rows = _v6_rows(np.random.default_rng(SEED + 9), count, n)
+    out = _out(count)
+    ctx.batch_device(_dev(rows), count, out, stride=n, family="v6")
+    np.testing.assert_array_equal(_u32(out), oracle_c.icrc_batch(rows, stride=n, family="v6", threads=16))

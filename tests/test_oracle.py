@@ -105,3 +105,41 @@ def test_gf_helpers_against_bruteforce():
         r, n = rng.getrandbits(32), rng.randrange(0, 300)
         x8n = O.crc_shift(0x80000000, n)
         assert O.gf_mul(r, x8n) == O.crc_shift(r, n)
+
+
+def test_ack_matches_calc_icrc_field_list():
+    """For the packet calc_icrc() was written for -- the switch's write ACK,
+    IPv4 || UDP || BTH || AETH || ICRC (48 B, shuffle_ingress.p4:514-560) --
+    the oracle's "0xFF x 8 || masked L3[0, n-4)" hashes exactly the P4 field
+    list of shuffle_egress.p4:464-491, concatenated in order (network byte
+    order), through the CRC32 preset (= zlib.crc32).  Everything beyond that
+    shape is the deliberate IBTA generalisation (icrc_oracle.py header)."""
+    import struct
+    import zlib
+
+    rng = random.Random(17)
+    for _ in range(200):
+        f = dict(ver_ihl=0x45, diffserv=rng.getrandbits(8), total_len=48, ident=rng.getrandbits(16),
+                 flag_offset=rng.getrandbits(16), ttl=rng.getrandbits(8), proto=17, csum=rng.getrandbits(16),
+                 src=rng.getrandbits(32), dst=rng.getrandbits(32), sport=rng.getrandbits(16), dport=4791,
+                 ulen=28, ucsum=rng.getrandbits(16), opcode=0x11, se=rng.getrandbits(8), pkey=rng.getrandbits(16),
+                 fbr=rng.getrandbits(8), dqpn=rng.getrandbits(24), psn=rng.getrandbits(32),
+                 syndrome=rng.getrandbits(8), msn=rng.getrandbits(24))
+        l3 = (struct.pack(">BBHHHBBHII", f["ver_ihl"], f["diffserv"], f["total_len"], f["ident"], f["flag_offset"],
+                          f["ttl"], f["proto"], f["csum"], f["src"], f["dst"])
+              + struct.pack(">HHHH", f["sport"], f["dport"], f["ulen"], f["ucsum"])
+              + struct.pack(">BBHB", f["opcode"], f["se"], f["pkey"], f["fbr"]) + f["dqpn"].to_bytes(3, "big")
+              + struct.pack(">I", f["psn"]) + struct.pack(">B", f["syndrome"]) + f["msn"].to_bytes(3, "big")
+              + b"\0\0\0\0")
+        assert len(l3) == 48
+        fields = (b"\xff" * 8                                                      # :465
+                  + struct.pack(">B", f["ver_ihl"]) + b"\xff"                       # :466-467
+                  + struct.pack(">HHH", f["total_len"], f["ident"], f["flag_offset"])  # :468-470
+                  + b"\xff" + struct.pack(">B", f["proto"]) + b"\xff\xff"           # :471-473
+                  + struct.pack(">II", f["src"], f["dst"])                          # :474-475
+                  + struct.pack(">HHH", f["sport"], f["dport"], f["ulen"]) + b"\xff\xff"  # :477-480
+                  + struct.pack(">BBH", f["opcode"], f["se"], f["pkey"]) + b"\xff"  # :482-485
+                  + f["dqpn"].to_bytes(3, "big") + struct.pack(">I", f["psn"])     # :486-487
+                  + struct.pack(">B", f["syndrome"]) + f["msn"].to_bytes(3, "big"))  # :489-490
+        assert len(fields) == 52
+        assert O.icrc(l3) == zlib.crc32(fields)
