@@ -548,7 +548,8 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
 // a wave fold the same number of blocks Kmax (a multiple of 4: lanes with
 // shorter packets start with all-zero blocks), so the loop has no divergence
 // and no exec-masked memory op.  Block j needs the 16-byte native units N and
-// N + 16 (N = e - (e & 15) - 16 (Kmax - j)); loads are clamped to the units
+// N + 16 (N = e - (e & 15) - 16 (Kmax - j)), requested up to 17 at a time
+// before the fold (memory-level parallelism); loads are clamped to the units
 // that hold packet bytes (never another page) and whatever a clamped unit
 // holds is masked away by packet-relative offset.  A block's words come out
 // of the two units by a 2-level word funnel and v_alignbyte (phase e & 15).
@@ -563,6 +564,85 @@ __device__ __forceinline__ uint32_t small_word(uint32_t w, int r) {  // r = pack
   return (w & keep) | pre | (expand_nibble(bits) & keep);
 }
 
+// small_word for a word-aligned r (a multiple of 4): whole-word keep, the
+// 0xFF prefix word at -4, the IPv4 mask words of offsets 0, 8, 24, 32.
+__device__ __forceinline__ uint32_t small_word_aligned(uint32_t w, int r) {
+  const uint32_t keep = (uint32_t)(r >= 0) * 0xFFFFFFFFu;
+  const uint32_t orm = ((uint32_t)(r == -4) * 0xFFFFFFFFu) | ((uint32_t)(r == 0) * kMaskW0) |
+                       ((uint32_t)(r == 8) * kMaskW2) | ((uint32_t)(r == 24) * kMaskW6) |
+                       ((uint32_t)(r == 32) * kMaskW8);
+  return (w & keep) | orm;
+}
+
+// One packet's stream in icrc_rsmall_kernel.
+struct SmallPk {
+  uint64_t ufirst, ulast, N0;  // the packet's first / last 16-byte unit, native unit of block 0
+  uint32_t sb, m2, m1;         // end phase: byte shift, word-shift selects (all ones / zero)
+  int rel;                     // packet-relative offset of the next block
+  uint32_t reg;
+
+  __device__ __forceinline__ void init(const RsDesc &d, uint32_t Kmax) {
+    const uint64_t addr = ((uint64_t)(d.hi & 0xFFFFu) << 32) | d.lo;
+    const uint32_t M = (d.hi >> 16) - 4u;
+    const uint64_t e = addr + M;
+    const uint32_t t = (uint32_t)(e & 15u);
+    sb = t & 3u;
+    m2 = 0u - ((t >> 3) & 1u);
+    m1 = 0u - ((t >> 2) & 1u);
+    ufirst = addr & ~15ull;
+    ulast = (e - 1u) & ~15ull;
+    N0 = e - t - 16ull * Kmax;
+    rel = (int)M - 16 * (int)Kmax;
+    reg = 0u;
+  }
+  __device__ __forceinline__ u32x4 unit(uint32_t k) const {  // native unit k, clamped to the packet's
+    uint64_t u = N0 + 16ull * k;
+    u = u < ufirst ? ufirst : (u > ulast ? ulast : u);
+    return gload16(u);
+  }
+  // Blocks j0 .. j0 + KB - 1: all KB + 1 units they need are requested at
+  // once, then folded.  (A ring of 4-8 units in flight measured ~2x slower
+  // on C4's scattered small packets, tools/microbench/mb_scatter.hip: the
+  // memory-level parallelism of one lane is what these reads need.)
+  // WA: every packet of the wave starts and ends on a 4-byte word (the wave-
+  // uniform common case: C4, NIC rings): no byte shift, whole-word masks.
+  // MASK: which blocks get the head masks (prefix / invariant fields / bytes
+  // before the packet), branch-free: 1 = blocks 0..3 (the first chunk of a
+  // wave whose packets all start their heads there: M >= 16 Kmax - 24), 2 = all
+  // (lanes with shorter packets start later), 0 = none.  (A wave-uniform
+  // branch on "is some lane in its head" made the compiler wait for every
+  // outstanding load (vmcnt(0)) before each block: 2x slower.)
+  template <int KB, bool WA, int MASK>
+  __device__ __forceinline__ void chunk(const uint32_t *lds, const LaneTab &lt, uint32_t j0) {
+    u32x4 U[KB + 1];
+#pragma unroll
+    for (int k = 0; k <= KB; ++k) U[k] = unit(j0 + k);
+#pragma unroll
+    for (int j = 0; j < KB; ++j) {
+      // Block j's 4 words from units j, j + 1: X[k] = W[(t >> 2) + k] by
+      // bitwise selects (written as ternaries, the compiler turned the
+      // funnel into a dynamically indexed array in scratch), then
+      // v_alignbyte by the byte phase.
+      const u32x4 c = U[j], n = U[j + 1];
+      const uint32_t W[8] = {c[0], c[1], c[2], c[3], n[0], n[1], n[2], n[3]};
+      uint32_t V[6], X[5], w[4];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) V[k] = __builtin_amdgcn_bitop3_b32(m2, W[k + 2], W[k], 0xCA);
+#pragma unroll
+      for (int k = 0; k < 5; ++k) X[k] = __builtin_amdgcn_bitop3_b32(m1, V[k + 1], V[k], 0xCA);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) w[i] = WA ? X[i] : __builtin_amdgcn_alignbyte(X[i + 1], X[i], sb);
+      if (MASK == 2 || (MASK == 1 && j < 4)) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) w[i] = WA ? small_word_aligned(w[i], rel + 4 * i) : small_word(w[i], rel + 4 * i);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) reg = step4(lds, lt, reg, w[i]);
+      rel += 16;
+    }
+  }
+};
+
 __global__ __launch_bounds__(kBlock) void icrc_rsmall_kernel(RsckArgs a) {
   __shared__ uint32_t lds[kLdsWords];
   const uint32_t tab_v = table_entry(g_tab);
@@ -574,73 +654,44 @@ __global__ __launch_bounds__(kBlock) void icrc_rsmall_kernel(RsckArgs a) {
   const LaneTab lt{(lane & 31) << 2, ((lane & 31) << 2) | 0x10000u};
   const uint32_t step = gridDim.x * kWaves * 64u;
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.res, 4u * count);
-  constexpr int D = 4;  // units in the load ring (= the unroll)
   auto desc_at = [&](uint32_t pos) -> RsDesc { return a.desc[pos < count ? pos : (count ? count - 1u : 0u)]; };
   uint32_t base = (blockIdx.x * kWaves + wid) * 64u;
-  RsDesc dcur = desc_at(base + lane);
+  RsDesc dn = desc_at(base + lane);
   for (; base < count; base += step) {
     const uint32_t pos = base + lane;
-    const RsDesc d = dcur;
-    dcur = desc_at(pos + step);  // the next round's descriptor, in flight meanwhile
-    const uint64_t addr = ((uint64_t)(d.hi & 0xFFFFu) << 32) | d.lo;
-    const uint32_t M = (d.hi >> 16) - 4u;
-    const uint64_t e = addr + M;
-    uint32_t K = (M + 4u + 15u) >> 4;
+    const RsDesc d = dn;
+    dn = desc_at(pos + step);  // the next round's descriptor, in flight meanwhile
+    uint32_t K = (((d.hi >> 16) - 4u) + 4u + 15u) >> 4;  // this lane's blocks
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) K = max(K, (uint32_t)__shfl_xor((int)K, o));
-    const uint32_t Kmax = __builtin_amdgcn_readfirstlane((K + (D - 1)) & ~(uint32_t)(D - 1));
-    const uint32_t t = (uint32_t)(e & 15u), sb = t & 3u;
-    const uint32_t m2 = 0u - ((t >> 3) & 1u), m1 = 0u - ((t >> 2) & 1u);  // all-ones word-shift selects
-    const uint64_t ufirst = addr & ~15ull, ulast = (e - 1u) & ~15ull;
-    const uint64_t N0 = e - t - 16ull * Kmax;  // native unit of block 0
-    auto unit = [&](uint32_t k) -> u32x4 {     // native unit k (block k's first), clamped to the packet's
-      uint64_t u = N0 + 16ull * k;
-      u = u < ufirst ? ufirst : (u > ulast ? ulast : u);
-      return gload16(u);
-    };
-    // Block j folds units j and j + 1, held in a ring of D slots (unit k in
-    // slot k % D); after the fold the slot of unit j -- dead now -- is
-    // refilled with unit j + D, so the load lands in the registers it frees
-    // and the unrolled loop needs no register rotation (an earlier refill
-    // made the compiler rotate the ring with copies and drain vmcnt(0) at
-    // the back edge).  D - 1 units are in flight while a block folds.
-    u32x4 ring[D];
-#pragma unroll
-    for (int k = 0; k < D; ++k) {
-      __builtin_amdgcn_sched_barrier(0);
-      ring[k] = unit(k);
-    }
-    uint32_t reg = 0u;
-    int rel = (int)M - 16 * (int)Kmax;  // packet-relative offset of the next block
-    for (uint32_t j = 0; j < Kmax; j += D) {  // wave-uniform
-#pragma unroll
-      for (int u = 0; u < D; ++u) {
-        __builtin_amdgcn_sched_barrier(0);
-        const u32x4 c = ring[u], n = ring[(u + 1) % D];
-        // W = c0..c3 n0..n3; X[k] = W[(t >> 2) + k] by bitwise selects
-        // (written as ternaries, the compiler turned the funnel into a
-        // dynamically indexed array in scratch).
-        const uint32_t W[8] = {c[0], c[1], c[2], c[3], n[0], n[1], n[2], n[3]};
-        uint32_t V[6], X[5], w[4];
-#pragma unroll
-        for (int k = 0; k < 6; ++k) V[k] = __builtin_amdgcn_bitop3_b32(m2, W[k + 2], W[k], 0xCA);
-#pragma unroll
-        for (int k = 0; k < 5; ++k) X[k] = __builtin_amdgcn_bitop3_b32(m1, V[k + 1], V[k], 0xCA);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) w[i] = __builtin_amdgcn_alignbyte(X[i + 1], X[i], sb);
-        __builtin_amdgcn_sched_barrier(0);
-        ring[u] = unit(j + u + D);
-        __builtin_amdgcn_sched_barrier(0);
-        if (__builtin_amdgcn_ballot_w64(rel < 40) != 0) {  // wave-uniform: some lane is in its head
-#pragma unroll
-          for (int i = 0; i < 4; ++i) w[i] = small_word(w[i], rel + 4 * i);
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) reg = step4(lds, lt, reg, w[i]);
-        rel += 16;
+    const uint32_t Kmax = __builtin_amdgcn_readfirstlane((K + 3u) & ~3u);
+    SmallPk P;
+    P.init(d, Kmax);
+    // Kmax = 16 q + r (r a multiple of 4): one chunk of r blocks, then q of
+    // 16 (wave-uniform choices; at most 17 units = 68 VGPRs in flight).
+    // wave-uniform variants: word-aligned packets; every packet Kmax blocks long
+    const bool wa = __builtin_amdgcn_ballot_w64(((d.lo | (d.hi >> 16)) & 3u) != 0) == 0;
+    // heads in blocks 0..3: rel_4 = M - 16 Kmax + 64 >= 40 for every lane
+    const bool uk = __builtin_amdgcn_ballot_w64((d.hi >> 16) - 4u + 24u < 16u * Kmax) == 0;
+    auto run = [&](auto words, auto uniform) {
+      constexpr bool WA = decltype(words)::value;
+      constexpr int M1 = decltype(uniform)::value ? 1 : 2, M2 = decltype(uniform)::value ? 0 : 2;
+      uint32_t j = 0;
+      switch (Kmax & 15u) {
+        case 4: P.chunk<4, WA, M1>(lds, lt, 0); j = 4; break;
+        case 8: P.chunk<8, WA, M1>(lds, lt, 0); j = 8; break;
+        case 12: P.chunk<12, WA, M1>(lds, lt, 0); j = 12; break;
+        default: P.chunk<16, WA, M1>(lds, lt, 0); j = 16; break;
       }
-    }
-    __builtin_amdgcn_raw_buffer_store_b32(~reg, ro, pos < count ? 4u * pos : 0x7FFFFFF0u, 0, 0);
+      for (; j < Kmax; j += 16) P.chunk<16, WA, M2>(lds, lt, j);
+    };
+    if (wa && uk)
+      run(std::true_type{}, std::true_type{});
+    else if (uk)
+      run(std::false_type{}, std::true_type{});
+    else
+      run(std::false_type{}, std::false_type{});
+    __builtin_amdgcn_raw_buffer_store_b32(~P.reg, ro, pos < count ? 4u * pos : 0x7FFFFFF0u, 0, 0);
   }
 }
 

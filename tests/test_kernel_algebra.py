@@ -259,3 +259,31 @@ def test_small_lane_end_aligned_stream():
             rel += 16
             N += 16
         assert (~reg) & 0xFFFFFFFF == o.icrc(bytes(mem[addr:addr + n])), (addr, n, Kmax)
+
+
+def test_small_word_aligned_matches_bytewise():
+    """icrc_rsck.hip small_word_aligned (whole-word masks, word-aligned waves)
+    == small_word for every word-aligned packet-relative offset."""
+    W0, W2, W6, W8 = 0x0000FF00, 0xFFFF00FF, 0xFFFF0000, 0x000000FF  # icrc_math.h kMaskW*
+    rng = random.Random(8)
+    for r in range(-64, 80, 4):
+        for _ in range(20):
+            w = rng.getrandbits(32)
+            keep = 0xFFFFFFFF if r >= 0 else 0
+            orm = (0xFFFFFFFF if r == -4 else 0) | (W0 if r == 0 else 0) | (W2 if r == 8 else 0) \
+                | (W6 if r == 24 else 0) | (W8 if r == 32 else 0)
+            assert (w & keep) | orm == _small_word(w, r), r
+
+
+def test_small_lane_static_head_window():
+    """icrc_rsmall_kernel masks only blocks 0..3 when every lane of the wave has
+    M >= 16 Kmax - 24: then no byte at packet offset < 40 (prefix, invariant
+    fields) or before the packet lies in a block >= 4."""
+    for M in range(40, 400):
+        K = (M + 4 + 15) >> 4
+        for Kmax in range((K + 3) & ~3, ((K + 3) & ~3) + 12, 4):
+            if M + 24 < 16 * Kmax:
+                continue
+            rel4 = M - 16 * Kmax + 64
+            assert rel4 >= 40, (M, Kmax)
+            assert M - 16 * Kmax >= -24
