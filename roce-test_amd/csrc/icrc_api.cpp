@@ -32,6 +32,7 @@ namespace {
 constexpr uint64_t kStageBytes = 256ull << 20;  // per staging slot (bytes of packets)
 constexpr uint64_t kStagePkts = 1ull << 20;     // per staging slot (packets)
 constexpr uint32_t kWorkSlots = 64;
+constexpr size_t kMaxWorkspaces = 4;  // ragged-path workspaces per device (one per recent stream)
 
 struct Slot {
   uint8_t *d_buf = nullptr;
@@ -58,6 +59,18 @@ struct Dev {
   uint32_t work_next = 0;      // round-robin slot: launches in flight on different streams never share one
   Slot slot[2];
   bool staged = false;
+  // Ragged-path workspaces, one per stream that used this device (work on
+  // one stream is ordered, so its workspace is never shared by two calls in
+  // flight), grown on demand with the stream-ordered allocator; the class
+  // counters inside are zeroed on allocation and re-zeroed by the last pass
+  // of every call (rsck_gather), so a call costs no allocation and no memset.
+  struct Ws {
+    hipStream_t st;
+    void *p;
+    uint64_t bytes;
+    bool dirty;  // a call failed part-way: zero the counters before the next one
+  };
+  std::vector<Ws> ws;
 };
 
 int hip_err(hipError_t e) {
@@ -173,6 +186,9 @@ void free_dev(Dev &d) {
     (void)hipHostFree(s.h_buf), (void)hipHostFree(s.h_off), (void)hipHostFree(s.h_len), (void)hipHostFree(s.h_out);
     if (s.st) (void)hipStreamDestroy(s.st);
   }
+  if (!d.ws.empty()) (void)hipDeviceSynchronize();  // the workspaces' streams may be gone already
+  for (Dev::Ws &w : d.ws) (void)hipFree(w.p);
+  d.ws.clear();
   (void)hipFree(d.d_inv);
   (void)hipFree(d.d_inv4);
   (void)hipFree(d.d_tzb);
@@ -185,6 +201,37 @@ int ilog2_ceil(uint32_t v) {
   int l = 0;
   while ((1u << l) < v) ++l;
   return l;
+}
+
+// The ragged-path workspace of stream st on device d, at least `bytes`.
+int ragged_ws(Dev &d, hipStream_t st, uint64_t bytes, Dev::Ws **out) {
+  Dev::Ws *w = nullptr;
+  for (Dev::Ws &x : d.ws)
+    if (x.st == st) w = &x;
+  if (!w) {
+    if (d.ws.size() >= kMaxWorkspaces) {  // bound the pool: drop the oldest (its stream may be gone)
+      HIP_TRY(hipDeviceSynchronize());
+      (void)hipFree(d.ws.front().p);
+      d.ws.erase(d.ws.begin());
+    }
+    d.ws.push_back(Dev::Ws{st, nullptr, 0, true});
+    w = &d.ws.back();
+  }
+  if (w->bytes < bytes) {
+    if (w->p) HIP_TRY(hipFreeAsync(w->p, st));
+    w->p = nullptr;
+    w->bytes = 0;
+    const uint64_t grow = std::max<uint64_t>(bytes, bytes + bytes / 4);
+    HIP_TRY(hipMallocAsync(&w->p, grow, st));
+    w->bytes = grow;
+    w->dirty = true;
+  }
+  if (w->dirty) {
+    HIP_TRY(rs_zero_counters(w->p, st));
+    w->dirty = false;
+  }
+  *out = w;
+  return 0;
 }
 
 // Kernel selection + launch for one device-resident batch.
@@ -309,14 +356,15 @@ int launch_batch_v4(Dev &d, const uint8_t *base, const uint64_t *off, const uint
     small.inv_tab = d.d_inv;
     small.inv4 = reinterpret_cast<const u32x4_t *>(d.d_inv4);
     for (uint32_t l = 0; l < 64; ++l) small.K[l] = x8n_host(64ull * (63 - l));
-    void *ws = nullptr;
-    HIP_TRY(hipMallocAsync(&ws, rs_workspace_bytes(count), st));
-    rs_bind_workspace(k, ws);
+    Dev::Ws *ws = nullptr;
+    const int wrc = ragged_ws(d, st, rs_workspace_bytes(count), &ws);
+    if (wrc) return wrc;
+    rs_bind_workspace(k, ws->p);
     int rgrid = d.n_cu;
     if (const char *e = getenv("RICRC_RSCK_GRID")) rgrid = std::max(1, std::min(rgrid, atoi(e)));  // tests
     const hipError_t e = launch_rsck(k, small, rgrid, st);
-    const hipError_t e2 = hipFreeAsync(ws, st);
-    return hip_err(e != hipSuccess ? e : e2);
+    if (e != hipSuccess) ws->dirty = true;
+    return hip_err(e);
   }
   // The piece-based ragged kernel.  Pieces from a device-side scan of the
   // descriptors, or arithmetic when every packet has the same length and

@@ -131,6 +131,9 @@ struct RsckArgs {
 uint64_t rs_workspace_bytes(uint64_t count);
 // Carves the workspace (rs_workspace_bytes(count) bytes at ws) into a.
 void rs_bind_workspace(RsckArgs &a, void *ws);
+// Zeroes a workspace's class counters (on allocation; afterwards every call
+// leaves them zero).
+hipError_t rs_zero_counters(void *ws, hipStream_t st);
 // The whole ragged pipeline on `st`: count/classify, plan, scatter, fold, gather.
 // `small` carries the piece kernel's tables (inv_tab, inv4, K) for the small packets.
 hipError_t launch_rsck(RsckArgs &a, const RaggedArgs &small, int grid, hipStream_t st);

@@ -236,6 +236,10 @@ __global__ __launch_bounds__(kPassBlock) void rsck_scatter(RsckArgs a) {
 }
 
 __global__ __launch_bounds__(256) void rsck_gather(RsckArgs a) {
+  // The class counters are dead now (plan, scatter and both folds have read
+  // them): zero them for the next call on this workspace.
+  if (blockIdx.x == 0)
+    for (uint32_t t = threadIdx.x; t <= (uint32_t)kRsClasses; t += blockDim.x) a.counts[t] = 0u;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.count;
        i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t p = a.pos_of[i];
@@ -702,6 +706,10 @@ uint64_t rs_workspace_bytes(uint64_t count) {
          al(4ull * kRsClasses * kPassBlocks) + al(8 * (npos + 1)) + al(4);
 }
 
+hipError_t rs_zero_counters(void *ws, hipStream_t st) {  // counts is the workspace's first region
+  return hipMemsetAsync(ws, 0, 4ull * (kRsClasses + 1), st);
+}
+
 void rs_bind_workspace(RsckArgs &a, void *ws) {
   const uint64_t npos = a.count + 8ull * kRsClasses;
   auto al = [](uint64_t b) { return (b + 255) & ~255ull; };
@@ -720,8 +728,9 @@ void rs_bind_workspace(RsckArgs &a, void *ws) {
 
 hipError_t launch_rsck(RsckArgs &a, const RaggedArgs &small, int grid, hipStream_t st) {
   if (a.count == 0) return hipSuccess;
-  hipError_t e = hipMemsetAsync(a.counts, 0, 4ull * (kRsClasses + 1), st);  // + the misaligned flag
-  if (e != hipSuccess) return e;
+  // a.counts (+ the misaligned flag) is zero here: zeroed when the workspace
+  // was allocated, and again by rsck_gather at the end of every call.
+  hipError_t e = hipSuccess;
   const uint64_t want = (a.count + kPassBlock - 1) / kPassBlock;
   const int pgrid = (int)(want < kPassBlocks ? want : kPassBlocks);
   hipLaunchKernelGGL(rsck_count, dim3(pgrid), dim3(kPassBlock), 0, st, a);

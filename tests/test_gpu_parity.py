@@ -419,3 +419,27 @@ def test_strided_chain_dynamic_schedule(ctx, monkeypatch):
             out = _out(count)
             ctx.batch_device(d, count, out, stride=n, stream=_stream())
             np.testing.assert_array_equal(_host_u32(out), want)
+
+
+def test_ragged_workspace_reuse_across_sizes_and_streams(ctx):
+    """The ragged path's context-owned workspaces (one per stream, grown on
+    demand, class counters re-zeroed by the last pass of every call): calls of
+    growing and shrinking sizes on one stream, then interleaved on two more
+    streams, all bit-exact."""
+    rng = np.random.default_rng(77)
+    cases = []
+    for count in (500, 20000, 3, 70000, 1000):
+        lens = rng.choice([64, 256, 1024, 4096, 61, 333], count).astype(np.uint32)
+        offs = np.zeros(count, np.uint64)
+        offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + 3)
+        buf = rng.integers(0, 256, int(offs[-1]) + int(lens[-1]) + 16, dtype=np.uint8)
+        cases.append((buf, offs, lens, oracle_c.icrc_batch(buf, offsets=offs, lengths=lens, threads=8)))
+    streams = [torch.cuda.current_stream(), torch.cuda.Stream(), torch.cuda.Stream()]
+    for rep in range(2):
+        for k, (buf, offs, lens, want) in enumerate(cases):
+            st = streams[0] if rep == 0 else streams[k % 3]
+            out = _out(len(lens))
+            with torch.cuda.stream(st):
+                ctx.batch_device(_dev(buf), len(lens), out, offsets=_dev(offs), lengths=_dev(lens), stream=st)
+            st.synchronize()
+            np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), want)
