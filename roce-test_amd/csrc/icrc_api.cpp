@@ -55,7 +55,7 @@ struct Dev {
   uint32_t *d_inv4 = nullptr;  // t: x^(8 (k - t)), k = 0..3, t <= 4096
   uint32_t *d_tzb = nullptr;   // [128][8]: basis words 4q of x^(-8 tz) (ragged strided-chain path)
   uint32_t *d_x8n = nullptr;   // x^(8 k), k < 65536 (incremental repair)
-  uint32_t *d_work = nullptr;  // kWorkSlots x {group counter, finished waves} (dynamic SCK schedule)
+  uint32_t *d_work = nullptr;  // kWorkSlots x kSckWorkWords counters (dynamic SCK schedule)
   uint32_t work_next = 0;      // round-robin slot: launches in flight on different streams never share one
   Slot slot[2];
   bool staged = false;
@@ -154,8 +154,8 @@ int init_dev(Dev &d) {
   }
   HIP_TRY(hipMalloc(&d.d_x8n, x8n.size() * sizeof(uint32_t)));
   HIP_TRY(hipMemcpy(d.d_x8n, x8n.data(), x8n.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-  HIP_TRY(hipMalloc(&d.d_work, kWorkSlots * 2 * sizeof(uint32_t)));
-  HIP_TRY(hipMemset(d.d_work, 0, kWorkSlots * 2 * sizeof(uint32_t)));
+  HIP_TRY(hipMalloc(&d.d_work, kWorkSlots * kSckWorkWords * sizeof(uint32_t)));
+  HIP_TRY(hipMemset(d.d_work, 0, kWorkSlots * kSckWorkWords * sizeof(uint32_t)));
   return 0;
 }
 
@@ -304,7 +304,7 @@ int launch_batch_v4(Dev &d, const uint8_t *base, const uint64_t *off, const uint
           // kernels (RCCL) hold CUs while this one starts.  RICRC_SCK_STATIC=1:
           // contiguous per-wave blocks.
           k.dynamic = getenv("RICRC_SCK_DYNAMIC") != nullptr ? 1u : 0u;
-          k.work = d.d_work + 2 * (d.work_next++ % kWorkSlots);
+          k.work = d.d_work + kSckWorkWords * (d.work_next++ % kWorkSlots);
           return hip_err(launch_sck(k, sgrid, st));
         }
       }

@@ -41,7 +41,8 @@ namespace ricrc {
 // groups and the block leaves in one coalesced 64-dword store.
 //
 // ABL (timing-only ablations for tools/microbench; the product uses 0):
-// 1 no table fold, 2 no finish, 8 no global loads, 16 no stores.
+// 1 no table fold, 2 no finish, 8 no global loads, 16 no stores, 64 per-wave
+// start/end s_memrealtime stamps into a.stamps.
 // D: lines in flight per wave; QLDS: lane bases read from LDS instead of 32
 // VGPRs (frees registers for a deeper ring); XT: the Horner multiplies by
 // x^-32 through a conflict-free nibble table in LDS.
@@ -74,34 +75,59 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
   const uint32_t vo = (lane >> 3) * N + 16u * s;
 
   // The wave's sequence of groups.  Static: the contiguous block [g0, g1).
-  // DYN: groups taken one at a time from a device counter (a.work[0]) with
-  // two grabs in flight, so a workgroup that starts late -- its CU held by
-  // RCCL's all-gather of the previous step -- simply takes fewer groups; the
-  // last wave to finish resets the counter for the next launch.  A buffer
-  // atomic whose other 63 lanes fall outside the range-checked record keeps
-  // the grab free of exec masking.
-  const __amdgpu_buffer_rsrc_t wrs = make_rsrc(a.work, 8u);
-  // grab(): the raw per-lane result (lane 0 holds the value); it is made
-  // wave-uniform only one group later, when it is needed -- reading it at
-  // once would drain vmcnt(0) at every group end.
-  auto grab = [&]() -> uint32_t {
-    return (uint32_t)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, wrs, lane == 0 ? 0u : 0x7FFFFFF0u, 0, 0);
+  // DYN (hybrid): the first 7/8 of the groups in static blocks, the last 1/8
+  // a pool handed out one group at a time by per-XCD device counters -- XCD
+  // x (workgroup w runs on XCD w % 8) owns pool groups [base_x, base_x +
+  // size_x), its counter work[x * kSckCtrStride] hands them out, and a wave
+  // whose XCD's share is used up steals from the next XCD's counter.  Why
+  // (tools/microbench/sck_tail.hip, profiles/r02/sck_tail.txt): with static
+  // blocks, waves with equal work finish between 0.46x and 1.0x of the
+  // launch, the odd XCDs ~9 % after the even ones; a fully dynamic schedule
+  // balanced them but ran slower (one counter serves ~74 M grabs/s, and every
+  // wave waited for its first grab), so only the tail is dynamic.  The pool
+  // grab runs one group ahead (made wave-uniform only one group later:
+  // reading it at once would drain vmcnt(0)).  The last wave to finish
+  // resets the counters for the next launch.  Buffer atomics whose other 63
+  // lanes fall outside the range-checked record keep the grab free of exec
+  // masking.
+  const __amdgpu_buffer_rsrc_t wrs = make_rsrc(a.work, 4u * kSckWorkWords);
+  auto grab = [&](uint32_t x) -> uint32_t {  // raw per-lane result (lane 0 holds it)
+    return (uint32_t)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(
+        1, wrs, lane == 0 ? 4u * kSckCtrStride * x : 0x7FFFFFF0u, 0, 0);
   };
   auto uni = [](uint32_t v) -> uint32_t { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
   uint32_t g0 = 0, g1 = 0, qcur, qnext, qpend = 0;
-  if (DYN) {
-    qcur = grab();
-    qnext = grab();
-    qpend = grab();
-    qcur = uni(qcur);
-    qnext = uni(qnext);
-  } else {
-    const uint64_t per = (G + nwaves - 1) / nwaves;
+  {
+    const uint64_t per = DYN ? (uint64_t)(G - G / 8) / nwaves : (G + nwaves - 1) / nwaves;
     g0 = (uint32_t)(wave * per < G ? wave * per : G);
     g1 = (uint32_t)(g0 + per < G ? g0 + per : G);
-    qcur = g0 < g1 ? g0 : G;
-    qnext = g0 + 1 < g1 ? g0 + 1 : G;
   }
+  const uint32_t pool0 = DYN ? (uint32_t)(nwaves * ((uint64_t)(G - G / 8) / nwaves)) : G;
+  const uint32_t Pq = (G - pool0) >> 3, Pr = (G - pool0) & 7u;
+  auto pbase = [&](uint32_t x) -> uint32_t { return pool0 + x * Pq + (x < Pr ? x : Pr); };
+  auto psize = [&](uint32_t x) -> uint32_t { return Pq + (x < Pr ? 1u : 0u); };
+  uint32_t xs = blockIdx.x & 7u, xtries = 0;  // pool partition being drawn from; partitions found empty
+  // Pool group for a grab result v of partition xs; steals (synchronously:
+  // only at the very end) while xs is used up; G once every partition is.
+  auto take_group = [&](uint32_t v) -> uint32_t {
+    while (v >= psize(xs)) {  // wave-uniform
+      if (++xtries >= 8) return G;
+      xs = (xs + 1) & 7u;
+      v = uni(grab(xs));
+    }
+    return pbase(xs) + v;
+  };
+  // The group after q in this wave's sequence.
+  auto after = [&](uint32_t q) -> uint32_t {
+    if (q + 1 < g1) return q + 1;  // static block (pool groups are >= g1)
+    if (!DYN || xtries >= 8) return G;
+    const uint32_t r = take_group(uni(qpend));
+    if (xtries < 8) qpend = grab(xs);
+    return r;
+  };
+  if (DYN) qpend = grab(xs);
+  qcur = g0 < g1 ? g0 : after(G);
+  qnext = qcur < G ? after(qcur) : G;
 
   // Line `line` of absolute group q (q >= G: no group, the range check reads zeros).
   auto load = [&](uint32_t q, uint32_t line) -> u32x4 {
@@ -113,6 +139,7 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
   };
   // The first D lines are in flight while the workgroup builds its tables
   // (the table load is issued first, so waiting for it leaves them in flight).
+  const uint64_t t_start = (ABL & 64) ? __builtin_amdgcn_s_memrealtime() : 0u;
   const uint32_t tab_v = table_entry(g_tab128);
   u32x4 ring[D];
 #pragma unroll
@@ -330,12 +357,7 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
     pf.tr = tr;
     qprev = qcur;
     qcur = qnext;  // advance the group sequence (wave-uniform)
-    if (DYN) {
-      qnext = uni(qpend);
-      qpend = grab();
-    } else {
-      qnext = qnext + 1 < g1 ? qnext + 1 : G;
-    }
+    qnext = qcur < G ? after(qcur) : G;
   }
   if (j > 0) {
     __builtin_amdgcn_sched_barrier(0);
@@ -345,18 +367,23 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
     flush(j);
   }
   if (ABL & 16) a.out[wave * 64 + lane] = sink;
+  if ((ABL & 64) && lane == 0) {  // diagnostic builds (tools/microbench/sck_tail.hip): start / end times
+    a.stamps[2 * wave] = t_start;
+    a.stamps[2 * wave + 1] = __builtin_amdgcn_s_memrealtime();
+  }
   if (DYN) {
     // All of this wave's grabs have returned before it checks in, so when the
-    // last wave checks in nobody touches the counter any more: reset it.
-    const __amdgpu_buffer_rsrc_t drs = make_rsrc(a.work, 8u);
-    const uint32_t mine = lane == 0 ? 4u : 0x7FFFFFF0u;
+    // last wave checks in nobody touches the counters any more: reset them.
+    const uint32_t done_off = 4u * kSckCtrStride * 8u;
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): every grab of this wave has returned
-    const uint32_t seen = (uint32_t)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, drs, mine, 0, 0);
+    const uint32_t seen = (uint32_t)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(
+        1, wrs, lane == 0 ? done_off : 0x7FFFFFF0u, 0, 0);
     if (__builtin_amdgcn_readfirstlane((int)seen) == (int)(nwaves - 1)) {
-      __builtin_amdgcn_raw_buffer_store_b32(0u, drs, lane == 0 ? 0u : 0x7FFFFFF0u, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b32(0u, drs, mine, 0, 0);
+      // lanes 0..7: the XCD counters, lane 8: the check-in counter
+      __builtin_amdgcn_raw_buffer_store_b32(0u, wrs, lane <= 8u ? 4u * kSckCtrStride * lane : 0x7FFFFFF0u, 0, 0);
     }
   }
+
 }
 
 // ----------------------------------------------------------- host launcher
