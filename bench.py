@@ -77,6 +77,8 @@ def parse(argv=None):
     ap.add_argument("--prime-ms", type=float, default=25.0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="wall budget of the CPU baseline")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--plan-only", action="store_true",
+                    help="print the shard plan every rank would run (gloo, no GPU) and exit")
     a = ap.parse_args(argv)
     if a.count is None:
         a.count = (4 << 20) if a.mix else (1 << 20)
@@ -277,19 +279,31 @@ def c0_latency():
             "us_per_packet_ctypes_call": round(dt1 / m * 1e6, 3)}
 
 
+def shard_plan(args, world):
+    """The global batch and its per-rank cuts (no GPU): (T, cuts, lens_global).
+    Fixed size: shard_range of T packets; --mix: one global length vector
+    (PCG64 on the seed) cut at equal bytes."""
+    import numpy as np
+
+    from roce_icrc.dist import byte_balanced_cuts, shard_range
+
+    T = args.global_count if args.global_count is not None else args.count * world
+    if args.mix:
+        lens_g = np.random.default_rng(args.seed).choice(np.array(MIX_SIZES, np.uint32), size=T)
+        return T, byte_balanced_cuts(lens_g, world), lens_g
+    return T, [shard_range(T, world, r)[0] for r in range(world)] + [T], None
+
+
 def build_batch(torch, np, ctx, dev, stream, args, world, rank):
     """This rank's shard of the global batch, generated on `dev`.  Returns a
     dict: buf, d_offs, d_lens, h_offs, h_lens (ragged), cuts, sizes,
     lens_global (ragged), rank_bytes."""
-    from roce_icrc.dist import byte_balanced_cuts, cuts_to_sizes, shard_range
+    from roce_icrc.dist import cuts_to_sizes
 
-    T = args.global_count if args.global_count is not None else args.count * world
+    T, cuts, lens_g = shard_plan(args, world)
+    lo, hi = cuts[rank], cuts[rank + 1]
     b = {}
     if args.mix:
-        rng = np.random.default_rng(args.seed)
-        lens_g = rng.choice(np.array(MIX_SIZES, np.uint32), size=T)
-        cuts = byte_balanced_cuts(lens_g, world)
-        lo, hi = cuts[rank], cuts[rank + 1]
         lens = np.ascontiguousarray(lens_g[lo:hi])
         offs = np.zeros(len(lens), np.uint64)
         if len(lens) > 1:
@@ -302,13 +316,44 @@ def build_batch(torch, np, ctx, dev, stream, args, world, rank):
         b.update(buf=buf, d_offs=d_offs, d_lens=d_lens, h_offs=offs, h_lens=lens, lens_global=lens_g,
                  rank_bytes=nbytes)
     else:
-        cuts = [shard_range(T, world, r)[0] for r in range(world)] + [T]
-        lo, hi = cuts[rank], cuts[rank + 1]
         buf = torch.empty(max((hi - lo) * args.size, 1), dtype=torch.uint8, device=dev)
         ctx.synth_device(buf, args.seed, lo, hi - lo, args.size, stream=stream)
         b.update(buf=buf, d_offs=None, d_lens=None, lens_global=None, rank_bytes=(hi - lo) * args.size)
     b.update(cuts=cuts, sizes=cuts_to_sizes(cuts), T=T)
     return b
+
+
+def plan_only(args, world, rank):
+    """--plan-only: every rank computes the shard plan it would run, the ranks
+    check over gloo (CPU, no GPU touched) that they agree, and rank 0 prints it
+    as one JSON line -- the launcher / rendezvous / sharding exercised without
+    a GPU."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from roce_icrc.dist import cuts_to_sizes
+
+    T, cuts, lens_g = shard_plan(args, world)
+    sizes = cuts_to_sizes(cuts)
+    lo, hi = cuts[rank], cuts[rank + 1]
+    mine = int(lens_g[lo:hi].sum(dtype=np.uint64)) if lens_g is not None else (hi - lo) * args.size
+    if world > 1:
+        dist.init_process_group("gloo")
+        got = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(got, torch.tensor([hi - lo, mine], dtype=torch.int64))
+        counts = [int(g[0]) for g in got]
+        nbytes = [int(g[1]) for g in got]
+        dist.destroy_process_group()
+        if counts != sizes:
+            raise SystemExit(f"bench: rank {rank}: ranks disagree on the shard plan {counts} != {sizes}")
+    else:
+        nbytes = [mine]
+    if rank == 0:
+        print(json.dumps({"plan_only": True, "n_gpus": world, "packets_total": T, "shard_packets": sizes,
+                          "shard_bytes": nbytes, "scaling": "strong" if args.global_count is not None else "weak",
+                          "workload": "mix" if args.mix else f"{args.size} B"}), flush=True)
+    return 0
 
 
 def relaunch(args, argv):
@@ -330,6 +375,8 @@ def main(argv=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.plan_only:
+        return plan_only(args, world, rank)
 
     import numpy as np
     import torch

@@ -133,3 +133,24 @@ def test_traffic_is_tied_to_the_kernel_source(tmp_path):
 
 def test_bench_compiles_standalone():
     subprocess.check_call([sys.executable, "-m", "py_compile", os.path.join(ROOT, "bench.py")])
+
+
+def test_gpus_2_relaunch_end_to_end_plan_only():
+    """The real re-launch: `bench.py --gpus 2` outside torchrun starts 2 ranks
+    through torch.distributed.run (rendezvous on 127.0.0.1), the ranks agree
+    over gloo on the shard plan -- byte-balanced unequal shards for --mix,
+    shard_range for --global-count -- and rank 0 prints one JSON line."""
+    def run(*args):
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--plan-only", *args],
+                           capture_output=True, text=True, timeout=300,
+                           env={k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")})
+        assert r.returncode == 0, r.stderr[-2000:]
+        lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        assert len(lines) == 1, r.stdout
+        return json.loads(lines[0])
+
+    d = run("--mix", "--count", "5000")
+    assert d["n_gpus"] == 2 and d["packets_total"] == 10000 and sum(d["shard_packets"]) == 10000
+    assert d["scaling"] == "weak" and abs(d["shard_bytes"][0] - d["shard_bytes"][1]) <= 4096
+    d = run("--global-count", "4194304")
+    assert d["scaling"] == "strong" and d["shard_packets"] == [2097152, 2097152]
