@@ -151,6 +151,6 @@ def test_gpus_2_relaunch_end_to_end_plan_only():
 
     d = run("--mix", "--count", "5000")
     assert d["n_gpus"] == 2 and d["packets_total"] == 10000 and sum(d["shard_packets"]) == 10000
-    assert d["scaling"] == "weak" and abs(d["shard_bytes"][0] - d["shard_bytes"][1]) <= 4096
+    assert d["scaling"] == "weak" and abs(d["shard_bytes"][0] - d["shard_bytes"][1]) <= 2 * 4096
     d = run("--global-count", "4194304")
     assert d["scaling"] == "strong" and d["shard_packets"] == [2097152, 2097152]
