@@ -131,6 +131,20 @@ def test_traffic_is_tied_to_the_kernel_source(tmp_path):
     assert (got is not None) == (d.get("kernel_src") == h)
 
 
+def test_committed_traffic_matches_headline_kernel():
+    """The committed PMC pass is of the headline config (1 M x 4 KiB) and of
+    the SCK source at HEAD, so the default bench line carries a non-null
+    roofline.traffic. An SCK edit fails this until tools/pmc_traffic.py is
+    re-run on the GPU and profiles/pmc_traffic.json refreshed."""
+    a = bench.parse([])
+    with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
+        d = json.load(f)
+    assert (d["size"], d["count"]) == (a.size, 1 << 20)
+    assert d["kernel_src"] == bench.kernel_source_hash()
+    assert 0.99 < d["traffic_over_algorithmic"] < 1.05
+    assert bench.load_traffic(a.size, 1 << 20) == d["hbm_bytes_per_launch"]
+
+
 def test_bench_compiles_standalone():
     subprocess.check_call([sys.executable, "-m", "py_compile", os.path.join(ROOT, "bench.py")])
 
