@@ -91,7 +91,10 @@ __host__ __device__ inline uint32_t ragged_pieces(uintptr_t start, uint32_t n) {
 // 1 + P for packets spanning <= kRsSmallL lines, by their 64-byte piece count P
 // (they go to the piece kernel: 8 lanes per packet is too coarse for them);
 // kRsBigBase + L for the rest, by line count L (the strided-chain fold).
-constexpr int kRsSmallL = 3;
+#ifndef RICRC_RS_SMALL_L  // tools/microbench only
+#define RICRC_RS_SMALL_L 1
+#endif
+constexpr int kRsSmallL = RICRC_RS_SMALL_L;
 constexpr int kRsBigBase = 8;                  // small classes 2..8 (P <= 7 for L <= 3)
 constexpr int kRsClasses = kRsBigBase + 514;   // L <= 513 (n <= 65535, any start offset)
 struct RsPlan {

@@ -283,7 +283,9 @@ __device__ __forceinline__ uint32_t edge_word_aligned(uint32_t w, int rel, int M
 
 }  // namespace
 
-// ABL (timing-only ablations, tools/microbench): 1 no table fold, 2 no finish.
+// ABL (timing-only ablations, tools/microbench/rsck_abl.hip): 1 no table
+// fold, 2 no finish, 4 descriptors by arithmetic (uniform batch in natural
+// order: packet 8 q + g at base + (8 q + g) stride, no descriptor ring).
 template <int ABL>
 __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   constexpr uint32_t kSlots = 64, kRound = kSlots / 8;   // result slots per wave, groups per round
@@ -291,10 +293,12 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   constexpr uint32_t kBlk = 128;                          // words per descriptor block (8 groups x 8 x 8 B)
   constexpr uint32_t kWaveWords = kSlots + 2 * kBlk + 64;  // slots | 2-block ring | 8-group info FIFO
   constexpr int D = 8;                                    // lines in flight per wave
-  // 128 KiB tables | 4 KiB tz bases | 8 lane bases | 1.5 KiB per wave = 157 KiB
-  __shared__ uint32_t lds[kLdsWords + 128 * 8 + 8 * kQStride + kWaves * kWaveWords];
+  // 128 KiB tables | 4 KiB tz bases | 8 lane bases | 1.5 KiB per wave |
+  // 512 B x^-32 nibble table = 157.6 KiB
+  __shared__ uint32_t lds[kLdsWords + 128 * 8 + 8 * kQStride + kWaves * kWaveWords + 128];
   uint32_t *tzl = lds + kLdsWords;
   uint32_t *qsl = tzl + 128 * 8;
+  uint32_t *xtl = qsl + 8 * kQStride + kWaves * kWaveWords;
 
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -311,6 +315,13 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
     for (int k = 1; k < 8; ++k) v = bs == (uint32_t)k ? a.QS[k] : v;
     for (uint32_t t = j; t < 31; ++t) v = gf_mulx(v);
     qsl[bs * kQStride + j] = v;
+  }
+  if (threadIdx.x < 128) {  // entry 16 w + v: (nibble v at bits 4w..4w+3) * x^-32
+    const uint32_t w = threadIdx.x >> 4, v = threadIdx.x & 15u;
+    uint32_t t = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) t ^= ((v >> b) & 1u) ? a.XB[4 * w + b] : 0u;
+    xtl[threadIdx.x] = t;
   }
   __syncthreads();
 
@@ -365,8 +376,8 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   auto put_block = [&](uint32_t b, const u32x2 &v) {
     *reinterpret_cast<u32x2 *>(dring + (b & 1u) * kBlk + 2u * lane) = v;
   };
-  u32x2 NB;
-  {
+  u32x2 NB = {0u, 0u};
+  if (!(ABL & 4)) {
     const uint32_t b = q_begin >> 3;
     put_block(b, load_block(b));
     put_block(b + 1, load_block(b + 1));
@@ -379,9 +390,17 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   };
   // Load cursor enters group q: line base, L, and (a, M) into the FIFO.
   auto ld_enter = [&](uint32_t q, LInfo &li) -> uint32_t {
-    const u32x2 d = *reinterpret_cast<const u32x2 *>(dring + ((q >> 3) & 1u) * kBlk + 2u * (8u * (q & 7u) + g));
-    const uint64_t addr = ((uint64_t)(d[1] & 0xFFFFu) << 32) | d[0];
-    const uint32_t ga = d[0] & 127u, gM = (d[1] >> 16) - 4u;
+    uint64_t addr;
+    uint32_t gM;
+    if (ABL & 4) {
+      addr = (uint64_t)(uintptr_t)a.base + (8ull * q + g) * a.stride;
+      gM = a.fixed_len - 4u;
+    } else {
+      const u32x2 d = *reinterpret_cast<const u32x2 *>(dring + ((q >> 3) & 1u) * kBlk + 2u * (8u * (q & 7u) + g));
+      addr = ((uint64_t)(d[1] & 0xFFFFu) << 32) | d[0];
+      gM = (d[1] >> 16) - 4u;
+    }
+    const uint32_t ga = (uint32_t)addr & 127u;
     li.line0 = (addr & ~127ull) + 16u * s;
     fifo[((q & 7u) << 3) | g] = (gM << 7) | ga;
     return __builtin_amdgcn_readfirstlane((ga + gM + 127u) >> 7);  // equal within a group
@@ -404,7 +423,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
       ld_k = 0;
       if (ld_q + 1 < q_end) {
         ++ld_q;
-        if ((ld_q & 7u) == 0) {
+        if (!(ABL & 4) && (ld_q & 7u) == 0) {
           put_block((ld_q >> 3) + 1, NB);
           NB = load_block((ld_q >> 3) + 2);
         }
@@ -438,9 +457,17 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
     if (ABL & 2) {
       R = group_xor(r[0] ^ r[1] ^ r[2] ^ r[3], 3);
     } else {
+      // Horner by x^-32 through the nibble table: 8 lookups per multiply
+      // (one copy: the 16 entries of a nibble position sit in 16 banks, so
+      // any lane pattern is conflict-free) instead of 32 bit-selects.
       uint32_t u = r[3];
 #pragma unroll
-      for (int i = 2; i >= 0; --i) u = mul_basis(u, a.XB) ^ r[i];
+      for (int i = 2; i >= 0; --i) {
+        uint32_t m = r[i];
+#pragma unroll
+        for (int w = 0; w < 8; ++w) m ^= xtl[16 * w + ((u >> (4 * w)) & 15u)];
+        u = m;
+      }
       uint32_t acc[4] = {0u, 0u, 0u, 0u};  // u * x^(-128 s), basis rows from LDS
 #pragma unroll
       for (int q4 = 0; q4 < 8; ++q4) {
