@@ -12,22 +12,20 @@
 //                   128), histogram the classes; packets too short for a
 //                   RoCEv2 header (4 <= n < 44) are computed right there by a
 //                   scalar loop, invalid lengths yield 0 (as the ragged kernel
-//                   always did);
-//  2. rsck_plan     one workgroup scans the 513 class counts: each class gets
-//                   a bucket padded to whole 8-packet groups, a first group and
-//                   a first step (line);
-//  3. rsck_scatter  writes each packet's descriptor {addr, n, idx} into its
-//                   class bucket (block-aggregated atomics) and its position;
+//                   always did).  Its last workgroup runs
+//  2. rsck_plan     a scan of the class counts: each class gets a bucket
+//                   padded to whole 8-packet groups, a first group and a
+//                   first step (line);
+//  3. rsck_scatter  writes each packet's descriptor {addr, n} into its class
+//                   bucket (block-aggregated atomics) and its position;
 //  4. icrc_rsck_kernel  folds groups of 8 equal-L packets (L > kRsSmallL)
-//                   exactly like the
-//                   SCK -- lane 8g+s owns slot s of every line of packet g,
-//                   four chains per lane, T_124..T_127 tables in LDS -- with
-//                   a load cursor running 8 lines ahead of the fold cursor
-//                   across group boundaries (groups of 64-byte packets are
-//                   one line long), descriptors read 64 at a time;
-//     icrc_ragged_kernel<4> folds the small packets (<= kRsSmallL lines; 8
-//                   lanes per packet is too coarse for them), bucketed by
-//                   64-byte piece count so their piece prefix is arithmetic;
+//                   exactly like the SCK -- lane 8g+s owns slot s of every
+//                   line of packet g, four chains per lane, T_124..T_127
+//                   tables in LDS -- with a load cursor running 8 lines ahead
+//                   of the fold cursor across group boundaries, descriptors
+//                   read 64 at a time;
+//     icrc_rsmall_kernel folds the one-line packets (C4's 64 B; 8 lanes per
+//                   packet is too coarse for them) one lane per packet;
 //  5. rsck_gather   out[i] = res[pos(i)] (verify mode: the trailer compared
 //                   with it).
 //
@@ -60,6 +58,14 @@ __device__ __forceinline__ u32x4 gload16_nt(uint64_t addr) {
   return __builtin_nontemporal_load(reinterpret_cast<gptr_u32x4_t>((uintptr_t)addr));
 }
 
+// Packet i's L3 address and length.  OFF / LEN: the batch has per-packet
+// offsets / lengths (template parameters of the pass kernels, so the loads of
+// several packets issue back to back instead of behind per-packet branches).
+template <bool OFF, bool LEN>
+__device__ __forceinline__ void rs_packet(const RsckArgs &a, uint64_t i, uint64_t &addr, uint32_t &n) {
+  addr = (uint64_t)(uintptr_t)a.base + (OFF ? a.off[i] : i * a.stride) + a.l3_offset;
+  n = LEN ? a.len[i] : a.fixed_len;
+}
 __device__ __forceinline__ void rs_packet(const RsckArgs &a, uint64_t i, uint64_t &addr, uint32_t &n) {
   addr = (uint64_t)(uintptr_t)a.base + (a.off ? a.off[i] : i * a.stride) + a.l3_offset;
   n = a.len ? a.len[i] : a.fixed_len;
@@ -99,6 +105,10 @@ constexpr int kPassBlock = 1024;
 // line per group) ran ~8x longer than one that drew 4 KiB packets.
 constexpr uint32_t kGroupCost = 6;
 constexpr int kPassBlocks = 512;  // pass grid cap (per-block class histograms: 1 MiB)
+constexpr int kPassUnroll = 8;    // packets per thread whose descriptors are read at once
+// a.counts: [0, kRsClasses) class counts, [kRsClasses] misaligned flag,
+// [kRsTicket] count-pass workgroups done
+constexpr int kRsTicket = kRsClasses + 1;
 __device__ __forceinline__ void pass_range(uint64_t count, uint64_t &lo, uint64_t &hi) {
   const uint64_t per = ((count + gridDim.x - 1) / gridDim.x + kPassBlock - 1) / kPassBlock * kPassBlock;
   lo = (uint64_t)blockIdx.x * per;
@@ -106,45 +116,18 @@ __device__ __forceinline__ void pass_range(uint64_t count, uint64_t &lo, uint64_
   hi = lo + per < count ? lo + per : count;
 }
 
-__global__ __launch_bounds__(kPassBlock) void rsck_count(RsckArgs a) {
-  __shared__ uint32_t h[kRsClasses];
-  for (int t = threadIdx.x; t < kRsClasses; t += blockDim.x) h[t] = 0;
-  __syncthreads();
-  uint64_t lo, hi;
-  pass_range(a.count, lo, hi);
-  int odd = 0;  // a strided-chain packet not starting or ending on a 4-byte word
-  for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-    uint64_t addr;
-    uint32_t n;
-    rs_packet(a, i, addr, n);
-    const uint32_t c = rs_class(addr, n);
-    if (c) {
-      atomicAdd(&h[c], 1u);
-      odd |= (c >= (uint32_t)kRsBigBase && ((addr | n) & 3u)) ? 1 : 0;
-    } else {
-      uint32_t v = 0u;
-      if (n >= 4u && n <= kMaxLen) {
-        v = icrc_small(addr, n);
-        if (a.verify) v = gload4_unaligned((uintptr_t)(addr + n - 4u)) == v ? 1u : 0u;
-      }
-      a.out[i] = v;
-    }
-  }
-  if (__syncthreads_or(odd) && threadIdx.x == 0) atomicOr(&a.counts[kRsClasses], 1u);
-  for (int t = threadIdx.x; t < kRsClasses; t += blockDim.x) {
-    a.hist[(uint64_t)blockIdx.x * kRsClasses + t] = h[t];
-    if (h[t]) atomicAdd(&a.counts[t], h[t]);
-  }
-}
-
 // One workgroup: exclusive scans over the classes of groups (bucket
 // positions), of weighted work and of the non-empty big classes (the fold's
 // class table), and of pieces of the small classes (the piece kernel's prefix).
-__global__ __launch_bounds__(1024) void rsck_plan(RsckArgs a) {
+// Run by the count pass's last workgroup (1024 threads), after every
+// workgroup's class counts have landed in a.counts.
+__device__ void rsck_plan(const RsckArgs &a) {
   __shared__ uint32_t sg[1024], sf[1024];
   __shared__ uint64_t ss[1024], sp[1024];
   const uint32_t t = threadIdx.x;
-  const uint32_t cnt = (t >= 1 && t < (uint32_t)kRsClasses) ? a.counts[t] : 0u;
+  const uint32_t cnt = (t >= 1 && t < (uint32_t)kRsClasses)
+                           ? __hip_atomic_load(&a.counts[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                           : 0u;
   const bool big = t > (uint32_t)kRsBigBase;
   const uint32_t G = (cnt + 7u) >> 3, f = (big && cnt) ? 1u : 0u;
   const uint32_t L = big ? t - (uint32_t)kRsBigBase : 0u;
@@ -189,22 +172,100 @@ __global__ __launch_bounds__(1024) void rsck_plan(RsckArgs a) {
   }
 }
 
+template <bool OFF, bool LEN>
+__global__ __launch_bounds__(kPassBlock) void rsck_count(RsckArgs a) {
+  __shared__ uint32_t h[kRsClasses];
+  for (int t = threadIdx.x; t < kRsClasses; t += blockDim.x) h[t] = 0;
+  __syncthreads();
+  uint64_t lo, hi;
+  pass_range(a.count, lo, hi);
+  int odd = 0;  // a strided-chain packet not starting or ending on a 4-byte word
+  // kPassUnroll packets per thread in flight at once: one at a time, the
+  // pass was a chain of dependent memory latencies.
+  for (uint64_t i0 = lo + threadIdx.x; i0 < hi; i0 += kPassUnroll * blockDim.x) {
+    // Raw loads first, unconditional (index clamped), arithmetic after: an
+    // add on a loaded value inside a per-packet branch made the compiler wait
+    // for each load before issuing the next.
+    uint64_t addr[kPassUnroll];
+    uint32_t n[kPassUnroll];
+#pragma unroll
+    for (int k = 0; k < kPassUnroll; ++k) {
+      uint64_t i = i0 + (uint64_t)k * blockDim.x;
+      i = i < hi ? i : hi - 1;
+      addr[k] = OFF ? a.off[i] : i * a.stride;
+      n[k] = LEN ? a.len[i] : a.fixed_len;
+    }
+#pragma unroll
+    for (int k = 0; k < kPassUnroll; ++k) addr[k] += (uint64_t)(uintptr_t)a.base + a.l3_offset;
+#pragma unroll
+    for (int k = 0; k < kPassUnroll; ++k) {
+      const uint64_t i = i0 + (uint64_t)k * blockDim.x;
+      if (i >= hi) break;
+      const uint32_t c = rs_class(addr[k], n[k]);
+      if (c) {
+        atomicAdd(&h[c], 1u);
+        odd |= (c >= (uint32_t)kRsBigBase && ((addr[k] | n[k]) & 3u)) ? 1 : 0;
+      } else {
+        uint32_t v = 0u;
+        if (n[k] >= 4u && n[k] <= kMaxLen) {
+          v = icrc_small(addr[k], n[k]);
+          if (a.verify) v = gload4_unaligned((uintptr_t)(addr[k] + n[k] - 4u)) == v ? 1u : 0u;
+        }
+        a.out[i] = v;
+      }
+    }
+  }
+  if (__syncthreads_or(odd) && threadIdx.x == 0) atomicOr(&a.counts[kRsClasses], 1u);
+  for (int t = threadIdx.x; t < kRsClasses; t += blockDim.x) {
+    a.hist[(uint64_t)blockIdx.x * kRsClasses + t] = h[t];
+    if (h[t]) atomicAdd(&a.counts[t], h[t]);
+  }
+  // The last workgroup to finish plans the buckets (one launch fewer).  Only
+  // the class-count atomics need ordering before the ticket: each thread
+  // waits for its own to be acknowledged (vmcnt(0)), not a __threadfence (an
+  // agent-scope release writes the XCD's L2 back: 130 us over the pass).
+  __shared__ uint32_t last;
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  __syncthreads();
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add(&a.counts[kRsTicket], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                   gridDim.x - 1
+               ? 1u
+               : 0u;
+  __syncthreads();
+  if (last) rsck_plan(a);
+}
+
+template <bool OFF, bool LEN>
 __global__ __launch_bounds__(kPassBlock) void rsck_scatter(RsckArgs a) {
-  __shared__ uint32_t lc[kRsClasses], base[kRsClasses];
+  // The class tables in LDS: per-round global reads of them were a
+  // dependent latency in every round.
+  __shared__ uint32_t lc[kRsClasses], base[kRsClasses], sbk[kRsClasses], send[kRsClasses];
+  __shared__ uint64_t sps0[kRsBigBase + 1];
   for (int t = threadIdx.x; t < kRsClasses; t += blockDim.x) {
     const uint32_t hb = a.hist[(uint64_t)blockIdx.x * kRsClasses + t];
-    base[t] = hb ? a.bucket[t] + atomicAdd(&a.cursor[t], hb) : 0u;
+    const uint32_t bk = a.bucket[t];
+    base[t] = hb ? bk + atomicAdd(&a.cursor[t], hb) : 0u;
+    sbk[t] = bk;
+    send[t] = bk + a.counts[t];
+    if (t <= kRsBigBase) sps0[t] = a.plan->ps0[t];
   }
   uint64_t lo, hi;
   pass_range(a.count, lo, hi);
+  // The next round's packet is read while this round is placed (software
+  // pipelining: the rounds are serialised by the block's LDS counters).
+  uint64_t addr_n = 0;
+  uint32_t n_n = 0;
+  if (lo + threadIdx.x < hi) rs_packet<OFF, LEN>(a, lo + threadIdx.x, addr_n, n_n);
   for (uint64_t b0 = lo; b0 < hi; b0 += blockDim.x) {
     for (int t = threadIdx.x; t < kRsClasses; t += blockDim.x) lc[t] = 0;
-    __syncthreads();
     const uint64_t i = b0 + threadIdx.x;
-    uint64_t addr = 0;
-    uint32_t n = 0, c = 0, r = 0;
+    const uint64_t addr = addr_n;
+    const uint32_t n = n_n;
+    if (i + blockDim.x < hi) rs_packet<OFF, LEN>(a, i + blockDim.x, addr_n, n_n);
+    __syncthreads();
+    uint32_t c = 0, r = 0;
     if (i < hi) {
-      rs_packet(a, i, addr, n);
       c = rs_class(addr, n);
       if (c) r = atomicAdd(&lc[c], 1u);
     }
@@ -214,12 +275,12 @@ __global__ __launch_bounds__(kPassBlock) void rsck_scatter(RsckArgs a) {
         const uint32_t pos = base[c] + r;
         const RsDesc d{(uint32_t)addr, (uint32_t)(addr >> 32) | (n << 16)};
         const bool small = c <= (uint32_t)kRsBigBase;
-        const uint64_t psb = small ? a.plan->ps0[c] : 0u;
-        const uint32_t bk = a.bucket[c];
+        const uint64_t psb = small ? sps0[c] : 0u;
+        const uint32_t bk = sbk[c];
         a.desc[pos] = d;
         a.pos_of[i] = pos;
         if (small) a.ps[pos] = psb + (uint64_t)(pos - bk) * (c - 1u);
-        const uint32_t end = bk + a.counts[c];
+        const uint32_t end = send[c];
         if (pos + 1 == end)  // the class's last packet pads its group with copies of itself
           for (uint32_t p = end; (p - bk) & 7u; ++p) {
             a.desc[p] = d;
@@ -239,19 +300,27 @@ __global__ __launch_bounds__(256) void rsck_gather(RsckArgs a) {
   // The class counters are dead now (plan, scatter and both folds have read
   // them): zero them for the next call on this workspace.
   if (blockIdx.x == 0)
-    for (uint32_t t = threadIdx.x; t <= (uint32_t)kRsClasses; t += blockDim.x) a.counts[t] = 0u;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.count;
-       i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t p = a.pos_of[i];
-    if (p == 0xFFFFFFFFu) continue;  // done by the count pass
-    uint32_t v = a.res[p];
-    if (a.verify) {  // out = trailer holds the ICRC
-      uint64_t addr;
-      uint32_t n;
-      rs_packet(a, i, addr, n);
-      v = gload4_unaligned((uintptr_t)(addr + n - 4u)) == v ? 1u : 0u;
+    for (uint32_t t = threadIdx.x; t <= (uint32_t)kRsTicket; t += blockDim.x) a.counts[t] = 0u;
+  constexpr int U = 4;  // packets per thread in flight at once
+  const uint64_t T = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < a.count; i0 += U * T) {
+    uint32_t p[U], v[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) p[k] = i0 + k * T < a.count ? a.pos_of[i0 + k * T] : 0xFFFFFFFFu;
+#pragma unroll
+    for (int k = 0; k < U; ++k) v[k] = p[k] != 0xFFFFFFFFu ? a.res[p[k]] : 0u;
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const uint64_t i = i0 + k * T;
+      if (p[k] == 0xFFFFFFFFu) continue;  // past the end, or done by the count pass
+      if (a.verify) {  // out = trailer holds the ICRC
+        uint64_t addr;
+        uint32_t n;
+        rs_packet(a, i, addr, n);
+        v[k] = gload4_unaligned((uintptr_t)(addr + n - 4u)) == v[k] ? 1u : 0u;
+      }
+      a.out[i] = v[k];
     }
-    a.out[i] = v;
   }
 }
 
@@ -734,7 +803,7 @@ uint64_t rs_workspace_bytes(uint64_t count) {
 }
 
 hipError_t rs_zero_counters(void *ws, hipStream_t st) {  // counts is the workspace's first region
-  return hipMemsetAsync(ws, 0, 4ull * (kRsClasses + 1), st);
+  return hipMemsetAsync(ws, 0, 4ull * (kRsTicket + 1), st);
 }
 
 void rs_bind_workspace(RsckArgs &a, void *ws) {
@@ -753,6 +822,26 @@ void rs_bind_workspace(RsckArgs &a, void *ws) {
   a.small_pos = reinterpret_cast<uint32_t *>(p);
 }
 
+// Gather: one round of 4 packets per thread where the grid allows.
+static int gather_grid(uint64_t count) {
+  const uint64_t want = (count + 1023) / 1024;
+  return (int)(want < 16384 ? (want ? want : 1) : 16384);
+}
+
+template <bool OFF, bool LEN>
+static void launch_passes_t(const RsckArgs &a, int pgrid, hipStream_t st) {
+  static_assert(kPassBlock == 1024, "the count pass's last workgroup runs the 1024-thread plan");
+  hipLaunchKernelGGL((rsck_count<OFF, LEN>), dim3(pgrid), dim3(kPassBlock), 0, st, a);
+  hipLaunchKernelGGL((rsck_scatter<OFF, LEN>), dim3(pgrid), dim3(kPassBlock), 0, st, a);
+}
+// count, plan, scatter
+static void launch_passes(const RsckArgs &a, int pgrid, hipStream_t st) {
+  if (a.off && a.len) launch_passes_t<true, true>(a, pgrid, st);
+  else if (a.off) launch_passes_t<true, false>(a, pgrid, st);
+  else if (a.len) launch_passes_t<false, true>(a, pgrid, st);
+  else launch_passes_t<false, false>(a, pgrid, st);
+}
+
 hipError_t launch_rsck(RsckArgs &a, const RaggedArgs &small, int grid, hipStream_t st) {
   if (a.count == 0) return hipSuccess;
   // a.counts (+ the misaligned flag) is zero here: zeroed when the workspace
@@ -760,13 +849,11 @@ hipError_t launch_rsck(RsckArgs &a, const RaggedArgs &small, int grid, hipStream
   hipError_t e = hipSuccess;
   const uint64_t want = (a.count + kPassBlock - 1) / kPassBlock;
   const int pgrid = (int)(want < kPassBlocks ? want : kPassBlocks);
-  hipLaunchKernelGGL(rsck_count, dim3(pgrid), dim3(kPassBlock), 0, st, a);
-  hipLaunchKernelGGL(rsck_plan, dim3(1), dim3(1024), 0, st, a);
-  hipLaunchKernelGGL(rsck_scatter, dim3(pgrid), dim3(kPassBlock), 0, st, a);
+  launch_passes(a, pgrid, st);
   hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, st, a);
   if (getenv("RICRC_RS_PIECE") == nullptr) {  // the small region [0, *small_pos): one lane per packet
     hipLaunchKernelGGL(icrc_rsmall_kernel, dim3(grid), dim3(kBlock), 0, st, a);
-    hipLaunchKernelGGL(rsck_gather, dim3(pgrid), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(rsck_gather, dim3(gather_grid(a.count)), dim3(256), 0, st, a);
     return hipGetLastError();
   }
   RaggedArgs r = small;  // the small region [0, *small_pos) of the buckets: piece kernel, ICRCs into res
@@ -783,7 +870,7 @@ hipError_t launch_rsck(RsckArgs &a, const RaggedArgs &small, int grid, hipStream
   r.l3_offset = 0;
   e = launch_ragged(r, grid, st);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(rsck_gather, dim3(pgrid), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(rsck_gather, dim3(gather_grid(a.count)), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 

@@ -46,9 +46,7 @@ int main(int argc, char **argv) {
     rs_bind_workspace(a, ws);
     const uint64_t want = (count + kPassBlock - 1) / kPassBlock;
     const int pgrid = (int)(want < kPassBlocks ? want : kPassBlocks);
-    hipLaunchKernelGGL(rsck_count, dim3(pgrid), dim3(kPassBlock), 0, 0, a);
-    hipLaunchKernelGGL(rsck_plan, dim3(1), dim3(1024), 0, 0, a);
-    hipLaunchKernelGGL(rsck_scatter, dim3(pgrid), dim3(kPassBlock), 0, 0, a);
+    launch_passes(a, pgrid, 0);
     CK(hipDeviceSynchronize());
     char nm[128];
     for (int r = 0; r < 2; ++r) {
