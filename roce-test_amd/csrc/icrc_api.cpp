@@ -53,7 +53,7 @@ struct Dev {
   hipStream_t stream = nullptr;
   uint32_t *d_inv = nullptr;   // x^(-8 z), z <= 4096
   uint32_t *d_inv4 = nullptr;  // t: x^(8 (k - t)), k = 0..3, t <= 4096
-  uint32_t *d_tzb = nullptr;   // [128][8]: basis words 4q of x^(-8 tz) (ragged strided-chain path)
+  uint32_t *d_tzb = nullptr;   // [kTzWords]: basis words 4q of x^(-8 tz) at 2 tz + q (ragged strided-chain path)
   uint32_t *d_x8n = nullptr;   // x^(8 k), k < 65536 (incremental repair)
   uint32_t *d_work = nullptr;  // kWorkSlots x kSckWorkWords counters (dynamic SCK schedule)
   uint32_t work_next = 0;      // round-robin slot: launches in flight on different streams never share one
@@ -139,10 +139,12 @@ int init_dev(Dev &d) {
     for (int k = 0; k < 4; ++k) inv4[4 * t + k] = k >= t ? gf_x8n((uint64_t)(k - t)) : gf_xinv8n((uint64_t)(t - k));
   HIP_TRY(hipMalloc(&d.d_inv4, inv4.size() * sizeof(uint32_t)));
   HIP_TRY(hipMemcpy(d.d_inv4, inv4.data(), inv4.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-  std::vector<uint32_t> tzb(128 * 8);  // basis words 4q of x^(-8 tz): the kernel derives 4q+1..4q+3 by x^-1
-  for (int tz = 0; tz < 128; ++tz) {
-    const uint32_t c = gf_xinv8n((uint64_t)tz);
-    for (int q = 0; q < 8; ++q) tzb[8 * tz + q] = gf_mul(c, 1u << (4 * q));
+  // Basis word 4q of x^(-8 tz) is x^(-8 tz) x^(31 - 4q) = x^(31 - 4 (2 tz + q)):
+  // one entry per m = 2 tz + q; the kernel derives words 4q+1..4q+3 by x^-1.
+  std::vector<uint32_t> tzb(kTzWords);
+  for (int m = 0; m < kTzWords; ++m) {
+    const int tz = std::min(m >> 1, 127), q = m - 2 * tz;
+    tzb[m] = q < 8 ? gf_mul(gf_xinv8n((uint64_t)tz), 1u << (4 * q)) : 0u;
   }
   HIP_TRY(hipMalloc(&d.d_tzb, tzb.size() * sizeof(uint32_t)));
   HIP_TRY(hipMemcpy(d.d_tzb, tzb.data(), tzb.size() * sizeof(uint32_t), hipMemcpyHostToDevice));

@@ -97,6 +97,7 @@ __host__ __device__ inline uint32_t ragged_pieces(uintptr_t start, uint32_t n) {
 constexpr int kRsSmallL = RICRC_RS_SMALL_L;
 constexpr int kRsBigBase = 8;                  // small classes 2..8 (P <= 7 for L <= 3)
 constexpr int kRsClasses = kRsBigBase + 514;   // L <= 513 (n <= 65535, any start offset)
+constexpr int kTzWords = 264;                  // tz bases: m = 2 tz + q <= 2 * 127 + 7
 struct RsPlan {
   uint32_t nc;        // non-empty big classes
   uint32_t ngroups;   // 8-packet groups over all classes
@@ -127,7 +128,7 @@ struct RsckArgs {
   uint32_t *hist;     // [pass blocks][kRsClasses] per-block class counts
   uint64_t *ps;       // [count + 8 kRsClasses + 1] piece prefix of the small region
   uint32_t *small_pos;  // positions of the small region (device count for the piece kernel)
-  const uint32_t *tzb;  // [128][8]: words 0, 4, ..., 28 of the basis of x^(-8 tz)
+  const uint32_t *tzb;  // [kTzWords]: entry m = x^(31 - 4 m), i.e. basis word 4 q of x^(-8 tz) at m = 2 tz + q
   uint32_t XB[32];      // basis of x^-32
   uint32_t QS[8];       // x^(-8*16 s): lane slot s -> line start
 };

@@ -354,19 +354,24 @@ __device__ __forceinline__ uint32_t edge_word_aligned(uint32_t w, int rel, int M
 
 // ABL (timing-only ablations, tools/microbench/rsck_abl.hip): 1 no table
 // fold, 2 no finish, 4 descriptors by arithmetic (uniform batch in natural
-// order: packet 8 q + g at base + (8 q + g) stride, no descriptor ring).
+// order: packet 8 q + g at base + (8 q + g) stride, no descriptor ring),
+// 8 no edge masks, 16 no result slots / stores, 32 no global stores (slots kept).
 template <int ABL>
 __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
-  constexpr uint32_t kSlots = 64, kRound = kSlots / 8;   // result slots per wave, groups per round
+  // Result slots per wave and groups per round of them: a round leaves in
+  // one burst of stores, and a store holds back every load queued behind it
+  // in vmcnt until its write is acknowledged (the stores of rounds of 8
+  // groups cost ~4 % of the fold on a 4 GiB mix, tools/microbench/rsck_abl.hip).
+  constexpr uint32_t kSlots = 128, kRound = kSlots / 8;
   constexpr uint32_t kQStride = 36;                       // padded lane-basis rows: conflict-free ds_read_b128
   constexpr uint32_t kBlk = 128;                          // words per descriptor block (8 groups x 8 x 8 B)
   constexpr uint32_t kWaveWords = kSlots + 2 * kBlk + 64;  // slots | 2-block ring | 8-group info FIFO
   constexpr int D = 8;                                    // lines in flight per wave
-  // 128 KiB tables | 4 KiB tz bases | 8 lane bases | 1.5 KiB per wave |
-  // 512 B x^-32 nibble table = 157.6 KiB
-  __shared__ uint32_t lds[kLdsWords + 128 * 8 + 8 * kQStride + kWaves * kWaveWords + 128];
+  // 128 KiB tables | 1 KiB tz bases | 8 lane bases | 1.75 KiB per wave |
+  // 512 B x^-32 nibble table = 158.7 KiB
+  __shared__ uint32_t lds[kLdsWords + kTzWords + 8 * kQStride + kWaves * kWaveWords + 128];
   uint32_t *tzl = lds + kLdsWords;
-  uint32_t *qsl = tzl + 128 * 8;
+  uint32_t *qsl = tzl + kTzWords;
   uint32_t *xtl = qsl + 8 * kQStride + kWaves * kWaveWords;
 
   const uint32_t lane = threadIdx.x & 63;
@@ -374,9 +379,9 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   const uint32_t s = lane & 7, g = lane >> 3;
 
   const uint32_t tab_v = table_entry(g_tab128);
-  const uint32_t tz_v = a.tzb[threadIdx.x];
+  const uint32_t tz_v = a.tzb[threadIdx.x < kTzWords ? threadIdx.x : 0];
   table_store(lds, tab_v);
-  tzl[threadIdx.x] = tz_v;
+  if (threadIdx.x < kTzWords) tzl[threadIdx.x] = tz_v;
   if (threadIdx.x < 256) {  // word j of lane slot s's basis: x^(-128 s) x^(31 - j)
     const uint32_t bs = threadIdx.x >> 5, j = threadIdx.x & 31;
     uint32_t v = a.QS[0];
@@ -519,7 +524,19 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
     const uint32_t valid = 8u * (q_stop - round_q0);
     const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.res + 8ull * round_q0, 4u * valid);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the slot writes have landed
-    __builtin_amdgcn_raw_buffer_store_b32(slots[lane], ro, 4u * lane, 0, 0);
+    if (ABL & 32) {
+      r[1] ^= slots[lane] ^ slots[kSlots - 64 + lane];  // keep the slot reads
+      return;
+    }
+    if (valid == kSlots) {  // a full round: one 8-byte store per lane
+      typedef uint32_t u32x2s __attribute__((ext_vector_type(2)));
+      const u32x2s v = *reinterpret_cast<const u32x2s *>(slots + 2 * lane);
+      __builtin_amdgcn_raw_buffer_store_b64(v, ro, 8u * lane, 0, 0);
+    } else {  // the wave's last, partial round: slots past `valid` fall outside the range check
+#pragma unroll
+      for (uint32_t h = 0; h < kSlots / 64; ++h)
+        __builtin_amdgcn_raw_buffer_store_b32(slots[64 * h + lane], ro, 4u * (64 * h + lane), 0, 0);
+    }
   };
   auto finish = [&]() {
     uint32_t R;
@@ -549,7 +566,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
       // x^(-8 tz), distributed: lane s takes bits 4s..4s+3 of R; basis word
       // 4s from LDS, 4s+1..4s+3 by successive x^-1.
       const uint32_t tz = 128u * fd_L - fd_a - fd_M;
-      uint32_t bw = tzl[8u * tz + s], p = 0;
+      uint32_t bw = tzl[2u * tz + s], p = 0;
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)R, (int)(4u * s + t), 1);
@@ -557,6 +574,10 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
         bw = and_xor((uint32_t)((int32_t)bw >> 31), kXInv, bw << 1);
       }
       R = group_xor(p, 3);
+    }
+    if (ABL & 16) {
+      r[0] ^= R;  // keep the value live
+      return;
     }
     slots[((fd_q - round_q0) << 3) | g] = ~R;
     if (fd_q + 1 - round_q0 == kRound) {  // wave-uniform
@@ -576,7 +597,9 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
     for (int u = 0; u < D; ++u) {
       __builtin_amdgcn_sched_barrier(0);
       u32x4 w = ring[u];
-      if (fd_k == 0 || (fd_k == 1 && fd_head2) || fd_k + 1 == fd_L) {  // wave-uniform
+      if (!(ABL & 8) && (fd_k == 0 || (fd_k == 1 && fd_head2) || fd_k + 1 == fd_L)) {  // wave-uniform
+        // (A cheaper keep-only branch for tail lines made the compiler copy
+        // the ring register and wait for it, vmcnt(0).)
         const int rel0 = (int)(128u * fd_k + 16u * s) - (int)fd_a;
         if constexpr (decltype(words)::value) {
 #pragma unroll
@@ -624,7 +647,8 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
     fold_loop(std::true_type{});
   else
     fold_loop(std::false_type{});
-  if (q_end != round_q0) flush(q_end);
+  if (!(ABL & 16) && q_end != round_q0) flush(q_end);
+  if ((ABL & 48) && r[0] == 0x12345678u) a.res[0] = r[1];
 }
 
 

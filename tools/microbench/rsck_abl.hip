@@ -56,6 +56,14 @@ int main(int argc, char **argv) {
       rep(nm, timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<2>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10), b);
       snprintf(nm, sizeof nm, "%s rsck memory path", tag);
       rep(nm, timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<3>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10), b);
+      snprintf(nm, sizeof nm, "%s rsck no edges", tag);
+      rep(nm, timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<8>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10), b);
+      snprintf(nm, sizeof nm, "%s rsck no stores", tag);
+      rep(nm, timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<16>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10), b);
+      snprintf(nm, sizeof nm, "%s rsck no global stores", tag);
+      rep(nm, timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<32>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10), b);
+      snprintf(nm, sizeof nm, "%s rsck memory path, no edges, no stores", tag);
+      rep(nm, timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<3 | 8 | 16>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10), b);
       if (!d_off) {
         snprintf(nm, sizeof nm, "%s rsck arith desc", tag);
         rep(nm, timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<4>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10), b);
@@ -64,46 +72,6 @@ int main(int argc, char **argv) {
       }
       snprintf(nm, sizeof nm, "%s small kernel", tag);
       rep(nm, timeit([&] { hipLaunchKernelGGL(icrc_rsmall_kernel, dim3(grid), dim3(kBlock), 0, 0, a); }, 10), b);
-    }
-    if (d_off) {  // fold and small kernel concurrently on two streams, CUs split
-      hipStream_t s1, s2; CK(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking)); CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
-      hipEvent_t ef, ej; CK(hipEventCreateWithFlags(&ef, hipEventDisableTiming)); CK(hipEventCreateWithFlags(&ej, hipEventDisableTiming));
-      for (int r = 0; r < 2; ++r) {
-        snprintf(nm, sizeof nm, "%s sequential fold(%d) + small(%d)", tag, grid, grid);
-        rep(nm, timeit([&] {
-          hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, 0, a);
-          hipLaunchKernelGGL(icrc_rsmall_kernel, dim3(grid), dim3(kBlock), 0, 0, a);
-        }, 10), b);
-        for (int g2 : {16, 32, 48, 64, 96}) {
-          for (int order = 0; order < 2; ++order) {
-            snprintf(nm, sizeof nm, "%s concurrent fold(%d) | small(%d)%s", tag, grid - g2, g2, order ? " small first" : "");
-            rep(nm, timeit([&] {
-              CK(hipEventRecord(ef, 0));
-              CK(hipStreamWaitEvent(s1, ef, 0));
-              CK(hipStreamWaitEvent(s2, ef, 0));
-              if (order) hipLaunchKernelGGL(icrc_rsmall_kernel, dim3(g2), dim3(kBlock), 0, s2, a);
-              hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid - g2), dim3(kBlock), 0, s1, a);
-              if (!order) hipLaunchKernelGGL(icrc_rsmall_kernel, dim3(g2), dim3(kBlock), 0, s2, a);
-              CK(hipEventRecord(ej, s2));
-              CK(hipStreamWaitEvent(s1, ej, 0));
-              CK(hipEventRecord(ef, s1));
-              CK(hipStreamWaitEvent(0, ef, 0));
-            }, 10), b);
-          }
-        }
-        snprintf(nm, sizeof nm, "%s concurrent fold(%d) | small(%d)", tag, grid, grid);
-        rep(nm, timeit([&] {
-          CK(hipEventRecord(ef, 0));
-          CK(hipStreamWaitEvent(s1, ef, 0));
-          CK(hipStreamWaitEvent(s2, ef, 0));
-          hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, s1, a);
-          hipLaunchKernelGGL(icrc_rsmall_kernel, dim3(grid), dim3(kBlock), 0, s2, a);
-          CK(hipEventRecord(ej, s2));
-          CK(hipStreamWaitEvent(s1, ej, 0));
-          CK(hipEventRecord(ef, s1));
-          CK(hipStreamWaitEvent(0, ef, 0));
-        }, 10), b);
-      }
     }
     CK(hipFree(ws));
   };
