@@ -358,21 +358,25 @@ __device__ __forceinline__ uint32_t edge_word_aligned(uint32_t w, int rel, int M
 // 8 no edge masks, 16 no result slots / stores, 32 no global stores (slots kept).
 template <int ABL>
 __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
-  // Result slots per wave and groups per round of them: a round leaves in
-  // one burst of stores, and a store holds back every load queued behind it
-  // in vmcnt until its write is acknowledged (the stores of rounds of 8
-  // groups cost ~4 % of the fold on a 4 GiB mix, tools/microbench/rsck_abl.hip).
-  constexpr uint32_t kSlots = 128, kRound = kSlots / 8;
-  constexpr uint32_t kQStride = 36;                       // padded lane-basis rows: conflict-free ds_read_b128
+  // Result slots per wave (a round of 8 groups leaves in one store; a store
+  // holds back every load queued behind it in vmcnt until its write is
+  // acknowledged: the stores cost ~4 % of the fold on a 4 GiB mix, the same
+  // for rounds of 8 or 16 groups and 4- or 8-byte stores, rsck_abl.hip).
+  constexpr uint32_t kSlots = 64, kRound = kSlots / 8;
   constexpr uint32_t kBlk = 128;                          // words per descriptor block (8 groups x 8 x 8 B)
   constexpr uint32_t kWaveWords = kSlots + 2 * kBlk + 64;  // slots | 2-block ring | 8-group info FIFO
   constexpr int D = 8;                                    // lines in flight per wave
-  // 128 KiB tables | 1 KiB tz bases | 8 lane bases | 1.75 KiB per wave |
-  // 512 B x^-32 nibble table = 158.7 KiB
-  __shared__ uint32_t lds[kLdsWords + kTzWords + 8 * kQStride + kWaves * kWaveWords + 128];
-  uint32_t *tzl = lds + kLdsWords;
-  uint32_t *qsl = tzl + kTzWords;
-  uint32_t *xtl = qsl + 8 * kQStride + kWaves * kWaveWords;
+  // Finish tables first, so every lookup's constant part fits a ds_read's
+  // 16-bit offset: x^-32 nibble table (128 words) | x^(-128 s) nibble tables
+  // (8 x 132 words: rows padded by 4 words so the 8 lane slots spread over
+  // the banks) | 128 KiB slice-by-4 tables | 1 KiB tz bases | 1.5 KiB per
+  // wave = 157.7 KiB.
+  constexpr uint32_t kQtStride = 132, kSmallWords = 128 + 8 * kQtStride;  // 1184: a multiple of 32 words
+  __shared__ uint32_t lds[kSmallWords + kLdsWords + kTzWords + kWaves * kWaveWords];
+  uint32_t *xtl = lds;
+  uint32_t *qtl = lds + 128;
+  uint32_t *tab = lds + kSmallWords;
+  uint32_t *tzl = tab + kLdsWords;
 
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -380,15 +384,22 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
 
   const uint32_t tab_v = table_entry(g_tab128);
   const uint32_t tz_v = a.tzb[threadIdx.x < kTzWords ? threadIdx.x : 0];
-  table_store(lds, tab_v);
+  table_store(tab, tab_v);
   if (threadIdx.x < kTzWords) tzl[threadIdx.x] = tz_v;
-  if (threadIdx.x < 256) {  // word j of lane slot s's basis: x^(-128 s) x^(31 - j)
-    const uint32_t bs = threadIdx.x >> 5, j = threadIdx.x & 31;
-    uint32_t v = a.QS[0];
+  {  // entry (s, w, v) = (nibble v at bits 4w..4w+3) * x^(-128 s), where bit
+     // j of a value stands for QS[s] x^(31 - j)
+    const uint32_t bs = threadIdx.x >> 7, w = (threadIdx.x >> 4) & 7u, v = threadIdx.x & 15u;
+    uint32_t p = a.QS[0];
 #pragma unroll
-    for (int k = 1; k < 8; ++k) v = bs == (uint32_t)k ? a.QS[k] : v;
-    for (uint32_t t = j; t < 31; ++t) v = gf_mulx(v);
-    qsl[bs * kQStride + j] = v;
+    for (int k = 1; k < 8; ++k) p = bs == (uint32_t)k ? a.QS[k] : p;
+    for (uint32_t t = 0; t < 28u - 4u * w; ++t) p = gf_mulx(p);  // bit 4w + 3
+    uint32_t e = 0;
+#pragma unroll
+    for (int b = 3; b >= 0; --b) {
+      e ^= ((v >> b) & 1u) ? p : 0u;
+      p = gf_mulx(p);
+    }
+    qtl[bs * kQtStride + 16u * w + v] = e;
   }
   if (threadIdx.x < 128) {  // entry 16 w + v: (nibble v at bits 4w..4w+3) * x^-32
     const uint32_t w = threadIdx.x >> 4, v = threadIdx.x & 15u;
@@ -424,8 +435,8 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   if (q_begin >= q_end) return;  // no barrier below
 
   const LaneTab lt{(lane & 31) << 2, ((lane & 31) << 2) | 0x10000u};
-  const uint32_t *qrow = qsl + s * kQStride;
-  uint32_t *slots = qsl + 8 * kQStride + wid * kWaveWords;
+  const uint32_t *qrow = qtl + s * kQtStride;
+  uint32_t *slots = tzl + kTzWords + wid * kWaveWords;
   uint32_t *dring = slots + kSlots;
   uint32_t *fifo = dring + 2 * kBlk;
   const uint64_t npos = 8ull * NG;
@@ -528,15 +539,9 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
       r[1] ^= slots[lane] ^ slots[kSlots - 64 + lane];  // keep the slot reads
       return;
     }
-    if (valid == kSlots) {  // a full round: one 8-byte store per lane
-      typedef uint32_t u32x2s __attribute__((ext_vector_type(2)));
-      const u32x2s v = *reinterpret_cast<const u32x2s *>(slots + 2 * lane);
-      __builtin_amdgcn_raw_buffer_store_b64(v, ro, 8u * lane, 0, 0);
-    } else {  // the wave's last, partial round: slots past `valid` fall outside the range check
 #pragma unroll
-      for (uint32_t h = 0; h < kSlots / 64; ++h)
-        __builtin_amdgcn_raw_buffer_store_b32(slots[64 * h + lane], ro, 4u * (64 * h + lane), 0, 0);
-    }
+    for (uint32_t h = 0; h < kSlots / 64; ++h)  // slots past `valid` fall outside the range check
+      __builtin_amdgcn_raw_buffer_store_b32(slots[64 * h + lane], ro, 4u * (64 * h + lane), 0, 0);
   };
   auto finish = [&]() {
     uint32_t R;
@@ -546,23 +551,17 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
       // Horner by x^-32 through the nibble table: 8 lookups per multiply
       // (one copy: the 16 entries of a nibble position sit in 16 banks, so
       // any lane pattern is conflict-free) instead of 32 bit-selects.
+      // v * (table's constant) ^ x: 8 nibble lookups, an XOR tree of 3-input XORs
+      auto nib_mul = [](const uint32_t *t, uint32_t v, uint32_t x) -> uint32_t {
+        uint32_t e[8];
+#pragma unroll
+        for (int w = 0; w < 8; ++w) e[w] = t[16 * w + __builtin_amdgcn_ubfe(v, 4 * w, 4)];
+        return xor3(xor3(e[0], e[1], e[2]), xor3(e[3], e[4], e[5]), xor3(e[6], e[7], x));
+      };
       uint32_t u = r[3];
 #pragma unroll
-      for (int i = 2; i >= 0; --i) {
-        uint32_t m = r[i];
-#pragma unroll
-        for (int w = 0; w < 8; ++w) m ^= xtl[16 * w + ((u >> (4 * w)) & 15u)];
-        u = m;
-      }
-      uint32_t acc[4] = {0u, 0u, 0u, 0u};  // u * x^(-128 s), basis rows from LDS
-#pragma unroll
-      for (int q4 = 0; q4 < 8; ++q4) {
-        const u32x4 b = *reinterpret_cast<const u32x4 *>(qrow + 4 * q4);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          acc[i] = and_xor((uint32_t)(((int32_t)(u << (31 - (4 * q4 + i)))) >> 31), b[i], acc[i]);
-      }
-      R = group_xor(xor3(acc[0], acc[1], acc[2] ^ acc[3]), 3);
+      for (int i = 2; i >= 0; --i) u = nib_mul(xtl, u, r[i]);
+      R = group_xor(nib_mul(qrow, u, 0u), 3);  // u * x^(-128 s): lane slot s's nibble table
       // x^(-8 tz), distributed: lane s takes bits 4s..4s+3 of R; basis word
       // 4s from LDS, 4s+1..4s+3 by successive x^-1.
       const uint32_t tz = 128u * fd_L - fd_a - fd_M;
@@ -615,10 +614,10 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
         if (ABL & 1) {
           r[i] = __builtin_amdgcn_perm(x, lt.lo0, 0x0C0C0400u) ^ (x >> 7);
         } else {
-          const uint32_t t3 = lds_at(lds, __builtin_amdgcn_perm(x, lt.lo0, 0x0C0C0400u));
-          const uint32_t t2 = lds_at(lds, __builtin_amdgcn_perm(x, lt.lo0, 0x0C0C0500u) + 128);
-          const uint32_t t1 = lds_at(lds, __builtin_amdgcn_perm(x, lt.lo1, 0x0C020600u));
-          const uint32_t t0 = lds_at(lds, __builtin_amdgcn_perm(x, lt.lo1, 0x0C020700u) + 128);
+          const uint32_t t3 = lds_at(tab, __builtin_amdgcn_perm(x, lt.lo0, 0x0C0C0400u));
+          const uint32_t t2 = lds_at(tab, __builtin_amdgcn_perm(x, lt.lo0, 0x0C0C0500u) + 128);
+          const uint32_t t1 = lds_at(tab, __builtin_amdgcn_perm(x, lt.lo1, 0x0C020600u));
+          const uint32_t t0 = lds_at(tab, __builtin_amdgcn_perm(x, lt.lo1, 0x0C020700u) + 128);
           r[i] = xor3(t3, t2, t1 ^ t0);
         }
       }

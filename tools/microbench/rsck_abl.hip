@@ -73,6 +73,28 @@ int main(int argc, char **argv) {
       snprintf(nm, sizeof nm, "%s small kernel", tag);
       rep(nm, timeit([&] { hipLaunchKernelGGL(icrc_rsmall_kernel, dim3(grid), dim3(kBlock), 0, 0, a); }, 10), b);
     }
+    if (d_off) {  // the bench's order: passes, fold, small, gather per step; fold timed inside
+      hipEvent_t f0, f1; CK(hipEventCreate(&f0)); CK(hipEventCreate(&f1));
+      for (int r = 0; r < 2; ++r) {
+        float tot = 0;
+        for (int it = 0; it < 13; ++it) {
+          // the counters (and the count pass's ticket) must start at zero: the
+          // product's gather zeroes them, the variants above never ran it
+          CK(rs_zero_counters(ws, 0));
+          launch_passes(a, pgrid, 0);
+          CK(hipEventRecord(f0, 0));
+          hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, 0, a);
+          CK(hipEventRecord(f1, 0));
+          hipLaunchKernelGGL(icrc_rsmall_kernel, dim3(grid), dim3(kBlock), 0, 0, a);
+          hipLaunchKernelGGL(rsck_gather, dim3(gather_grid(a.count)), dim3(256), 0, 0, a);
+          CK(hipEventSynchronize(f1));
+          float ms; CK(hipEventElapsedTime(&ms, f0, f1));
+          if (it >= 3) tot += ms;
+        }
+        snprintf(nm, sizeof nm, "%s rsck full, inside the bench's step sequence", tag);
+        rep(nm, tot / 10, b);
+      }
+    }
     CK(hipFree(ws));
   };
 
