@@ -494,8 +494,8 @@ def main(argv=None):
         workload = (f"{b['T']} RoCEv2 packets in all ({'fixed total' if strong else f'{args.count} per GPU'}), "
                     "lengths uniform over 64/256/1024/4096 B, packed, uint64 offsets + uint32 lengths, "
                     f"shards cut at equal bytes; rank 0: {sizes[0]} packets, {rank_bytes if rank == 0 else '?'} B; "
-                    "device-resident, ragged strided-chain path (bucketing passes + icrc_rsck_kernel + piece "
-                    "kernel + gather)")
+                    "device-resident, ragged strided-chain path (count/plan + scatter passes, icrc_rsck_kernel "
+                    "for packets of >= 2 lines, icrc_rsmall_kernel for one-line packets, gather)")
     else:
         workload = (f"{b['T']} x {args.size} B RoCEv2 packets in all ({count} on rank 0), device-resident, "
                     + kernel_label(args.size))
