@@ -116,9 +116,10 @@ struct RsckArgs {
   uint32_t fixed_len;
   uint32_t l3_offset;
   uint32_t verify;
+  uint32_t piece;       // the small region goes to the piece kernel (RICRC_RS_PIECE): write its piece prefix
   uint32_t *out;
   // device workspace (icrc_api.cpp sizes it: rs_workspace_bytes)
-  uint32_t *counts;   // [kRsClasses + 1], zeroed before the count pass; the last: "misaligned" flag
+  uint32_t *counts;   // [kRsClasses + 2], zeroed before the count pass: class counts, "misaligned" flag, count-pass ticket
   uint32_t *cursor;   // [kRsClasses], zeroed by the plan pass
   uint32_t *bucket;   // [kRsClasses] first position of each class
   RsPlan *plan;

@@ -279,12 +279,12 @@ __global__ __launch_bounds__(kPassBlock) void rsck_scatter(RsckArgs a) {
         const uint32_t bk = sbk[c];
         a.desc[pos] = d;
         a.pos_of[i] = pos;
-        if (small) a.ps[pos] = psb + (uint64_t)(pos - bk) * (c - 1u);
+        if (small && a.piece) a.ps[pos] = psb + (uint64_t)(pos - bk) * (c - 1u);
         const uint32_t end = send[c];
         if (pos + 1 == end)  // the class's last packet pads its group with copies of itself
           for (uint32_t p = end; (p - bk) & 7u; ++p) {
             a.desc[p] = d;
-            if (small) a.ps[p] = psb + (uint64_t)(p - bk) * (c - 1u);
+            if (small && a.piece) a.ps[p] = psb + (uint64_t)(p - bk) * (c - 1u);
           }
       } else {
         a.pos_of[i] = 0xFFFFFFFFu;
@@ -867,6 +867,7 @@ static void launch_passes(const RsckArgs &a, int pgrid, hipStream_t st) {
 
 hipError_t launch_rsck(RsckArgs &a, const RaggedArgs &small, int grid, hipStream_t st) {
   if (a.count == 0) return hipSuccess;
+  a.piece = getenv("RICRC_RS_PIECE") != nullptr ? 1u : 0u;
   // a.counts (+ the misaligned flag) is zero here: zeroed when the workspace
   // was allocated, and again by rsck_gather at the end of every call.
   hipError_t e = hipSuccess;
@@ -874,7 +875,7 @@ hipError_t launch_rsck(RsckArgs &a, const RaggedArgs &small, int grid, hipStream
   const int pgrid = (int)(want < kPassBlocks ? want : kPassBlocks);
   launch_passes(a, pgrid, st);
   hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, st, a);
-  if (getenv("RICRC_RS_PIECE") == nullptr) {  // the small region [0, *small_pos): one lane per packet
+  if (!a.piece) {  // the small region [0, *small_pos): one lane per packet
     hipLaunchKernelGGL(icrc_rsmall_kernel, dim3(grid), dim3(kBlock), 0, st, a);
     hipLaunchKernelGGL(rsck_gather, dim3(gather_grid(a.count)), dim3(256), 0, st, a);
     return hipGetLastError();

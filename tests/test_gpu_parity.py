@@ -141,6 +141,31 @@ def test_ragged_kernel_c4_mix_many_waves(ctx):
     np.testing.assert_array_equal(_host_u32(out), want)
 
 
+@pytest.mark.parametrize("knob", ["RICRC_RS_PIECE", "RICRC_NO_RSCK", "RICRC_NO_SCK"])
+def test_ragged_selectable_kernels_agree(ctx, knob, monkeypatch):
+    """The kernels kept selectable for comparison (the round-1 piece kernel for
+    the one-line region, the piece-based ragged kernel instead of the whole
+    ragged strided-chain path) give the same ICRCs as the oracle, on a C4-shaped
+    mix with odd starts and Ethernet framing, before and after the default path
+    ran on the same context (its workspace counters must be left clean)."""
+    rng = np.random.default_rng(31)
+    count = 20_000
+    lens = rng.choice(np.array([64, 100, 256, 1024, 1500, 4096], np.uint32), size=count)
+    offs = np.zeros(count, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + 14, dtype=np.uint64)
+    buf = rng.integers(0, 256, size=int(offs[-1] + lens[-1]) + 64 + 14, dtype=np.uint8)
+    want = oracle_c.icrc_batch(buf[14:], offsets=offs, lengths=lens, threads=16)
+    d_buf, d_offs, d_lens = _dev(buf), _dev(offs), _dev(lens)
+    for env in (None, knob, None):
+        if env:
+            monkeypatch.setenv(env, "1")
+        else:
+            monkeypatch.delenv(knob, raising=False)
+        out = _out(count)
+        ctx.batch_device(d_buf, count, out, offsets=d_offs, lengths=d_lens, l3_offset=14, stream=_stream())
+        np.testing.assert_array_equal(_host_u32(out), want, err_msg=str(env))
+
+
 def test_ragged_kernel_offsets_only_and_lengths_only(ctx):
     """Descriptor modes: offsets with a fixed length (stride - l3_offset), and
     per-packet lengths at a fixed stride."""
