@@ -355,14 +355,15 @@ __device__ __forceinline__ uint32_t edge_word_aligned(uint32_t w, int rel, int M
 // ABL (timing-only ablations, tools/microbench/rsck_abl.hip): 1 no table
 // fold, 2 no finish, 4 descriptors by arithmetic (uniform batch in natural
 // order: packet 8 q + g at base + (8 q + g) stride, no descriptor ring),
-// 8 no edge masks, 16 no result slots / stores, 32 no global stores (slots kept).
+// 8 no edge masks, 16 no result slots / stores, 32 no global stores (slots kept),
+// 512 (with 2) 192 result slots, 1024 / 2048 / 4096 result stores nt / default / sc0 sc1.
 template <int ABL>
 __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   // Result slots per wave (a round of 8 groups leaves in one store; a store
   // holds back every load queued behind it in vmcnt until its write is
   // acknowledged: the stores cost ~4 % of the fold on a 4 GiB mix, the same
   // for rounds of 8 or 16 groups and 4- or 8-byte stores, rsck_abl.hip).
-  constexpr uint32_t kSlots = 64, kRound = kSlots / 8;
+  constexpr uint32_t kSlots = (ABL & 512) ? 192 : 64, kRound = kSlots / 8;
   constexpr uint32_t kBlk = 128;                          // words per descriptor block (8 groups x 8 x 8 B)
   constexpr uint32_t kWaveWords = kSlots + 2 * kBlk + 64;  // slots | 2-block ring | 8-group info FIFO
   constexpr int D = 8;                                    // lines in flight per wave
@@ -371,8 +372,11 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   // (8 x 132 words: rows padded by 4 words so the 8 lane slots spread over
   // the banks) | 128 KiB slice-by-4 tables | 1 KiB tz bases | 1.5 KiB per
   // wave = 157.7 KiB.
-  constexpr uint32_t kQtStride = 132, kSmallWords = 128 + 8 * kQtStride;  // 1184: a multiple of 32 words
-  __shared__ uint32_t lds[kSmallWords + kLdsWords + kTzWords + kWaves * kWaveWords];
+  // (ABL 512, timing only, with 2: 192 result slots per wave in the room of
+  // the finish tables.)
+  constexpr uint32_t kQtStride = 132, kSmallWords = (ABL & 512) ? 0 : 128 + 8 * kQtStride;  // 1184: a multiple of 32 words
+  constexpr uint32_t kTzW = (ABL & 512) ? 0 : kTzWords;
+  __shared__ uint32_t lds[kSmallWords + kLdsWords + kTzW + kWaves * kWaveWords];
   uint32_t *xtl = lds;
   uint32_t *qtl = lds + 128;
   uint32_t *tab = lds + kSmallWords;
@@ -385,8 +389,8 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   const uint32_t tab_v = table_entry(g_tab128);
   const uint32_t tz_v = a.tzb[threadIdx.x < kTzWords ? threadIdx.x : 0];
   table_store(tab, tab_v);
-  if (threadIdx.x < kTzWords) tzl[threadIdx.x] = tz_v;
-  {  // entry (s, w, v) = (nibble v at bits 4w..4w+3) * x^(-128 s), where bit
+  if (!(ABL & 512) && threadIdx.x < kTzWords) tzl[threadIdx.x] = tz_v;
+  if (!(ABL & 512)) {  // entry (s, w, v) = (nibble v at bits 4w..4w+3) * x^(-128 s), where bit
      // j of a value stands for QS[s] x^(31 - j)
     const uint32_t bs = threadIdx.x >> 7, w = (threadIdx.x >> 4) & 7u, v = threadIdx.x & 15u;
     uint32_t p = a.QS[0];
@@ -401,7 +405,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
     }
     qtl[bs * kQtStride + 16u * w + v] = e;
   }
-  if (threadIdx.x < 128) {  // entry 16 w + v: (nibble v at bits 4w..4w+3) * x^-32
+  if (!(ABL & 512) && threadIdx.x < 128) {  // entry 16 w + v: (nibble v at bits 4w..4w+3) * x^-32
     const uint32_t w = threadIdx.x >> 4, v = threadIdx.x & 15u;
     uint32_t t = 0;
 #pragma unroll
@@ -436,7 +440,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
 
   const LaneTab lt{(lane & 31) << 2, ((lane & 31) << 2) | 0x10000u};
   const uint32_t *qrow = qtl + s * kQtStride;
-  uint32_t *slots = tzl + kTzWords + wid * kWaveWords;
+  uint32_t *slots = tzl + kTzW + wid * kWaveWords;
   uint32_t *dring = slots + kSlots;
   uint32_t *fifo = dring + 2 * kBlk;
   const uint64_t npos = 8ull * NG;
@@ -545,7 +549,8 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
     }
 #pragma unroll
     for (uint32_t h = 0; h < kSlots / 64; ++h)  // slots past `valid` fall outside the range check
-      __builtin_amdgcn_raw_buffer_store_b32(slots[64 * h + lane], ro, 4u * (64 * h + lane), 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(slots[64 * h + lane], ro, 4u * (64 * h + lane), 0,
+                                            (ABL & 1024) ? 2 : (ABL & 2048) ? 0 : (ABL & 4096) ? 17 : 16);
   };
   auto finish = [&]() {
     uint32_t R;
@@ -593,42 +598,51 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   // pass found every strided-chain packet word-aligned in start and length
   // (a per-group choice inside the loop made the compiler rotate the load
   // ring through copies and drain vmcnt(0) at the loop head).
+  // The fold keeps xr = r ^ (the current line's word), the lookup input: the
+  // XOR with the next line's word rides in the step's last 3-input XOR (as in
+  // the SCK), 4 VALU per line fewer.  An edge line corrects xr by
+  // w ^ masked(w) on its own step; a group's last line leaves the next
+  // group's first word alone in xr (its chains start from zero).
+  uint32_t xr[4] = {ring[0][0], ring[0][1], ring[0][2], ring[0][3]};
   auto fold_loop = [&](auto words) {
   bool done = false;
   while (!done) {
 #pragma unroll
     for (int u = 0; u < D; ++u) {
       __builtin_amdgcn_sched_barrier(0);
-      u32x4 w = ring[u];
+      const u32x4 wn = ring[(u + 1) % D];  // the next line, raw
       if (!(ABL & 8) && ((fd_k < fd_hl) | (fd_k + 1 == fd_L))) {  // wave-uniform
-        // (A cheaper keep-only branch for tail lines made the compiler copy
-        // the ring register and wait for it, vmcnt(0).)
+        const u32x4 wc = ring[u];
         const int rel0 = (int)(128u * fd_k + 16u * s) - (int)fd_a;
         if constexpr (decltype(words)::value) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) w[i] = edge_word_aligned(w[i], rel0 + 4 * i, (int)fd_M);
+          for (int i = 0; i < 4; ++i) xr[i] = xor3(xr[i], wc[i], edge_word_aligned(wc[i], rel0 + 4 * i, (int)fd_M));
         } else {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) w[i] = edge_word(w[i], rel0 + 4 * i, (int)fd_M);
+          for (int i = 0; i < 4; ++i) xr[i] = xor3(xr[i], wc[i], edge_word(wc[i], rel0 + 4 * i, (int)fd_M));
         }
       }
+      uint32_t t[4][4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const uint32_t x = r[i] ^ w[i];
         if (ABL & 1) {
-          r[i] = __builtin_amdgcn_perm(x, lt.lo0, 0x0C0C0400u) ^ (x >> 7);
+          t[i][0] = __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0400u);
+          t[i][1] = xr[i] >> 7;
+          t[i][2] = 0u;
+          t[i][3] = 0u;
         } else {
-          const uint32_t t3 = lds_at(tab, __builtin_amdgcn_perm(x, lt.lo0, 0x0C0C0400u));
-          const uint32_t t2 = lds_at(tab, __builtin_amdgcn_perm(x, lt.lo0, 0x0C0C0500u) + 128);
-          const uint32_t t1 = lds_at(tab, __builtin_amdgcn_perm(x, lt.lo1, 0x0C020600u));
-          const uint32_t t0 = lds_at(tab, __builtin_amdgcn_perm(x, lt.lo1, 0x0C020700u) + 128);
-          r[i] = xor3(t3, t2, t1 ^ t0);
+          t[i][0] = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0400u));
+          t[i][1] = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0500u) + 128);
+          t[i][2] = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo1, 0x0C020600u));
+          t[i][3] = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo1, 0x0C020700u) + 128);
         }
       }
       if (++fd_k == fd_L) {  // wave-uniform: group fd_q folded
+#pragma unroll
+        for (int i = 0; i < 4; ++i) r[i] = xor3(t[i][0], t[i][1], t[i][2] ^ t[i][3]);
         finish();
 #pragma unroll
-        for (int i = 0; i < 4; ++i) r[i] = 0u;
+        for (int i = 0; i < 4; ++i) xr[i] = wn[i];
         fd_k = 0;
         if (fd_q + 1 < q_end) {
           ++fd_q;
@@ -638,6 +652,9 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
           done = true;
           fd_L = 0xFFFFFFFFu;
         }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) xr[i] = xor3(t[i][0], t[i][1], xor3(t[i][2], t[i][3], wn[i]));
       }
       // Refill after folding: the FIFO entry the fold just read may be
       // rewritten by this step's load-cursor advance.

@@ -60,6 +60,16 @@ int main(int argc, char **argv) {
       rep(nm, timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<8>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10), b);
       snprintf(nm, sizeof nm, "%s rsck no stores", tag);
       rep(nm, timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<16>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10), b);
+      snprintf(nm, sizeof nm, "%s rsck no finish, 192 slots", tag);
+      rep(nm, timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<2 | 512>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10), b);
+      snprintf(nm, sizeof nm, "%s rsck no finish, no global stores", tag);
+      rep(nm, timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<2 | 32>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10), b);
+      snprintf(nm, sizeof nm, "%s rsck no finish, nt stores", tag);
+      rep(nm, timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<2 | 1024>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10), b);
+      snprintf(nm, sizeof nm, "%s rsck no finish, default-policy stores", tag);
+      rep(nm, timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<2 | 2048>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10), b);
+      snprintf(nm, sizeof nm, "%s rsck no finish, sc0 sc1 stores", tag);
+      rep(nm, timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<2 | 4096>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10), b);
       snprintf(nm, sizeof nm, "%s rsck no global stores", tag);
       rep(nm, timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<32>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10), b);
       snprintf(nm, sizeof nm, "%s rsck memory path, no edges, no stores", tag);
@@ -132,6 +142,11 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&d_off, 8 * off.size())); CK(hipMalloc(&d_len, 4 * len.size()));
     CK(hipMemcpy(d_off, off.data(), 8 * off.size(), hipMemcpyHostToDevice));
     CK(hipMemcpy(d_len, len.data(), 4 * len.size(), hipMemcpyHostToDevice));
+    if (getenv("SYNTH")) {  // the bench's bytes: RoCEv2 headers from the P4 template, mix64 payload
+      SynthArgs sa{}; sa.buf = buf; sa.seed = 0x5EED; sa.first = 0; sa.count = off.size(); sa.off = d_off; sa.len = d_len;
+      CK(launch_synth_ragged(sa, 0)); CK(hipDeviceSynchronize());
+      printf("(synthetic RoCEv2 packets)\n");
+    }
     printf("mix: %zu packets, %llu B (%llu B in 1/4 KiB packets)\n", off.size(), (unsigned long long)pos, (unsigned long long)big);
     ragged("mix", off.size(), d_off, d_len, 0, (double)big);
   }
