@@ -277,8 +277,11 @@ __global__ __launch_bounds__(kPassBlock) void rsck_scatter(RsckArgs a) {
         const bool small = c <= (uint32_t)kRsBigBase;
         const uint64_t psb = small ? sps0[c] : 0u;
         const uint32_t bk = sbk[c];
-        a.desc[pos] = d;
-        a.pos_of[i] = pos;
+        // streaming stores: the fold that follows reads these once, and dirty
+        // lines left in the caches would be written back into its read stream
+        __builtin_nontemporal_store(d.lo, &a.desc[pos].lo);
+        __builtin_nontemporal_store(d.hi, &a.desc[pos].hi);
+        __builtin_nontemporal_store(pos, &a.pos_of[i]);
         if (small && a.piece) a.ps[pos] = psb + (uint64_t)(pos - bk) * (c - 1u);
         const uint32_t end = send[c];
         if (pos + 1 == end)  // the class's last packet pads its group with copies of itself
