@@ -31,7 +31,7 @@ int main(int argc, char **argv) {
     for (auto &v : h) { x ^= x << 13; x ^= x >> 7; x ^= x << 17; v = x; }
     CK(hipMemcpy(buf, h.data(), bytes, hipMemcpyHostToDevice));
   }
-  uint32_t *out; CK(hipMalloc(&out, 4ull * (8u << 20)));
+  uint32_t *out; CK(hipMalloc(&out, 4ull * (17u << 20)));
   uint32_t *tzb; CK(hipMalloc(&tzb, 4 * 1024)); CK(hipMemset(tzb, 0x35, 4 * 1024));
   auto rep = [&](const char *nm, float ms, double b) { printf("%-44s %8.1f us  %7.1f GB/s\n", nm, ms * 1e3, b / (ms * 1e-3) / 1e9); };
 
@@ -113,22 +113,25 @@ int main(int argc, char **argv) {
     for (int i = 0; i < 300; ++i) hipLaunchKernelGGL((icrc_sck_kernel<32, 0, 8, false, false, true>), dim3(grid), dim3(kBlock), 0, 0, s);
     CK(hipDeviceSynchronize());
   }
-  const bool mix_only = argc > 1;
+  const bool mix_only = argc > 1 && argv[1][0] == 'm';  // "mix": the mixed batch only
+  const bool u256_only = argc > 1 && argv[1][0] == 'u';  // "u256": uniform 256 B only
   // uniform 4 KiB and 1 KiB, natural order (SCK reference on the same bytes)
-  for (uint32_t n : {4096u, 1024u}) {
+  for (uint32_t n : {4096u, 1024u, 256u}) {
     if (mix_only) break;
+    if (u256_only && n != 256) continue;
     const uint64_t count = bytes / n;
     SckArgs s{}; s.base = buf; s.count = count; s.out = out; s.n = n;
     for (int j = 0; j < 32; ++j) s.XB[j] = 0x85EBCA6Bu * (j + 3);
     for (int k = 0; k < 8; ++k) s.QS[k] = 0x9E3779B9u * (k + 1);
     char tag[32]; snprintf(tag, sizeof tag, "%u B x %llu", n, (unsigned long long)count);
     char nm[128]; snprintf(nm, sizeof nm, "%s sck", tag);
-    if (n == 4096) rep(nm, timeit([&] { hipLaunchKernelGGL((icrc_sck_kernel<32, 0, 8, false, false, true>), dim3(grid), dim3(kBlock), 0, 0, s); }, 10), (double)bytes);
+    if (n == 256) {}
+    else if (n == 4096) rep(nm, timeit([&] { hipLaunchKernelGGL((icrc_sck_kernel<32, 0, 8, false, false, true>), dim3(grid), dim3(kBlock), 0, 0, s); }, 10), (double)bytes);
     else rep(nm, timeit([&] { hipLaunchKernelGGL((icrc_sck_kernel<8, 0, 8, false, false, true>), dim3(grid), dim3(kBlock), 0, 0, s); }, 10), (double)bytes);
     ragged(tag, count, nullptr, nullptr, n, (double)bytes);
   }
   // C4 mix: 64/256/1024/4096 uniformly, packed, within the 4 GiB buffer
-  {
+  if (!u256_only) {
     std::vector<uint64_t> off; std::vector<uint32_t> len;
     uint64_t x = 0x1234567ull, pos = 0, big = 0;
     const uint32_t sizes[4] = {64, 256, 1024, 4096};
