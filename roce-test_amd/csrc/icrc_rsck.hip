@@ -341,17 +341,6 @@ __device__ __forceinline__ uint32_t edge_word(uint32_t w, int rel, int M) {
   return ((w & keep) | orm) ^ sx;
 }
 
-// The same for a word-aligned packet start and length (rel and M multiples
-// of 4): whole-word keep, the mask words of offsets 0, 8, 24, 32, the seed at 0.
-__device__ __forceinline__ uint32_t edge_word_aligned(uint32_t w, int rel, int M) {
-  // Arithmetic masks, not ternaries: a select chain on rel lowers to a
-  // divergent switch (and a vmcnt(0) drain at the loop head).
-  const uint32_t keep = (uint32_t)((unsigned)rel < (unsigned)M) * 0xFFFFFFFFu;
-  const uint32_t z0 = (uint32_t)(rel == 0) * 0xFFFFFFFFu;
-  const uint32_t orm = (z0 & kMaskW0) | ((uint32_t)(rel == 8) * kMaskW2) | ((uint32_t)(rel == 24) * kMaskW6) |
-                       ((uint32_t)(rel == 32) * kMaskW8);
-  return ((w & keep) | orm) ^ (z0 & kSeed);  // M >= 40: the mask words are always kept
-}
 
 }  // namespace
 
@@ -377,11 +366,12 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   // wave = 157.7 KiB.
   // (ABL 512, timing only, with 2: 192 result slots per wave in the room of
   // the finish tables.)
-  constexpr uint32_t kQtStride = 132, kSmallWords = (ABL & 512) ? 0 : 128 + 8 * kQtStride;  // 1184: a multiple of 32 words
+  constexpr uint32_t kQtStride = 132, kSmallWords = (ABL & 512) ? 0 : 128 + 8 * kQtStride + 32;  // 1216: a multiple of 32 words
   constexpr uint32_t kTzW = (ABL & 512) ? 0 : kTzWords;
   __shared__ uint32_t lds[kSmallWords + kLdsWords + kTzW + kWaves * kWaveWords];
   uint32_t *xtl = lds;
   uint32_t *qtl = lds + 128;
+  uint32_t *etl = lds + 128 + 8 * kQtStride;  // whole-word head masks: (or, xor) of word k = rel / 4
   uint32_t *tab = lds + kSmallWords;
   uint32_t *tzl = tab + kLdsWords;
 
@@ -407,6 +397,12 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
       p = gf_mulx(p);
     }
     qtl[bs * kQtStride + 16u * w + v] = e;
+  }
+  if (!(ABL & 512) && threadIdx.x < 16) {  // word k of the header (rel = 4k): IPv4 invariant fields -> 0xFF, the seed at 0
+    const uint32_t k = threadIdx.x;
+    const uint32_t orm = k == 0 ? kMaskW0 : k == 2 ? kMaskW2 : k == 6 ? kMaskW6 : k == 8 ? kMaskW8 : 0u;
+    etl[2 * k] = orm;
+    etl[2 * k + 1] = k == 0 ? kSeed : 0u;
   }
   if (!(ABL & 512) && threadIdx.x < 128) {  // entry 16 w + v: (nibble v at bits 4w..4w+3) * x^-32
     const uint32_t w = threadIdx.x >> 4, v = threadIdx.x & 15u;
@@ -619,7 +615,17 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
         const int rel0 = (int)(128u * fd_k + 16u * s) - (int)fd_a;
         if constexpr (decltype(words)::value) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) xr[i] = xor3(xr[i], wc[i], edge_word_aligned(wc[i], rel0 + 4 * i, (int)fd_M));
+          for (int i = 0; i < 4; ++i) {
+            // whole words: keep 0 <= rel < M by sign arithmetic (compare +
+            // select pairs needed hazard NOPs), head masks from a 16-entry
+            // table (rel >= 40 and rel < 0 index the zero entry 15)
+            const int rel = rel0 + 4 * i;
+            const uint32_t keep = (uint32_t)(((rel - (int)fd_M) & ~rel) >> 31);
+            const uint32_t k = __builtin_elementwise_min((uint32_t)rel >> 2, 15u);
+            typedef uint32_t u32x2e __attribute__((ext_vector_type(2)));
+            const u32x2e e = *reinterpret_cast<const u32x2e *>(etl + 2 * k);
+            xr[i] = xor3(xr[i], wc[i], ((wc[i] & keep) | e[0]) ^ e[1]);
+          }
         } else {
 #pragma unroll
           for (int i = 0; i < 4; ++i) xr[i] = xor3(xr[i], wc[i], edge_word(wc[i], rel0 + 4 * i, (int)fd_M));
