@@ -115,10 +115,30 @@ int main(int argc, char **argv) {
   }
   const bool mix_only = argc > 1 && argv[1][0] == 'm';  // "mix": the mixed batch only
   const bool u256_only = argc > 1 && argv[1][0] == 'u';  // "u256": uniform 256 B only
+  const bool s1k = argc > 1 && argv[1][0] == 's';        // "s1k": uniform 1 KiB, full vs no global stores only (PMC)
   // uniform 4 KiB and 1 KiB, natural order (SCK reference on the same bytes)
   for (uint32_t n : {4096u, 1024u, 256u}) {
     if (mix_only) break;
     if (u256_only && n != 256) continue;
+    if (s1k) {
+      if (n != 1024) continue;
+      RsckArgs a{};
+      a.base = buf; a.stride = n; a.count = bytes / n; a.fixed_len = n; a.out = out; a.tzb = tzb;
+      for (int j = 0; j < 32; ++j) a.XB[j] = 0x85EBCA6Bu * (j + 3);
+      for (int k = 0; k < 8; ++k) a.QS[k] = 0x9E3779B9u * (k + 1);
+      void *ws; CK(hipMalloc(&ws, rs_workspace_bytes(a.count)));
+      CK(rs_zero_counters(ws, 0));
+      rs_bind_workspace(a, ws);
+      const uint64_t want = (a.count + kPassBlock - 1) / kPassBlock;
+      launch_passes(a, (int)(want < kPassBlocks ? want : kPassBlocks), 0);
+      CK(hipDeviceSynchronize());
+      for (int r = 0; r < 3; ++r) {
+        rep("1 KiB full", timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, 0, a); }, 5), (double)bytes);
+        rep("1 KiB no global stores", timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<32>), dim3(grid), dim3(kBlock), 0, 0, a); }, 5), (double)bytes);
+      }
+      CK(hipFree(ws));
+      return 0;
+    }
     const uint64_t count = bytes / n;
     SckArgs s{}; s.base = buf; s.count = count; s.out = out; s.n = n;
     for (int j = 0; j < 32; ++j) s.XB[j] = 0x85EBCA6Bu * (j + 3);
