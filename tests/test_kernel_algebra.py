@@ -287,3 +287,92 @@ def test_small_lane_static_head_window():
             rel4 = M - 16 * Kmax + 64
             assert rel4 >= 40, (M, Kmax)
             assert M - 16 * Kmax >= -24
+
+
+def _nib_mul(table, v):
+    """icrc_rsck.hip nib_mul: v * (the table's constant) by 8 nibble lookups."""
+    r = 0
+    for w in range(8):
+        r ^= table[16 * w + ((v >> (4 * w)) & 15)]
+    return r
+
+
+def test_ragged_finish_nibble_tables():
+    """The ragged fold's finish tables (icrc_rsck_kernel): the x^-32 table
+    entry (w, v) = (nibble v at bits 4w..4w+3) * x^-32, and lane slot s's
+    table built the way the kernel builds it -- p = QS[s] x^(28 - 4w), then
+    one x per bit from bit 4w + 3 down -- turn 8 lookups into the GF(2)
+    multiply, so Horner and the x^(-128 s) alignment are unchanged."""
+    rng = random.Random(17)
+    X = _xinv8n_fast(4)
+    xt = [o.gf_mul(X, v << (4 * w)) for w in range(8) for v in range(16)]
+    mulx = lambda p: o.gf_mul(p, ONE >> 1)  # noqa: E731
+    for s in range(8):
+        qs = _xinv8n_fast(16 * s)  # host: QS[s] = x^(-128 s)
+        qt = []
+        for w in range(8):
+            for v in range(16):
+                p = qs
+                for _ in range(28 - 4 * w):
+                    p = mulx(p)
+                e = 0
+                for b in (3, 2, 1, 0):
+                    e ^= p if (v >> b) & 1 else 0
+                    p = mulx(p)
+                qt.append(e)
+        for _ in range(20):
+            u = rng.getrandbits(32)
+            assert _nib_mul(qt, u) == o.gf_mul(u, qs)
+    for _ in range(200):
+        u = rng.getrandbits(32)
+        assert _nib_mul(xt, u) == o.gf_mul(u, X)
+
+
+def test_ragged_tz_bases_compact():
+    """Basis word 4q of x^(-8 tz) is x^(-8 tz) x^(31 - 4q) = x^(31 - 4 (2 tz + q)),
+    so the kernel's table needs one entry per m = 2 tz + q (264 words, host
+    icrc_api.cpp) instead of 128 x 8: every split of m gives the same word."""
+    table = {}
+    for tz in range(128):
+        c = _xinv8n_fast(tz)
+        for q in range(8):
+            table.setdefault(2 * tz + q, set()).add(o.gf_mul(c, 1 << (4 * q)))
+    assert len(table) == 262 and all(len(v) == 1 for v in table.values())
+    for m, (v,) in table.items():  # the host's split: tz = min(m >> 1, 127), q = m - 2 tz
+        tz = min(m >> 1, 127)
+        assert o.gf_mul(_xinv8n_fast(tz), 1 << (4 * (m - 2 * tz))) == v
+
+
+def test_ragged_whole_word_edges():
+    """Whole-word edge masking of the ragged fold (word-aligned packets): keep
+    = sign of ((rel - M) & ~rel) for 0 <= rel < M, then the head table's
+    (or, xor) pair at k = min(rel >> 2, 15) -- equal to the bytewise rule:
+    bytes outside [0, M) zeroed, the invariant fields forced to 0xFF, the seed
+    XORed into bytes 0..3."""
+    rng = random.Random(19)
+    mask_off = {1, 8, 10, 11, 26, 27, 32}
+    orm = [0] * 16
+    for k in range(10):
+        for b in range(4):
+            if 4 * k + b in mask_off:
+                orm[k] |= 0xFF << (8 * b)
+    seed = [SEED_REG] + [0] * 15
+    for _ in range(3000):
+        M = 4 * rng.randrange(10, 1200)
+        rel = 4 * rng.randrange(-40, 1300)
+        w = rng.getrandbits(32)
+        x = (rel - M) & ~rel & 0xFFFFFFFF
+        keep = 0xFFFFFFFF if x >> 31 else 0
+        k = min((rel & 0xFFFFFFFF) >> 2, 15)
+        got = ((w & keep) | orm[k]) ^ seed[k]
+        want = bytearray(w.to_bytes(4, "little"))
+        for b in range(4):
+            off = rel + b
+            if not 0 <= off < M:
+                want[b] = 0
+            elif off in mask_off:
+                want[b] = 0xFF
+        wv = int.from_bytes(want, "little")
+        if rel == 0:
+            wv ^= SEED_REG
+        assert got == wv, (rel, M)
