@@ -75,6 +75,12 @@ def parse(argv=None):
     # (profiles/r02/ramp_probe.jsonl); ricrc_prime keeps the device busy this
     # long right before the warmup (untimed).
     ap.add_argument("--prime-ms", type=float, default=25.0)
+    # HIP events bracket the K timed steps as a whole (kernel_ms = their span
+    # / K, inter-kernel gaps included: a conservative launch duration); with
+    # --step-events every step's kernel(s) get their own pair -- two event
+    # records between consecutive kernels cost ~5 us of GPU time per step
+    # (each is a release to system scope), which the wall-clock value pays.
+    ap.add_argument("--step-events", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="wall budget of the CPU baseline")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--plan-only", action="store_true",
@@ -437,15 +443,21 @@ def main(argv=None):
     for i in range(args.warmup):
         step(i)
     drain()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
+    n_ev = args.steps if args.step_events else 1
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_ev)]
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i, evs[i])
+    if args.step_events:
+        for i in range(args.steps):
+            step(i, evs[i])
+    else:
+        evs[0][0].record(stream)
+        for i in range(args.steps):
+            step(i)
+        evs[0][1].record(stream)
     drain()
     torch.cuda.synchronize()
     if distributed:

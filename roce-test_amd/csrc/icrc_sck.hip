@@ -44,22 +44,33 @@ namespace ricrc {
 // 1 no table fold, 2 no finish, 8 no global loads, 16 no stores, 64 per-wave
 // start/end s_memrealtime stamps into a.stamps.
 // D: lines in flight per wave; QLDS: lane bases read from LDS instead of 32
-// VGPRs (frees registers for a deeper ring); XT: the Horner multiplies by
-// x^-32 through a conflict-free nibble table in LDS.
+// VGPRs (frees registers for a deeper ring); XT 1: the Horner multiplies by
+// x^-32 through a nibble table in LDS, 32 copies (one per bank); XT 2 (the
+// product): every finish multiply through nibble tables, ONE copy each (the
+// 16 entries of a nibble position sit in 16 banks: any lane pattern is
+// conflict-free) -- x^-32 (128 words) and, per lane slot s, x^(-32 (4 s + 1))
+// (8 x 132 words) -- so the lane-basis multiply is 8 lookups instead of 32
+// bit-select pairs and the 32 basis VGPRs are free; the finish tables sit at
+// the bottom of LDS so each lookup's constant part is a ds_read offset.
 // =======================================================================
 // FAM: the address family's invariant masks, applied natively on line 0
 // (kFamV4 = the reference's IPv4 masks; kFamV6; kFamAuto per packet from the
 // IP version nibble, broadcast from lane 8 g to the packet's 8 lanes).
-template <int L, int ABL, int D = 8, bool QLDS = false, bool DYN = false, bool XT = false, int FAM = kFamV4>
+template <int L, int ABL, int D = 8, bool QLDS = false, bool DYN = false, int XT = 0, int FAM = kFamV4>
 __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
-  // 128 KiB of tables + result slots per wave (+ DYN: the slots' group
-  // indices; QLDS: the 8 lane bases; XT: 16 KiB nibble table of x^-32).
-  constexpr uint32_t kSlots = (DYN && XT) ? 128 : (QLDS || DYN || XT) ? 256 : 512;
+  // [XT 2: finish tables] 128 KiB of tables + result slots per wave (+ DYN:
+  // the slots' group indices; QLDS: the 8 lane bases; XT 1: 16 KiB nibble
+  // table of x^-32).
+  constexpr uint32_t kSlots = (DYN && XT == 1) ? 128 : (QLDS || DYN || XT) ? 256 : 512;
   constexpr uint32_t kRoundMask = kSlots / 8 - 1;  // groups per round of slots - 1
   constexpr uint32_t kWaveWords = kSlots + (DYN ? kSlots / 8 : 0);
   constexpr uint32_t kQStride = 36;  // words per lane-slot basis (padded: conflict-free ds_read_b128)
-  constexpr uint32_t kXtWord = kLdsWords + kWaves * kWaveWords + (QLDS ? 8 * kQStride : 0);
-  __shared__ uint32_t lds[kXtWord + (XT ? 128 * 32 : 0)];
+  constexpr uint32_t kQtStride = 132;  // XT 2: words per lane slot's nibble table (padded across banks)
+  constexpr uint32_t kFin = XT == 2 ? 128 + 8 * kQtStride + 32 : 0;  // XT 2 finish tables: a multiple of 32 words
+  constexpr uint32_t kXtWord = kFin + kLdsWords + kWaves * kWaveWords + (QLDS ? 8 * kQStride : 0);
+  __shared__ uint32_t lds[kXtWord + (XT == 1 ? 128 * 32 : 0)];
+  uint32_t *tab = lds + kFin;  // slice-by-4 tables
+  const uint32_t *xtl = lds, *qtl = lds + 128;  // XT 2
 
   // D: lines in flight per wave
   static_assert(L % D == 0 || D == L, "ring indices must repeat every group");
@@ -148,8 +159,31 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
     ring[k] = load(k < L ? qcur : qnext, (uint32_t)(k % L));
   }
   __builtin_amdgcn_sched_barrier(0);
-  table_store(lds, tab_v);
-  if (XT) {  // entry (w, v) = (nibble v at bits 4w..4w+3) * x^-32, 32 copies: 8 threads x 4 copies each
+  table_store(tab, tab_v);
+  if (XT == 2) {
+    if (threadIdx.x < 128) {  // entry 16 w + v: (nibble v at bits 4w..4w+3) * x^-32
+      const uint32_t w = threadIdx.x >> 4, v = threadIdx.x & 15u;
+      uint32_t t = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) t ^= ((v >> b) & 1u) ? a.XB[4 * w + b] : 0u;
+      lds[threadIdx.x] = t;
+    }
+    // slot s, entry 16 w + v: (nibble v at bits 4w..4w+3) * QS[s], where bit
+    // j of a value stands for x^(31 - j)
+    const uint32_t bs = threadIdx.x >> 7, w = (threadIdx.x >> 4) & 7u, v = threadIdx.x & 15u;
+    uint32_t p = a.QS[0];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) p = bs == (uint32_t)k ? a.QS[k] : p;
+    for (uint32_t t = 0; t < 28u - 4u * w; ++t) p = gf_mulx(p);  // bit 4w + 3
+    uint32_t e = 0;
+#pragma unroll
+    for (int b = 3; b >= 0; --b) {
+      e ^= ((v >> b) & 1u) ? p : 0u;
+      p = gf_mulx(p);
+    }
+    lds[128 + bs * kQtStride + 16u * w + v] = e;
+  }
+  if (XT == 1) {  // entry (w, v) = (nibble v at bits 4w..4w+3) * x^-32, 32 copies: 8 threads x 4 copies each
     const uint32_t e = threadIdx.x >> 3, w = e >> 4, v = e & 15u;
     uint32_t t = 0;
 #pragma unroll
@@ -162,11 +196,11 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
 #pragma unroll
     for (int k = 1; k < 8; ++k) v = bs == (uint32_t)k ? a.QS[k] : v;
     for (uint32_t t = j; t < 31; ++t) v = gf_mulx(v);
-    lds[kLdsWords + kWaves * kWaveWords + bs * kQStride + j] = v;
+    lds[kFin + kLdsWords + kWaves * kWaveWords + bs * kQStride + j] = v;
   }
   __syncthreads();
 
-  uint32_t *slots = lds + kLdsWords + wid * kWaveWords;
+  uint32_t *slots = lds + kFin + kLdsWords + wid * kWaveWords;
   const uint32_t xt_lane = 4u * kXtWord + ((lane & 31u) << 2);  // byte address of the lane's XT copy
   uint32_t *gtab = slots + kSlots;  // DYN: absolute group of each slot row
   const LaneTab lt{(lane & 31) << 2, ((lane & 31) << 2) | 0x10000u};
@@ -179,8 +213,9 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
   const uint32_t m6w3 = s == 2 ? kMaskV6W11 : 0u;
   const uint32_t keep3 = s == 7 ? 0u : 0xFFFFFFFFu;                  // the trailer word
   uint32_t Q[32];  // lane basis in registers (!QLDS)
-  const uint32_t *qlds = lds + kLdsWords + kWaves * kWaveWords + s * kQStride;
-  if (!QLDS) {
+  const uint32_t *qlds = lds + kFin + kLdsWords + kWaves * kWaveWords + s * kQStride;
+  const uint32_t *qrow = qtl + s * kQtStride;  // XT 2
+  if (!QLDS && XT != 2) {
     uint32_t qs = 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) qs = s == (uint32_t)k ? a.QS[k] : qs;
@@ -212,7 +247,11 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) f.acc[k] = 0u;
     }
-    if (sl < 6 && XT) {  // 4 nibble lookups: 2 VALU + 1 ds_read_b32 each instead of 8 bfe/bitop3 pairs
+    if (XT == 2) {  // 4 nibble lookups of one table copy (x^-32, then the lane slot's)
+      const uint32_t *t = sl < 6 ? xtl : qrow;
+#pragma unroll
+      for (int w = 4 * (sl & 1); w < 4 * (sl & 1) + 4; ++w) f.acc[w & 3] ^= t[16 * w + __builtin_amdgcn_ubfe(f.u, 4 * w, 4)];
+    } else if (sl < 6 && XT) {  // 4 nibble lookups: 2 VALU + 1 ds_read_b32 each instead of 8 bfe/bitop3 pairs
 #pragma unroll
       for (int w = 4 * (sl & 1); w < 4 * (sl & 1) + 4; ++w) {
         const uint32_t nib = (f.u >> (4 * w)) & 15u;
@@ -334,10 +373,10 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
           t[i][2] = x[i] * 3u;
           t[i][3] = 0u;
         } else {
-          t[i][0] = lds_at(lds, __builtin_amdgcn_perm(x[i], lt.lo0, 0x0C0C0400u));
-          t[i][1] = lds_at(lds, __builtin_amdgcn_perm(x[i], lt.lo0, 0x0C0C0500u) + 128);
-          t[i][2] = lds_at(lds, __builtin_amdgcn_perm(x[i], lt.lo1, 0x0C020600u));
-          t[i][3] = lds_at(lds, __builtin_amdgcn_perm(x[i], lt.lo1, 0x0C020700u) + 128);
+          t[i][0] = lds_at(tab, __builtin_amdgcn_perm(x[i], lt.lo0, 0x0C0C0400u));
+          t[i][1] = lds_at(tab, __builtin_amdgcn_perm(x[i], lt.lo0, 0x0C0C0500u) + 128);
+          t[i][2] = lds_at(tab, __builtin_amdgcn_perm(x[i], lt.lo1, 0x0C020600u));
+          t[i][3] = lds_at(tab, __builtin_amdgcn_perm(x[i], lt.lo1, 0x0C020700u) + 128);
         }
       }
       // The previous group's finish, in the shadow of the reads (for j = 0 it
@@ -392,13 +431,13 @@ hipError_t launch_sck_fam(const SckArgs &a, int grid, hipStream_t st) {
   const dim3 g(grid), b(kBlock);
   // XT (x^-32 nibble table): 0.735 -> 0.703 ms on 4 M x 1 KiB, ~1 % on 1 M x 4 KiB (tools/microbench/sck_abl.hip).
   if (a.dynamic) {
-    if (a.n == 4096) hipLaunchKernelGGL((icrc_sck_kernel<32, 0, 8, false, true, true, FAM>), g, b, 0, st, a);
-    else if (a.n == 2048) hipLaunchKernelGGL((icrc_sck_kernel<16, 0, 8, false, true, true, FAM>), g, b, 0, st, a);
-    else if (a.n == 1024) hipLaunchKernelGGL((icrc_sck_kernel<8, 0, 8, false, true, true, FAM>), g, b, 0, st, a);
+    if (a.n == 4096) hipLaunchKernelGGL((icrc_sck_kernel<32, 0, 8, false, true, 2, FAM>), g, b, 0, st, a);
+    else if (a.n == 2048) hipLaunchKernelGGL((icrc_sck_kernel<16, 0, 8, false, true, 2, FAM>), g, b, 0, st, a);
+    else if (a.n == 1024) hipLaunchKernelGGL((icrc_sck_kernel<8, 0, 8, false, true, 2, FAM>), g, b, 0, st, a);
     else return hipErrorInvalidValue;
-  } else if (a.n == 4096) hipLaunchKernelGGL((icrc_sck_kernel<32, 0, 8, false, false, true, FAM>), g, b, 0, st, a);
-  else if (a.n == 2048) hipLaunchKernelGGL((icrc_sck_kernel<16, 0, 8, false, false, true, FAM>), g, b, 0, st, a);
-  else if (a.n == 1024) hipLaunchKernelGGL((icrc_sck_kernel<8, 0, 8, false, false, true, FAM>), g, b, 0, st, a);
+  } else if (a.n == 4096) hipLaunchKernelGGL((icrc_sck_kernel<32, 0, 8, false, false, 2, FAM>), g, b, 0, st, a);
+  else if (a.n == 2048) hipLaunchKernelGGL((icrc_sck_kernel<16, 0, 8, false, false, 2, FAM>), g, b, 0, st, a);
+  else if (a.n == 1024) hipLaunchKernelGGL((icrc_sck_kernel<8, 0, 8, false, false, 2, FAM>), g, b, 0, st, a);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }

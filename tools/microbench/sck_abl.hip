@@ -7,7 +7,7 @@
 #include <stdlib.h>
 using namespace ricrc;
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s\n", hipGetErrorString(e)); exit(1); } } while (0)
-template <int L, int ABL, int D = 8, bool QL = false, bool XT = false> float run(SckArgs a, int grid, int reps) {
+template <int L, int ABL, int D = 8, bool QL = false, int XT = 0> float run(SckArgs a, int grid, int reps) {
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   for (int w = 0; w < 3; ++w) hipLaunchKernelGGL((icrc_sck_kernel<L, ABL, D, QL, false, XT>), dim3(grid), dim3(kBlock), 0, 0, a);
   CK(hipDeviceSynchronize()); CK(hipEventRecord(e0));
@@ -30,10 +30,15 @@ int main(int argc, char **argv) {
   for (int s = 0; s < 8; ++s) a.QS[s] = 0x9E3779B9u * (s + 1);
   const int grid = p.multiProcessorCount;
   auto rep = [&](const char *nm, float ms) { printf("%-36s %7.3f ms  %7.1f GB/s\n", nm, ms, 4294967296.0 / (ms * 1e-3) / 1e9); };
+  const bool quick = argc > 1 && argv[1][0] == 'x';  // "xt": finish-table variants only
   for (int r = 0; r < 2; ++r) {
+    rep("full XT1 (32-copy x^-32 table)", run<32, 0, 8, false, 1>(a, grid, 20));
+    rep("full XT2 (one-copy finish tables)", run<32, 0, 8, false, 2>(a, grid, 20));
+    rep("no loads XT1", run<32, 8, 8, false, 1>(a, grid, 20));
+    rep("no loads XT2", run<32, 8, 8, false, 2>(a, grid, 20));
+    rep("memory path XT2", run<32, 1 | 2, 8, false, 2>(a, grid, 20));
+    if (quick) continue;
     rep("full D8", run<32, 0>(a, grid, 20));
-    rep("full D8 XT", run<32, 0, 8, false, true>(a, grid, 20));
-    rep("no loads XT", run<32, 8, 8, false, true>(a, grid, 20));
     rep("no stores", run<32, 16>(a, grid, 20));
     rep("no fold (VALU stand-in)", run<32, 1>(a, grid, 20));
     rep("no finish", run<32, 2>(a, grid, 20));
@@ -42,16 +47,23 @@ int main(int argc, char **argv) {
     rep("no loads, no finish (fold only)", run<32, 8 | 2>(a, grid, 20));
     rep("no loads, no fold (finish only)", run<32, 8 | 1>(a, grid, 20));
   }
-  // 1 KiB packets (C2): L = 8, the ring spans exactly one group
-  SckArgs b = a; b.n = 1024; b.count = 4ull << 20;
-  for (int r = 0; r < 2; ++r) {
-    rep("L8 full", run<8, 0>(b, grid, 20));
-    rep("L8 full XT", run<8, 0, 8, false, true>(b, grid, 20));
-    rep("L8 no loads XT", run<8, 8, 8, false, true>(b, grid, 20));
-    rep("L8 no finish", run<8, 2>(b, grid, 20));
-    rep("L8 no fold", run<8, 1>(b, grid, 20));
-    rep("L8 memory path", run<8, 1 | 2>(b, grid, 20));
-    rep("L8 no loads", run<8, 8>(b, grid, 20));
+  // 1 KiB packets (C2): L = 8, the ring spans exactly one group; 4 M and 1 M packets
+  for (uint64_t cnt : {4ull << 20, 1ull << 20}) {
+    SckArgs b = a; b.n = 1024; b.count = cnt;
+    const double by = 1024.0 * cnt;
+    auto rep8 = [&](const char *nm, float ms) { printf("%-36s %7.3f ms  %7.1f GB/s  (%llu x 1 KiB)\n", nm, ms, by / (ms * 1e-3) / 1e9, (unsigned long long)cnt); };
+    for (int r = 0; r < 2; ++r) {
+      rep8("L8 full XT1", run<8, 0, 8, false, 1>(b, grid, 20));
+      rep8("L8 full XT2", run<8, 0, 8, false, 2>(b, grid, 20));
+      rep8("L8 no loads XT1", run<8, 8, 8, false, 1>(b, grid, 20));
+      rep8("L8 no loads XT2", run<8, 8, 8, false, 2>(b, grid, 20));
+      rep8("L8 memory path", run<8, 1 | 2, 8, false, 2>(b, grid, 20));
+      if (quick) continue;
+      rep8("L8 full", run<8, 0>(b, grid, 20));
+      rep8("L8 no finish", run<8, 2>(b, grid, 20));
+      rep8("L8 no fold", run<8, 1>(b, grid, 20));
+      rep8("L8 no loads", run<8, 8>(b, grid, 20));
+    }
   }
   return 0;
 }
