@@ -56,8 +56,20 @@ namespace ricrc {
 // FAM: the address family's invariant masks, applied natively on line 0
 // (kFamV4 = the reference's IPv4 masks; kFamV6; kFamAuto per packet from the
 // IP version nibble, broadcast from lane 8 g to the packet's 8 lanes).
-template <int L, int ABL, int D = 8, bool QLDS = false, bool DYN = false, int XT = 0, int FAM = kFamV4>
+// PL < L (super-groups, 1 and 2 KiB packets): the wave streams lines exactly
+// as for L-line packets -- a "super-packet" is S = L / PL consecutive packets,
+// a group 8 S packets (32 KiB for L = 32) -- but each lane's chains are
+// finished and restarted every PL lines, at the packet boundaries.  Load k of
+// a group then reads line k of 8 super-packets 4 KiB apart, the access
+// pattern of the 4 KiB packets, whose memory path alone streams ~8 % faster
+// than 8 packets of 1 KiB side by side (profiles/r02/sck_abl_xt1_vs_xt2.txt:
+// 0.628 ms per 4 GiB against 0.678 ms).  Sub-group m of a group (packets
+// 8 S Q + S g + m) is finished S times per group; its results land in the
+// slots in packet order, so the flush is unchanged.
+template <int L, int ABL, int D = 8, bool QLDS = false, bool DYN = false, int XT = 0, int FAM = kFamV4, int PL = L>
 __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
+  static_assert(L % PL == 0 && PL >= 8 && (PL == L || !DYN), "super-groups: static schedule, whole packets");
+  constexpr uint32_t S = L / PL;  // packets per super-packet
   // [XT 2: finish tables] 128 KiB of tables + result slots per wave (+ DYN:
   // the slots' group indices; QLDS: the 8 lane bases; XT 1: 16 KiB nibble
   // table of x^-32).
@@ -81,8 +93,8 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
 
   const uint64_t wave = (uint64_t)blockIdx.x * kWaves + wid;
   const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
-  const uint32_t G = (uint32_t)((a.count + 7) >> 3);
-  const uint64_t total = a.count * N;
+  const uint32_t G = (uint32_t)((a.count + 8 * S - 1) / (8 * S));  // groups (of 8 S packets)
+  const uint64_t total = a.count * (128u * PL);
   const uint32_t vo = (lane >> 3) * N + 16u * s;
 
   // The wave's sequence of groups.  Static: the contiguous block [g0, g1).
@@ -297,7 +309,7 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
         __builtin_amdgcn_raw_buffer_store_b32(slots[64 * h + lane], ro, live ? 4u * (8u * q + s) : 0x7FFFFFF0u, 0, 0);
       }
     } else {  // consecutive groups: coalesced
-      const uint64_t pb = ((uint64_t)g0 + j_lo) * 8u;
+      const uint64_t pb = ((uint64_t)g0 * S + j_lo) * 8u;
       const uint32_t valid = (j_end - j_lo) * 8u;  // slots written this round
       const uint32_t nout = (uint32_t)(a.count - pb < valid ? a.count - pb : valid);
       const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out + pb, 4u * nout);
@@ -318,21 +330,18 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
       sink ^= val;
       return;
     }
-    slots[((jf & kRoundMask) << 3) | (lane >> 3)] = val;
+    // sub-group jf's packet of lane group g: S (jf / S) * 8 + S g + jf % S in the round
+    slots[(((jf & kRoundMask) & ~(S - 1)) << 3) | ((lane >> 3) * S) | (jf & (S - 1))] = val;
     if (DYN) gtab[jf & kRoundMask] = qf;
   };
 
-  // Finish slices of the previous group ride in steps 0..7 (0..6 for L = 8,
-  // two in step 0), its result is written in the step after.
-  constexpr int kStoreStep = L >= 16 ? 8 : L - 1;
-  auto slice_step = [](int sl) constexpr { return L >= 16 ? sl : sl * (L - 1) / 8; };
-  static_assert(L >= 8, "finish needs 8 fold steps");
-  Fin pf{};
-  uint32_t qprev = 0;
-  uint32_t j = 0;
-  for (; qcur < G; ++j) {  // qcur: wave-uniform
-    u32x4 w = ring[0];
-    ring[0] = load(D < L ? qcur : qnext, (uint32_t)(D % L));
+  // Finish slices of the previous packet ride in its successor's steps 0..7
+  // (0..6 for PL = 8, two in step 0), its result is written in the step after.
+  constexpr int kStoreStep = PL >= 16 ? 8 : PL - 1;
+  auto slice_step = [](int sl) constexpr { return PL >= 16 ? sl : sl * (PL - 1) / 8; };
+  static_assert(PL >= 8, "finish needs 8 fold steps");
+  // A packet's first line: the family's invariant masks and the seed.
+  auto first_line = [&](u32x4 w, uint32_t (&x)[4]) {
     if constexpr (FAM == kFamV4) {
       w[0] = or_xor(w[0], mw0, xw0);
       w[2] |= mw2;
@@ -348,20 +357,37 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
       w[2] |= ~v6 & mw2;
       w[3] |= v6 & m6w3;
     }
-    uint32_t x[4] = {w[0], w[1], w[2], w[3]};  // chain register (0) ^ line-0 word
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[i] = w[i];  // chain register (0) ^ line-0 word
+  };
+  Fin pf{};
+  uint32_t qprev = 0;
+  uint32_t j = 0;  // the wave's packets of lane group 0 started so far (sub-groups)
+  while (qcur < G) {  // qcur: wave-uniform
+    const u32x4 w = ring[0];
+    ring[0] = load(D < L ? qcur : qnext, (uint32_t)(D % L));
+    uint32_t x[4];
+    first_line(w, x);
     uint32_t tr = 0;
 #pragma unroll
     for (int k = 0; k < L; ++k) {
+      const int kp = k % PL;              // line within the packet
+      const bool last = kp == PL - 1;     // the packet's last line
       // Fence each step: the scheduler would otherwise hoist the whole
       // group's ring refills to the top and drain vmcnt to zero there.
       __builtin_amdgcn_sched_barrier(0);
-      u32x4 wn = {0u, 0u, 0u, 0u};
+      u32x4 wn = {0u, 0u, 0u, 0u}, wf = {0u, 0u, 0u, 0u};
       if (k + 1 < L) {
-        wn = ring[(k + 1) % D];
+        const u32x4 nx = ring[(k + 1) % D];
         ring[(k + 1) % D] = load(k + 1 + D < L ? qcur : qnext, (uint32_t)((k + 1 + D) % L));
-        if (k + 1 == L - 1) {
-          tr = keep3 ? 0u : wn[3];
-          wn[3] &= keep3;
+        if (last) {
+          wf = nx;  // the next packet's first line (PL < L)
+        } else {
+          wn = nx;
+          if (kp + 1 == PL - 1) {
+            tr = keep3 ? 0u : wn[3];
+            wn[3] &= keep3;
+          }
         }
       }
       uint32_t t[4][4];
@@ -379,22 +405,29 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
           t[i][3] = lds_at(tab, __builtin_amdgcn_perm(x[i], lt.lo1, 0x0C020700u) + 128);
         }
       }
-      // The previous group's finish, in the shadow of the reads (for j = 0 it
-      // runs on zeros; its slot write is overwritten before any flush).
+      // The previous packet's finish, in the shadow of the reads (for j = 0
+      // it runs on zeros; its slot write is overwritten before any flush).
 #pragma unroll
       for (int sl = 0; sl < 8; ++sl)
-        if (slice_step(sl) == k) fin_slice(pf, sl);
-      if (k == kStoreStep) {
+        if (slice_step(sl) == kp) fin_slice(pf, sl);
+      if (kp == kStoreStep) {
         fin_store(pf, j - 1, qprev);
         if (j > 0 && ((j - 1) & kRoundMask) == kRoundMask) flush(j);  // wave-uniform: a full round of slots
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) x[i] = xor3(t[i][0], t[i][1], xor3(t[i][2], t[i][3], wn[i]));
-    }
+      if (last) {  // the packet is folded: hand its chains to the finish
 #pragma unroll
-    for (int i = 0; i < 4; ++i) pf.r[i] = x[i];
-    pf.tr = tr;
-    qprev = qcur;
+        for (int i = 0; i < 4; ++i) pf.r[i] = x[i];
+        pf.tr = tr;
+        qprev = qcur;
+        ++j;
+        if (k + 1 < L) {
+          first_line(wf, x);
+          tr = 0;
+        }
+      }
+    }
     qcur = qnext;  // advance the group sequence (wave-uniform)
     qnext = qcur < G ? after(qcur) : G;
   }
@@ -436,8 +469,9 @@ hipError_t launch_sck_fam(const SckArgs &a, int grid, hipStream_t st) {
     else if (a.n == 1024) hipLaunchKernelGGL((icrc_sck_kernel<8, 0, 8, false, true, 2, FAM>), g, b, 0, st, a);
     else return hipErrorInvalidValue;
   } else if (a.n == 4096) hipLaunchKernelGGL((icrc_sck_kernel<32, 0, 8, false, false, 2, FAM>), g, b, 0, st, a);
-  else if (a.n == 2048) hipLaunchKernelGGL((icrc_sck_kernel<16, 0, 8, false, false, 2, FAM>), g, b, 0, st, a);
-  else if (a.n == 1024) hipLaunchKernelGGL((icrc_sck_kernel<8, 0, 8, false, false, 2, FAM>), g, b, 0, st, a);
+  // 1 and 2 KiB packets stream in 4 KiB super-packets (S = 4 / 2 packets each)
+  else if (a.n == 2048) hipLaunchKernelGGL((icrc_sck_kernel<32, 0, 8, false, false, 2, FAM, 16>), g, b, 0, st, a);
+  else if (a.n == 1024) hipLaunchKernelGGL((icrc_sck_kernel<32, 0, 8, false, false, 2, FAM, 8>), g, b, 0, st, a);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }
