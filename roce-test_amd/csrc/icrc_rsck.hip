@@ -116,15 +116,29 @@ __device__ __forceinline__ void pass_range(uint64_t count, uint64_t &lo, uint64_
   hi = lo + per < count ? lo + per : count;
 }
 
+// Inclusive sum over the wave's lanes (6 bpermute steps).
+template <typename T>
+__device__ __forceinline__ T wave_scan(T v) {
+  const int lane = (int)(threadIdx.x & 63u);
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const T u = __shfl_up(v, (unsigned)d);
+    if (lane >= d) v += u;
+  }
+  return v;
+}
+
 // One workgroup: exclusive scans over the classes of groups (bucket
 // positions), of weighted work and of the non-empty big classes (the fold's
 // class table), and of pieces of the small classes (the piece kernel's prefix).
 // Run by the count pass's last workgroup (1024 threads), after every
-// workgroup's class counts have landed in a.counts.
+// workgroup's class counts have landed in a.counts.  One barrier: each wave
+// scans its 64 classes, then adds the totals of the waves before it (the
+// 10-round LDS scan before it cost ~0.2 % of C4's step, tools/ab_env.sh).
 __device__ void rsck_plan(const RsckArgs &a) {
-  __shared__ uint32_t sg[1024], sf[1024];
-  __shared__ uint64_t ss[1024], sp[1024];
-  const uint32_t t = threadIdx.x;
+  __shared__ uint32_t wg[16], wf[16];
+  __shared__ uint64_t wsum[16], wp[16];
+  const uint32_t t = threadIdx.x, wid = t >> 6;
   const uint32_t cnt = (t >= 1 && t < (uint32_t)kRsClasses)
                            ? __hip_atomic_load(&a.counts[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                            : 0u;
@@ -132,24 +146,24 @@ __device__ void rsck_plan(const RsckArgs &a) {
   const uint32_t G = (cnt + 7u) >> 3, f = (big && cnt) ? 1u : 0u;
   const uint32_t L = big ? t - (uint32_t)kRsBigBase : 0u;
   const uint64_t S = big ? (uint64_t)G * (L + kGroupCost) : 0u;
-  const uint64_t PC = big ? 0u : 8ull * G * (t >= 1 ? t - 1 : 0);  // small class t: pieces of t - 1 each
-  sg[t] = G;
-  sf[t] = f;
-  ss[t] = S;
-  sp[t] = PC;
-  __syncthreads();
-  for (uint32_t d = 1; d < 1024; d <<= 1) {
-    const uint32_t g2 = t >= d ? sg[t - d] : 0u, f2 = t >= d ? sf[t - d] : 0u;
-    const uint64_t s2 = t >= d ? ss[t - d] : 0u, p2 = t >= d ? sp[t - d] : 0u;
-    __syncthreads();
-    sg[t] += g2;
-    sf[t] += f2;
-    ss[t] += s2;
-    sp[t] += p2;
-    __syncthreads();
+  const uint64_t PC = big ? 0u : 8ull * G * (t >= 1 ? t - 1 : 0);
+  uint32_t ig = wave_scan(G), jf = wave_scan(f);
+  uint64_t is = wave_scan(S), ip = wave_scan(PC);
+  if ((t & 63u) == 63u) {
+    wg[wid] = ig;
+    wf[wid] = jf;
+    wsum[wid] = is;
+    wp[wid] = ip;
   }
-  const uint32_t g0 = sg[t] - G, ci = sf[t] - f;
-  const uint64_t s0 = ss[t] - S, p0 = sp[t] - PC;
+  __syncthreads();
+  for (uint32_t w = 0; w < wid; ++w) {  // wave-uniform
+    ig += wg[w];
+    jf += wf[w];
+    is += wsum[w];
+    ip += wp[w];
+  }
+  const uint32_t g0 = ig - G, ci = jf - f;
+  const uint64_t s0 = is - S, p0 = ip - PC;
   RsPlan *P = a.plan;
   if (f) {
     P->L[ci] = L;
@@ -161,14 +175,14 @@ __device__ void rsck_plan(const RsckArgs &a) {
     a.cursor[t] = 0u;
     P->ps0[t] = p0;
   }
-  if (t == (uint32_t)kRsBigBase + 1) {  // end of the small region (all small classes come first)
+  if (t == (uint32_t)kRsBigBase + 1) {
     *a.small_pos = 8u * g0;
     a.ps[8u * g0] = p0;
   }
   if (t == 1023) {
-    P->nc = sf[t];
-    P->ngroups = sg[t];
-    P->nsteps = ss[t];
+    P->nc = jf;
+    P->ngroups = ig;
+    P->nsteps = is;
   }
 }
 
@@ -240,7 +254,7 @@ template <bool OFF, bool LEN>
 __global__ __launch_bounds__(kPassBlock) void rsck_scatter(RsckArgs a) {
   // The class tables in LDS: per-round global reads of them were a
   // dependent latency in every round.
-  __shared__ uint32_t lc[kRsClasses], base[kRsClasses], sbk[kRsClasses], send[kRsClasses];
+  __shared__ uint32_t base[kRsClasses], sbk[kRsClasses], send[kRsClasses];
   __shared__ uint64_t sps0[kRsBigBase + 1];
   for (int t = threadIdx.x; t < kRsClasses; t += blockDim.x) {
     const uint32_t hb = a.hist[(uint64_t)blockIdx.x * kRsClasses + t];
@@ -252,50 +266,56 @@ __global__ __launch_bounds__(kPassBlock) void rsck_scatter(RsckArgs a) {
   }
   uint64_t lo, hi;
   pass_range(a.count, lo, hi);
-  // The next round's packet is read while this round is placed (software
-  // pipelining: the rounds are serialised by the block's LDS counters).
-  uint64_t addr_n = 0;
-  uint32_t n_n = 0;
-  if (lo + threadIdx.x < hi) rs_packet<OFF, LEN>(a, lo + threadIdx.x, addr_n, n_n);
-  for (uint64_t b0 = lo; b0 < hi; b0 += blockDim.x) {
-    for (int t = threadIdx.x; t < kRsClasses; t += blockDim.x) lc[t] = 0;
-    const uint64_t i = b0 + threadIdx.x;
-    const uint64_t addr = addr_n;
-    const uint32_t n = n_n;
-    if (i + blockDim.x < hi) rs_packet<OFF, LEN>(a, i + blockDim.x, addr_n, n_n);
-    __syncthreads();
-    uint32_t c = 0, r = 0;
-    if (i < hi) {
-      c = rs_class(addr, n);
-      if (c) r = atomicAdd(&lc[c], 1u);
+  // Rounds of kPassUnroll packets per thread (descriptors read at once),
+  // positions by returning LDS atomics on the block's class cursors: no
+  // barrier per round (per-round ranks with two barriers each measured 0.3 %
+  // slower on C4's step, tools/ab_env.sh); the order of packets within a
+  // class does not matter.
+  __syncthreads();
+  for (uint64_t r0 = lo; r0 < hi; r0 += kPassUnroll * blockDim.x) {  // block-uniform
+    uint64_t addr[kPassUnroll];
+    uint32_t n[kPassUnroll];
+#pragma unroll
+    for (int k = 0; k < kPassUnroll; ++k) {
+      uint64_t i = r0 + (uint64_t)k * blockDim.x + threadIdx.x;
+      i = i < hi ? i : hi - 1;
+      addr[k] = OFF ? a.off[i] : i * a.stride;
+      n[k] = LEN ? a.len[i] : a.fixed_len;
     }
-    __syncthreads();
-    if (i < hi) {
-      if (c) {
-        const uint32_t pos = base[c] + r;
-        const RsDesc d{(uint32_t)addr, (uint32_t)(addr >> 32) | (n << 16)};
-        const bool small = c <= (uint32_t)kRsBigBase;
-        const uint64_t psb = small ? sps0[c] : 0u;
-        const uint32_t bk = sbk[c];
-        // streaming stores: the fold that follows reads these once, and dirty
-        // lines left in the caches would be written back into its read stream
-        __builtin_nontemporal_store(d.lo, &a.desc[pos].lo);
-        __builtin_nontemporal_store(d.hi, &a.desc[pos].hi);
-        __builtin_nontemporal_store(pos, &a.pos_of[i]);
-        if (small && a.piece) a.ps[pos] = psb + (uint64_t)(pos - bk) * (c - 1u);
-        const uint32_t end = send[c];
-        if (pos + 1 == end)  // the class's last packet pads its group with copies of itself
-          for (uint32_t p = end; (p - bk) & 7u; ++p) {
-            a.desc[p] = d;
-            if (small && a.piece) a.ps[p] = psb + (uint64_t)(p - bk) * (c - 1u);
-          }
-      } else {
+#pragma unroll
+    for (int k = 0; k < kPassUnroll; ++k) addr[k] += (uint64_t)(uintptr_t)a.base + a.l3_offset;
+    uint32_t c[kPassUnroll], pos[kPassUnroll];
+#pragma unroll
+    for (int k = 0; k < kPassUnroll; ++k) {
+      const uint64_t i = r0 + (uint64_t)k * blockDim.x + threadIdx.x;
+      c[k] = i < hi ? rs_class(addr[k], n[k]) : 0u;
+      pos[k] = c[k] ? atomicAdd(&base[c[k]], 1u) : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < kPassUnroll; ++k) {
+      const uint64_t i = r0 + (uint64_t)k * blockDim.x + threadIdx.x;
+      if (i >= hi) continue;
+      if (!c[k]) {
         a.pos_of[i] = 0xFFFFFFFFu;
+        continue;
       }
+      const RsDesc d{(uint32_t)addr[k], (uint32_t)(addr[k] >> 32) | (n[k] << 16)};
+      const bool small = c[k] <= (uint32_t)kRsBigBase;
+      const uint64_t psb = small ? sps0[c[k]] : 0u;
+      const uint32_t bk = sbk[c[k]];
+      // streaming stores: the fold that follows reads these once, and dirty
+      // lines left in the caches would be written back into its read stream
+      __builtin_nontemporal_store(d.lo, &a.desc[pos[k]].lo);
+      __builtin_nontemporal_store(d.hi, &a.desc[pos[k]].hi);
+      __builtin_nontemporal_store(pos[k], &a.pos_of[i]);
+      if (small && a.piece) a.ps[pos[k]] = psb + (uint64_t)(pos[k] - bk) * (c[k] - 1u);
+      const uint32_t end = send[c[k]];
+      if (pos[k] + 1 == end)  // the class's last packet pads its group with copies of itself
+        for (uint32_t p = end; (p - bk) & 7u; ++p) {
+          a.desc[p] = d;
+          if (small && a.piece) a.ps[p] = psb + (uint64_t)(p - bk) * (c[k] - 1u);
+        }
     }
-    __syncthreads();
-    for (int t = threadIdx.x; t < kRsClasses; t += blockDim.x) base[t] += lc[t];
-    __syncthreads();
   }
 }
 
