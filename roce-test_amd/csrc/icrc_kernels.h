@@ -117,6 +117,7 @@ struct RsckArgs {
   uint32_t l3_offset;
   uint32_t verify;
   uint32_t piece;       // the small region goes to the piece kernel (RICRC_RS_PIECE): write its piece prefix
+  uint32_t group_cost;  // a group's finish in line-steps of the fold's work split (launch_rsck sets it)
   uint32_t *out;
   // device workspace (icrc_api.cpp sizes it: rs_workspace_bytes)
   uint32_t *counts;   // [kRsClasses + 2], zeroed before the count pass: class counts, "misaligned" flag, count-pass ticket

@@ -38,7 +38,7 @@ int main(int argc, char **argv) {
   auto ragged = [&](const char *tag, uint64_t count, const uint64_t *d_off, const uint32_t *d_len, uint32_t n, double b) {
     RsckArgs a{};
     a.base = buf; a.off = d_off; a.len = d_len; a.stride = n; a.count = count; a.fixed_len = n;
-    a.out = out; a.tzb = tzb;
+    a.out = out; a.tzb = tzb; a.group_cost = kGroupCost;
     for (int j = 0; j < 32; ++j) a.XB[j] = 0x85EBCA6Bu * (j + 3);
     for (int s = 0; s < 8; ++s) a.QS[s] = 0x9E3779B9u * (s + 1);
     void *ws; CK(hipMalloc(&ws, rs_workspace_bytes(count)));
@@ -123,7 +123,7 @@ int main(int argc, char **argv) {
     if (s1k) {
       if (n != 1024) continue;
       RsckArgs a{};
-      a.base = buf; a.stride = n; a.count = bytes / n; a.fixed_len = n; a.out = out; a.tzb = tzb;
+      a.base = buf; a.stride = n; a.count = bytes / n; a.fixed_len = n; a.out = out; a.tzb = tzb; a.group_cost = kGroupCost;
       for (int j = 0; j < 32; ++j) a.XB[j] = 0x85EBCA6Bu * (j + 3);
       for (int k = 0; k < 8; ++k) a.QS[k] = 0x9E3779B9u * (k + 1);
       void *ws; CK(hipMalloc(&ws, rs_workspace_bytes(a.count)));
