@@ -352,7 +352,12 @@ int launch_batch_v4(Dev &d, const uint8_t *base, const uint64_t *off, const uint
     k.out = out;
     k.tzb = d.d_tzb;
     const uint32_t xi = gf_xinv8n(4);
-    for (int j = 0; j < 32; ++j) k.XB[j] = gf_mul(xi, 1u << j);
+    const uint32_t xi2 = gf_xinv8n(8), xi3 = gf_xinv8n(12);
+    for (int j = 0; j < 32; ++j) {
+      k.XB[j] = gf_mul(xi, 1u << j);
+      k.XB2[j] = gf_mul(xi2, 1u << j);
+      k.XB3[j] = gf_mul(xi3, 1u << j);
+    }
     for (int s = 0; s < 8; ++s) k.QS[s] = gf_xinv8n(16ull * s);
     RaggedArgs small{};
     small.inv_tab = d.d_inv;

@@ -132,6 +132,8 @@ struct RsckArgs {
   uint32_t *small_pos;  // positions of the small region (device count for the piece kernel)
   const uint32_t *tzb;  // [kTzWords]: entry m = x^(31 - 4 m), i.e. basis word 4 q of x^(-8 tz) at m = 2 tz + q
   uint32_t XB[32];      // basis of x^-32
+  uint32_t XB2[32];     // basis of x^-64
+  uint32_t XB3[32];     // basis of x^-96
   uint32_t QS[8];       // x^(-8*16 s): lane slot s -> line start
 };
 uint64_t rs_workspace_bytes(uint64_t count);

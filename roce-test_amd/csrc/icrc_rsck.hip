@@ -389,12 +389,14 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   // wave = 157.7 KiB.
   // (ABL 512, timing only, with 2: 192 result slots per wave in the room of
   // the finish tables.)
-  constexpr uint32_t kQtStride = 132, kSmallWords = (ABL & 512) ? 0 : 128 + 8 * kQtStride + 32;  // 1216: a multiple of 32 words
+  // (+ x^-64 and x^-96 nibble tables, 2 x 128 words, after the head masks)
+  constexpr uint32_t kQtStride = 132, kSmallWords = (ABL & 512) ? 0 : 128 + 8 * kQtStride + 32 + 256;  // 1472: a multiple of 32 words
   constexpr uint32_t kTzW = (ABL & 512) ? 0 : kTzWords;
   __shared__ uint32_t lds[kSmallWords + kLdsWords + kTzW + kWaves * kWaveWords];
   uint32_t *xtl = lds;
   uint32_t *qtl = lds + 128;
   uint32_t *etl = lds + 128 + 8 * kQtStride;  // whole-word head masks: (or, xor) of word k = rel / 4
+  uint32_t *x2tl = etl + 32, *x3tl = etl + 160;  // nibble tables of x^-64, x^-96
   uint32_t *tab = lds + kSmallWords;
   uint32_t *tzl = tab + kLdsWords;
 
@@ -433,6 +435,14 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
 #pragma unroll
     for (int b = 0; b < 4; ++b) t ^= ((v >> b) & 1u) ? a.XB[4 * w + b] : 0u;
     xtl[threadIdx.x] = t;
+    uint32_t t2 = 0, t3 = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      t2 ^= ((v >> b) & 1u) ? a.XB2[4 * w + b] : 0u;
+      t3 ^= ((v >> b) & 1u) ? a.XB3[4 * w + b] : 0u;
+    }
+    x2tl[threadIdx.x] = t2;
+    x3tl[threadIdx.x] = t3;
   }
   __syncthreads();
 
@@ -589,9 +599,10 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
         for (int w = 0; w < 8; ++w) e[w] = t[16 * w + __builtin_amdgcn_ubfe(v, 4 * w, 4)];
         return xor3(xor3(e[0], e[1], e[2]), xor3(e[3], e[4], e[5]), xor3(e[6], e[7], x));
       };
-      uint32_t u = r[3];
-#pragma unroll
-      for (int i = 2; i >= 0; --i) u = nib_mul(xtl, u, r[i]);
+      // r3 x^-96 + r2 x^-64 + r1 x^-32 + r0: three independent multiplies
+      // (Horner chained them: four dependent LDS round trips per finish,
+      // which the 2-3-line groups of 256-byte packets could not hide)
+      const uint32_t u = nib_mul(x3tl, r[3], nib_mul(x2tl, r[2], nib_mul(xtl, r[1], r[0])));
       R = group_xor(nib_mul(qrow, u, 0u), 3);  // u * x^(-128 s): lane slot s's nibble table
       // x^(-8 tz), distributed: lane s takes bits 4s..4s+3 of R; basis word
       // 4s from LDS, 4s+1..4s+3 by successive x^-1.

@@ -39,7 +39,7 @@ int main(int argc, char **argv) {
     RsckArgs a{};
     a.base = buf; a.off = d_off; a.len = d_len; a.stride = n; a.count = count; a.fixed_len = n;
     a.out = out; a.tzb = tzb; a.group_cost = kGroupCost;
-    for (int j = 0; j < 32; ++j) a.XB[j] = 0x85EBCA6Bu * (j + 3);
+    for (int j = 0; j < 32; ++j) { a.XB[j] = 0x85EBCA6Bu * (j + 3); a.XB2[j] = 0x27D4EB2Fu * (j + 5); a.XB3[j] = 0x165667B1u * (j + 7); }
     for (int s = 0; s < 8; ++s) a.QS[s] = 0x9E3779B9u * (s + 1);
     void *ws; CK(hipMalloc(&ws, rs_workspace_bytes(count)));
     CK(rs_zero_counters(ws, 0));
@@ -124,7 +124,7 @@ int main(int argc, char **argv) {
       if (n != 1024) continue;
       RsckArgs a{};
       a.base = buf; a.stride = n; a.count = bytes / n; a.fixed_len = n; a.out = out; a.tzb = tzb; a.group_cost = kGroupCost;
-      for (int j = 0; j < 32; ++j) a.XB[j] = 0x85EBCA6Bu * (j + 3);
+      for (int j = 0; j < 32; ++j) { a.XB[j] = 0x85EBCA6Bu * (j + 3); a.XB2[j] = 0x27D4EB2Fu * (j + 5); a.XB3[j] = 0x165667B1u * (j + 7); }
       for (int k = 0; k < 8; ++k) a.QS[k] = 0x9E3779B9u * (k + 1);
       void *ws; CK(hipMalloc(&ws, rs_workspace_bytes(a.count)));
       CK(rs_zero_counters(ws, 0));
