@@ -110,9 +110,8 @@ constexpr uint32_t kGroupCost = 3;
 constexpr int kPassBlocks = 512;  // pass grid cap (per-block class histograms: 1 MiB)
 constexpr int kPassUnroll = 8;    // packets per thread whose descriptors are read at once
 // a.counts: [0, kRsClasses) class counts, [kRsClasses] misaligned flag,
-// [kRsTicket] count-pass workgroups done, [kRsBarrier] the fused pass's grid barrier
+// [kRsTicket] count-pass workgroups done
 constexpr int kRsTicket = kRsClasses + 1;
-constexpr int kRsBarrier = kRsClasses + 2;
 __device__ __forceinline__ void pass_range(uint64_t count, uint64_t &lo, uint64_t &hi) {
   const uint64_t per = ((count + gridDim.x - 1) / gridDim.x + kPassBlock - 1) / kPassBlock * kPassBlock;
   lo = (uint64_t)blockIdx.x * per;
@@ -139,12 +138,7 @@ __device__ __forceinline__ T wave_scan(T v) {
 // workgroup's class counts have landed in a.counts.  One barrier: each wave
 // scans its 64 classes, then adds the totals of the waves before it (the
 // 10-round LDS scan before it cost ~0.2 % of C4's step, tools/ab_env.sh).
-// publish: write the plan for the later kernels (bucket bases, the fold's
-// class table, the small region); fused (rsck_bucket): leave a.cursor alone
-// and also give this block the bucket bases, class counts and small-class
-// piece bases in LDS (bkl, cnl, ps0l).
-__device__ void rsck_plan(const RsckArgs &a, bool publish = true, bool fused = false, uint32_t *bkl = nullptr,
-                          uint32_t *cnl = nullptr, uint64_t *ps0l = nullptr) {
+__device__ void rsck_plan(const RsckArgs &a) {
   __shared__ uint32_t wg[16], wf[16];
   __shared__ uint64_t wsum[16], wp[16];
   const uint32_t t = threadIdx.x, wid = t >> 6;
@@ -173,12 +167,6 @@ __device__ void rsck_plan(const RsckArgs &a, bool publish = true, bool fused = f
   }
   const uint32_t g0 = ig - G, ci = jf - f;
   const uint64_t s0 = is - S, p0 = ip - PC;
-  if (fused && t < (uint32_t)kRsClasses) {
-    bkl[t] = 8u * g0;
-    cnl[t] = cnt;
-    if (t <= (uint32_t)kRsBigBase) ps0l[t] = p0;
-  }
-  if (!publish) return;
   RsPlan *P = a.plan;
   if (f) {
     P->L[ci] = L;
@@ -187,7 +175,7 @@ __device__ void rsck_plan(const RsckArgs &a, bool publish = true, bool fused = f
   }
   if (t < (uint32_t)kRsClasses) {
     a.bucket[t] = 8u * g0;
-    if (!fused) a.cursor[t] = 0u;
+    a.cursor[t] = 0u;
     P->ps0[t] = p0;
   }
   if (t == (uint32_t)kRsBigBase + 1) {
@@ -334,134 +322,11 @@ __global__ __launch_bounds__(kPassBlock) void rsck_scatter(RsckArgs a) {
   }
 }
 
-// A packet outside the buckets (n < 44: shorter than a RoCEv2 header; n > 65535
-// or n < 4: invalid, 0): computed right here by the Sarwate loop.
-__device__ __forceinline__ void rs_unbucketed(const RsckArgs &a, uint64_t i, uint64_t addr, uint32_t n) {
-  uint32_t v = 0u;
-  if (n >= 4u && n <= kMaxLen) {
-    v = icrc_small(addr, n);
-    if (a.verify) v = gload4_unaligned((uintptr_t)(addr + n - 4u)) == v ? 1u : 0u;
-  }
-  a.out[i] = v;
-  a.pos_of[i] = 0xFFFFFFFFu;
-}
-
-// Count, plan and scatter in ONE cooperative launch (all workgroups resident:
-// hipLaunchCooperativeKernel) when every workgroup's packets fit one round of
-// U per thread (C4: 4 M packets = 256 workgroups, one per CU, x 16384): the
-// descriptors stay in registers across the grid barrier, so the second read
-// of offsets and lengths and a launch are gone.  Cross-workgroup data goes
-// only through device-scope atomics (class counts, reservations, barrier),
-// never through plain stores inside the kernel: an agent-scope release would
-// write every XCD's L2 back (130 us, round 2), and a plain store could sit in
-// one XCD's L2 unseen by the others.  Every workgroup computes the plan from
-// the counts itself; workgroup 0 also publishes it for the fold.
-constexpr int kFusedU = 16;  // packets per thread of the fused pass
-template <bool OFF, bool LEN, int U>
-__global__ __launch_bounds__(kPassBlock) void rsck_bucket(RsckArgs a) {
-  __shared__ uint32_t h[kRsClasses], bkl[kRsClasses], cnl[kRsClasses];
-  __shared__ uint64_t ps0l[kRsBigBase + 1];
-  for (int t = threadIdx.x; t < kRsClasses; t += blockDim.x) h[t] = 0;
-  if (blockIdx.x == 0)  // the reservation cursors start at zero (read only after the barrier)
-    for (int t = threadIdx.x; t < kRsClasses; t += blockDim.x) atomicExch(&a.cursor[t], 0u);
-  __syncthreads();
-  uint64_t lo, hi;
-  pass_range(a.count, lo, hi);  // one round: hi - lo <= U * blockDim.x (host-checked)
-  // The packets, held as their final 8-byte descriptors (2 VGPRs each; the
-  // class is recomputed from them; packets outside the buckets get n = 0).
-  RsDesc d[U];
-  {
-    uint64_t addr[U];
-    uint32_t n[U];
-    // buffer loads from the block's range (32-bit offsets: no 64-bit address
-    // per load; past hi the range check reads zeros), non-temporal: their
-    // only read
-    const __amdgpu_buffer_rsrc_t ro = make_rsrc(OFF ? a.off + lo : a.off, OFF ? (uint32_t)(8 * (hi - lo)) : 0u);
-    const __amdgpu_buffer_rsrc_t rl = make_rsrc(LEN ? a.len + lo : a.len, LEN ? (uint32_t)(4 * (hi - lo)) : 0u);
-    typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
-#pragma unroll
-    for (int k = 0; k < U; ++k) {
-      const uint32_t j = (uint32_t)k * blockDim.x + threadIdx.x;  // packet lo + j
-      if (OFF) {
-        const u32x2v o = __builtin_bit_cast(u32x2v, __builtin_amdgcn_raw_buffer_load_b64(ro, 8u * j, 0, 2));
-        addr[k] = ((uint64_t)o[1] << 32) | o[0];
-      } else {
-        addr[k] = (lo + j) * a.stride;
-      }
-      n[k] = LEN ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rl, 4u * j, 0, 2) : a.fixed_len;
-    }
-    int odd = 0;
-    uint32_t rare = 0;  // bit k: packet k is outside the buckets
-#pragma unroll
-    for (int k = 0; k < U; ++k) {
-      const uint64_t i = lo + (uint64_t)k * blockDim.x + threadIdx.x;
-      addr[k] += (uint64_t)(uintptr_t)a.base + a.l3_offset;
-      const uint32_t c = i < hi ? rs_class(addr[k], n[k]) : 0u;
-      if (c) {
-        atomicAdd(&h[c], 1u);
-        odd |= (c >= (uint32_t)kRsBigBase && ((addr[k] | n[k]) & 3u)) ? 1 : 0;
-      }
-      rare |= (!c && i < hi) ? 1u << k : 0u;
-      d[k] = RsDesc{(uint32_t)addr[k], c ? (uint32_t)(addr[k] >> 32) | (n[k] << 16) : 0u};
-    }
-    // Packets outside the buckets (rare): their descriptors read again, one
-    // at a time, so the unrolled registers are never indexed at run time.
-    for (uint32_t m = rare; m; m &= m - 1u) {
-      const uint64_t i = lo + (uint64_t)__builtin_ctz(m) * blockDim.x + threadIdx.x;
-      const uint64_t ad = (uint64_t)(uintptr_t)a.base + (OFF ? a.off[i] : i * a.stride) + a.l3_offset;
-      rs_unbucketed(a, i, ad, LEN ? a.len[i] : a.fixed_len);
-    }
-    if (__syncthreads_or(odd) && threadIdx.x == 0) atomicOr(&a.counts[kRsClasses], 1u);
-  }
-  for (int t = threadIdx.x; t < kRsClasses; t += blockDim.x)
-    if (h[t]) atomicAdd(&a.counts[t], h[t]);
-  // Grid barrier: every workgroup's count atomics acknowledged (vmcnt(0)),
-  // then one arrival per workgroup; bounded spin (a launch that somehow did
-  // not get every workgroup resident gives wrong results, not a hang).
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add(&a.counts[kRsBarrier], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (uint32_t spin = 0; spin < (1u << 24); ++spin) {
-      if (__hip_atomic_load(&a.counts[kRsBarrier], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= gridDim.x) break;
-      __builtin_amdgcn_s_sleep(2);
-    }
-  }
-  __syncthreads();
-  rsck_plan(a, blockIdx.x == 0, true, bkl, cnl, ps0l);
-  __syncthreads();
-  for (int t = threadIdx.x; t < kRsClasses; t += blockDim.x)  // the block's ranges in the buckets
-    if (h[t]) h[t] = bkl[t] + atomicAdd(&a.cursor[t], h[t]);
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < U; ++k) {
-    const uint64_t i = lo + (uint64_t)k * blockDim.x + threadIdx.x;
-    const uint32_t n = d[k].hi >> 16;
-    const uint32_t c = n ? rs_class(((uint64_t)(d[k].hi & 0xFFFFu) << 32) | d[k].lo, n) : 0u;
-    if (!c) continue;
-    const uint32_t pos = atomicAdd(&h[c], 1u);
-    const bool small = c <= (uint32_t)kRsBigBase;
-    const uint64_t psb = small ? ps0l[c] : 0u;
-    const uint32_t bk = bkl[c];
-    // streaming stores: the fold that follows reads these once
-    __builtin_nontemporal_store(d[k].lo, &a.desc[pos].lo);
-    __builtin_nontemporal_store(d[k].hi, &a.desc[pos].hi);
-    __builtin_nontemporal_store(pos, &a.pos_of[i]);
-    if (small && a.piece) a.ps[pos] = psb + (uint64_t)(pos - bk) * (c - 1u);
-    const uint32_t end = bk + cnl[c];
-    if (pos + 1 == end)  // the class's last packet pads its group with copies of itself
-      for (uint32_t p = end; (p - bk) & 7u; ++p) {
-        a.desc[p] = d[k];
-        if (small && a.piece) a.ps[p] = psb + (uint64_t)(p - bk) * (c - 1u);
-      }
-  }
-}
-
 __global__ __launch_bounds__(256) void rsck_gather(RsckArgs a) {
   // The class counters are dead now (plan, scatter and both folds have read
   // them): zero them for the next call on this workspace.
   if (blockIdx.x == 0)
-    for (uint32_t t = threadIdx.x; t <= (uint32_t)kRsBarrier; t += blockDim.x) a.counts[t] = 0u;
+    for (uint32_t t = threadIdx.x; t <= (uint32_t)kRsTicket; t += blockDim.x) a.counts[t] = 0u;
   constexpr int U = 4;  // packets per thread in flight at once
   const uint64_t T = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < a.count; i0 += U * T) {
@@ -1025,7 +890,7 @@ uint64_t rs_workspace_bytes(uint64_t count) {
 }
 
 hipError_t rs_zero_counters(void *ws, hipStream_t st) {  // counts is the workspace's first region
-  return hipMemsetAsync(ws, 0, 4ull * (kRsBarrier + 1), st);
+  return hipMemsetAsync(ws, 0, 4ull * (kRsTicket + 1), st);
 }
 
 void rs_bind_workspace(RsckArgs &a, void *ws) {
@@ -1064,40 +929,6 @@ static void launch_passes(const RsckArgs &a, int pgrid, hipStream_t st) {
   else launch_passes_t<false, false>(a, pgrid, st);
 }
 
-// Workgroups of the fused pass that fit the device at once (occupancy x CUs), per variant.
-template <bool OFF, bool LEN>
-static int fused_capacity(int n_cu) {
-  static int per_cu = -1;
-  if (per_cu < 0) {
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(rsck_bucket<OFF, LEN, kFusedU>),
-                                                    kPassBlock, 0) != hipSuccess)
-      nb = 0;
-    per_cu = nb;
-  }
-  return per_cu * n_cu;
-}
-
-// The fused pass if the batch fits one round of it on the device (C4 does);
-// false: the count and scatter passes.
-template <bool OFF, bool LEN>
-static bool launch_fused_t(RsckArgs &a, int n_cu, hipStream_t st, hipError_t &e) {
-  const uint64_t per = (uint64_t)kFusedU * kPassBlock;
-  const uint64_t need = (a.count + per - 1) / per;
-  if (need == 0 || need > (uint64_t)fused_capacity<OFF, LEN>(n_cu)) return false;
-  void *args[] = {&a};
-  e = hipLaunchCooperativeKernel(reinterpret_cast<const void *>(rsck_bucket<OFF, LEN, kFusedU>), dim3((unsigned)need),
-                                 dim3(kPassBlock), args, 0, st);
-  return true;
-}
-static bool launch_fused(RsckArgs &a, int n_cu, hipStream_t st, hipError_t &e) {
-  if (getenv("RICRC_RS_FUSED") == nullptr) return false;  // opt-in until measured on the GPU
-  if (a.off && a.len) return launch_fused_t<true, true>(a, n_cu, st, e);
-  if (a.off) return launch_fused_t<true, false>(a, n_cu, st, e);
-  if (a.len) return launch_fused_t<false, true>(a, n_cu, st, e);
-  return launch_fused_t<false, false>(a, n_cu, st, e);
-}
-
 hipError_t launch_rsck(RsckArgs &a, const RaggedArgs &small, int grid, hipStream_t st) {
   if (a.count == 0) return hipSuccess;
   a.piece = getenv("RICRC_RS_PIECE") != nullptr ? 1u : 0u;
@@ -1106,14 +937,9 @@ hipError_t launch_rsck(RsckArgs &a, const RaggedArgs &small, int grid, hipStream
   // a.counts (+ the misaligned flag) is zero here: zeroed when the workspace
   // was allocated, and again by rsck_gather at the end of every call.
   hipError_t e = hipSuccess;
-  // count + plan + scatter: one cooperative pass when the batch fits it
-  if (!launch_fused(a, grid, st, e)) {
-    const uint64_t want = (a.count + kPassBlock - 1) / kPassBlock;
-    const int pgrid = (int)(want < kPassBlocks ? want : kPassBlocks);
-    launch_passes(a, pgrid, st);
-  } else if (e != hipSuccess) {
-    return e;
-  }
+  const uint64_t want = (a.count + kPassBlock - 1) / kPassBlock;
+  const int pgrid = (int)(want < kPassBlocks ? want : kPassBlocks);
+  launch_passes(a, pgrid, st);
   hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, st, a);
   if (!a.piece) {  // the small region [0, *small_pos): one lane per packet
     hipLaunchKernelGGL(icrc_rsmall_kernel, dim3(grid), dim3(kBlock), 0, st, a);
