@@ -105,8 +105,10 @@ constexpr int kPassBlock = 1024;
 // than one that drew 4 KiB packets.  Swept on C4 (same box, tools/ab_env.sh
 // with RICRC_RS_GCOST, profiles/r02/ab_c4_group_cost.txt): 0 -> 1.52 ms per
 // step, 1 -> 1.16, 2 -> 1.060-1.081, 3 -> 1.061-1.062, 4 -> 1.065-1.086,
-// 6 (round 1's estimate) -> 1.073-1.076, 10 -> 1.09, 16 -> 1.13.
-constexpr uint32_t kGroupCost = 3;
+// 6 (round 1's estimate) -> 1.073-1.076, 10 -> 1.09, 16 -> 1.13.  In quarter
+// line-steps 10..14 are within the run-to-run noise (profiles/r02/
+// ab_c4_group_cost_quarters.txt).
+constexpr uint32_t kGroupCost = 12;  // quarter line-steps (3 lines)
 constexpr int kPassBlocks = 512;  // pass grid cap (per-block class histograms: 1 MiB)
 constexpr int kPassUnroll = 8;    // packets per thread whose descriptors are read at once
 // a.counts: [0, kRsClasses) class counts, [kRsClasses] misaligned flag,
@@ -148,7 +150,7 @@ __device__ void rsck_plan(const RsckArgs &a) {
   const bool big = t > (uint32_t)kRsBigBase;
   const uint32_t G = (cnt + 7u) >> 3, f = (big && cnt) ? 1u : 0u;
   const uint32_t L = big ? t - (uint32_t)kRsBigBase : 0u;
-  const uint64_t S = big ? (uint64_t)G * (L + a.group_cost) : 0u;
+  const uint64_t S = big ? (uint64_t)G * (4u * L + a.group_cost) : 0u;  // quarter line-steps
   const uint64_t PC = big ? 0u : 8ull * G * (t >= 1 ? t - 1 : 0);
   uint32_t ig = wave_scan(G), jf = wave_scan(f);
   uint64_t is = wave_scan(S), ip = wave_scan(PC);
@@ -462,7 +464,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
     }
     const uint32_t c = __builtin_amdgcn_readfirstlane(cnt - 1u);  // s0[0] = 0 <= x
     const uint32_t L = P->L[c], g0 = P->g0[c], gend = c + 1 < nc ? P->g0[c + 1] : NG;
-    const uint64_t w = L + a.group_cost;
+    const uint64_t w = 4u * L + a.group_cost;  // quarter line-steps
     const uint64_t q = g0 + (x - P->s0[c] + w - 1) / w;
     return q < gend ? (uint32_t)q : gend;
   };
@@ -933,7 +935,7 @@ hipError_t launch_rsck(RsckArgs &a, const RaggedArgs &small, int grid, hipStream
   if (a.count == 0) return hipSuccess;
   a.piece = getenv("RICRC_RS_PIECE") != nullptr ? 1u : 0u;
   a.group_cost = kGroupCost;
-  if (const char *e = getenv("RICRC_RS_GCOST")) a.group_cost = (uint32_t)atoi(e);  // schedule study
+  if (const char *e = getenv("RICRC_RS_GCOST")) a.group_cost = (uint32_t)atoi(e);  // schedule study, quarter lines
   // a.counts (+ the misaligned flag) is zero here: zeroed when the workspace
   // was allocated, and again by rsck_gather at the end of every call.
   hipError_t e = hipSuccess;
