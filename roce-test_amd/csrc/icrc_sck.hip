@@ -469,8 +469,10 @@ hipError_t launch_sck_fam(const SckArgs &a, int grid, hipStream_t st) {
     else if (a.n == 1024) hipLaunchKernelGGL((icrc_sck_kernel<8, 0, 8, false, true, 2, FAM>), g, b, 0, st, a);
     else return hipErrorInvalidValue;
   } else if (a.n == 4096) hipLaunchKernelGGL((icrc_sck_kernel<32, 0, 8, false, false, 2, FAM>), g, b, 0, st, a);
-  // 1 and 2 KiB packets stream in 4 KiB super-packets (S = 4 / 2 packets each)
-  else if (a.n == 2048) hipLaunchKernelGGL((icrc_sck_kernel<32, 0, 8, false, false, 2, FAM, 16>), g, b, 0, st, a);
+  // 1 KiB packets stream in 4 KiB super-packets (S = 4 packets each): 0.180 ->
+  // 0.176 ms on 1 M; 2 KiB packets measured 2 % slower that way (0.346 ->
+  // 0.353 ms, same box, profiles/r02/ab_super_1k_2k/) and keep L = 16
+  else if (a.n == 2048) hipLaunchKernelGGL((icrc_sck_kernel<16, 0, 8, false, false, 2, FAM>), g, b, 0, st, a);
   else if (a.n == 1024) hipLaunchKernelGGL((icrc_sck_kernel<32, 0, 8, false, false, 2, FAM, 8>), g, b, 0, st, a);
   else return hipErrorInvalidValue;
   return hipGetLastError();
