@@ -92,14 +92,15 @@ int ricrc_is_rocev2(const uint8_t *l3, uint32_t n);
 #define RICRC_F_IPV4 0u
 #define RICRC_F_IPV6 1u
 #define RICRC_F_AUTO 2u
-#define RICRC_F_STRICT 0x100u /* ricrc_icrc only: reject packets that do not classify */
+#define RICRC_F_STRICT 0x100u /* ricrc_icrc / *_st calls: reject packets that do not classify */
 
 uint32_t ricrc_one_ex(const uint8_t *l3, uint32_t n, uint32_t flags);
 int ricrc_verify_one_ex(const uint8_t *l3, uint32_t n, uint32_t flags);
 int ricrc_stamp_one_ex(uint8_t *l3, uint32_t n, uint32_t flags);
 
 /* 4: RoCEv2 over IPv4 (as ricrc_is_rocev2), 6: RoCEv2 over IPv6 (version 6,
- * next header 17, payload length n-40, UDP dport 4791), 0: neither. */
+ * next header 17, payload length n-40, UDP dport 4791, n >= 64), 0: neither
+ * (also for n outside [RICRC_MIN_LEN, RICRC_MAX_LEN]). */
 int ricrc_classify(const uint8_t *l3, uint32_t n);
 
 /* Incremental repair after a header rewrite (the switch's PSN/MSN/opcode
@@ -146,10 +147,13 @@ int ricrc_device_count(const ricrc_ctx *ctx);
  * ricrc_batch_device: device-resident batch on context device `dev`
  * (pointers are device pointers on that device; off/len may be NULL).
  * Asynchronous on `stream` (a hipStream_t; NULL = the HIP null stream;
- * ricrc_stream() returns the context's own non-blocking stream).  Lengths are not read on the host: a device length outside
- * [4, RICRC_MAX_LEN] yields out[i] = 0.  16-byte aligned packet starts with a
- * fixed length take the streaming kernels; anything else (offsets, lengths,
- * any alignment or mix of sizes) the ragged kernel, several packets per wave. */
+ * ricrc_stream() returns the context's own non-blocking stream).  Lengths
+ * are not read on the host: a device length outside [4, RICRC_MAX_LEN]
+ * yields out[i] = 0 -- which is also a possible ICRC: callers that must tell
+ * bad descriptors apart use ricrc_batch_device_st (a status per packet).
+ * 16-byte aligned packet starts with a fixed length take the streaming
+ * kernels; anything else (offsets, lengths, any alignment or mix of sizes)
+ * the ragged pipeline, several packets per wave. */
 int ricrc_batch_host(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *off, const uint32_t *len,
                      uint32_t stride, uint64_t count, uint32_t l3_offset, uint32_t *out);
 int ricrc_batch_device(ricrc_ctx *ctx, int dev, const void *d_base, const uint64_t *d_off,
@@ -177,6 +181,49 @@ int ricrc_batch_device_ex(ricrc_ctx *ctx, int dev, const void *d_base, const uin
 int ricrc_verify_device_ex(ricrc_ctx *ctx, int dev, const void *d_base, const uint64_t *d_off,
                            const uint32_t *d_len, uint32_t stride, uint64_t count, uint32_t l3_offset,
                            uint32_t *d_out, void *stream, uint32_t flags);
+
+/* ------------------------------------------- batches with a per-packet status
+ * For NIC rings that carry more than RoCEv2 and descriptors that may be bad.
+ * The reference only ever computes an ICRC for frames its ingress parser
+ * accepted as RoCEv2 (EtherType 0x0800 -> IPv4 protocol 17 -> UDP dport 4791,
+ * p4/shuffle/shuffle_ingress_parser.p4:12-36, header.p4:8,14); these calls
+ * apply that accept path per packet on the device and report, per packet:
+ *   RICRC_ST_OK       out[i] is the ICRC (RICRC_F_VERIFY: 1/0, trailer check);
+ *   RICRC_ST_BADLEN   its length is outside [RICRC_MIN_LEN, RICRC_MAX_LEN];
+ *   RICRC_ST_NOTROCE  RICRC_F_STRICT and the packet is not RoCEv2 of an
+ *                     accepted family: ricrc_classify's rules (IPv4: version
+ *                     4 + IHL 5, protocol 17, total_len == n, dport 4791;
+ *                     IPv6: version 6, next header 17, payload length n-40,
+ *                     dport 4791), and, for Ethernet frames (l3_offset >=
+ *                     14), the EtherType in the two bytes before L3 must be
+ *                     the family's (0x0800 / 0x86DD);
+ * and out[i] = 0 whenever status[i] != RICRC_ST_OK.
+ * flags = a family (RICRC_F_IPV4 / IPV6 / AUTO; with RICRC_F_STRICT, IPV4 or
+ * IPV6 accepts only that family, AUTO either) | RICRC_F_STRICT |
+ * RICRC_F_VERIFY.  A batch without per-packet lengths whose one length
+ * (stride - l3_offset) is out of range is a call error (-EINVAL).
+ *
+ * ricrc_batch_device_st: as ricrc_batch_device_ex, plus d_status (count
+ *   bytes, device).  Asynchronous on `stream`.
+ * ricrc_batch_host_st: as ricrc_batch_host_ex, plus status (count bytes,
+ *   host); a bad descriptor length is a per-packet RICRC_ST_BADLEN here, not
+ *   -EINVAL, and its bytes are never read.
+ * ricrc_classify_device: d_class[i] = ricrc_classify of packet i (4 / 6 / 0),
+ *   with the EtherType check above when l3_offset >= 14.  No ICRC.
+ * 0, -EINVAL (NULL, bad flags), -ENODEV, -ENOMEM, -EIO. */
+#define RICRC_F_VERIFY 0x200u /* *_st calls: out[i] = 1 if the trailer holds the ICRC, else 0 */
+#define RICRC_ST_OK 0
+#define RICRC_ST_BADLEN 1
+#define RICRC_ST_NOTROCE 2
+int ricrc_batch_device_st(ricrc_ctx *ctx, int dev, const void *d_base, const uint64_t *d_off,
+                          const uint32_t *d_len, uint32_t stride, uint64_t count, uint32_t l3_offset,
+                          uint32_t *d_out, uint8_t *d_status, void *stream, uint32_t flags);
+int ricrc_batch_host_st(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *off, const uint32_t *len,
+                        uint32_t stride, uint64_t count, uint32_t l3_offset, uint32_t *out, uint8_t *status,
+                        uint32_t flags);
+int ricrc_classify_device(ricrc_ctx *ctx, int dev, const void *d_base, const uint64_t *d_off,
+                          const uint32_t *d_len, uint32_t stride, uint64_t count, uint32_t l3_offset,
+                          uint8_t *d_class, void *stream);
 
 /* Batch incremental repair on the device, after a header rewrite of packets
  * that were already stamped -- the switch egress's PSN/MSN/opcode patches

@@ -162,3 +162,73 @@ def crc_shift(reg: int, nbytes: int) -> int:
         for _ in range(8):
             reg = (reg >> 1) ^ (POLY_REFLECTED if reg & 1 else 0)
     return reg
+
+
+# --------------------------------------------------------------------------
+# RoCEv2 classification: the ingress parser's accept path
+# (p4/shuffle/shuffle_ingress_parser.p4:12-36) -- Ethernet ether_type
+# ETHERTYPE_IPV4 0x0800 (header.p4:8) -> parse_ipv4 -> protocol
+# IP_PROTOCOLS_UDP 17 (header.p4:11) -> parse_udp -> dst_port UDP_PORT_ROCE
+# 4791 (header.p4:14) -> parse_bth.  Every other frame falls through to
+# `accept` without a BTH: not RoCE, no ICRC.  The ipv4_h of header.p4:42-53
+# has no options (IHL 5), and the packet is the IPv4 datagram (total_len = n).
+# IPv6 (not in the reference): IBTA Annex A17's RoCEv2 over IPv6 -- version 6,
+# next header 17, payload length n - 40, UDP dst_port 4791.
+# --------------------------------------------------------------------------
+ETHERTYPE_IPV4 = 0x0800                   # header.p4:8
+ETHERTYPE_IPV6 = 0x86DD
+IP_PROTOCOLS_UDP = 17                     # header.p4:11
+MAX_PKT = 65535                           # IPv4 total_len is 16 bits (header.p4:45)
+
+
+def classify(l3: bytes, ethertype: int | None = None) -> int:
+    """4 (RoCEv2 over IPv4), 6 (over IPv6) or 0.  ``ethertype``: the frame's
+    EtherType when the packet came in an Ethernet frame (it must be the
+    family's), None for a bare L3 packet."""
+    n = len(l3)
+    if n < MIN_PKT or n > MAX_PKT:
+        return 0
+    be16 = lambda o: (l3[o] << 8) | l3[o + 1]  # noqa: E731
+    c = 0
+    if l3[0] == 0x45 and l3[9] == IP_PROTOCOLS_UDP and be16(2) == n and be16(22) == ROCE_UDP_PORT:
+        c = 4
+    elif (l3[0] >> 4) == 6 and n >= 40 + 8 + 12 + 4 and l3[6] == IP_PROTOCOLS_UDP and be16(4) == n - 40 \
+            and be16(42) == ROCE_UDP_PORT:
+        c = 6
+    if c and ethertype is not None and ethertype != (ETHERTYPE_IPV4 if c == 4 else ETHERTYPE_IPV6):
+        c = 0
+    return c
+
+
+ST_OK, ST_BADLEN, ST_NOTROCE = 0, 1, 2
+
+
+def status_batch(buf: np.ndarray, offsets=None, lengths=None, stride: int = 0, count: int | None = None,
+                 l3_offset: int = 0, family: str = "v4", strict: bool = False, verify: bool = False):
+    """(out, status) of ricrc_batch_*_st on a packed batch: per packet
+    ST_BADLEN for a length outside [MIN_PKT, MAX_PKT], ST_NOTROCE under
+    ``strict`` for a packet :func:`classify` rejects (EtherType checked when
+    l3_offset >= 14) or of a family not asked for, else ST_OK with the ICRC
+    (``verify``: 1/0 trailer check); out = 0 where status != ST_OK."""
+    mv = memoryview(np.ascontiguousarray(buf).reshape(-1).view(np.uint8))
+    if count is None:
+        count = len(offsets) if offsets is not None else len(mv) // stride
+    out = np.zeros(count, dtype=np.uint32)
+    st = np.zeros(count, dtype=np.uint8)
+    accept = {"v4": (4,), "v6": (6,), "auto": (4, 6)}[family]
+    for i in range(count):
+        o = int(offsets[i]) if offsets is not None else i * stride
+        n = int(lengths[i]) if lengths is not None else stride - l3_offset
+        if n < MIN_PKT or n > MAX_PKT:
+            st[i] = ST_BADLEN
+            continue
+        s = o + l3_offset
+        pkt = mv[s: s + n].tobytes()
+        if strict:
+            et = (mv[s - 2] << 8 | mv[s - 1]) if l3_offset >= 14 else None
+            if classify(pkt, et) not in accept:
+                st[i] = ST_NOTROCE
+                continue
+        v = icrc(pkt, family)
+        out[i] = (1 if struct.unpack("<I", pkt[-4:])[0] == v else 0) if verify else v
+    return out, st

@@ -31,8 +31,23 @@ namespace {
 
 constexpr uint64_t kStageBytes = 256ull << 20;  // per staging slot (bytes of packets)
 constexpr uint64_t kStagePkts = 1ull << 20;     // per staging slot (packets)
-constexpr uint32_t kWorkSlots = 64;
-constexpr size_t kMaxWorkspaces = 4;  // ragged-path workspaces per device (one per recent stream)
+// Ragged-path workspaces per device, one per recently used stream: batch_host's
+// two slot streams + the context stream + callers' streams.
+constexpr size_t kMaxWorkspaces = 8;
+constexpr uint64_t kRsChunk = 1ull << 30;  // the ragged pipeline's positions are 32-bit: longer batches are cut
+
+// Environment knobs, read ONCE by ricrc_create (diagnostics, tests and
+// schedule studies; the launch path never calls getenv).
+struct Knobs {
+  bool no_sck = false;     // RICRC_NO_SCK: fixed 1/2/4 KiB batches take the transposed kernel
+  bool no_tsk = false;     // RICRC_NO_TSK: ... and 128-512 B batches the direct streaming kernel
+  int sck_grid = 0;        // RICRC_SCK_GRID: cap the strided-chain grid (tests: many groups per wave)
+  int rsck_grid = 0;       // RICRC_RSCK_GRID: cap the ragged fold grid (tests)
+  uint32_t gcost = 0;      // RICRC_RS_GCOST: the ragged fold's per-group cost, quarter lines (0: kRsGroupCost)
+  long fail_chunk = -1;    // RICRC_FAIL_CHUNK: the next ricrc_batch_host fails after queueing chunk k (tests; once)
+  int host_threads = 16;   // RICRC_HOST_THREADS: CPU copy threads of ricrc_batch_host
+};
+bool g_debug = false;  // RICRC_DEBUG: print the HIP/RCCL error behind an -EIO
 
 struct Slot {
   uint8_t *d_buf = nullptr;
@@ -50,31 +65,35 @@ struct Slot {
 struct Dev {
   int id = 0;
   int n_cu = 0;
+  Knobs knobs;
   hipStream_t stream = nullptr;
-  uint32_t *d_inv = nullptr;   // x^(-8 z), z <= 4096
-  uint32_t *d_inv4 = nullptr;  // t: x^(8 (k - t)), k = 0..3, t <= 4096
   uint32_t *d_tzb = nullptr;   // [kTzWords]: basis words 4q of x^(-8 tz) at 2 tz + q (ragged strided-chain path)
   uint32_t *d_x8n = nullptr;   // x^(8 k), k < 65536 (incremental repair)
-  uint32_t *d_work = nullptr;  // kWorkSlots x kSckWorkWords counters (dynamic SCK schedule)
-  uint32_t work_next = 0;      // round-robin slot: launches in flight on different streams never share one
   Slot slot[2];
+  uint8_t *d_status[2] = {nullptr, nullptr};  // batch_host_st: per-slot status staging (device / pinned)
+  uint8_t *h_status[2] = {nullptr, nullptr};
   bool staged = false;
   // Ragged-path workspaces, one per stream that used this device (work on
   // one stream is ordered, so its workspace is never shared by two calls in
   // flight), grown on demand with the stream-ordered allocator; the class
   // counters inside are zeroed on allocation and re-zeroed by the last pass
   // of every call (rsck_gather), so a call costs no allocation and no memset.
+  // Kept in LRU order (front = least recently used).  `done` is recorded
+  // after every use: evicting a workspace (or reusing it on a stream handle
+  // that may name a new stream) orders the free / the reuse after that event
+  // on the GPU -- no host or device-wide wait.
   struct Ws {
     hipStream_t st;
     void *p;
     uint64_t bytes;
     bool dirty;  // a call failed part-way: zero the counters before the next one
+    hipEvent_t done;
   };
   std::vector<Ws> ws;
 };
 
 int hip_err(hipError_t e) {
-  if (e != hipSuccess && getenv("RICRC_DEBUG")) fprintf(stderr, "libroceicrc: HIP error %d: %s\n", (int)e, hipGetErrorString(e));
+  if (e != hipSuccess && g_debug) fprintf(stderr, "libroceicrc: HIP error %d: %s\n", (int)e, hipGetErrorString(e));
   return e == hipSuccess ? 0 : (e == hipErrorOutOfMemory ? -ENOMEM : -EIO);
 }
 
@@ -112,7 +131,7 @@ struct HostRange {
 struct ricrc_ctx {
   std::vector<Dev> devs;
   std::vector<HostRange> pinned;  // host ranges the DMA engines may read directly
-  int host_threads = 1;           // CPU copy threads for pageable host batches
+  Knobs knobs;
   std::vector<ncclComm_t> comms;  // ricrc_comm_init: one RCCL communicator per device
 };
 
@@ -125,20 +144,6 @@ int init_dev(Dev &d) {
   HIP_TRY(hipGetDeviceProperties(&prop, d.id));
   d.n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
-  std::vector<uint32_t> inv(4097);  // z in [0, 4096]
-  const uint32_t step = gf_xinv8n(1);
-  uint32_t v = kOne;
-  for (int z = 0; z <= 4096; ++z) {
-    inv[z] = v;
-    v = gf_mul(v, step);
-  }
-  HIP_TRY(hipMalloc(&d.d_inv, 4097 * sizeof(uint32_t)));
-  HIP_TRY(hipMemcpy(d.d_inv, inv.data(), 4097 * sizeof(uint32_t), hipMemcpyHostToDevice));
-  std::vector<uint32_t> inv4(4097 * 4);  // t, k: x^(8 (k - t))
-  for (int t = 0; t <= 4096; ++t)
-    for (int k = 0; k < 4; ++k) inv4[4 * t + k] = k >= t ? gf_x8n((uint64_t)(k - t)) : gf_xinv8n((uint64_t)(t - k));
-  HIP_TRY(hipMalloc(&d.d_inv4, inv4.size() * sizeof(uint32_t)));
-  HIP_TRY(hipMemcpy(d.d_inv4, inv4.data(), inv4.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
   // Basis word 4q of x^(-8 tz) is x^(-8 tz) x^(31 - 4q) = x^(31 - 4 (2 tz + q)):
   // one entry per m = 2 tz + q; the kernel derives words 4q+1..4q+3 by x^-1.
   std::vector<uint32_t> tzb(kTzWords);
@@ -156,8 +161,6 @@ int init_dev(Dev &d) {
   }
   HIP_TRY(hipMalloc(&d.d_x8n, x8n.size() * sizeof(uint32_t)));
   HIP_TRY(hipMemcpy(d.d_x8n, x8n.data(), x8n.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-  HIP_TRY(hipMalloc(&d.d_work, kWorkSlots * kSckWorkWords * sizeof(uint32_t)));
-  HIP_TRY(hipMemset(d.d_work, 0, kWorkSlots * kSckWorkWords * sizeof(uint32_t)));
   return 0;
 }
 
@@ -176,6 +179,10 @@ int ensure_staging(Dev &d) {
     HIP_TRY(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
   }
+  for (int k = 0; k < 2; ++k) {
+    HIP_TRY(hipMalloc(&d.d_status[k], kStagePkts));
+    HIP_TRY(hipHostMalloc(&d.h_status[k], kStagePkts, hipHostMallocDefault));
+  }
   d.staged = true;
   return 0;
 }
@@ -188,14 +195,14 @@ void free_dev(Dev &d) {
     (void)hipHostFree(s.h_buf), (void)hipHostFree(s.h_off), (void)hipHostFree(s.h_len), (void)hipHostFree(s.h_out);
     if (s.st) (void)hipStreamDestroy(s.st);
   }
-  if (!d.ws.empty()) (void)hipDeviceSynchronize();  // the workspaces' streams may be gone already
-  for (Dev::Ws &w : d.ws) (void)hipFree(w.p);
+  for (int k = 0; k < 2; ++k) (void)hipFree(d.d_status[k]), (void)hipHostFree(d.h_status[k]);
+  for (Dev::Ws &w : d.ws) {  // wait for each workspace's last use (its stream may be gone already)
+    if (w.done) (void)hipEventSynchronize(w.done), (void)hipEventDestroy(w.done);
+    (void)hipFree(w.p);
+  }
   d.ws.clear();
-  (void)hipFree(d.d_inv);
-  (void)hipFree(d.d_inv4);
   (void)hipFree(d.d_tzb);
   (void)hipFree(d.d_x8n);
-  (void)hipFree(d.d_work);
   if (d.stream) (void)hipStreamDestroy(d.stream);
 }
 
@@ -206,19 +213,36 @@ int ilog2_ceil(uint32_t v) {
 }
 
 // The ragged-path workspace of stream st on device d, at least `bytes`.
+// launch_rsck_range records the workspace's `done` event after the call's kernels.
 int ragged_ws(Dev &d, hipStream_t st, uint64_t bytes, Dev::Ws **out) {
-  Dev::Ws *w = nullptr;
-  for (Dev::Ws &x : d.ws)
-    if (x.st == st) w = &x;
-  if (!w) {
-    if (d.ws.size() >= kMaxWorkspaces) {  // bound the pool: drop the oldest (its stream may be gone)
-      HIP_TRY(hipDeviceSynchronize());
-      (void)hipFree(d.ws.front().p);
+  size_t at = d.ws.size();
+  for (size_t k = 0; k < d.ws.size(); ++k)
+    if (d.ws[k].st == st) at = k;
+  if (at < d.ws.size()) {
+    Dev::Ws w = d.ws[at];
+    d.ws.erase(d.ws.begin() + at);
+    // Same handle: the same stream (ordered already) or a new stream that
+    // reuses a destroyed one's handle (not ordered after its last call).
+    // The HIP runtime torch ships has no hipStreamGetId to tell them apart,
+    // so a last use that is still in flight is waited for on the GPU.
+    const hipError_t q = hipEventQuery(w.done);
+    if (q == hipErrorNotReady) HIP_TRY(hipStreamWaitEvent(st, w.done, 0));
+    else if (q != hipSuccess) return hip_err(q);
+    d.ws.push_back(w);  // most recently used
+  } else {
+    Dev::Ws w{st, nullptr, 0, true, nullptr};
+    if (d.ws.size() >= kMaxWorkspaces) {  // evict the least recently used, in stream order on st
+      Dev::Ws old = d.ws.front();
       d.ws.erase(d.ws.begin());
+      HIP_TRY(hipStreamWaitEvent(st, old.done, 0));
+      if (old.p) HIP_TRY(hipFreeAsync(old.p, st));
+      w.done = old.done;  // re-recorded after this call
+    } else {
+      HIP_TRY(hipEventCreateWithFlags(&w.done, hipEventDisableTiming));
     }
-    d.ws.push_back(Dev::Ws{st, nullptr, 0, true});
-    w = &d.ws.back();
+    d.ws.push_back(w);
   }
+  Dev::Ws *w = &d.ws.back();
   if (w->bytes < bytes) {
     if (w->p) HIP_TRY(hipFreeAsync(w->p, st));
     w->p = nullptr;
@@ -237,17 +261,54 @@ int ragged_ws(Dev &d, hipStream_t st, uint64_t bytes, Dev::Ws **out) {
 }
 
 // Kernel selection + launch for one device-resident batch.
-// True if the batch takes the strided-chain kernel (back-to-back 1, 2 or 4
-// KiB packets, 16-byte aligned), which applies any address family natively.
-bool sck_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride, uint64_t count,
-               uint32_t l3_offset, int n_cu) {
-  if (off || len || l3_offset != 0 || ((uintptr_t)base % 16) != 0 || getenv("RICRC_NO_SCK") != nullptr) return false;
-  if (stride != 1024 && stride != 2048 && stride != 4096) return false;
+// The strided-chain kernel's grid for a batch, or 0 if the batch does not
+// take it (it needs back-to-back 1, 2 or 4 KiB packets, 16-byte aligned); it
+// applies any address family natively.
+int sck_grid(const Dev &d, const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
+             uint64_t count, uint32_t l3_offset) {
+  if (off || len || l3_offset != 0 || ((uintptr_t)base % 16) != 0 || d.knobs.no_sck || count == 0) return 0;
+  if (stride != 1024 && stride != 2048 && stride != 4096) return 0;
   const uint64_t groups = (count + 7) / 8;
-  int sgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)n_cu, (groups + 15) / 16));
-  if (const char *e = getenv("RICRC_SCK_GRID")) sgrid = std::max(1, std::min(sgrid, atoi(e)));  // tests
-  const uint64_t waves = 16ull * (uint64_t)sgrid;
-  return (groups + waves - 1) / waves * 8ull * stride < (1ull << 31);  // each wave's span: a 31-bit buffer offset
+  int g = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)d.n_cu, (groups + 15) / 16));
+  if (d.knobs.sck_grid > 0) g = std::min(g, d.knobs.sck_grid);
+  return g;
+}
+
+// The ragged strided-chain pipeline (icrc_rsck.hip) on packets [0, count) of
+// the batch, count < 2^31.
+int launch_rsck_range(Dev &d, const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
+                      uint64_t count, uint32_t fixed_len, uint32_t l3_offset, uint32_t *out, hipStream_t st,
+                      bool verify) {
+  RsckArgs k{};
+  k.base = base;
+  k.off = off;
+  k.len = len;
+  k.stride = stride;
+  k.count = count;
+  k.fixed_len = fixed_len;
+  k.l3_offset = l3_offset;
+  k.verify = verify ? 1u : 0u;
+  k.group_cost = d.knobs.gcost ? d.knobs.gcost : kRsGroupCost;
+  k.out = out;
+  k.tzb = d.d_tzb;
+  const uint32_t xi = gf_xinv8n(4);
+  const uint32_t xi2 = gf_xinv8n(8), xi3 = gf_xinv8n(12);
+  for (int j = 0; j < 32; ++j) {
+    k.XB[j] = gf_mul(xi, 1u << j);
+    k.XB2[j] = gf_mul(xi2, 1u << j);
+    k.XB3[j] = gf_mul(xi3, 1u << j);
+  }
+  for (int s = 0; s < 8; ++s) k.QS[s] = gf_xinv8n(16ull * s);
+  Dev::Ws *ws = nullptr;
+  const int wrc = ragged_ws(d, st, rs_workspace_bytes(count), &ws);
+  if (wrc) return wrc;
+  rs_bind_workspace(k, ws->p);
+  int rgrid = d.n_cu;
+  if (d.knobs.rsck_grid > 0) rgrid = std::min(rgrid, d.knobs.rsck_grid);
+  const hipError_t e = launch_rsck(k, rgrid, st);
+  if (e != hipSuccess) ws->dirty = true;
+  const hipError_t e2 = hipEventRecord(ws->done, st);
+  return hip_err(e != hipSuccess ? e : e2);
 }
 
 int launch_batch_v4(Dev &d, const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
@@ -258,6 +319,20 @@ int launch_batch_v4(Dev &d, const uint8_t *base, const uint64_t *off, const uint
   const uint32_t fixed_len = stride > l3_offset ? (uint32_t)std::min<uint64_t>(stride - l3_offset, 0xFFFFFFFFu) : 0u;
   const bool aligned = ((uintptr_t)first % 16 == 0) && (stride % 16 == 0);
   if (!off && !len && aligned && fixed_len >= kMinLen && fixed_len <= kMaxLen && fixed_len % 4 == 0) {
+    // Back-to-back 1, 2 or 4 KiB packets: the strided-chain kernel (no LDS transpose).
+    if (const int sgrid = sck_grid(d, base, off, len, stride, count, l3_offset)) {
+      SckArgs k{};
+      k.family = family;
+      k.base = base;
+      k.count = count;
+      k.out = out;
+      k.n = fixed_len;
+      k.verify = verify ? 1u : 0u;
+      const uint32_t xi = gf_xinv8n(4);
+      for (int j = 0; j < 32; ++j) k.XB[j] = gf_mul(xi, 1u << j);
+      for (int s = 0; s < 8; ++s) k.QS[s] = gf_xinv8n(16ull * s + 4);
+      return hip_err(launch_sck(k, sgrid, st));
+    }
     const uint32_t M = fixed_len - 4;
     int cpl = 0;
     for (int c : {1, 2, 4})
@@ -265,7 +340,29 @@ int launch_batch_v4(Dev &d, const uint8_t *base, const uint64_t *off, const uint
         cpl = c;
         break;
       }
-    if (cpl) {
+    // Back-to-back packets of 32 * 2^j bytes: coalesced + LDS-transposed kernel.
+    // (64-byte packets: the direct streaming kernel is faster, 20.1 vs 23.8 us on 1 M x 64 B.)
+    if (cpl && l3_offset == 0 && stride == fixed_len && fixed_len >= 128 && fixed_len <= 4096 &&
+        (fixed_len & (fixed_len - 1)) == 0 && ((uintptr_t)base % 16 == 0) && !d.knobs.no_tsk) {
+      TskArgs t{};
+      t.base = base;
+      t.stride = stride;
+      t.count = count;
+      t.out = out;
+      t.n_iters = (count * stride + 4095) / 4096;
+      t.log2C = (uint32_t)ilog2_ceil(fixed_len / 32);
+      t.verify = verify ? 1u : 0u;
+      for (uint32_t p = 0; p < 128; ++p) {
+        const int64_t dd = (int64_t)M - 32 * (int64_t)(p + 1);
+        t.K[p] = p < fixed_len / 32 ? (dd >= 0 ? gf_x8n((uint64_t)dd) : gf_xinv8n((uint64_t)-dd)) : 0u;
+      }
+      const uint32_t y = gf_x8n(2048);
+      for (int j = 0; j < 32; ++j) t.YB[j] = gf_mul(y, 1u << j);
+      const uint64_t tw = (t.n_iters + 15) / 16;
+      const int tgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)d.n_cu, tw));
+      return hip_err(launch_tsk(t, tgrid, st));
+    }
+    if (cpl) {  // any other fixed length up to 16 KiB: lanes fold 64 CPL-byte chunks
       StreamArgs a{};
       const uint32_t chunk = 64u * cpl;
       a.base = first;
@@ -285,122 +382,20 @@ int launch_batch_v4(Dev &d, const uint8_t *base, const uint64_t *off, const uint
       }
       const uint64_t want = (a.n_iters + 15) / 16;
       const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)d.n_cu, want));
-      // Back-to-back 1, 2 or 4 KiB packets: the strided-chain kernel (no LDS
-      // transpose), as long as each wave's span fits a 31-bit buffer offset.
-      if (sck_batch(base, off, len, stride, count, l3_offset, d.n_cu)) {
-        const uint64_t groups = (count + 7) / 8;
-        int sgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)d.n_cu, (groups + 15) / 16));
-        if (const char *e = getenv("RICRC_SCK_GRID")) sgrid = std::max(1, std::min(sgrid, atoi(e)));  // tests
-        {
-          SckArgs k{};
-          k.family = family;
-          k.base = base;
-          k.count = count;
-          k.out = out;
-          k.n = fixed_len;
-          k.verify = verify ? 1u : 0u;
-          const uint32_t xi = gf_xinv8n(4);
-          for (int j = 0; j < 32; ++j) k.XB[j] = gf_mul(xi, 1u << j);
-          for (int s = 0; s < 8; ++s) k.QS[s] = gf_xinv8n(16ull * s + 4);
-          // Dynamic schedule (groups from a device counter): robust when other
-          // kernels (RCCL) hold CUs while this one starts.  RICRC_SCK_STATIC=1:
-          // contiguous per-wave blocks.
-          k.dynamic = getenv("RICRC_SCK_DYNAMIC") != nullptr ? 1u : 0u;
-          k.work = d.d_work + kSckWorkWords * (d.work_next++ % kWorkSlots);
-          return hip_err(launch_sck(k, sgrid, st));
-        }
-      }
-      // Back-to-back packets of 32 * 2^j bytes: coalesced + LDS-transposed kernel.
-      // (64-byte packets: the direct streaming kernel is faster, 20.1 vs 23.8 us on 1 M x 64 B.)
-      if (l3_offset == 0 && stride == fixed_len && fixed_len >= 128 && fixed_len <= 4096 &&
-          (fixed_len & (fixed_len - 1)) == 0 && ((uintptr_t)base % 16 == 0) && getenv("RICRC_NO_TSK") == nullptr) {
-        TskArgs t{};
-        t.base = base;
-        t.stride = stride;
-        t.count = count;
-        t.out = out;
-        t.n_iters = (count * stride + 4095) / 4096;
-        t.log2C = (uint32_t)ilog2_ceil(fixed_len / 32);
-        t.verify = verify ? 1u : 0u;
-        for (uint32_t p = 0; p < 128; ++p) {
-          const int64_t dd = (int64_t)M - 32 * (int64_t)(p + 1);
-          t.K[p] = p < fixed_len / 32 ? (dd >= 0 ? gf_x8n((uint64_t)dd) : gf_xinv8n((uint64_t)-dd)) : 0u;
-        }
-        const uint32_t y = gf_x8n(2048);
-        for (int j = 0; j < 32; ++j) t.YB[j] = gf_mul(y, 1u << j);
-        const uint64_t tw = (t.n_iters + 15) / 16;
-        const int tgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)d.n_cu, tw));
-        return hip_err(launch_tsk(t, tgrid, st));
-      }
       return hip_err(launch_stream(a, cpl, grid, st));
     }
   }
   // Everything else (offsets, lengths, any alignment, Ethernet framing): the
-  // ragged strided-chain pipeline (icrc_rsck.hip), packets bucketed on the
-  // device by line count.  RICRC_NO_RSCK=1 selects the older piece-based
-  // ragged kernel below (kept for comparison and as a second implementation).
-  if (getenv("RICRC_NO_RSCK") == nullptr && count < (1ull << 31)) {
-    RsckArgs k{};
-    k.base = base;
-    k.off = off;
-    k.len = len;
-    k.stride = stride;
-    k.count = count;
-    k.fixed_len = fixed_len;
-    k.l3_offset = l3_offset;
-    k.verify = verify ? 1u : 0u;
-    k.out = out;
-    k.tzb = d.d_tzb;
-    const uint32_t xi = gf_xinv8n(4);
-    const uint32_t xi2 = gf_xinv8n(8), xi3 = gf_xinv8n(12);
-    for (int j = 0; j < 32; ++j) {
-      k.XB[j] = gf_mul(xi, 1u << j);
-      k.XB2[j] = gf_mul(xi2, 1u << j);
-      k.XB3[j] = gf_mul(xi3, 1u << j);
-    }
-    for (int s = 0; s < 8; ++s) k.QS[s] = gf_xinv8n(16ull * s);
-    RaggedArgs small{};
-    small.inv_tab = d.d_inv;
-    small.inv4 = reinterpret_cast<const u32x4_t *>(d.d_inv4);
-    for (uint32_t l = 0; l < 64; ++l) small.K[l] = x8n_host(64ull * (63 - l));
-    Dev::Ws *ws = nullptr;
-    const int wrc = ragged_ws(d, st, rs_workspace_bytes(count), &ws);
-    if (wrc) return wrc;
-    rs_bind_workspace(k, ws->p);
-    int rgrid = d.n_cu;
-    if (const char *e = getenv("RICRC_RSCK_GRID")) rgrid = std::max(1, std::min(rgrid, atoi(e)));  // tests
-    const hipError_t e = launch_rsck(k, small, rgrid, st);
-    if (e != hipSuccess) ws->dirty = true;
-    return hip_err(e);
+  // ragged strided-chain pipeline, packets bucketed on the device by line
+  // count; cut into ranges of kRsChunk packets (its positions are 32-bit).
+  for (uint64_t lo = 0; lo < count; lo += kRsChunk) {
+    const uint64_t m = std::min<uint64_t>(kRsChunk, count - lo);
+    const uint8_t *b = off ? base : base + lo * stride;  // no offsets: the range's first frame at lo * stride
+    const int rc = launch_rsck_range(d, b, off ? off + lo : nullptr, len ? len + lo : nullptr, stride, m,
+                                     fixed_len, l3_offset, out + lo, st, verify);
+    if (rc) return rc;
   }
-  // The piece-based ragged kernel.  Pieces from a device-side scan of the
-  // descriptors, or arithmetic when every packet has the same length and
-  // 16-byte phase.
-  RaggedArgs r{};
-  r.base = base;
-  r.off = off;
-  r.len = len;
-  r.stride = stride;
-  r.count = count;
-  r.out = out;
-  r.inv_tab = d.d_inv;
-  r.inv4 = reinterpret_cast<const u32x4_t *>(d.d_inv4);
-  r.fixed_len = fixed_len;
-  r.l3_offset = l3_offset;
-  r.verify = verify ? 1u : 0u;
-  for (uint32_t l = 0; l < 64; ++l) r.K[l] = x8n_host(64ull * (63 - l));
-  const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)d.n_cu, (count + 63) / 64));
-  if (!off && !len && stride % 16 == 0) {
-    r.P = ragged_pieces((uintptr_t)base + l3_offset, fixed_len);
-    return hip_err(launch_ragged(r, grid, st));
-  }
-  uint64_t *ps = nullptr;
-  HIP_TRY(hipMallocAsync((void **)&ps, (count + 1) * sizeof(uint64_t), st));
-  r.ps = ps;
-  hipError_t e = ragged_piece_scan(r, ps, st);
-  if (e == hipSuccess) e = launch_ragged(r, grid, st);
-  const hipError_t e2 = hipFreeAsync(ps, st);
-  return hip_err(e != hipSuccess ? e : e2);
+  return 0;
 }
 
 // Any address family: the IPv4-mask kernels, then (IPv6 / AUTO) the linear
@@ -410,7 +405,7 @@ int launch_batch(Dev &d, const uint8_t *base, const uint64_t *off, const uint32_
                  uint32_t family = kFamV4) {
   if (family == kFamV4 || count == 0)
     return launch_batch_v4(d, base, off, len, stride, count, l3_offset, out, st, verify);
-  if (sck_batch(base, off, len, stride, count, l3_offset, d.n_cu))  // masks native in the kernel
+  if (sck_grid(d, base, off, len, stride, count, l3_offset))  // masks native in the kernel
     return launch_batch_v4(d, base, off, len, stride, count, l3_offset, out, st, verify, family);
   const int rc = launch_batch_v4(d, base, off, len, stride, count, l3_offset, out, st, false);
   if (rc) return rc;
@@ -468,7 +463,7 @@ Rccl &rccl() {
 
 int nccl_err(ncclResult_t e) {
   if (e == ncclSuccess) return 0;
-  if (getenv("RICRC_DEBUG")) fprintf(stderr, "libroceicrc: RCCL error %d: %s\n", (int)e, rccl().err_str(e));
+  if (g_debug) fprintf(stderr, "libroceicrc: RCCL error %d: %s\n", (int)e, rccl().err_str(e));
   return -EIO;
 }
 
@@ -514,6 +509,65 @@ int comm_allgather(ricrc_ctx *ctx, const uint64_t *counts, uint32_t *const *d_ou
   return rc ? rc : rc2;
 }
 
+// Per-packet status (or classification) of a batch after its ICRC kernels,
+// in stream order (icrc_status.hip).  accept: bit 0 RoCEv2/IPv4, bit 1
+// RoCEv2/IPv6 (0: lengths only); ether: check the EtherType before L3.
+// A fixed-length batch checked for lengths only is all RICRC_ST_OK (its one
+// length was validated by the caller): a memset, no kernel.
+int launch_status_pass(Dev &d, const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
+                       uint64_t count, uint32_t l3_offset, uint32_t accept, bool ether, uint32_t *out,
+                       uint8_t *status, uint8_t *cls, hipStream_t st) {
+  if (count == 0) return 0;
+  if (!cls && !len && !accept) return hip_err(hipMemsetAsync(status, (int)kStOk, count, st));
+  StatusArgs a{};
+  a.base = base;
+  a.off = off;
+  a.len = len;
+  a.stride = stride;
+  a.count = count;
+  a.fixed_len = stride > l3_offset ? (uint32_t)std::min<uint64_t>(stride - l3_offset, 0xFFFFFFFFu) : 0u;
+  a.l3_offset = l3_offset;
+  a.accept = accept;
+  a.ether = ether ? 1u : 0u;
+  a.out = out;
+  a.status = status;
+  a.cls = cls;
+  return hip_err(launch_status(a, d.n_cu, st));
+}
+
+// flags of the *_st calls: a family | RICRC_F_STRICT | RICRC_F_VERIFY.
+struct StFlags {
+  uint32_t fam;
+  bool strict, verify;
+  uint32_t accept;  // StatusArgs::accept
+};
+bool decode_st_flags(uint32_t flags, StFlags &f) {
+  if (flags & ~(3u | RICRC_F_STRICT | RICRC_F_VERIFY)) return false;
+  f.fam = flags & 3u;
+  if (f.fam > RICRC_F_AUTO) return false;
+  f.strict = (flags & RICRC_F_STRICT) != 0;
+  f.verify = (flags & RICRC_F_VERIFY) != 0;
+  f.accept = !f.strict ? 0u : f.fam == RICRC_F_IPV4 ? 1u : f.fam == RICRC_F_IPV6 ? 2u : 3u;
+  return true;
+}
+
+Knobs read_knobs() {
+  Knobs k;
+  auto num = [](const char *name, long dflt) -> long {
+    const char *e = getenv(name);
+    return e ? atol(e) : dflt;
+  };
+  k.no_sck = getenv("RICRC_NO_SCK") != nullptr;
+  k.no_tsk = getenv("RICRC_NO_TSK") != nullptr;
+  k.sck_grid = (int)std::max(0L, num("RICRC_SCK_GRID", 0));
+  k.rsck_grid = (int)std::max(0L, num("RICRC_RSCK_GRID", 0));
+  k.gcost = (uint32_t)std::max(0L, num("RICRC_RS_GCOST", 0));
+  k.fail_chunk = num("RICRC_FAIL_CHUNK", -1);
+  const unsigned hw = std::thread::hardware_concurrency();
+  k.host_threads = (int)std::max(1L, std::min(64L, num("RICRC_HOST_THREADS", (long)std::min(16u, std::max(1u, hw)))));
+  return k;
+}
+
 }  // namespace
 
 extern "C" {
@@ -530,15 +584,12 @@ int ricrc_create_devices(ricrc_ctx **ctx, const int *devices, int n) {
     if (devices[i] < 0 || devices[i] >= avail) return -ENODEV;
   ricrc_ctx *c = new (std::nothrow) ricrc_ctx;
   if (!c) return -ENOMEM;
-  {
-    const unsigned hw = std::thread::hardware_concurrency();
-    int t = (int)std::min(16u, std::max(1u, hw));
-    if (const char *e = getenv("RICRC_HOST_THREADS")) t = std::max(1, std::min(64, atoi(e)));
-    c->host_threads = t;
-  }
+  c->knobs = read_knobs();
+  g_debug = getenv("RICRC_DEBUG") != nullptr;
   c->devs.resize(n);
   for (int i = 0; i < n; ++i) {
     c->devs[i].id = devices[i];
+    c->devs[i].knobs = c->knobs;
     const int rc = init_dev(c->devs[i]);
     if (rc) {
       ricrc_destroy(c);
@@ -620,6 +671,42 @@ int ricrc_verify_device_ex(ricrc_ctx *ctx, int dev, const void *d_base, const ui
                            const uint32_t *d_len, uint32_t stride, uint64_t count, uint32_t l3_offset,
                            uint32_t *d_out, void *stream, uint32_t flags) {
   return batch_device_impl(ctx, dev, d_base, d_off, d_len, stride, count, l3_offset, d_out, stream, true, flags);
+}
+
+int ricrc_batch_device_st(ricrc_ctx *ctx, int dev, const void *d_base, const uint64_t *d_off,
+                          const uint32_t *d_len, uint32_t stride, uint64_t count, uint32_t l3_offset,
+                          uint32_t *d_out, uint8_t *d_status, void *stream, uint32_t flags) {
+  StFlags f;
+  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size() || !decode_st_flags(flags, f)) return -EINVAL;
+  if (count == 0) return 0;
+  if (!d_base || !d_out || !d_status) return -EINVAL;
+  if (!d_off && stride == 0) return -EINVAL;
+  if (!d_len && (stride <= l3_offset || stride - l3_offset < kMinLen || stride - l3_offset > kMaxLen))
+    return -EINVAL;  // one length for the whole batch: a call error, not a per-packet status
+  Dev &d = ctx->devs[dev];
+  DeviceGuard g(d.id);
+  if (!g.ok()) return -ENODEV;
+  hipStream_t st = (hipStream_t)stream;
+  const uint8_t *base = (const uint8_t *)d_base;
+  const int rc = launch_batch(d, base, d_off, d_len, stride, count, l3_offset, d_out, st, f.verify, f.fam);
+  if (rc) return rc;
+  return launch_status_pass(d, base, d_off, d_len, stride, count, l3_offset, f.accept,
+                            f.strict && l3_offset >= 14, d_out, d_status, nullptr, st);
+}
+
+int ricrc_classify_device(ricrc_ctx *ctx, int dev, const void *d_base, const uint64_t *d_off,
+                          const uint32_t *d_len, uint32_t stride, uint64_t count, uint32_t l3_offset,
+                          uint8_t *d_class, void *stream) {
+  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size()) return -EINVAL;
+  if (count == 0) return 0;
+  if (!d_base || !d_class) return -EINVAL;
+  if (!d_off && stride == 0) return -EINVAL;
+  if (!d_len && stride <= l3_offset) return -EINVAL;
+  Dev &d = ctx->devs[dev];
+  DeviceGuard g(d.id);
+  if (!g.ok()) return -ENODEV;
+  return launch_status_pass(d, (const uint8_t *)d_base, d_off, d_len, stride, count, l3_offset, 3u,
+                            l3_offset >= 14, nullptr, nullptr, d_class, (hipStream_t)stream);
 }
 
 int ricrc_repair_device(ricrc_ctx *ctx, int dev, void *d_base, const uint64_t *d_off, const uint32_t *d_len,
@@ -859,8 +946,6 @@ void par_for(uint64_t n, int threads, uint64_t grain, F fn) {
 
 }  // namespace
 
-extern "C" {
-
 // Host batches (host in, host out; the NIC-ring path of SURVEY §8f-4).  The
 // batch is cut into byte-balanced shards, one per device; each device walks
 // its shard in chunks alternating between two staging slots with their own
@@ -873,25 +958,31 @@ extern "C" {
 //   span/copy  same span in pageable memory: parallel memcpy into the pinned
 //              slot, then one DMA;
 //   gather     anything else: packets copied one by one (in parallel) into
-//              the pinned slot, 16-byte aligned, with new offsets.
-int ricrc_batch_host(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *off, const uint32_t *len,
-                     uint32_t stride, uint64_t count, uint32_t l3_offset, uint32_t *out) {
-  return ricrc_batch_host_ex(ctx, base, off, len, stride, count, l3_offset, out, RICRC_F_IPV4);
-}
-
-int ricrc_batch_host_ex(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *off, const uint32_t *len,
-                        uint32_t stride, uint64_t count, uint32_t l3_offset, uint32_t *out, uint32_t flags) {
-  if (!ctx || ctx->devs.empty() || flags > RICRC_F_AUTO) return -EINVAL;
+//              the pinned slot, 16-byte aligned, with new offsets (and, when
+//              the EtherType is checked, the 2 bytes before each L3 header).
+// With a status array (ricrc_batch_host_st) a descriptor length outside
+// [RICRC_MIN_LEN, RICRC_MAX_LEN] is not an error: the packet is staged as 0
+// bytes, the device reports RICRC_ST_BADLEN for it and out[i] = 0.
+static int batch_host_impl(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *off, const uint32_t *len,
+                           uint32_t stride, uint64_t count, uint32_t l3_offset, uint32_t *out, uint8_t *status,
+                           const StFlags &f) {
+  if (!ctx || ctx->devs.empty()) return -EINVAL;
   if (count == 0) return 0;
   if (!base || !out) return -EINVAL;
   if (!off && stride == 0) return -EINVAL;
-  auto pkt_len = [&](uint64_t i) -> uint64_t { return len ? len[i] : (uint64_t)stride - l3_offset; };
-  auto frame = [&](uint64_t i) -> uint64_t { return off ? off[i] : i * (uint64_t)stride; };
   if (!len && stride <= l3_offset) return -EINVAL;
+  auto len_ok = [](uint64_t n) { return n >= kMinLen && n <= kMaxLen; };
+  // Bytes staged for packet i (0 for a bad length under a status array).
+  auto pkt_len = [&](uint64_t i) -> uint64_t {
+    const uint64_t n = len ? len[i] : (uint64_t)stride - l3_offset;
+    return (status && !len_ok(n)) ? 0 : n;
+  };
+  auto frame = [&](uint64_t i) -> uint64_t { return off ? off[i] : i * (uint64_t)stride; };
+  if (!len && !len_ok((uint64_t)stride - l3_offset)) return -EINVAL;  // the batch's one length
   uint64_t total = 0;
   for (uint64_t i = 0; i < count; ++i) {
     const uint64_t n = pkt_len(i);
-    if (n < kMinLen || n > kMaxLen) return -EINVAL;
+    if (!status && !len_ok(n)) return -EINVAL;
     total += n;
   }
   const int ndev = (int)ctx->devs.size();
@@ -918,20 +1009,22 @@ int ricrc_batch_host_ex(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *off
   };
   std::vector<Cur> cur(ndev);
   for (int k = 0; k < ndev; ++k) cur[k] = Cur{cut[k], cut[k + 1], 0, {0, 0}, {0, 0}, {false, false}};
-  const int T = ctx->host_threads;
+  const int T = ctx->knobs.host_threads;
+  const bool ether = f.strict && l3_offset >= 14;  // the EtherType is checked: gather keeps its 2 bytes
 
   auto drain = [&](Dev &d, Cur &c, int s) -> int {
     if (!c.pend[s]) return 0;
     HIP_TRY(hipEventSynchronize(d.slot[s].done));
     memcpy(out + c.pend_lo[s], d.slot[s].h_out, (c.pend_hi[s] - c.pend_lo[s]) * sizeof(uint32_t));
+    if (status) memcpy(status + c.pend_lo[s], d.h_status[s], c.pend_hi[s] - c.pend_lo[s]);
     c.pend[s] = false;
     return 0;
   };
 
-  // Debug knob (tests): RICRC_FAIL_CHUNK=k fails the call with -EIO right
-  // after chunk k (0-based, counted over devices) has been queued.
-  long fail_chunk = -1;
-  if (const char *e = getenv("RICRC_FAIL_CHUNK")) fail_chunk = atol(e);
+  // Debug knob (tests): RICRC_FAIL_CHUNK=k fails the context's next host
+  // call with -EIO right after chunk k (0-based, counted over devices) has
+  // been queued; later calls run normally.
+  const long fail_chunk = ctx->knobs.fail_chunk;
   long chunk_no = 0;
 
   auto run = [&]() -> int {
@@ -982,42 +1075,57 @@ int ricrc_batch_host_ex(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *off
           if (off || len)
             for (uint64_t i = lo; i < hi; ++i) sl.h_off[i - lo] = frame(i) - s_lo + pad;
         } else {
-          // Gather: packed L3 packets, 16-byte aligned each.
+          // Gather: packed L3 packets, 16-byte aligned each (after `pre`
+          // EtherType bytes when those are checked).
+          const uint32_t pre = ether ? 2u : 0u;
           hi = lo;
           bytes = 0;
           while (hi < c.end && hi - lo < kStagePkts) {
-            const uint64_t padded = (pkt_len(hi) + 15) & ~15ull;
+            const uint64_t padded = (pre ? 16u : 0u) + ((pkt_len(hi) + 15) & ~15ull);
             if (bytes + padded > kStageBytes) break;
-            sl.h_off[hi - lo] = bytes;
+            sl.h_off[hi - lo] = bytes + (pre ? 16u - pre : 0u);
             bytes += padded;
             ++hi;
           }
           m = hi - lo;
           par_for(m, T, 4096, [&](uint64_t a, uint64_t b) {
-            for (uint64_t i = a; i < b; ++i)
-              memcpy(sl.h_buf + sl.h_off[i], base + frame(lo + i) + l3_offset, pkt_len(lo + i));
+            for (uint64_t i = a; i < b; ++i) {
+              const uint64_t n = pkt_len(lo + i);
+              if (n) memcpy(sl.h_buf + sl.h_off[i], base + frame(lo + i) + l3_offset - pre, n + pre);
+            }
           });
           HIP_TRY(hipMemcpyAsync(sl.d_buf, sl.h_buf, bytes, hipMemcpyHostToDevice, sl.st));
-          kl3 = 0;
+          kl3 = pre;
         }
         const bool fixed = span && !off && !len;  // frames at i*stride from d_buf + pad
-        if (fixed) {
-          rc = launch_batch(d, sl.d_buf + pad, nullptr, nullptr, stride, m, kl3, sl.d_out, sl.st, false, flags);
-        } else {
+        const uint8_t *dbase = fixed ? sl.d_buf + pad : sl.d_buf;
+        const uint64_t *doff = nullptr;
+        const uint32_t *dlen = nullptr;
+        const uint32_t dstride = fixed ? stride : 0;
+        if (!fixed) {
           HIP_TRY(hipMemcpyAsync(sl.d_off, sl.h_off, m * sizeof(uint64_t), hipMemcpyHostToDevice, sl.st));
           for (uint64_t i = 0; i < m; ++i) sl.h_len[i] = (uint32_t)pkt_len(lo + i);
           HIP_TRY(hipMemcpyAsync(sl.d_len, sl.h_len, m * sizeof(uint32_t), hipMemcpyHostToDevice, sl.st));
-          rc = launch_batch(d, sl.d_buf, sl.d_off, sl.d_len, 0, m, kl3, sl.d_out, sl.st, false, flags);
+          doff = sl.d_off;
+          dlen = sl.d_len;
         }
+        rc = launch_batch(d, dbase, doff, dlen, dstride, m, kl3, sl.d_out, sl.st, f.verify, f.fam);
+        if (!rc && status)
+          rc = launch_status_pass(d, dbase, doff, dlen, dstride, m, kl3, f.accept, ether, sl.d_out, d.d_status[s],
+                                  nullptr, sl.st);
         if (rc) return rc;
         HIP_TRY(hipMemcpyAsync(sl.h_out, sl.d_out, m * sizeof(uint32_t), hipMemcpyDeviceToHost, sl.st));
+        if (status) HIP_TRY(hipMemcpyAsync(d.h_status[s], d.d_status[s], m, hipMemcpyDeviceToHost, sl.st));
         HIP_TRY(hipEventRecord(sl.done, sl.st));
         c.pend[s] = true;
         c.pend_lo[s] = lo;
         c.pend_hi[s] = hi;
         c.next = hi;
         c.slot ^= 1;
-        if (chunk_no++ == fail_chunk) return -EIO;
+        if (chunk_no++ == fail_chunk) {
+          ctx->knobs.fail_chunk = -1;
+          return -EIO;
+        }
       }
     }
     for (int k = 0; k < ndev; ++k)
@@ -1042,6 +1150,28 @@ int ricrc_batch_host_ex(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *off
     return rc;
   }
   return 0;
+}
+
+extern "C" {
+
+int ricrc_batch_host(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *off, const uint32_t *len,
+                     uint32_t stride, uint64_t count, uint32_t l3_offset, uint32_t *out) {
+  return ricrc_batch_host_ex(ctx, base, off, len, stride, count, l3_offset, out, RICRC_F_IPV4);
+}
+
+int ricrc_batch_host_ex(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *off, const uint32_t *len,
+                        uint32_t stride, uint64_t count, uint32_t l3_offset, uint32_t *out, uint32_t flags) {
+  StFlags f;
+  if (flags > RICRC_F_AUTO || !decode_st_flags(flags, f)) return -EINVAL;
+  return batch_host_impl(ctx, base, off, len, stride, count, l3_offset, out, nullptr, f);
+}
+
+int ricrc_batch_host_st(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *off, const uint32_t *len,
+                        uint32_t stride, uint64_t count, uint32_t l3_offset, uint32_t *out, uint8_t *status,
+                        uint32_t flags) {
+  StFlags f;
+  if (!decode_st_flags(flags, f) || (count && !status)) return -EINVAL;
+  return batch_host_impl(ctx, base, off, len, stride, count, l3_offset, out, status, f);
 }
 
 }  // extern "C"

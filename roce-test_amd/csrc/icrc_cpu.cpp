@@ -119,7 +119,7 @@ int ricrc_repair_one(const uint8_t *l3, uint32_t n, uint32_t off, const uint8_t 
 }
 
 int ricrc_classify(const uint8_t *l3, uint32_t n) {
-  if (!l3 || n < 4) return 0;
+  if (!l3 || n < RICRC_MIN_LEN || n > RICRC_MAX_LEN) return 0;
   if (ricrc_is_rocev2(l3, n)) return 4;
   // IPv6: version 6, next header UDP, payload length = n - 40, dport 4791.
   if (n < 40 + 8 + 12 + 4 || (l3[0] >> 4) != 6 || l3[6] != 17) return 0;

@@ -8,10 +8,6 @@
 
 namespace ricrc {
 
-struct u32x4_t {
-  uint32_t v[4];
-};
-
 // Fixed-length batch, packet i at base + i*stride, 16-byte aligned.
 struct StreamArgs {
   const uint8_t *base;  // first packet's L3 start
@@ -49,48 +45,14 @@ struct RsDesc {
   uint32_t lo, hi;
 };
 
-// Ragged batches (any alignment, per-packet offsets and/or lengths): the
-// batch is cut into 64-byte pieces, packet by packet -- packet i covers
-// pieces [ps[i], ps[i+1]) laid from its start rounded down to 16 B -- and a
-// wave step maps 64 consecutive pieces onto its 64 lanes, however many
-// packets they belong to.
-struct RaggedArgs {
-  const uint8_t *base;
-  const uint64_t *off;     // may be null (then p * stride)
-  const uint32_t *len;     // may be null (then fixed_len)
-  const uint64_t *ps;      // exclusive prefix of pieces, count + 1 entries; null: uniform
-  uint64_t stride;
-  uint64_t count;
-  uint32_t *out;
-  const uint32_t *inv_tab;  // x^(-8 z), z in [0, 4096]
-  const u32x4_t *inv4;      // entry t: x^(8 (k - t)) for k = 0..3, t in [0, 4096]
-  uint32_t fixed_len;
-  uint32_t l3_offset;
-  uint32_t verify;
-  uint32_t P;              // pieces per packet when ps == null
-  uint32_t K[64];          // x^(8*64*(63-lane)): lane piece end -> step end
-  // Descriptor mode (the small packets of the ragged strided-chain path):
-  // packet i is desc[i], the count is *dev_count (device memory).
-  const RsDesc *desc;
-  const uint32_t *dev_count;
-};
-
-// Pieces of a packet of n bytes whose L3 header starts at address `start`:
-// the CRC'd bytes [0, n-4) plus the start's offset inside its 16-byte unit,
-// in 64-byte pieces (at least one; invalid lengths get one and yield 0).
-__host__ __device__ inline uint32_t ragged_pieces(uintptr_t start, uint32_t n) {
-  if (n < 4 || n > 65535) return 1u;
-  const uint32_t p = ((uint32_t)(start & 15u) + (n - 4u) + 63u) >> 6;
-  return p ? p : 1u;
-}
-
 // Ragged strided-chain path (icrc_rsck.hip): any packet addresses and
 // lengths, packets bucketed by their number of 128-byte lines on the device,
 // 8 packets of equal line count per group, folded as in the SCK.
 // Classes: 0 = not bucketed (n < 44 or n > 65535: done in the count pass);
 // 1 + P for packets spanning <= kRsSmallL lines, by their 64-byte piece count P
-// (they go to the piece kernel: 8 lanes per packet is too coarse for them);
-// kRsBigBase + L for the rest, by line count L (the strided-chain fold).
+// (one lane per packet, icrc_rsmall_kernel: 8 lanes per packet is too coarse
+// for them); kRsBigBase + L for the rest, by line count L (the strided-chain
+// fold).
 #ifndef RICRC_RS_SMALL_L  // tools/microbench only
 #define RICRC_RS_SMALL_L 1
 #endif
@@ -105,7 +67,6 @@ struct RsPlan {
   uint32_t L[kRsClasses];   // compact, ascending
   uint32_t g0[kRsClasses];  // first group of the class
   uint64_t s0[kRsClasses];  // weighted work before the class's first group
-  uint64_t ps0[kRsClasses]; // small classes: first piece of the class (by class index)
 };
 struct RsckArgs {
   const uint8_t *base;
@@ -116,7 +77,6 @@ struct RsckArgs {
   uint32_t fixed_len;
   uint32_t l3_offset;
   uint32_t verify;
-  uint32_t piece;       // the small region goes to the piece kernel (RICRC_RS_PIECE): write its piece prefix
   uint32_t group_cost;  // a group's finish in line-steps of the fold's work split (launch_rsck sets it)
   uint32_t *out;
   // device workspace (icrc_api.cpp sizes it: rs_workspace_bytes)
@@ -128,14 +88,25 @@ struct RsckArgs {
   uint32_t *pos_of;   // [count] position of packet i, or ~0 (written by the scatter pass)
   uint32_t *res;      // [count + 8 kRsClasses] results in class order
   uint32_t *hist;     // [pass blocks][kRsClasses] per-block class counts
-  uint64_t *ps;       // [count + 8 kRsClasses + 1] piece prefix of the small region
-  uint32_t *small_pos;  // positions of the small region (device count for the piece kernel)
+  uint32_t *small_pos;  // positions of the small region [0, *small_pos) (device count)
   const uint32_t *tzb;  // [kTzWords]: entry m = x^(31 - 4 m), i.e. basis word 4 q of x^(-8 tz) at m = 2 tz + q
   uint32_t XB[32];      // basis of x^-32
   uint32_t XB2[32];     // basis of x^-64
   uint32_t XB3[32];     // basis of x^-96
   uint32_t QS[8];       // x^(-8*16 s): lane slot s -> line start
 };
+// Work of a group in line-steps: its L lines plus the per-group finish
+// (GF(2) multiplies through nibble tables, reductions, descriptor and slot
+// traffic).  Waves split the total weighted work, not the lines: split by
+// lines, a wave that drew 64-byte packets (one line per group) ran ~8x longer
+// than one that drew 4 KiB packets.  Swept on C4 (same box, tools/ab_env.sh
+// with RICRC_RS_GCOST, profiles/r02/ab_c4_group_cost.txt): 0 -> 1.52 ms per
+// step, 1 -> 1.16, 2 -> 1.060-1.081, 3 -> 1.061-1.062, 4 -> 1.065-1.086,
+// 6 (round 1's estimate) -> 1.073-1.076, 10 -> 1.09, 16 -> 1.13.  In quarter
+// line-steps 10..14 are within the run-to-run noise (profiles/r02/
+// ab_c4_group_cost_quarters.txt).
+// (RICRC_RS_GCOST, read by ricrc_create, overrides it for schedule studies.)
+constexpr uint32_t kRsGroupCost = 12;  // quarter line-steps (3 lines)
 uint64_t rs_workspace_bytes(uint64_t count);
 // Carves the workspace (rs_workspace_bytes(count) bytes at ws) into a.
 void rs_bind_workspace(RsckArgs &a, void *ws);
@@ -143,8 +114,8 @@ void rs_bind_workspace(RsckArgs &a, void *ws);
 // leaves them zero).
 hipError_t rs_zero_counters(void *ws, hipStream_t st);
 // The whole ragged pipeline on `st`: count/classify, plan, scatter, fold, gather.
-// `small` carries the piece kernel's tables (inv_tab, inv4, K) for the small packets.
-hipError_t launch_rsck(RsckArgs &a, const RaggedArgs &small, int grid, hipStream_t st);
+// count < 2^31 (the host cuts larger batches).
+hipError_t launch_rsck(RsckArgs &a, int grid, hipStream_t st);
 
 struct SynthArgs {
   uint8_t *buf;
@@ -190,11 +161,24 @@ hipError_t launch_family_fix(const FamilyFixArgs &a, int grid, hipStream_t st);
 
 hipError_t launch_stream(const StreamArgs &a, int cpl, int grid, hipStream_t st);
 hipError_t launch_tsk(const TskArgs &a, int grid, hipStream_t st);
-hipError_t launch_ragged(const RaggedArgs &a, int grid, hipStream_t st);
-// ps[0..count] = exclusive prefix of ragged_pieces over the batch (stream
-// ordered; temporary storage from the stream-ordered allocator).
-hipError_t ragged_piece_scan(const RaggedArgs &a, uint64_t *ps, hipStream_t st);
 hipError_t launch_synth(const SynthArgs &a, hipStream_t st);
+
+// Per-packet status / RoCEv2 classification after a batch ran (icrc_status.hip):
+// the reference's ingress accept path, shuffle_ingress_parser.p4:12-36.
+constexpr uint32_t kStOk = 0, kStBadLen = 1, kStNotRoce = 2;  // RICRC_ST_* (include/roce_icrc.h)
+struct StatusArgs {
+  const uint8_t *base;
+  const uint64_t *off;  // may be null (then i * stride)
+  const uint32_t *len;  // may be null (then fixed_len)
+  uint64_t stride, count;
+  uint32_t fixed_len, l3_offset;
+  uint32_t accept;  // bit 0: RoCEv2/IPv4, bit 1: RoCEv2/IPv6 accepted; 0: lengths only (no header read)
+  uint32_t ether;   // frames are Ethernet: the EtherType (2 bytes before L3) must match the family
+  uint32_t *out;    // zeroed where status != OK (may be null)
+  uint8_t *status;  // status mode: per-packet RICRC_ST_*
+  uint8_t *cls;     // classify mode (non-null): per-packet 4 / 6 / 0 instead of a status
+};
+hipError_t launch_status(const StatusArgs &a, int n_cu, hipStream_t st);
 hipError_t launch_synth_ragged(const SynthArgs &a, hipStream_t st);
 // ricrc_prime's streaming read of `bytes` (a multiple of 16) of scratch.
 hipError_t launch_prime(const void *scratch, uint64_t bytes, uint32_t *sink, int n_cu, hipStream_t st);

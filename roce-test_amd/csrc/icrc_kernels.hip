@@ -496,406 +496,6 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
 }
 
 // =======================================================================
-// Ragged kernel: any alignment, per-packet offsets and/or lengths, any mix
-// of sizes.  The batch is a sequence of 64-byte pieces (packet i owns pieces
-// [ps[i], ps[i+1]), laid from its L3 start rounded down to 16 B, so every
-// load is an aligned 16-byte unit that holds packet bytes), and a wave step
-// puts 64 consecutive pieces on its 64 lanes whatever packets they belong
-// to: a 64-byte packet costs one lane, not one wave.
-//
-// Per step, lane l:
-//  * finds its packet: lanes j load the starts of packets pc+j, a
-//    ds_permute marks the lanes where packets begin, mbcnt over that ballot
-//    gives each lane its packet, ds_bpermute fetches the packet's start,
-//    length and first piece from the lane that loaded them;
-//  * folds its piece from a zero register (bytes outside [0, n-4) zeroed,
-//    invariant masks and the seed applied by packet-relative offset) and
-//    aligns it to the step's end with its lane constant x^(512 (63-l)) (a
-//    precomputed basis, as in the streaming kernel);
-//  * an inclusive prefix XOR over the wave (DPP row shifts + readlane row
-//    totals) gives every packet's XOR as P[last] ^ P[first-1];
-//  * the packet's last lane removes the alignment and the zero tail with
-//    one multiply by x^-(8 z + 512 (63-l)) (basis row from a table) and
-//    stores.
-// A packet still open at lane 63 is carried into lane 0 of the next step,
-// shifted by x^(8*4096).  Waves own contiguous piece ranges cut at packet
-// boundaries, so no packet is split between waves.
-// =======================================================================
-__device__ constexpr Basis g_x4096 = make_const_basis(gf_x8n(4096));
-
-// r * K for a wave-uniform r and a constant basis: scalar ALU code.
-__device__ __forceinline__ uint32_t mul_const_uniform(uint32_t r, const Basis &B) {
-  uint32_t acc = 0u;
-#pragma unroll
-  for (int j = 0; j < 32; ++j) acc ^= ((r >> j) & 1u) ? B.q[j] : 0u;
-  return acc;
-}
-
-// Inclusive prefix XOR over the 64 lanes.
-__device__ __forceinline__ uint32_t wave_prefix_xor(uint32_t v, uint32_t lane) {
-  v ^= __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xF, 0xF, true);  // row_shr:1
-  v ^= __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xF, 0xF, true);  // row_shr:2
-  v ^= __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xF, 0xF, true);  // row_shr:4
-  v ^= __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xF, 0xF, true);  // row_shr:8
-  const uint32_t t0 = __builtin_amdgcn_readlane(v, 15), t1 = __builtin_amdgcn_readlane(v, 31);
-  const uint32_t t2 = __builtin_amdgcn_readlane(v, 47);
-  const uint32_t row = lane >> 4;
-  const uint32_t add = row == 0 ? 0u : row == 1 ? t0 : row == 2 ? (t0 ^ t1) : (t0 ^ t1 ^ t2);
-  return v ^ add;
-}
-
-// Software pipeline per wave: step i maps step i+1 (its descriptors were
-// loaded during step i-1), issues step i+1's piece loads and step i+2's
-// descriptor loads, then folds step i -- every global load has one step of
-// slack.  Loads are unconditional (lanes without a unit read a device table
-// the kernel owns) so the compiler counts vmcnt instead of draining at a
-// branch join.  MODE: 4 RsDesc descriptors + device-side count (the small
-// packets of the ragged strided-chain path), 0 uniform (no descriptors), 1 offsets + lengths,
-// 2 offsets only, 3 lengths only.
-// ABL: timing-only ablation mask for tools/microbench/ragged_abl.hip (the
-// product instantiates 0): 1 no table fold, 2 no finish slices, 4 no piece
-// loads, 8 no word masking, 32 no result stores (folded into one per wave),
-// 64 no end-lane multiply, 128 no carry multiply, 256 no lane alignment.
-template <int MODE, int kRaggedBlock, int ABL = 0>
-__global__ __launch_bounds__(kRaggedBlock) void icrc_ragged_kernel(RaggedArgs a) {
-  constexpr bool UNI = MODE == 0, HAS_OFF = MODE == 1 || MODE == 2, HAS_LEN = MODE == 1 || MODE == 3;
-  constexpr bool DESC = MODE == 4;
-  // 128 KiB slice tables + the lanes' alignment bases (8 KiB, shared by all
-  // waves: word 4q+i of lane l's basis at 16-byte slot q*64 + l, so the
-  // eight ds_read_b128 of a multiply are conflict-free).
-  __shared__ uint32_t lds[kLdsWords + 64 * 32];
-  fill_tables(lds);
-  if (threadIdx.x < 64) {
-    uint32_t Qb[32];
-    make_basis(a.K[threadIdx.x], Qb);
-#pragma unroll
-    for (int j = 0; j < 32; ++j) lds[kLdsWords + (((j >> 2) * 64 + threadIdx.x) << 2) + (j & 3)] = Qb[j];
-  }
-  __syncthreads();
-
-  const uint32_t lane = threadIdx.x & 63;
-  const LaneTab lt{(lane & 31) << 2, ((lane & 31) << 2) | 0x10000u};
-  const u32x4 *qrow = reinterpret_cast<const u32x4 *>(lds + kLdsWords) + lane;
-  // Half h of r * x^(512 (63 - lane)): basis words 16h..16h+15 from LDS.
-  auto mul_lane_part = [&](uint32_t r, int h, uint32_t (&acc)[4]) {
-#pragma unroll
-    for (int q = 4 * h; q < 4 * h + 4; ++q) {
-      const u32x4 b = qrow[64 * q];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int j = 4 * q + i;
-        const uint32_t mk = (uint32_t)(((int32_t)(r << (31 - j))) >> 31);
-        acc[i] = and_xor(mk, b[i], acc[i]);
-      }
-    }
-  };
-
-  const uint64_t wave = (uint64_t)blockIdx.x * (kRaggedBlock / 64) + (threadIdx.x >> 6);
-  const uint64_t nwaves = (uint64_t)gridDim.x * (kRaggedBlock / 64);
-  auto PS = [&](uint64_t i) -> uint64_t { return UNI ? i * (uint64_t)a.P : a.ps[i]; };
-  const uint64_t count = DESC ? (uint64_t)*a.dev_count : a.count;
-
-  // This wave's packets: those whose first piece lies in its share.
-  const uint64_t total = PS(count);
-  const uint64_t share = (total + nwaves - 1) / nwaves;
-  const uint64_t q_lo = min(wave * share, total), q_hi = min(q_lo + share, total);
-  auto lower_bound = [&](uint64_t x) -> uint64_t {  // first packet p with PS(p) >= x
-    if (UNI) return (x + a.P - 1) / a.P;
-    uint64_t lo = 0, hi = count;  // PS(count) = total >= x
-    while (hi - lo > 64) {  // 64-ary search, one probe per lane
-      const uint64_t step = (hi - lo + 63) / 64;
-      const uint64_t probe = min(lo + step * (lane + 1), hi);
-      const uint64_t m = __ballot(PS(probe) >= x);  // lanes are in ascending probe order
-      const uint32_t f = m ? (uint32_t)__builtin_ctzll(m) : 64u;
-      const uint64_t nhi = f < 64 ? min(lo + step * (f + 1), hi) : hi;
-      lo = f == 0 ? lo : min(lo + step * f, hi);
-      hi = nhi;
-    }
-    const uint64_t probe = min(lo + lane, hi);
-    const uint64_t m = __ballot(PS(probe) >= x);
-    return m ? lo + (uint64_t)__builtin_ctzll(m) : hi;
-  };
-  const uint64_t p0 = lower_bound(q_lo), p1 = lower_bound(q_hi);
-  if (p0 >= p1) return;
-  const uint64_t g_end = PS(p1);
-  const uintptr_t safe = (uintptr_t)a.inv_tab;  // 16 KiB the kernel may always read
-
-  // Lane j's view of packet pc + j (clamped into [p0, p1)).
-  struct Desc {
-    int32_t rel;      // first piece - step's first piece, capped at 64 (past the wave's packets: 64)
-    uintptr_t start;  // L3 start address
-    uint32_t n;
-  };
-  auto load_desc = [&](uint64_t pc, uint64_t gstep) -> Desc {
-    const uint64_t pj = pc + lane;
-    const bool in = pj < p1;
-    const uint64_t pjc = in ? pj : p1 - 1;
-    Desc d;
-    const int64_t r64 = (int64_t)((in ? PS(pjc) : g_end) - gstep);
-    d.rel = r64 > 64 ? 64 : (int32_t)r64;
-    if (DESC) {
-      const RsDesc dd = a.desc[pjc];
-      d.start = (uintptr_t)(((uint64_t)(dd.hi & 0xFFFFu) << 32) | dd.lo);
-      d.n = dd.hi >> 16;
-    } else {
-      d.start = (uintptr_t)a.base + (HAS_OFF ? a.off[pjc] : pjc * a.stride) + a.l3_offset;
-      d.n = HAS_LEN ? a.len[pjc] : a.fixed_len;
-    }
-    return d;
-  };
-
-  // Lane l's packet for the step starting at piece g (packets from pc on).
-  struct Map {
-    uintptr_t start;
-    uint32_t n;
-    int32_t rel;   // lane of the packet's first piece (<= 0: began earlier)
-    uint32_t idx;  // packet = pc + idx
-    bool live;
-  };
-  auto map_step = [&](const Desc &d, uint64_t g) -> Map {
-    const int32_t relj = d.rel;
-    const int32_t tgt = (lane >= 1 && relj < 64) ? relj : 0;
-    const uint32_t recv = (uint32_t)__builtin_amdgcn_ds_permute(tgt << 2, 1);
-    const uint64_t starts = __ballot(recv != 0u) | 1ull;
-    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(starts >> 32),
-                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)starts, 0u));
-    Map m;
-    m.idx = below + (uint32_t)((starts >> lane) & 1ull) - 1u;
-    const int src = (int)(m.idx << 2);
-    m.rel = __builtin_amdgcn_ds_bpermute(src, relj);
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)d.start);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)((uint64_t)d.start >> 32));
-    m.n = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)d.n);
-    m.start = (uintptr_t)(((uint64_t)hi << 32) | lo);
-    m.live = g + lane < g_end;
-    return m;
-  };
-  auto is_end_of = [&](const Map &m) -> bool {
-    return m.live && (uint32_t)((int)lane - m.rel) + 1u == ragged_pieces(m.start, m.n);
-  };
-  auto next_pc = [&](const Map &m, uint64_t pc) -> uint64_t {
-    const bool open63 = __builtin_amdgcn_readlane((int)(m.live && !is_end_of(m)), 63) != 0;
-    return pc + (uint32_t)__builtin_amdgcn_readlane((int)m.idx, 63) + (open63 ? 0u : 1u);
-  };
-  auto load_pieces = [&](const Map &m, u32x4 (&v)[4]) {
-    const bool ok = m.live && m.n >= 4u && m.n <= kMaxLen;
-    const int M = ok ? (int)m.n - 4 : 0;
-    const int s = (int)(m.start & 15u);
-    const int rel0 = 64 * ((int)lane - m.rel) - s;
-    const uintptr_t pbase = m.start - (uintptr_t)s + (uintptr_t)(int64_t)(rel0 + s);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int ru = rel0 + 16 * q;
-      const bool use = ok && ru < M && ru + 16 > 0;
-      if (ABL & 4) v[q] = u32x4{(uint32_t)rel0, (uint32_t)M, lane, (uint32_t)q};
-      else v[q] = gload16(use ? pbase + 16 * q : safe);
-    }
-  };
-
-  // End lanes' x^-(8 z + 512 (63 - lane)) and trailers, loaded at the start
-  // of the step's stage -- before the next step's prefetch, so waiting for
-  // them never waits for the prefetch (gfx9 loads retire in order).  Every
-  // lane loads (others read entry 0 / the table), so no memory op sits under
-  // a divergent branch: a branch join would make the compiler drain vmcnt to
-  // zero and serialise the pipeline.
-  auto load_fin = [&](const Map &m, u32x4 &C, uint32_t &T) {
-    const bool e = is_end_of(m);
-    const uint32_t M = (m.n >= 4u && m.n <= kMaxLen) ? m.n - 4u : 0u;
-    const uint32_t z = 64u * ragged_pieces(m.start, m.n) - (uint32_t)(m.start & 15u) - M;
-    C = gload16((uintptr_t)(a.inv4 + (e ? z + 64u * (63u - lane) : 0u)));
-    T = gload4_unaligned(e ? m.start + M : safe);
-  };
-
-  // Part A of a step: mask the piece's words (wave-uniform branches, before
-  // the interleaved block).
-  auto mask_words = [&](const Map &m, const u32x4 (&v)[4], uint32_t (&w)[16]) {
-    const bool valid = m.n >= 4u && m.n <= kMaxLen;
-    const int M = valid ? (int)m.n - 4 : 0;
-    const int s = (int)(m.start & 15u);
-    const int k = (int)lane - m.rel;
-    const bool first = m.live && k == 0;
-    const int rel0 = 64 * k - s;  // packet-relative offset of the lane's first byte
-#pragma unroll
-    for (int j = 0; j < 16; ++j) w[j] = word_of(v[j >> 2], j & 3);
-    // Bytes outside [0, n-4) -> 0 (misaligned head of a first piece, tail
-    // of a last piece), only when some lane of the wave has such a piece;
-    // whole-word selects when every boundary in the wave is 4-byte aligned.
-    if (__ballot(rel0 < 0 || rel0 + 64 > M)) {
-      if (__ballot(((s | M) & 3) != 0) == 0) {
-        const int lo = -rel0, hi = M - rel0;  // valid bytes of the piece: [lo, hi)
-#pragma unroll
-        for (int j = 0; j < 16; ++j) w[j] = (4 * j >= lo && 4 * j < hi) ? w[j] : 0u;
-      } else {
-#pragma unroll
-        for (int j = 0; j < 16; ++j) w[j] &= byte_span_mask(-(rel0 + 4 * j), M - (rel0 + 4 * j));
-      }
-    }
-    // Invariant masks + seed on first pieces.  Fast path: every first piece
-    // starts 16-byte aligned and holds all masked bytes (n >= 37).
-    if (__ballot(first)) {
-      if (__ballot(first && (s != 0 || M < 33)) == 0) {
-        w[0] = first ? or_xor(w[0], kMaskW0, kSeed) : w[0];
-        w[2] = first ? (w[2] | kMaskW2) : w[2];
-        w[6] = first ? (w[6] | kMaskW6) : w[6];
-        w[8] = first ? (w[8] | kMaskW8) : w[8];
-      } else {
-#pragma unroll
-        for (int j = 0; j < 14; ++j) {  // rel < 40 needs j <= 13 (s <= 15)
-          const int r = rel0 + 4 * j;
-          uint32_t mb = 0u, xp = 0u;
-          if (r > -4 && r < 40) {
-            const uint64_t bits = r >= 0 ? (kMaskBits >> r) : (kMaskBits << (-r));
-            mb = expand_nibble((uint32_t)bits & 0xFu) & byte_span_mask(-r, M - r);
-          }
-          if (r > -4 && r < 4) xp = r >= 0 ? (kSeed >> (8 * r)) : (kSeed << (-8 * r));
-          w[j] = first ? ((w[j] | mb) ^ xp) : w[j];
-        }
-      }
-    }
-  };
-
-  // Part B of a step, run during the next step's fold: align to the step
-  // end, per-packet XOR, end-lane correction, store, carry.
-  struct Fin {
-    Map m;
-    uint32_t r, T;  // r: the piece's register
-    u32x4 C;  // x^(-8 t + 8 k), k = 0..3: starts of four independent multiply chains
-    uint64_t pc;
-    // in flight between slices (C doubles as the chains' running multiples)
-    uint32_t seg;
-    uint32_t acc[4];
-  };
-  uint32_t carry = 0;  // open packet's XOR, aligned to the previous step's end
-  uint32_t sink = 0;   // ABL & 32: results folded here instead of stored
-  auto fin_slice = [&](Fin &f, int sl) {
-    switch (sl) {
-      case 0:
-#pragma unroll
-        for (int k = 0; k < 4; ++k) f.acc[k] = 0u;
-        if (ABL & 256) f.acc[0] = f.r;
-        else mul_lane_part(f.r, 0, f.acc);  // align to the step end, basis words 0..15
-        break;
-      case 1: {
-        if (!(ABL & 256)) mul_lane_part(f.r, 1, f.acc);  // basis words 16..31
-        uint32_t val = f.m.live ? xor3(f.acc[0], f.acc[1], f.acc[2] ^ f.acc[3]) : 0u;
-        if (lane == 0) val ^= carry;
-        const uint32_t pre = wave_prefix_xor(val, lane);
-        const int first_lane = f.m.rel > 0 ? f.m.rel : 0;  // packet's first lane in this step
-        const uint32_t before = (uint32_t)__builtin_amdgcn_ds_bpermute((first_lane - 1) << 2, (int)pre);
-        f.seg = pre ^ (first_lane == 0 ? 0u : before);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) f.acc[k] = 0u;
-        break;
-      }
-      case 2:
-      case 3:
-      case 4:
-      case 5: {  // register = seg * x^-(8 z + 512 (63 - lane)): chain k takes bits 31-8k..24-8k
-        if (ABL & 64) {
-          f.acc[sl - 2] ^= f.seg ^ f.C[sl - 2];
-          break;
-        }
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int bit = 31 - 8 * k - (2 * (sl - 2) + i);
-            const uint32_t mk = (uint32_t)(((int32_t)(f.seg << (31 - bit))) >> 31);
-            f.acc[k] = and_xor(mk, f.C[k], f.acc[k]);
-            f.C[k] = gf_mulx(f.C[k]);
-          }
-        }
-        break;
-      }
-      case 6: {
-        const bool valid = f.m.n >= 4u && f.m.n <= kMaxLen;
-        const bool is_end = is_end_of(f.m);
-        const uint32_t v_icrc = ~xor3(f.acc[0], f.acc[1], f.acc[2] ^ f.acc[3]);
-        const uint32_t o = !valid ? 0u : a.verify ? (f.T == v_icrc ? 1u : 0u) : v_icrc;
-        // Range-checked store: other lanes' offsets are out of range and dropped.
-        const uint32_t ooff = is_end ? (uint32_t)(f.pc + f.m.idx) * 4u : 0x7FFFFFF0u;
-        if (ABL & 32) {
-          sink ^= o;
-        } else {
-          const __amdgpu_buffer_rsrc_t out_rsrc =
-              make_rsrc(a.out, count < (1ull << 30) ? (uint32_t)count * 4u : 0xFFFFFFF0u);
-          __builtin_amdgcn_raw_buffer_store_b32(o, out_rsrc, (int)ooff, 0, 0);
-        }
-        break;
-      }
-      default: {  // packet open at lane 63: carry it (wave-uniform, scalar ALU)
-        const bool open63 = __builtin_amdgcn_readlane((int)(f.m.live && !is_end_of(f.m)), 63) != 0;
-        const uint32_t seg63 = (uint32_t)__builtin_amdgcn_readlane((int)f.seg, 63);
-        carry = open63 ? ((ABL & 128) ? seg63 : mul_const_uniform(seg63, g_x4096)) : 0u;
-        break;
-      }
-    }
-  };
-
-  uint64_t g = PS(p0), pc = p0;
-  Map mA = map_step(load_desc(pc, g), g);
-  uint64_t pcn = next_pc(mA, pc);
-  Desc dn = load_desc(pcn, g + 64);
-  u32x4 v[4];  // pieces of the step being started; refilled with the next step's once masked
-  Map mB;
-  load_pieces(mA, v);
-  Fin prev{};
-  prev.m.live = false;  // pipeline primer: no lane ends or carries
-  prev.m.n = 0;
-  prev.m.rel = 0;
-  prev.m.idx = 0;
-  prev.m.start = safe;
-
-  // One pipeline stage: mask this step's words, map + prefetch the next
-  // step (into the same piece registers), then fold this step interleaved
-  // slice by slice with the finish of the previous one.
-  auto stage = [&](const Map &mc, Map &mn) -> bool {
-    Fin cur;
-    cur.m = mc;
-    cur.pc = pc;
-    load_fin(mc, cur.C, cur.T);
-    uint32_t w[16];
-    if (ABL & 8) {
-#pragma unroll
-      for (int j = 0; j < 16; ++j) w[j] = word_of(v[j >> 2], j & 3);
-    } else {
-      mask_words(mc, v, w);
-    }
-    const uint64_t gn = g + 64;
-    mn = map_step(dn, gn);
-    const uint64_t pcnn = next_pc(mn, pcn);
-    dn = load_desc(pcnn, gn + 64);
-    load_pieces(mn, v);
-    __builtin_amdgcn_sched_barrier(0);
-    // One 16-step chain: its LDS latency hides behind the interleaved
-    // finish work (measured faster than two chains joined by x^256).
-    uint32_t r = 0u;
-#pragma unroll
-    for (int sl = 0; sl < 8; ++sl) {
-      if (ABL & 1) {
-        r ^= w[2 * sl] ^ w[2 * sl + 1];
-      } else {
-        r = step4(lds, lt, r, w[2 * sl]);
-        r = step4(lds, lt, r, w[2 * sl + 1]);
-      }
-      if (!(ABL & 2)) fin_slice(prev, sl);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    cur.r = r;
-    prev = cur;
-    pc = pcn;
-    pcn = pcnn;
-    g = gn;
-    return gn < g_end;
-  };
-  while (stage(mA, mB) && stage(mB, mA)) {
-  }
-#pragma unroll
-  for (int sl = 0; sl < 8; ++sl) fin_slice(prev, sl);
-  if (ABL & 32) a.out[wave % count] = sink;
-}
-
-// =======================================================================
 // Synthetic SEND_ONLY generator (bench/tests; restated on the CPU by
 // oracle/icrc_oracle.c:oracle_synth_packet).  One thread per 8-byte block.
 // =======================================================================
@@ -1023,16 +623,6 @@ hipError_t launch_stream(const StreamArgs &a, int cpl, int grid, hipStream_t st)
 hipError_t launch_tsk(const TskArgs &a, int grid, hipStream_t st) {
   if (a.log2C == 7) hipLaunchKernelGGL((icrc_tsk_kernel<true, 0>), dim3(grid), dim3(kBlock), 0, st, a);
   else hipLaunchKernelGGL((icrc_tsk_kernel<false, 0>), dim3(grid), dim3(kBlock), 0, st, a);
-  return hipGetLastError();
-}
-
-hipError_t launch_ragged(const RaggedArgs &a, int grid, hipStream_t st) {
-  const dim3 b(1024);
-  if (a.desc) hipLaunchKernelGGL((icrc_ragged_kernel<4, 1024>), dim3(grid), b, 0, st, a);
-  else if (!a.ps) hipLaunchKernelGGL((icrc_ragged_kernel<0, 1024>), dim3(grid), b, 0, st, a);
-  else if (a.off && a.len) hipLaunchKernelGGL((icrc_ragged_kernel<1, 1024>), dim3(grid), b, 0, st, a);
-  else if (a.off) hipLaunchKernelGGL((icrc_ragged_kernel<2, 1024>), dim3(grid), b, 0, st, a);
-  else hipLaunchKernelGGL((icrc_ragged_kernel<3, 1024>), dim3(grid), b, 0, st, a);
   return hipGetLastError();
 }
 

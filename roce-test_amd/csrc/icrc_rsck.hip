@@ -42,8 +42,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <stdlib.h>
-
 #include <type_traits>
 
 #include "icrc_device.h"
@@ -98,17 +96,6 @@ __device__ uint32_t icrc_small(uint64_t addr, uint32_t n) {
 // atomic per class (per-chunk reservations serialised on the few hot class
 // counters: 50 us per million packets).
 constexpr int kPassBlock = 1024;
-// Work of a group in line-steps: its L lines plus the per-group finish
-// (GF(2) multiplies through nibble tables, reductions, descriptor and slot
-// traffic).  Waves split the total weighted work, not the lines: split by
-// lines, a wave that drew 64-byte packets (one line per group) ran ~8x longer
-// than one that drew 4 KiB packets.  Swept on C4 (same box, tools/ab_env.sh
-// with RICRC_RS_GCOST, profiles/r02/ab_c4_group_cost.txt): 0 -> 1.52 ms per
-// step, 1 -> 1.16, 2 -> 1.060-1.081, 3 -> 1.061-1.062, 4 -> 1.065-1.086,
-// 6 (round 1's estimate) -> 1.073-1.076, 10 -> 1.09, 16 -> 1.13.  In quarter
-// line-steps 10..14 are within the run-to-run noise (profiles/r02/
-// ab_c4_group_cost_quarters.txt).
-constexpr uint32_t kGroupCost = 12;  // quarter line-steps (3 lines)
 constexpr int kPassBlocks = 512;  // pass grid cap (per-block class histograms: 1 MiB)
 constexpr int kPassUnroll = 8;    // packets per thread whose descriptors are read at once
 // a.counts: [0, kRsClasses) class counts, [kRsClasses] misaligned flag,
@@ -135,14 +122,14 @@ __device__ __forceinline__ T wave_scan(T v) {
 
 // One workgroup: exclusive scans over the classes of groups (bucket
 // positions), of weighted work and of the non-empty big classes (the fold's
-// class table), and of pieces of the small classes (the piece kernel's prefix).
+// class table).
 // Run by the count pass's last workgroup (1024 threads), after every
 // workgroup's class counts have landed in a.counts.  One barrier: each wave
 // scans its 64 classes, then adds the totals of the waves before it (the
 // 10-round LDS scan before it cost ~0.2 % of C4's step, tools/ab_env.sh).
 __device__ void rsck_plan(const RsckArgs &a) {
   __shared__ uint32_t wg[16], wf[16];
-  __shared__ uint64_t wsum[16], wp[16];
+  __shared__ uint64_t wsum[16];
   const uint32_t t = threadIdx.x, wid = t >> 6;
   const uint32_t cnt = (t >= 1 && t < (uint32_t)kRsClasses)
                            ? __hip_atomic_load(&a.counts[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
@@ -151,24 +138,21 @@ __device__ void rsck_plan(const RsckArgs &a) {
   const uint32_t G = (cnt + 7u) >> 3, f = (big && cnt) ? 1u : 0u;
   const uint32_t L = big ? t - (uint32_t)kRsBigBase : 0u;
   const uint64_t S = big ? (uint64_t)G * (4u * L + a.group_cost) : 0u;  // quarter line-steps
-  const uint64_t PC = big ? 0u : 8ull * G * (t >= 1 ? t - 1 : 0);
   uint32_t ig = wave_scan(G), jf = wave_scan(f);
-  uint64_t is = wave_scan(S), ip = wave_scan(PC);
+  uint64_t is = wave_scan(S);
   if ((t & 63u) == 63u) {
     wg[wid] = ig;
     wf[wid] = jf;
     wsum[wid] = is;
-    wp[wid] = ip;
   }
   __syncthreads();
   for (uint32_t w = 0; w < wid; ++w) {  // wave-uniform
     ig += wg[w];
     jf += wf[w];
     is += wsum[w];
-    ip += wp[w];
   }
   const uint32_t g0 = ig - G, ci = jf - f;
-  const uint64_t s0 = is - S, p0 = ip - PC;
+  const uint64_t s0 = is - S;
   RsPlan *P = a.plan;
   if (f) {
     P->L[ci] = L;
@@ -178,12 +162,8 @@ __device__ void rsck_plan(const RsckArgs &a) {
   if (t < (uint32_t)kRsClasses) {
     a.bucket[t] = 8u * g0;
     a.cursor[t] = 0u;
-    P->ps0[t] = p0;
   }
-  if (t == (uint32_t)kRsBigBase + 1) {
-    *a.small_pos = 8u * g0;
-    a.ps[8u * g0] = p0;
-  }
+  if (t == (uint32_t)kRsBigBase + 1) *a.small_pos = 8u * g0;
   if (t == 1023) {
     P->nc = jf;
     P->ngroups = ig;
@@ -260,14 +240,12 @@ __global__ __launch_bounds__(kPassBlock) void rsck_scatter(RsckArgs a) {
   // The class tables in LDS: per-round global reads of them were a
   // dependent latency in every round.
   __shared__ uint32_t base[kRsClasses], sbk[kRsClasses], send[kRsClasses];
-  __shared__ uint64_t sps0[kRsBigBase + 1];
   for (int t = threadIdx.x; t < kRsClasses; t += blockDim.x) {
     const uint32_t hb = a.hist[(uint64_t)blockIdx.x * kRsClasses + t];
     const uint32_t bk = a.bucket[t];
     base[t] = hb ? bk + atomicAdd(&a.cursor[t], hb) : 0u;
     sbk[t] = bk;
     send[t] = bk + a.counts[t];
-    if (t <= kRsBigBase) sps0[t] = a.plan->ps0[t];
   }
   uint64_t lo, hi;
   pass_range(a.count, lo, hi);
@@ -305,21 +283,15 @@ __global__ __launch_bounds__(kPassBlock) void rsck_scatter(RsckArgs a) {
         continue;
       }
       const RsDesc d{(uint32_t)addr[k], (uint32_t)(addr[k] >> 32) | (n[k] << 16)};
-      const bool small = c[k] <= (uint32_t)kRsBigBase;
-      const uint64_t psb = small ? sps0[c[k]] : 0u;
       const uint32_t bk = sbk[c[k]];
       // streaming stores: the fold that follows reads these once, and dirty
       // lines left in the caches would be written back into its read stream
       __builtin_nontemporal_store(d.lo, &a.desc[pos[k]].lo);
       __builtin_nontemporal_store(d.hi, &a.desc[pos[k]].hi);
       __builtin_nontemporal_store(pos[k], &a.pos_of[i]);
-      if (small && a.piece) a.ps[pos[k]] = psb + (uint64_t)(pos[k] - bk) * (c[k] - 1u);
       const uint32_t end = send[c[k]];
       if (pos[k] + 1 == end)  // the class's last packet pads its group with copies of itself
-        for (uint32_t p = end; (p - bk) & 7u; ++p) {
-          a.desc[p] = d;
-          if (small && a.piece) a.ps[p] = psb + (uint64_t)(p - bk) * (c[k] - 1u);
-        }
+        for (uint32_t p = end; (p - bk) & 7u; ++p) a.desc[p] = d;
     }
   }
 }
@@ -721,8 +693,8 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
 // Small packets of the ragged path (<= kRsSmallL lines: the 64 / 256-byte
 // share of C4): ONE LANE PER PACKET, descriptors [0, *small_pos) of the
 // buckets.  8 lanes per packet (the fold above) is too coarse for them, and
-// the piece kernel (icrc_kernels.hip, one 64-byte piece per lane) pays a GF(2)
-// re-alignment, prefix XOR and end multiply per packet.  Here a lane folds its
+// the round-1 piece kernel (one 64-byte piece per lane; git history) paid a
+// GF(2) re-alignment, prefix XOR and end multiply per packet.  Here a lane folds its
 // packet's whole byte stream from a ZERO register with no multiply at all:
 //
 //   stream = 4 x 0xFF || masked L3[0, M)        (M = n - 4)
@@ -888,7 +860,7 @@ uint64_t rs_workspace_bytes(uint64_t count) {
   const uint64_t npos = count + 8ull * kRsClasses;
   auto al = [](uint64_t b) { return (b + 255) & ~255ull; };
   return 3 * al(4ull * kRsClasses) + al(sizeof(RsPlan)) + al(sizeof(RsDesc) * npos) + al(4 * count) + al(4 * npos) +
-         al(4ull * kRsClasses * kPassBlocks) + al(8 * (npos + 1)) + al(4);
+         al(4ull * kRsClasses * kPassBlocks) + al(4);
 }
 
 hipError_t rs_zero_counters(void *ws, hipStream_t st) {  // counts is the workspace's first region
@@ -907,7 +879,6 @@ void rs_bind_workspace(RsckArgs &a, void *ws) {
   a.pos_of = reinterpret_cast<uint32_t *>(p), p += al(4 * a.count);
   a.res = reinterpret_cast<uint32_t *>(p), p += al(4 * npos);
   a.hist = reinterpret_cast<uint32_t *>(p), p += al(4ull * kRsClasses * kPassBlocks);
-  a.ps = reinterpret_cast<uint64_t *>(p), p += al(8 * (npos + 1));
   a.small_pos = reinterpret_cast<uint32_t *>(p);
 }
 
@@ -931,37 +902,16 @@ static void launch_passes(const RsckArgs &a, int pgrid, hipStream_t st) {
   else launch_passes_t<false, false>(a, pgrid, st);
 }
 
-hipError_t launch_rsck(RsckArgs &a, const RaggedArgs &small, int grid, hipStream_t st) {
+hipError_t launch_rsck(RsckArgs &a, int grid, hipStream_t st) {
   if (a.count == 0) return hipSuccess;
-  a.piece = getenv("RICRC_RS_PIECE") != nullptr ? 1u : 0u;
-  a.group_cost = kGroupCost;
-  if (const char *e = getenv("RICRC_RS_GCOST")) a.group_cost = (uint32_t)atoi(e);  // schedule study, quarter lines
   // a.counts (+ the misaligned flag) is zero here: zeroed when the workspace
   // was allocated, and again by rsck_gather at the end of every call.
-  hipError_t e = hipSuccess;
   const uint64_t want = (a.count + kPassBlock - 1) / kPassBlock;
   const int pgrid = (int)(want < kPassBlocks ? want : kPassBlocks);
   launch_passes(a, pgrid, st);
   hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, st, a);
-  if (!a.piece) {  // the small region [0, *small_pos): one lane per packet
-    hipLaunchKernelGGL(icrc_rsmall_kernel, dim3(grid), dim3(kBlock), 0, st, a);
-    hipLaunchKernelGGL(rsck_gather, dim3(gather_grid(a.count)), dim3(256), 0, st, a);
-    return hipGetLastError();
-  }
-  RaggedArgs r = small;  // the small region [0, *small_pos) of the buckets: piece kernel, ICRCs into res
-  r.base = nullptr;
-  r.off = nullptr;
-  r.len = nullptr;
-  r.ps = a.ps;
-  r.desc = a.desc;
-  r.dev_count = a.small_pos;
-  r.count = 0;
-  r.out = a.res;
-  r.verify = 0;  // verify mode is applied by the gather pass
-  r.fixed_len = 0;
-  r.l3_offset = 0;
-  e = launch_ragged(r, grid, st);
-  if (e != hipSuccess) return e;
+  // the small region [0, *small_pos): one lane per packet
+  hipLaunchKernelGGL(icrc_rsmall_kernel, dim3(grid), dim3(kBlock), 0, st, a);
   hipLaunchKernelGGL(rsck_gather, dim3(gather_grid(a.count)), dim3(256), 0, st, a);
   return hipGetLastError();
 }

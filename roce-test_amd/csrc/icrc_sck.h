@@ -7,11 +7,6 @@
 
 namespace ricrc {
 
-// Dynamic-schedule counters of one launch (icrc_sck_kernel, DYN): 8 per-XCD
-// group counters and one check-in counter, kSckCtrStride words (256 B) apart.
-constexpr uint32_t kSckCtrStride = 64;
-constexpr uint32_t kSckWorkWords = 9 * kSckCtrStride;
-
 // Back-to-back packets of n = 128 * L bytes (L = 8, 16, 32), 16-byte aligned:
 // the strided-chain kernel.  8 lanes per packet, 8 packets per wave group.
 struct SckArgs {
@@ -22,8 +17,6 @@ struct SckArgs {
   uint32_t verify;
   uint32_t XB[32];   // basis of x^-32 (Horner step between a lane's chains)
   uint32_t QS[8];    // x^(-32 (4 s + 1)): lane slot s's chain 0 -> packet end
-  uint32_t *work;    // dynamic schedule: kSckWorkWords, zero between launches (below)
-  uint32_t dynamic;  // 1: groups from the counter (see icrc_sck_kernel), 0: static blocks
   uint32_t family;   // kFamV4 / kFamV6 / kFamAuto: masks applied by the kernel itself
   uint64_t *stamps;  // diagnostic builds only (tools/microbench); null in the product
 };

@@ -43,15 +43,15 @@ namespace ricrc {
 // ABL (timing-only ablations for tools/microbench; the product uses 0):
 // 1 no table fold, 2 no finish, 8 no global loads, 16 no stores, 64 per-wave
 // start/end s_memrealtime stamps into a.stamps.
-// D: lines in flight per wave; QLDS: lane bases read from LDS instead of 32
-// VGPRs (frees registers for a deeper ring); XT 1: the Horner multiplies by
-// x^-32 through a nibble table in LDS, 32 copies (one per bank); XT 2 (the
-// product): every finish multiply through nibble tables, ONE copy each (the
-// 16 entries of a nibble position sit in 16 banks: any lane pattern is
-// conflict-free) -- x^-32 (128 words) and, per lane slot s, x^(-32 (4 s + 1))
-// (8 x 132 words) -- so the lane-basis multiply is 8 lookups instead of 32
-// bit-select pairs and the 32 basis VGPRs are free; the finish tables sit at
-// the bottom of LDS so each lookup's constant part is a ds_read offset.
+// D: lines in flight per wave.  Every finish multiply goes through nibble
+// tables, ONE copy each (the 16 entries of a nibble position sit in 16 banks:
+// any lane pattern is conflict-free) -- x^-32 (128 words) and, per lane slot
+// s, x^(-32 (4 s + 1)) (8 x 132 words) -- so the lane-basis multiply is 8
+// lookups instead of 32 bit-select pairs and needs no basis VGPRs; the finish
+// tables sit at the bottom of LDS so each lookup's constant part is a ds_read
+// offset.  (Measured and retired in round 2, code in git history: the
+// per-XCD dynamic group schedule, lane bases in LDS, and 32-copy x^-32
+// tables with the lane basis in VGPRs -- DESIGN.md §4.)
 // =======================================================================
 // FAM: the address family's invariant masks, applied natively on line 0
 // (kFamV4 = the reference's IPv4 masks; kFamV6; kFamAuto per packet from the
@@ -66,23 +66,18 @@ namespace ricrc {
 // 0.628 ms per 4 GiB against 0.678 ms).  Sub-group m of a group (packets
 // 8 S Q + S g + m) is finished S times per group; its results land in the
 // slots in packet order, so the flush is unchanged.
-template <int L, int ABL, int D = 8, bool QLDS = false, bool DYN = false, int XT = 0, int FAM = kFamV4, int PL = L>
+template <int L, int ABL, int FAM = kFamV4, int PL = L, int D = 8>
 __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
-  static_assert(L % PL == 0 && PL >= 8 && (PL == L || !DYN), "super-groups: static schedule, whole packets");
+  static_assert(L % PL == 0 && PL >= 8, "super-groups: whole packets");
   constexpr uint32_t S = L / PL;  // packets per super-packet
-  // [XT 2: finish tables] 128 KiB of tables + result slots per wave (+ DYN:
-  // the slots' group indices; QLDS: the 8 lane bases; XT 1: 16 KiB nibble
-  // table of x^-32).
-  constexpr uint32_t kSlots = (DYN && XT == 1) ? 128 : (QLDS || DYN || XT) ? 256 : 512;
+  // finish tables | 128 KiB of slice-by-4 tables | result slots per wave
+  constexpr uint32_t kSlots = 256;
   constexpr uint32_t kRoundMask = kSlots / 8 - 1;  // groups per round of slots - 1
-  constexpr uint32_t kWaveWords = kSlots + (DYN ? kSlots / 8 : 0);
-  constexpr uint32_t kQStride = 36;  // words per lane-slot basis (padded: conflict-free ds_read_b128)
-  constexpr uint32_t kQtStride = 132;  // XT 2: words per lane slot's nibble table (padded across banks)
-  constexpr uint32_t kFin = XT == 2 ? 128 + 8 * kQtStride + 32 : 0;  // XT 2 finish tables: a multiple of 32 words
-  constexpr uint32_t kXtWord = kFin + kLdsWords + kWaves * kWaveWords + (QLDS ? 8 * kQStride : 0);
-  __shared__ uint32_t lds[kXtWord + (XT == 1 ? 128 * 32 : 0)];
+  constexpr uint32_t kQtStride = 132;  // words per lane slot's nibble table (padded across banks)
+  constexpr uint32_t kFin = 128 + 8 * kQtStride + 32;  // finish tables: a multiple of 32 words
+  __shared__ uint32_t lds[kFin + kLdsWords + kWaves * kSlots];
   uint32_t *tab = lds + kFin;  // slice-by-4 tables
-  const uint32_t *xtl = lds, *qtl = lds + 128;  // XT 2
+  const uint32_t *xtl = lds, *qtl = lds + 128;
 
   // D: lines in flight per wave
   static_assert(L % D == 0 || D == L, "ring indices must repeat every group");
@@ -97,60 +92,15 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
   const uint64_t total = a.count * (128u * PL);
   const uint32_t vo = (lane >> 3) * N + 16u * s;
 
-  // The wave's sequence of groups.  Static: the contiguous block [g0, g1).
-  // DYN (hybrid): the first 7/8 of the groups in static blocks, the last 1/8
-  // a pool handed out one group at a time by per-XCD device counters -- XCD
-  // x (workgroup w runs on XCD w % 8) owns pool groups [base_x, base_x +
-  // size_x), its counter work[x * kSckCtrStride] hands them out, and a wave
-  // whose XCD's share is used up steals from the next XCD's counter.  Why
-  // (tools/microbench/sck_tail.hip, profiles/r02/sck_tail.txt): with static
-  // blocks, waves with equal work finish between 0.46x and 1.0x of the
-  // launch, the odd XCDs ~9 % after the even ones; a fully dynamic schedule
-  // balanced them but ran slower (one counter serves ~74 M grabs/s, and every
-  // wave waited for its first grab), so only the tail is dynamic.  The pool
-  // grab runs one group ahead (made wave-uniform only one group later:
-  // reading it at once would drain vmcnt(0)).  The last wave to finish
-  // resets the counters for the next launch.  Buffer atomics whose other 63
-  // lanes fall outside the range-checked record keep the grab free of exec
-  // masking.
-  const __amdgpu_buffer_rsrc_t wrs = make_rsrc(a.work, 4u * kSckWorkWords);
-  auto grab = [&](uint32_t x) -> uint32_t {  // raw per-lane result (lane 0 holds it)
-    return (uint32_t)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(
-        1, wrs, lane == 0 ? 4u * kSckCtrStride * x : 0x7FFFFFF0u, 0, 0);
-  };
-  auto uni = [](uint32_t v) -> uint32_t { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
-  uint32_t g0 = 0, g1 = 0, qcur, qnext, qpend = 0;
-  {
-    const uint64_t per = DYN ? (uint64_t)(G - G / 8) / nwaves : (G + nwaves - 1) / nwaves;
-    g0 = (uint32_t)(wave * per < G ? wave * per : G);
-    g1 = (uint32_t)(g0 + per < G ? g0 + per : G);
-  }
-  const uint32_t pool0 = DYN ? (uint32_t)(nwaves * ((uint64_t)(G - G / 8) / nwaves)) : G;
-  const uint32_t Pq = (G - pool0) >> 3, Pr = (G - pool0) & 7u;
-  auto pbase = [&](uint32_t x) -> uint32_t { return pool0 + x * Pq + (x < Pr ? x : Pr); };
-  auto psize = [&](uint32_t x) -> uint32_t { return Pq + (x < Pr ? 1u : 0u); };
-  uint32_t xs = blockIdx.x & 7u, xtries = 0;  // pool partition being drawn from; partitions found empty
-  // Pool group for a grab result v of partition xs; steals (synchronously:
-  // only at the very end) while xs is used up; G once every partition is.
-  auto take_group = [&](uint32_t v) -> uint32_t {
-    while (v >= psize(xs)) {  // wave-uniform
-      if (++xtries >= 8) return G;
-      xs = (xs + 1) & 7u;
-      v = uni(grab(xs));
-    }
-    return pbase(xs) + v;
-  };
-  // The group after q in this wave's sequence.
-  auto after = [&](uint32_t q) -> uint32_t {
-    if (q + 1 < g1) return q + 1;  // static block (pool groups are >= g1)
-    if (!DYN || xtries >= 8) return G;
-    const uint32_t r = take_group(uni(qpend));
-    if (xtries < 8) qpend = grab(xs);
-    return r;
-  };
-  if (DYN) qpend = grab(xs);
-  qcur = g0 < g1 ? g0 : after(G);
-  qnext = qcur < G ? after(qcur) : G;
+  // The wave's groups: the contiguous block [g0, g1).  (A per-XCD dynamic
+  // tail schedule balanced the waves' end times but measured slower,
+  // tools/microbench/sck_tail.hip, profiles/r02/sck_tail.txt.)
+  const uint64_t per = (G + nwaves - 1) / nwaves;
+  const uint32_t g0 = (uint32_t)(wave * per < G ? wave * per : G);
+  const uint32_t g1 = (uint32_t)(g0 + per < G ? g0 + per : G);
+  auto after = [&](uint32_t q) -> uint32_t { return q + 1 < g1 ? q + 1 : G; };
+  uint32_t qcur = g0 < g1 ? g0 : G;
+  uint32_t qnext = qcur < G ? after(qcur) : G;
 
   // Line `line` of absolute group q (q >= G: no group, the range check reads zeros).
   auto load = [&](uint32_t q, uint32_t line) -> u32x4 {
@@ -172,7 +122,7 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
   }
   __builtin_amdgcn_sched_barrier(0);
   table_store(tab, tab_v);
-  if (XT == 2) {
+  {
     if (threadIdx.x < 128) {  // entry 16 w + v: (nibble v at bits 4w..4w+3) * x^-32
       const uint32_t w = threadIdx.x >> 4, v = threadIdx.x & 15u;
       uint32_t t = 0;
@@ -195,26 +145,9 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
     }
     lds[128 + bs * kQtStride + 16u * w + v] = e;
   }
-  if (XT == 1) {  // entry (w, v) = (nibble v at bits 4w..4w+3) * x^-32, 32 copies: 8 threads x 4 copies each
-    const uint32_t e = threadIdx.x >> 3, w = e >> 4, v = e & 15u;
-    uint32_t t = 0;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) t ^= ((v >> b) & 1u) ? a.XB[4 * w + b] : 0u;
-    *reinterpret_cast<u32x4 *>(lds + kXtWord + 32 * e + 4 * (threadIdx.x & 7)) = u32x4{t, t, t, t};
-  }
-  if (QLDS && threadIdx.x < 256) {  // basis word j of lane slot s: x^(-32 (4 s + 1)) * x^(31 - j)
-    const uint32_t bs = threadIdx.x >> 5, j = threadIdx.x & 31;
-    uint32_t v = a.QS[0];
-#pragma unroll
-    for (int k = 1; k < 8; ++k) v = bs == (uint32_t)k ? a.QS[k] : v;
-    for (uint32_t t = j; t < 31; ++t) v = gf_mulx(v);
-    lds[kFin + kLdsWords + kWaves * kWaveWords + bs * kQStride + j] = v;
-  }
   __syncthreads();
 
-  uint32_t *slots = lds + kFin + kLdsWords + wid * kWaveWords;
-  const uint32_t xt_lane = 4u * kXtWord + ((lane & 31u) << 2);  // byte address of the lane's XT copy
-  uint32_t *gtab = slots + kSlots;  // DYN: absolute group of each slot row
+  uint32_t *slots = lds + kFin + kLdsWords + wid * kSlots;
   const LaneTab lt{(lane & 31) << 2, ((lane & 31) << 2) | 0x10000u};
   const uint32_t mw0 = s == 0 ? kMaskW0 : (s == 2 ? kMaskW8 : 0u);  // bytes 1 / 32
   const uint32_t xw0 = s == 0 ? kSeed : 0u;
@@ -224,26 +157,13 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
   const uint32_t m6w1 = s == 0 ? kMaskV6W1 : (s == 3 ? kMaskV6W13 : 0u);
   const uint32_t m6w3 = s == 2 ? kMaskV6W11 : 0u;
   const uint32_t keep3 = s == 7 ? 0u : 0xFFFFFFFFu;                  // the trailer word
-  uint32_t Q[32];  // lane basis in registers (!QLDS)
-  const uint32_t *qlds = lds + kFin + kLdsWords + kWaves * kWaveWords + s * kQStride;
-  const uint32_t *qrow = qtl + s * kQtStride;  // XT 2
-  if (!QLDS && XT != 2) {
-    uint32_t qs = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) qs = s == (uint32_t)k ? a.QS[k] : qs;
-    make_basis(qs, Q);
-  }
+  const uint32_t *qrow = qtl + s * kQtStride;
 
   struct Fin {
     uint32_t r[4];    // chain registers
     uint32_t tr;      // trailer word (lane s = 7), for verify
     uint32_t acc[4];  // multiply accumulators
     uint32_t u;       // Horner value
-  };
-  auto mul_half = [&](Fin &f, const uint32_t(&B)[32], int h) {
-#pragma unroll
-    for (int j = 16 * h; j < 16 * h + 16; ++j)
-      f.acc[j & 3] = and_xor((uint32_t)(((int32_t)(f.u << (31 - j))) >> 31), B[j], f.acc[j & 3]);
   };
   auto take = [](Fin &f) -> uint32_t {
     const uint32_t v = xor3(f.acc[0], f.acc[1], f.acc[2] ^ f.acc[3]);
@@ -259,29 +179,10 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) f.acc[k] = 0u;
     }
-    if (XT == 2) {  // 4 nibble lookups of one table copy (x^-32, then the lane slot's)
+    {  // 4 nibble lookups of one table copy (x^-32, then the lane slot's)
       const uint32_t *t = sl < 6 ? xtl : qrow;
 #pragma unroll
       for (int w = 4 * (sl & 1); w < 4 * (sl & 1) + 4; ++w) f.acc[w & 3] ^= t[16 * w + __builtin_amdgcn_ubfe(f.u, 4 * w, 4)];
-    } else if (sl < 6 && XT) {  // 4 nibble lookups: 2 VALU + 1 ds_read_b32 each instead of 8 bfe/bitop3 pairs
-#pragma unroll
-      for (int w = 4 * (sl & 1); w < 4 * (sl & 1) + 4; ++w) {
-        const uint32_t nib = (f.u >> (4 * w)) & 15u;
-        f.acc[w & 3] ^= lds_at(lds, xt_lane + (nib << 7) + 2048u * w);
-      }
-    } else if (sl < 6) mul_half(f, a.XB, sl & 1);
-    else if (!QLDS) mul_half(f, Q, sl & 1);
-    else {
-      const int h = sl & 1;
-#pragma unroll
-      for (int q4 = 0; q4 < 4; ++q4) {
-        const u32x4 b = *reinterpret_cast<const u32x4 *>(qlds + 16 * h + 4 * q4);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int j = 16 * h + 4 * q4 + i;
-          f.acc[i] = and_xor((uint32_t)(((int32_t)(f.u << (31 - j))) >> 31), b[i], f.acc[i]);
-        }
-      }
     }
     if (sl == 1) f.u = take(f) ^ f.r[2];
     if (sl == 3) f.u = take(f) ^ f.r[1];
@@ -299,16 +200,7 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
     if (ABL & 16) return;
     const uint32_t j_lo = (j_end - 1) & ~kRoundMask;
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the slot writes have landed
-    if (DYN) {  // rows of 8 results to scattered groups: 32 B runs
-      const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out, (uint32_t)(a.count < (1ull << 30) ? 4 * a.count : 0xFFFFFFF0u));
-#pragma unroll
-      for (int h = 0; h < (int)kSlots / 64; ++h) {
-        const uint32_t row = 8u * h + (lane >> 3);  // slot row = local group (mod round)
-        const uint32_t q = gtab[row];
-        const bool live = j_lo + row < j_end;
-        __builtin_amdgcn_raw_buffer_store_b32(slots[64 * h + lane], ro, live ? 4u * (8u * q + s) : 0x7FFFFFF0u, 0, 0);
-      }
-    } else {  // consecutive groups: coalesced
+    {  // consecutive groups: coalesced
       const uint64_t pb = ((uint64_t)g0 * S + j_lo) * 8u;
       const uint32_t valid = (j_end - j_lo) * 8u;  // slots written this round
       const uint32_t nout = (uint32_t)(a.count - pb < valid ? a.count - pb : valid);
@@ -321,7 +213,7 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
       }
     }
   };
-  auto fin_store = [&](Fin &f, uint32_t jf, uint32_t qf) {
+  auto fin_store = [&](Fin &f, uint32_t jf) {
     const uint32_t crc = (ABL & 2) ? (f.r[0] ^ f.r[1] ^ f.r[2] ^ f.r[3]) : f.u;
     const uint32_t v = group_xor(crc, 3);
     const uint32_t chk = group_xor(f.tr, 3) == ~v ? 1u : 0u;
@@ -332,7 +224,6 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
     }
     // sub-group jf's packet of lane group g: S (jf / S) * 8 + S g + jf % S in the round
     slots[(((jf & kRoundMask) & ~(S - 1)) << 3) | ((lane >> 3) * S) | (jf & (S - 1))] = val;
-    if (DYN) gtab[jf & kRoundMask] = qf;
   };
 
   // Finish slices of the previous packet ride in its successor's steps 0..7
@@ -361,7 +252,6 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
     for (int i = 0; i < 4; ++i) x[i] = w[i];  // chain register (0) ^ line-0 word
   };
   Fin pf{};
-  uint32_t qprev = 0;
   uint32_t j = 0;  // the wave's packets of lane group 0 started so far (sub-groups)
   while (qcur < G) {  // qcur: wave-uniform
     const u32x4 w = ring[0];
@@ -411,7 +301,7 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
       for (int sl = 0; sl < 8; ++sl)
         if (slice_step(sl) == kp) fin_slice(pf, sl);
       if (kp == kStoreStep) {
-        fin_store(pf, j - 1, qprev);
+        fin_store(pf, j - 1);
         if (j > 0 && ((j - 1) & kRoundMask) == kRoundMask) flush(j);  // wave-uniform: a full round of slots
       }
 #pragma unroll
@@ -420,7 +310,6 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) pf.r[i] = x[i];
         pf.tr = tr;
-        qprev = qcur;
         ++j;
         if (k + 1 < L) {
           first_line(wf, x);
@@ -435,7 +324,7 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int sl = 0; sl < 8; ++sl) fin_slice(pf, sl);
-    fin_store(pf, j - 1, qprev);
+    fin_store(pf, j - 1);
     flush(j);
   }
   if (ABL & 16) a.out[wave * 64 + lane] = sink;
@@ -443,37 +332,18 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
     a.stamps[2 * wave] = t_start;
     a.stamps[2 * wave + 1] = __builtin_amdgcn_s_memrealtime();
   }
-  if (DYN) {
-    // All of this wave's grabs have returned before it checks in, so when the
-    // last wave checks in nobody touches the counters any more: reset them.
-    const uint32_t done_off = 4u * kSckCtrStride * 8u;
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): every grab of this wave has returned
-    const uint32_t seen = (uint32_t)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(
-        1, wrs, lane == 0 ? done_off : 0x7FFFFFF0u, 0, 0);
-    if (__builtin_amdgcn_readfirstlane((int)seen) == (int)(nwaves - 1)) {
-      // lanes 0..7: the XCD counters, lane 8: the check-in counter
-      __builtin_amdgcn_raw_buffer_store_b32(0u, wrs, lane <= 8u ? 4u * kSckCtrStride * lane : 0x7FFFFFF0u, 0, 0);
-    }
-  }
-
 }
 
 // ----------------------------------------------------------- host launcher
 template <int FAM>
 hipError_t launch_sck_fam(const SckArgs &a, int grid, hipStream_t st) {
   const dim3 g(grid), b(kBlock);
-  // XT (x^-32 nibble table): 0.735 -> 0.703 ms on 4 M x 1 KiB, ~1 % on 1 M x 4 KiB (tools/microbench/sck_abl.hip).
-  if (a.dynamic) {
-    if (a.n == 4096) hipLaunchKernelGGL((icrc_sck_kernel<32, 0, 8, false, true, 2, FAM>), g, b, 0, st, a);
-    else if (a.n == 2048) hipLaunchKernelGGL((icrc_sck_kernel<16, 0, 8, false, true, 2, FAM>), g, b, 0, st, a);
-    else if (a.n == 1024) hipLaunchKernelGGL((icrc_sck_kernel<8, 0, 8, false, true, 2, FAM>), g, b, 0, st, a);
-    else return hipErrorInvalidValue;
-  } else if (a.n == 4096) hipLaunchKernelGGL((icrc_sck_kernel<32, 0, 8, false, false, 2, FAM>), g, b, 0, st, a);
+  if (a.n == 4096) hipLaunchKernelGGL((icrc_sck_kernel<32, 0, FAM>), g, b, 0, st, a);
   // 1 KiB packets stream in 4 KiB super-packets (S = 4 packets each): 0.180 ->
   // 0.176 ms on 1 M; 2 KiB packets measured 2 % slower that way (0.346 ->
   // 0.353 ms, same box, profiles/r02/ab_super_1k_2k/) and keep L = 16
-  else if (a.n == 2048) hipLaunchKernelGGL((icrc_sck_kernel<16, 0, 8, false, false, 2, FAM>), g, b, 0, st, a);
-  else if (a.n == 1024) hipLaunchKernelGGL((icrc_sck_kernel<32, 0, 8, false, false, 2, FAM, 8>), g, b, 0, st, a);
+  else if (a.n == 2048) hipLaunchKernelGGL((icrc_sck_kernel<16, 0, FAM>), g, b, 0, st, a);
+  else if (a.n == 1024) hipLaunchKernelGGL((icrc_sck_kernel<32, 0, FAM, 8>), g, b, 0, st, a);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }

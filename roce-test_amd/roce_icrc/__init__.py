@@ -49,7 +49,12 @@ EXPORTED = CPU_EXPORTED + (
     "ricrc_batch_device_ex", "ricrc_verify_device_ex", "ricrc_host_alloc", "ricrc_host_free",
     "ricrc_host_register", "ricrc_host_unregister", "ricrc_synth_device", "ricrc_synth_ragged_device",
     "ricrc_prime", "ricrc_stream", "ricrc_comm_init", "ricrc_batch_device_all", "ricrc_allgather", "ricrc_sync",
+    "ricrc_batch_device_st", "ricrc_batch_host_st", "ricrc_classify_device",
 )
+
+# Per-packet status of the *_st batch calls (include/roce_icrc.h).
+ST_OK, ST_BADLEN, ST_NOTROCE = 0, 1, 2
+F_STRICT, F_VERIFY = 0x100, 0x200
 
 _vp = ctypes.c_void_p
 _u32, _u64, _i32 = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
@@ -92,6 +97,9 @@ _SIG = {
     "ricrc_batch_device_all": ([_vp, _PP, _PP, _PP, _u32, ctypes.POINTER(_u64), _u32, _PP, _u32], _i32),
     "ricrc_allgather": ([_vp, ctypes.POINTER(_u64), _PP], _i32),
     "ricrc_sync": ([_vp], _i32),
+    "ricrc_batch_device_st": ([_vp, _i32, _vp, _vp, _vp, _u32, _u64, _u32, _vp, _vp, _vp, _u32], _i32),
+    "ricrc_batch_host_st": ([_vp, _vp, _vp, _vp, _u32, _u64, _u32, _vp, _vp, _u32], _i32),
+    "ricrc_classify_device": ([_vp, _i32, _vp, _vp, _vp, _u32, _u64, _u32, _vp, _vp], _i32),
 }
 
 
@@ -343,6 +351,28 @@ class Context:
             raise ICRCError(rc, "ricrc_batch_host")
         return out
 
+    def batch_host_st(self, buf, offsets=None, lengths=None, stride: int = 0, l3_offset: int = 0,
+                      count: int | None = None, family: str = "v4", strict: bool = False,
+                      verify: bool = False):
+        """``ricrc_batch_host_st``: ``(out, status)`` -- a status per packet
+        (:data:`ST_OK`, :data:`ST_BADLEN`, :data:`ST_NOTROCE`) instead of
+        failing the call on a bad descriptor length; with ``strict`` only
+        packets the reference's ingress parser accepts as RoCEv2 get an ICRC
+        (shuffle_ingress_parser.p4:12-36); ``out[i] = 0`` where status != OK."""
+        buf = np.ascontiguousarray(buf).reshape(-1).view(np.uint8)
+        off = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint64)
+        ln = None if lengths is None else np.ascontiguousarray(lengths, dtype=np.uint32)
+        if count is None:
+            count = len(off) if off is not None else (len(ln) if ln is not None else buf.size // stride)
+        out = np.empty(count, dtype=np.uint32)
+        st = np.empty(count, dtype=np.uint8)
+        flags = _fam(family) | (F_STRICT if strict else 0) | (F_VERIFY if verify else 0)
+        rc = self._lib.ricrc_batch_host_st(self._h, buf.ctypes.data, _ptr(off), _ptr(ln), stride, count,
+                                           l3_offset, out.ctypes.data, st.ctypes.data, flags)
+        if rc:
+            raise ICRCError(rc, "ricrc_batch_host_st")
+        return out, st
+
     # -- device resident --------------------------------------------------
     def batch_device(self, base, count: int, out, stride: int = 0, offsets=None, lengths=None,
                      l3_offset: int = 0, dev: int = 0, stream=None, verify: bool = False,
@@ -352,6 +382,26 @@ class Context:
                 _ptr(out), _stream_ptr(stream), _fam(family))
         if rc:
             raise ICRCError(rc, "ricrc_verify_device" if verify else "ricrc_batch_device")
+
+    def batch_device_st(self, base, count: int, out, status, stride: int = 0, offsets=None, lengths=None,
+                        l3_offset: int = 0, dev: int = 0, stream=None, family: str = "v4",
+                        strict: bool = False, verify: bool = False) -> None:
+        """``ricrc_batch_device_st``: as :meth:`batch_device`, plus ``status``
+        (``count`` uint8 on the device, :data:`ST_OK` / :data:`ST_BADLEN` /
+        :data:`ST_NOTROCE`)."""
+        flags = _fam(family) | (F_STRICT if strict else 0) | (F_VERIFY if verify else 0)
+        rc = self._lib.ricrc_batch_device_st(self._h, dev, _ptr(base), _ptr(offsets), _ptr(lengths), stride, count,
+                                             l3_offset, _ptr(out), _ptr(status), _stream_ptr(stream), flags)
+        if rc:
+            raise ICRCError(rc, "ricrc_batch_device_st")
+
+    def classify_device(self, base, count: int, cls, stride: int = 0, offsets=None, lengths=None,
+                        l3_offset: int = 0, dev: int = 0, stream=None) -> None:
+        """``ricrc_classify_device``: ``cls[i]`` = 4 / 6 / 0 (uint8 on the device)."""
+        rc = self._lib.ricrc_classify_device(self._h, dev, _ptr(base), _ptr(offsets), _ptr(lengths), stride, count,
+                                             l3_offset, _ptr(cls), _stream_ptr(stream))
+        if rc:
+            raise ICRCError(rc, "ricrc_classify_device")
 
     def repair_device(self, base, count: int, off: int, old_bytes, out=None, stride: int = 0,
                       offsets=None, lengths=None, l3_offset: int = 0, old_stride: int | None = None,

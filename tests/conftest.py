@@ -21,3 +21,28 @@ def ctx():
     c = roce_icrc.Context(1)
     yield c
     c.close()
+
+
+@pytest.fixture
+def ctx_env(monkeypatch):
+    """Factory: a fresh one-GPU Context created under the given RICRC_*
+    environment knobs (libroceicrc reads them once, in ricrc_create), e.g.
+    ``ctx_env(RICRC_SCK_GRID=1)``."""
+    import roce_icrc
+
+    made = []
+
+    def make(**env):
+        for k, v in env.items():
+            monkeypatch.setenv(k, str(v))
+        try:
+            c = roce_icrc.Context(1)
+        finally:
+            for k in env:
+                monkeypatch.delenv(k)
+        made.append(c)
+        return c
+
+    yield make
+    for c in made:
+        c.close()

@@ -135,6 +135,40 @@ def test_errors_never_abort():
         assert roce_icrc.lib.ricrc_strerror(rc)
 
 
+def test_status_entry_points_reject_bad_arguments():
+    """The per-packet-status batch calls (ricrc_batch_device_st /
+    ricrc_batch_host_st / ricrc_classify_device): NULL context, bad flags ->
+    -EINVAL, never an abort; count 0 is a no-op only with a valid context."""
+    L = roce_icrc.lib
+    assert L.ricrc_batch_device_st(None, 0, None, None, None, 64, 1, 0, None, None, None, 0) == -errno.EINVAL
+    assert L.ricrc_batch_host_st(None, None, None, None, 64, 1, 0, None, None, 0) == -errno.EINVAL
+    assert L.ricrc_batch_host_st(None, None, None, None, 64, 1, 0, None, None, 0x400) == -errno.EINVAL
+    assert L.ricrc_classify_device(None, 0, None, None, None, 64, 1, 0, None, None) == -errno.EINVAL
+    assert roce_icrc.ST_OK == 0 and roce_icrc.ST_BADLEN == 1 and roce_icrc.ST_NOTROCE == 2
+    text = open(HEADER).read()
+    for name, v in (("RICRC_ST_OK", 0), ("RICRC_ST_BADLEN", 1), ("RICRC_ST_NOTROCE", 2),
+                    ("RICRC_F_STRICT", 0x100), ("RICRC_F_VERIFY", 0x200)):
+        assert re.search(rf"#define {name} {v:#x}u?\b" if v >= 0x100 else rf"#define {name} {v}\b", text), name
+
+
+def test_hip_library_needs_no_newer_hip_than_torchs():
+    """libroceicrc.so shares the process's HIP runtime with PyTorch-ROCm,
+    whichever is loaded first -- on the GPU box that is torch's bundled
+    libamdhip64 (ROCm 7.0), older than /opt/rocm's.  Every versioned HIP
+    symbol the library imports must exist there (round 3 found hipStreamGetId,
+    hip_7.1, missing from torch's copy: the library then fails to load)."""
+    torch = pytest.importorskip("torch")
+    thip = os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so")
+    if not os.path.exists(thip):
+        pytest.skip("torch ships no libamdhip64")
+    need = subprocess.run(["objdump", "-T", roce_icrc.LIB_PATH], capture_output=True, text=True).stdout
+    have = subprocess.run(["nm", "-D", "--defined-only", thip], capture_output=True, text=True).stdout
+    defined = set(re.findall(r"\b(hip\w+)@@?(hip_[\d.]+)", have))
+    missing = [(s, v) for v, s in re.findall(r"\*UND\*\s+\S+\s+\((hip_[\d.]+)\)\s+(hip\w+)", need)
+               if (s, v) not in defined]
+    assert not missing, missing
+
+
 def test_no_cpu_fallback_without_gpu():
     torch = pytest.importorskip("torch")
     if torch.cuda.is_available():

@@ -153,25 +153,24 @@ def test_prime_runs_for_the_requested_time(ctx):
     ctx.prime(0)
 
 
-def test_batch_host_failure_leaves_nothing_in_flight(ctx, monkeypatch):
-    """RICRC_FAIL_CHUNK=2: the call fails with -EIO after queueing chunk 2 of
-    4 (1 M packets per chunk); the next call on the same context -- reusing
-    the same staging slots and streams -- is bit-exact."""
+def test_batch_host_failure_leaves_nothing_in_flight(ctx_env):
+    """RICRC_FAIL_CHUNK=2 (read by ricrc_create, fires once): the call fails
+    with -EIO after queueing chunk 2 of 4 (1 M packets per chunk); the next
+    call on the same context -- reusing the same staging slots and streams --
+    is bit-exact."""
     import roce_icrc
 
     n, count = 64, (3 << 20) + 12345
     host = oracle_c.synth_batch(SEED, 0, count, n)
     want = oracle_c.icrc_batch(host, stride=n, threads=16)
-    monkeypatch.setenv("RICRC_FAIL_CHUNK", "2")
+    ctx = ctx_env(RICRC_FAIL_CHUNK=2)
     with pytest.raises(roce_icrc.ICRCError) as e:
         ctx.batch_host(host, stride=n)
     assert e.value.rc == -5
-    monkeypatch.delenv("RICRC_FAIL_CHUNK")
     np.testing.assert_array_equal(ctx.batch_host(host, stride=n), want)
     lens = np.full(count, n, np.uint32)
     offs = np.arange(count, dtype=np.uint64) * n
-    monkeypatch.setenv("RICRC_FAIL_CHUNK", "0")
+    ctx = ctx_env(RICRC_FAIL_CHUNK=0)
     with pytest.raises(roce_icrc.ICRCError):
         ctx.batch_host(host, offs, lens)
-    monkeypatch.delenv("RICRC_FAIL_CHUNK")
     np.testing.assert_array_equal(ctx.batch_host(host, offs, lens), want)

@@ -141,13 +141,13 @@ def test_bad_family_flags(ctx):
 @pytest.mark.parametrize("n", [1024, 2048, 4096])
 @pytest.mark.parametrize("family", ["v6", "auto"])
 @pytest.mark.parametrize("grid", [None, "1"])
-def test_sck_native_family_compute_and_verify(ctx, monkeypatch, n, family, grid):
+def test_sck_native_family_compute_and_verify(ctx, ctx_env, n, family, grid):
     """The strided-chain kernel applies the IPv6 / per-packet AUTO masks itself
     (no fix-up pass): every lane slot's mask words, the version nibble
     broadcast across a packet's 8 lanes, partial last groups, one workgroup
     walking many groups (RICRC_SCK_GRID=1), verify mode with corruptions."""
     if grid:
-        monkeypatch.setenv("RICRC_SCK_GRID", grid)
+        ctx = ctx_env(RICRC_SCK_GRID=grid)
     count = 8 * 16 * 5 + 3
     rng = np.random.default_rng(SEED + n)
     rows = _v6_rows(rng, count, n)

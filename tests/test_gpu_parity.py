@@ -110,15 +110,26 @@ def test_ragged_kernel_ethernet_offset(ctx):
     np.testing.assert_array_equal(_host_u32(out), want)
 
 
-def test_ragged_kernel_invalid_lengths_zero(ctx):
+def test_ragged_kernel_invalid_lengths_status(ctx):
+    """Bad descriptor lengths: the plain call writes 0 (indistinguishable from
+    an ICRC of 0); the status call tells them apart (RICRC_ST_BADLEN)."""
+    import roce_icrc
+
     buf = np.arange(256, dtype=np.uint8)
-    offs = np.array([0, 16, 32], dtype=np.uint64)
-    lens = np.array([3, 0, 100], dtype=np.uint32)
-    out = _out(3)
-    ctx.batch_device(_dev(buf), 3, out, offsets=_dev(offs), lengths=_dev(lens), stream=_stream())
+    offs = np.array([0, 16, 32, 40, 48], dtype=np.uint64)
+    lens = np.array([3, 0, 100, 43, 70000], dtype=np.uint32)
+    out = _out(5)
+    ctx.batch_device(_dev(buf), 5, out, offsets=_dev(offs), lengths=_dev(lens), stream=_stream())
     got = _host_u32(out)
-    assert got[0] == 0 and got[1] == 0
+    assert got[0] == 0 and got[1] == 0 and got[4] == 0
     assert got[2] == icrc_oracle.icrc(buf[32:132].tobytes())
+    assert got[3] == icrc_oracle.icrc(buf[40:83].tobytes())  # 4 <= n < 44: computed by the plain call
+    st = torch.empty(5, dtype=torch.uint8, device="cuda")
+    ctx.batch_device_st(_dev(buf), 5, out, st, offsets=_dev(offs), lengths=_dev(lens), stream=_stream())
+    torch.cuda.synchronize()
+    B, OK = roce_icrc.ST_BADLEN, roce_icrc.ST_OK
+    np.testing.assert_array_equal(st.cpu().numpy(), [B, B, OK, B, B])
+    np.testing.assert_array_equal(_host_u32(out), [0, 0, got[2], 0, 0])
 
 
 def test_ragged_kernel_c4_mix_many_waves(ctx):
@@ -141,13 +152,13 @@ def test_ragged_kernel_c4_mix_many_waves(ctx):
     np.testing.assert_array_equal(_host_u32(out), want)
 
 
-@pytest.mark.parametrize("knob", ["RICRC_RS_PIECE", "RICRC_NO_RSCK", "RICRC_NO_SCK"])
-def test_ragged_selectable_kernels_agree(ctx, knob, monkeypatch):
-    """The kernels kept selectable for comparison (the round-1 piece kernel for
-    the one-line region, the piece-based ragged kernel instead of the whole
-    ragged strided-chain path) give the same ICRCs as the oracle, on a C4-shaped
-    mix with odd starts and Ethernet framing, before and after the default path
-    ran on the same context (its workspace counters must be left clean)."""
+@pytest.mark.parametrize("gcost", [1, 4, 40])
+def test_ragged_work_split_does_not_change_results(ctx, ctx_env, gcost):
+    """The ragged fold splits weighted work (lines + a per-group cost,
+    RICRC_RS_GCOST, read by ricrc_create) over its waves: other splits move
+    groups between waves and descriptor blocks but give the same ICRCs, on a
+    C4-shaped mix with odd starts and Ethernet framing -- on the session
+    context before and after (its workspace counters must be left clean)."""
     rng = np.random.default_rng(31)
     count = 20_000
     lens = rng.choice(np.array([64, 100, 256, 1024, 1500, 4096], np.uint32), size=count)
@@ -156,14 +167,10 @@ def test_ragged_selectable_kernels_agree(ctx, knob, monkeypatch):
     buf = rng.integers(0, 256, size=int(offs[-1] + lens[-1]) + 64 + 14, dtype=np.uint8)
     want = oracle_c.icrc_batch(buf[14:], offsets=offs, lengths=lens, threads=16)
     d_buf, d_offs, d_lens = _dev(buf), _dev(offs), _dev(lens)
-    for env in (None, knob, None):
-        if env:
-            monkeypatch.setenv(env, "1")
-        else:
-            monkeypatch.delenv(knob, raising=False)
+    for c in (ctx, ctx_env(RICRC_RS_GCOST=gcost, RICRC_RSCK_GRID=37), ctx):
         out = _out(count)
-        ctx.batch_device(d_buf, count, out, offsets=d_offs, lengths=d_lens, l3_offset=14, stream=_stream())
-        np.testing.assert_array_equal(_host_u32(out), want, err_msg=str(env))
+        c.batch_device(d_buf, count, out, offsets=d_offs, lengths=d_lens, l3_offset=14, stream=_stream())
+        np.testing.assert_array_equal(_host_u32(out), want)
 
 
 def test_ragged_kernel_offsets_only_and_lengths_only(ctx):
@@ -341,35 +348,34 @@ def test_headline_full_size_bit_exact(ctx):
 @pytest.mark.parametrize("n", [1024, 2048, 4096])
 @pytest.mark.parametrize("count,grid", [(1, None), (7, None), (9, None), (8 * 16 * 64 + 3, 1),
                                          (8 * 16 * 130 + 5, 1), (8 * 16 * 200, 2), (70001, None)])
-def test_strided_chain_kernel(ctx, monkeypatch, n, count, grid):
+def test_strided_chain_kernel(ctx, ctx_env, n, count, grid):
     """icrc_sck_kernel (back-to-back 1/2/4 KiB packets): partial 8-packet
     groups, waves with no groups, and -- with the grid capped -- waves that
     flush their 512 LDS result slots several times; compared with the oracle
     and with the transposed kernel on the same bytes."""
     if grid is not None:
-        monkeypatch.setenv("RICRC_SCK_GRID", str(grid))
+        ctx = ctx_env(RICRC_SCK_GRID=grid)
     host = oracle_c.synth_batch(SEED ^ count, 3, count, n)
     want = oracle_c.icrc_batch(host, stride=n, threads=8)
     d = _dev(host)
     out = _out(count)
     ctx.batch_device(d, count, out, stride=n, stream=_stream())
     np.testing.assert_array_equal(_host_u32(out), want)
-    monkeypatch.setenv("RICRC_NO_SCK", "1")
     out2 = _out(count)
-    ctx.batch_device(d, count, out2, stride=n, stream=_stream())
+    ctx_env(RICRC_NO_SCK=1).batch_device(d, count, out2, stride=n, stream=_stream())
     np.testing.assert_array_equal(_host_u32(out2), want)
 
 
 @pytest.mark.parametrize("grid", [None, 1])
-def test_ragged_strided_chain_mixed(ctx, monkeypatch, grid):
+def test_ragged_strided_chain_mixed(ctx, ctx_env, grid):
     """Ragged strided-chain path: lengths from 44 B to 9 KiB, start offsets of
     any alignment (bytes before the first packet and between packets), so every
-    line-count class, the small-packet classes (piece kernel) and byte-granular
+    line-count class, the one-line classes (lane-per-packet kernel) and byte-granular
     head/tail masks occur; with the fold grid capped to one workgroup each wave
     crosses many descriptor blocks and result rounds.  Verify mode on the same
     batch with a few corrupted packets."""
     if grid is not None:
-        monkeypatch.setenv("RICRC_RSCK_GRID", str(grid))
+        ctx = ctx_env(RICRC_RSCK_GRID=grid)
     rng = np.random.default_rng(7)
     count = 6000
     lens = rng.integers(44, 9001, size=count).astype(np.uint32)
@@ -429,21 +435,6 @@ def test_ragged_strided_chain_word_aligned(ctx):
         ctx.batch_device(d, count, out, offsets=_dev(o.view(np.int64)), lengths=_dev(l.view(np.int32)),
                          stream=_stream())
         np.testing.assert_array_equal(_host_u32(out), want)
-
-
-def test_strided_chain_dynamic_schedule(ctx, monkeypatch):
-    """Opt-in dynamic schedule of the strided-chain kernel (groups from a
-    self-resetting device counter): same results as the oracle, launch after
-    launch (a counter left non-zero would skip groups in the next launch)."""
-    monkeypatch.setenv("RICRC_SCK_DYNAMIC", "1")
-    for n, count in ((4096, 20003), (1024, 70001), (2048, 9)):
-        host = oracle_c.synth_batch(SEED ^ n, 11, count, n)
-        want = oracle_c.icrc_batch(host, stride=n, threads=8)
-        d = _dev(host)
-        for _ in range(3):
-            out = _out(count)
-            ctx.batch_device(d, count, out, stride=n, stream=_stream())
-            np.testing.assert_array_equal(_host_u32(out), want)
 
 
 def test_ragged_workspace_reuse_across_sizes_and_streams(ctx):

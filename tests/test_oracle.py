@@ -143,3 +143,75 @@ def test_ack_matches_calc_icrc_field_list():
                   + struct.pack(">B", f["syndrome"]) + f["msn"].to_bytes(3, "big"))  # :489-490
         assert len(fields) == 52
         assert O.icrc(l3) == zlib.crc32(fields)
+
+
+def test_classify_restatement_matches_product_classifier():
+    """oracle.classify (the ingress parser's accept path restated,
+    shuffle_ingress_parser.p4:12-36) against the product's CPU ricrc_classify
+    on RoCEv2 packets of both families and on every single-field violation:
+    version/IHL, protocol, total_len / payload length, UDP dport, lengths at
+    and beyond the bounds -- and the EtherType rule for framed packets."""
+    import random
+
+    import roce_icrc
+
+    rng = random.Random(12)
+    ack = bytes.fromhex("450200301234400040110000c0a80164c0a80101457b12b7001c00001140ffff"
+                        "0000001100000005000000016c1f7922")
+    assert O.classify(ack) == roce_icrc.classify(ack) == 4
+    assert O.classify(ack, 0x0800) == 4 and O.classify(ack, 0x86DD) == 0 and O.classify(ack, 0x0806) == 0
+
+    def v6(n):
+        p = bytearray(rng.getrandbits(8) for _ in range(n))
+        p[0] = 0x60 | (p[0] & 15)
+        p[4:6] = (n - 40).to_bytes(2, "big")
+        p[6] = 17
+        p[42:44] = (4791).to_bytes(2, "big")
+        return p
+
+    def v4(n):
+        p = bytearray(rng.getrandbits(8) for _ in range(n))
+        p[0], p[9] = 0x45, 17
+        p[2:4] = n.to_bytes(2, "big")
+        p[22:24] = (4791).to_bytes(2, "big")
+        return p
+
+    cases = []
+    for n in (44, 45, 63, 64, 65, 100, 1024, 4096, 9000):
+        cases += [v4(n)] + ([v6(n)] if n >= 64 else [])
+        for off, val in ((0, 0x46), (0, 0x55), (9, 6), (2, 0), (23, 0xB8), (22, 0)):
+            p = v4(n)
+            p[off] = val
+            cases.append(p)
+        if n >= 64:
+            for off, val in ((0, 0x50), (6, 6), (4, 0xFF), (43, 0xB8)):
+                p = v6(n)
+                p[off] = val
+                cases.append(p)
+    cases += [v4(44)[:43], bytes(43), bytes(64)]
+    for p in cases:
+        p = bytes(p)
+        assert O.classify(p) == roce_icrc.classify(p), p[:8].hex()
+    assert sum(O.classify(bytes(p)) == 4 for p in cases) >= 9
+    assert sum(O.classify(bytes(p)) == 6 for p in cases) >= 6
+
+
+def test_status_batch_restatement_on_a_small_ring():
+    """oracle.status_batch on a hand-built ring: bad lengths, a non-RoCE frame
+    under strict, framed EtherType checks, verify mode."""
+    ack = bytearray.fromhex("450200301234400040110000c0a80164c0a80101457b12b7001c00001140ffff"
+                            "0000001100000005000000016c1f7922")
+    tcp = bytearray(ack)
+    tcp[9] = 6
+    frames = [b"\x01" * 12 + b"\x08\x00" + ack, b"\x01" * 12 + b"\x08\x00" + tcp,
+              b"\x01" * 12 + b"\x86\xdd" + ack, b"\x01" * 12 + b"\x08\x00" + ack]
+    buf = np.frombuffer(b"".join(frames), np.uint8)
+    offs = np.array([0, 62, 124, 186], np.uint64)
+    lens = np.array([48, 48, 48, 40], np.uint32)
+    out, st = O.status_batch(buf, offs, lens, l3_offset=14, strict=True)
+    assert st.tolist() == [O.ST_OK, O.ST_NOTROCE, O.ST_NOTROCE, O.ST_BADLEN]
+    assert out.tolist() == [0x22791F6C, 0, 0, 0]
+    out, st = O.status_batch(buf, offs, lens, l3_offset=14)
+    assert st.tolist() == [O.ST_OK, O.ST_OK, O.ST_OK, O.ST_BADLEN] and out[1] == O.icrc(bytes(tcp))
+    out, st = O.status_batch(buf, offs, lens, l3_offset=14, strict=True, verify=True)
+    assert out.tolist() == [1, 0, 0, 0]

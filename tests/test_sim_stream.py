@@ -4,8 +4,10 @@ The fixture (tests/golden/sim_stream.*) is the packet stream of the unchanged
 reference python/simulator.py for seeds 1-3, captured by
 tests/golden/gen_sim_stream.py with ICRCs from the oracle.  Here: the adapter
 re-serialises every Packet to the same bytes, ricrc_one (ctypes) reproduces
-every ICRC, the verify path accepts them, corruption is caught, and (GPU) the
-whole stream as one ragged batch through the ragged kernel matches."""
+every ICRC, the verify path accepts them and corruption is caught.  The GPU
+replay of the same fixture -- the whole stream as one ragged batch through the
+HIP kernels, host path, verify and status modes, against the ICRCs stored in
+the fixture -- is tests/test_gpu_fixtures.py."""
 import json
 import os
 import queue

@@ -38,7 +38,7 @@ int main(int argc, char **argv) {
   auto ragged = [&](const char *tag, uint64_t count, const uint64_t *d_off, const uint32_t *d_len, uint32_t n, double b) {
     RsckArgs a{};
     a.base = buf; a.off = d_off; a.len = d_len; a.stride = n; a.count = count; a.fixed_len = n;
-    a.out = out; a.tzb = tzb; a.group_cost = kGroupCost;
+    a.out = out; a.tzb = tzb; a.group_cost = kRsGroupCost;
     for (int j = 0; j < 32; ++j) { a.XB[j] = 0x85EBCA6Bu * (j + 3); a.XB2[j] = 0x27D4EB2Fu * (j + 5); a.XB3[j] = 0x165667B1u * (j + 7); }
     for (int s = 0; s < 8; ++s) a.QS[s] = 0x9E3779B9u * (s + 1);
     void *ws; CK(hipMalloc(&ws, rs_workspace_bytes(count)));
@@ -110,7 +110,7 @@ int main(int argc, char **argv) {
 
   {  // out of the idle power state before timing anything
     SckArgs s{}; s.base = buf; s.count = bytes / 4096; s.out = out; s.n = 4096;
-    for (int i = 0; i < 300; ++i) hipLaunchKernelGGL((icrc_sck_kernel<32, 0, 8, false, false, true>), dim3(grid), dim3(kBlock), 0, 0, s);
+    for (int i = 0; i < 300; ++i) hipLaunchKernelGGL((icrc_sck_kernel<32, 0>), dim3(grid), dim3(kBlock), 0, 0, s);
     CK(hipDeviceSynchronize());
   }
   const bool mix_only = argc > 1 && argv[1][0] == 'm';  // "mix": the mixed batch only
@@ -123,7 +123,7 @@ int main(int argc, char **argv) {
     if (s1k) {
       if (n != 1024) continue;
       RsckArgs a{};
-      a.base = buf; a.stride = n; a.count = bytes / n; a.fixed_len = n; a.out = out; a.tzb = tzb; a.group_cost = kGroupCost;
+      a.base = buf; a.stride = n; a.count = bytes / n; a.fixed_len = n; a.out = out; a.tzb = tzb; a.group_cost = kRsGroupCost;
       for (int j = 0; j < 32; ++j) { a.XB[j] = 0x85EBCA6Bu * (j + 3); a.XB2[j] = 0x27D4EB2Fu * (j + 5); a.XB3[j] = 0x165667B1u * (j + 7); }
       for (int k = 0; k < 8; ++k) a.QS[k] = 0x9E3779B9u * (k + 1);
       void *ws; CK(hipMalloc(&ws, rs_workspace_bytes(a.count)));
@@ -146,8 +146,8 @@ int main(int argc, char **argv) {
     char tag[32]; snprintf(tag, sizeof tag, "%u B x %llu", n, (unsigned long long)count);
     char nm[128]; snprintf(nm, sizeof nm, "%s sck", tag);
     if (n == 256) {}
-    else if (n == 4096) rep(nm, timeit([&] { hipLaunchKernelGGL((icrc_sck_kernel<32, 0, 8, false, false, true>), dim3(grid), dim3(kBlock), 0, 0, s); }, 10), (double)bytes);
-    else rep(nm, timeit([&] { hipLaunchKernelGGL((icrc_sck_kernel<8, 0, 8, false, false, true>), dim3(grid), dim3(kBlock), 0, 0, s); }, 10), (double)bytes);
+    else if (n == 4096) rep(nm, timeit([&] { hipLaunchKernelGGL((icrc_sck_kernel<32, 0>), dim3(grid), dim3(kBlock), 0, 0, s); }, 10), (double)bytes);
+    else rep(nm, timeit([&] { hipLaunchKernelGGL((icrc_sck_kernel<8, 0>), dim3(grid), dim3(kBlock), 0, 0, s); }, 10), (double)bytes);
     ragged(tag, count, nullptr, nullptr, n, (double)bytes);
   }
   // C4 mix: 64/256/1024/4096 uniformly, packed, within the 4 GiB buffer

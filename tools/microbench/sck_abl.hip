@@ -7,11 +7,11 @@
 #include <stdlib.h>
 using namespace ricrc;
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s\n", hipGetErrorString(e)); exit(1); } } while (0)
-template <int L, int ABL, int D = 8, bool QL = false, int XT = 0, int PL = L> float run(SckArgs a, int grid, int reps) {
+template <int L, int ABL, int PL = L> float run(SckArgs a, int grid, int reps) {
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-  for (int w = 0; w < 3; ++w) hipLaunchKernelGGL((icrc_sck_kernel<L, ABL, D, QL, false, XT, kFamV4, PL>), dim3(grid), dim3(kBlock), 0, 0, a);
+  for (int w = 0; w < 3; ++w) hipLaunchKernelGGL((icrc_sck_kernel<L, ABL, kFamV4, PL>), dim3(grid), dim3(kBlock), 0, 0, a);
   CK(hipDeviceSynchronize()); CK(hipEventRecord(e0));
-  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL((icrc_sck_kernel<L, ABL, D, QL, false, XT, kFamV4, PL>), dim3(grid), dim3(kBlock), 0, 0, a);
+  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL((icrc_sck_kernel<L, ABL, kFamV4, PL>), dim3(grid), dim3(kBlock), 0, 0, a);
   CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); float ms; CK(hipEventElapsedTime(&ms, e0, e1)); return ms / reps;
 }
 int main(int argc, char **argv) {
@@ -32,11 +32,9 @@ int main(int argc, char **argv) {
   auto rep = [&](const char *nm, float ms) { printf("%-36s %7.3f ms  %7.1f GB/s\n", nm, ms, 4294967296.0 / (ms * 1e-3) / 1e9); };
   const bool quick = argc > 1 && argv[1][0] == 'x';  // "xt": finish-table variants only
   for (int r = 0; r < 2; ++r) {
-    rep("full XT1 (32-copy x^-32 table)", run<32, 0, 8, false, 1>(a, grid, 20));
-    rep("full XT2 (one-copy finish tables)", run<32, 0, 8, false, 2>(a, grid, 20));
-    rep("no loads XT1", run<32, 8, 8, false, 1>(a, grid, 20));
-    rep("no loads XT2", run<32, 8, 8, false, 2>(a, grid, 20));
-    rep("memory path XT2", run<32, 1 | 2, 8, false, 2>(a, grid, 20));
+    rep("full (one-copy finish tables)", run<32, 0>(a, grid, 20));
+    rep("no loads", run<32, 8>(a, grid, 20));
+    rep("memory path", run<32, 1 | 2>(a, grid, 20));
     if (quick) continue;
     rep("full D8", run<32, 0>(a, grid, 20));
     rep("no stores", run<32, 16>(a, grid, 20));
@@ -53,14 +51,12 @@ int main(int argc, char **argv) {
     const double by = 1024.0 * cnt;
     auto rep8 = [&](const char *nm, float ms) { printf("%-36s %7.3f ms  %7.1f GB/s  (%llu x 1 KiB)\n", nm, ms, by / (ms * 1e-3) / 1e9, (unsigned long long)cnt); };
     for (int r = 0; r < 2; ++r) {
-      rep8("L8 full XT1", run<8, 0, 8, false, 1>(b, grid, 20));
-      rep8("L8 full XT2", run<8, 0, 8, false, 2>(b, grid, 20));
-      rep8("L8 no loads XT1", run<8, 8, 8, false, 1>(b, grid, 20));
-      rep8("L8 no loads XT2", run<8, 8, 8, false, 2>(b, grid, 20));
-      rep8("L8 memory path", run<8, 1 | 2, 8, false, 2>(b, grid, 20));
-      rep8("L32/PL8 super-groups full XT2", run<32, 0, 8, false, 2, 8>(b, grid, 20));
-      rep8("L32/PL8 super-groups no loads XT2", run<32, 8, 8, false, 2, 8>(b, grid, 20));
-      rep8("L32/PL8 super-groups memory path", run<32, 1 | 2, 8, false, 2, 8>(b, grid, 20));
+      rep8("L8 full", run<8, 0>(b, grid, 20));
+      rep8("L8 no loads", run<8, 8>(b, grid, 20));
+      rep8("L8 memory path", run<8, 1 | 2>(b, grid, 20));
+      rep8("L32/PL8 super-groups full", run<32, 0, 8>(b, grid, 20));
+      rep8("L32/PL8 super-groups no loads", run<32, 8, 8>(b, grid, 20));
+      rep8("L32/PL8 super-groups memory path", run<32, 1 | 2, 8>(b, grid, 20));
       if (quick) continue;
       rep8("L8 full", run<8, 0>(b, grid, 20));
       rep8("L8 no finish", run<8, 2>(b, grid, 20));

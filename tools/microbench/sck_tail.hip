@@ -12,7 +12,7 @@
 using namespace ricrc;
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s\n", hipGetErrorString(e)); exit(1); } } while (0)
 
-template <int L, bool DYN>
+template <int L>
 void run(uint8_t *buf, uint32_t *out, uint64_t count, int grid) {
   SckArgs a{};
   a.base = buf; a.count = count; a.out = out; a.n = 128 * L;
@@ -20,16 +20,14 @@ void run(uint8_t *buf, uint32_t *out, uint64_t count, int grid) {
   for (int s = 0; s < 8; ++s) a.QS[s] = 0x9E3779B9u * (s + 1);
   const int waves = grid * kWaves;
   CK(hipMalloc(&a.stamps, 16ull * waves));
-  CK(hipMalloc(&a.work, 4 * kSckWorkWords));
-  CK(hipMemset(a.work, 0, 4 * kSckWorkWords));
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-  for (int r = 0; r < 10; ++r) hipLaunchKernelGGL((icrc_sck_kernel<L, 64, 8, false, DYN, true>), dim3(grid), dim3(kBlock), 0, 0, a);
+  for (int r = 0; r < 10; ++r) hipLaunchKernelGGL((icrc_sck_kernel<L, 64>), dim3(grid), dim3(kBlock), 0, 0, a);
   CK(hipEventRecord(e0));
-  for (int r = 0; r < 20; ++r) hipLaunchKernelGGL((icrc_sck_kernel<L, 64, 8, false, DYN, true>), dim3(grid), dim3(kBlock), 0, 0, a);
+  for (int r = 0; r < 20; ++r) hipLaunchKernelGGL((icrc_sck_kernel<L, 64>), dim3(grid), dim3(kBlock), 0, 0, a);
   CK(hipEventRecord(e1));
   CK(hipDeviceSynchronize());
   float ms; CK(hipEventElapsedTime(&ms, e0, e1));
-  printf("%s L=%d count=%llu: %.1f us per launch (HIP events, 20 launches)\n", DYN ? "DYNAMIC" : "STATIC ", L,
+  printf("%s L=%d count=%llu: %.1f us per launch (HIP events, 20 launches)\n", "STATIC ", L,
          (unsigned long long)count, ms * 1000.f / 20);
   std::vector<uint64_t> st(2 * waves);
   CK(hipMemcpy(st.data(), a.stamps, 16ull * waves, hipMemcpyDeviceToHost));
@@ -50,7 +48,6 @@ void run(uint8_t *buf, uint32_t *out, uint64_t count, int grid) {
     printf("    xcd %d: end min %.1f max %.1f us\n", x, mn, mx);
   }
   CK(hipFree(a.stamps));
-  CK(hipFree(a.work));
 }
 
 int main() {
@@ -66,10 +63,8 @@ int main() {
   }
   hipDeviceProp_t p; CK(hipGetDeviceProperties(&p, 0));
   for (int r = 0; r < 2; ++r) {
-    run<32, false>(buf, out, 1ull << 20, p.multiProcessorCount);
-    run<32, true>(buf, out, 1ull << 20, p.multiProcessorCount);
-    run<8, false>(buf, out, 1ull << 20, p.multiProcessorCount);
-    run<8, true>(buf, out, 1ull << 20, p.multiProcessorCount);
+    run<32>(buf, out, 1ull << 20, p.multiProcessorCount);
+    run<8>(buf, out, 1ull << 20, p.multiProcessorCount);
   }
   return 0;
 }
