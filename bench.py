@@ -51,6 +51,8 @@ SEED = 0x1CEC0DE
 # Headline kernel's sources: PMC traffic (profiles/pmc_traffic.json) is only
 # reported for the exact sources it was measured on.
 SCK_SOURCES = ("icrc_sck.hip", "icrc_sck.h", "icrc_device.h", "icrc_math.h")
+# The ragged pipeline's (C4, --mix): passes, fold, one-line kernel, gather.
+RAGGED_SOURCES = ("icrc_rsck.hip", "icrc_kernels.h", "icrc_sck.h", "icrc_device.h", "icrc_math.h")
 
 
 def parse(argv=None):
@@ -117,26 +119,32 @@ def check_world(args, env=os.environ):
     return None
 
 
-def kernel_source_hash():
-    """sha256 of the headline kernel's sources (SCK_SOURCES)."""
+def kernel_source_hash(sources=None):
+    """sha256 of a kernel's sources (default: the headline kernel's, SCK_SOURCES)."""
     import hashlib
 
     h = hashlib.sha256()
-    for name in SCK_SOURCES:
+    for name in sources or SCK_SOURCES:
         with open(os.path.join(ROOT, "roce-test_amd", "csrc", name), "rb") as f:
             h.update(f.read())
     return h.hexdigest()[:16]
 
 
-def load_traffic(size, count):
+def load_traffic(args, count):
     """HBM bytes per launch measured by separate rocprofv3 --pmc passes
-    (profiles/pmc_traffic.json, from tools/pmc_traffic.py) on this very kernel
-    source, or None."""
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    (profiles/pmc_traffic*.json, from tools/pmc_traffic.py) on this very
+    workload and kernel source, or None."""
+    if args.family != "v4":
+        return None
+    name = "pmc_traffic_mix.json" if args.mix else "pmc_traffic.json"
+    srcs = RAGGED_SOURCES if args.mix else SCK_SOURCES
+    p = os.path.join(ROOT, "profiles", name)
     try:
         with open(p) as f:
             d = json.load(f)
-        if d.get("size") == size and d.get("count") == count and d.get("kernel_src") == kernel_source_hash():
+        same = d.get("count") == count and d.get("kernel_src") == kernel_source_hash(srcs)
+        same = same and (d.get("size") == "mix" if args.mix else d.get("size") == args.size)
+        if same:
             return d.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
@@ -209,10 +217,33 @@ def oracle_check(gathered, sizes, cuts, args, lens_global=None, per_rank=256):
     return bad
 
 
+def product_cpu(sample_host, got_sample, size, budget_s, threads, offsets=None, lengths=None, family="v4"):
+    """The product's own CPU batch path (ricrc_batch_cpu in libroceicrc_cpu.so:
+    the slice-by-16 fold of ricrc_one, icrc_cpu.cpp) on the same sample and
+    threads: GiB/s, or an error string if its ICRCs differ from the GPU's."""
+    import numpy as np
+
+    import roce_icrc
+
+    kw = dict(offsets=offsets, lengths=lengths) if offsets is not None else dict(stride=size)
+    if not np.array_equal(roce_icrc.icrc_batch_cpu(sample_host, threads=threads, family=family, **kw), got_sample):
+        return "mismatch"
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        roce_icrc.icrc_batch_cpu(sample_host, threads=threads, family=family, **kw)
+        reps += 1
+        dt = time.perf_counter() - t0
+        if dt >= budget_s:
+            break
+    nbytes = int(lengths.sum(dtype=np.uint64)) if lengths is not None else sample_host.size
+    return nbytes * reps / dt / 2**30
+
+
 def cpu_baseline(sample_host, got_sample, size, budget_s, offsets=None, lengths=None, family="v4"):
     """Time the C oracle (slice-by-8, pthreads over this host's CPU share) on a
     sample of the batch, check the GPU's ICRCs on it, and add a 1-core zlib
-    figure (the Python oracle, zlib.crc32 per packet)."""
+    figure (the Python oracle, zlib.crc32 per packet) and the product's own
+    CPU batch path (slice-by-16, same threads)."""
     import numpy as np
 
     oracle_c, icrc_oracle = _oracle()
@@ -251,6 +282,10 @@ def cpu_baseline(sample_host, got_sample, size, budget_s, offsets=None, lengths=
                   f"slice-by-8 on {threads} threads (this GPU's CPU share of {os.cpu_count()} visible host CPUs)",
         "cpu_model": cpu_model(),
         "zlib_1core_GiBs": round(zb / zdt / 2**30, 3),
+        "product_cpu_GiBs": (lambda v: round(v, 2) if isinstance(v, float) else v)(
+            product_cpu(sample_host, got_sample, size, min(3.0, budget_s), threads, offsets, lengths, family)),
+        "product_cpu": f"ricrc_batch_cpu (libroceicrc_cpu.so, slice-by-16 fold of ricrc_one) on the same sample "
+                       f"and {threads} threads -- the build's own CPU path, not the reference's",
     }
 
 
@@ -368,49 +403,108 @@ def relaunch(args, argv):
     return subprocess.call(cmd, env=env)
 
 
-def main(argv=None):
-    argv = sys.argv[1:] if argv is None else argv
-    args = parse(argv)
-    chk = check_world(args)
-    if chk is not None:
-        code, msg = chk
-        if msg == "relaunch":  # --gpus N > 1 outside torchrun: N ranks, before any GPU call
-            return relaunch(args, argv)
-        print(msg, file=sys.stderr)
-        return code
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.plan_only:
-        return plan_only(args, world, rank)
+def _count_label(n):
+    return f"{n >> 20}M" if n and n % (1 << 20) == 0 else str(n)
 
+
+def metric_for(args, T, count):
+    """The metric string of the workload actually run: BASELINE.json's
+    headline string only for its own config (1 M x 4096 B per GPU)."""
+    if args.mix:
+        scope = f"{_count_label(T)} in all" if args.global_count is not None else f"{_count_label(args.count)} per GPU"
+        return (f"device-resident ICRC GiB/s on mixed-MTU (64/256/1024/4096 B) RoCE packets ({scope}); "
+                "bit-exact vs reference")
+    if args.global_count is None and args.size == 4096 and args.count == 1 << 20:
+        return METRIC
+    if args.global_count is not None:
+        return (f"device-resident ICRC GiB/s on {_count_label(T)}\u00d7{args.size}B RoCE packets (fixed total); "
+                "bit-exact vs reference")
+    return f"device-resident ICRC GiB/s on {_count_label(args.count)}\u00d7{args.size}B RoCE packets; bit-exact vs reference"
+
+
+class HipBackend:
+    """The product path of one rank: libroceicrc's gfx950 kernels on the
+    rank's GPU (roce_icrc.Context), RCCL ("nccl") between ranks, HIP events on
+    the compute stream.  run() drives it; tests/test_bench_dist.py drives
+    run() with a CPU stand-in over gloo (the N > 1 loop without a GPU)."""
+
+    dist_backend = "nccl"
+
+    def __init__(self, local):
+        import torch
+
+        import roce_icrc
+
+        self.torch = torch
+        torch.cuda.set_device(local)
+        self.dev = torch.device("cuda", local)
+        self.ctx = roce_icrc.Context(devices=[local])
+        self.stream = torch.cuda.current_stream()
+
+    def init_dist(self):
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=self.dev)
+
+    def build(self, args, world, rank):
+        import numpy as np
+
+        return build_batch(self.torch, np, self.ctx, self.dev, self.stream, args, world, rank)
+
+    def compute(self, b, count, out, args):
+        if args.mix:
+            self.ctx.batch_device(b["buf"], count, out, offsets=b["d_offs"], lengths=b["d_lens"], stream=self.stream,
+                                  family=args.family)
+        else:
+            self.ctx.batch_device(b["buf"], count, out, stride=args.size, stream=self.stream, family=args.family)
+
+    def sync(self):
+        self.torch.cuda.synchronize()
+
+    def event(self):
+        return self.torch.cuda.Event(enable_timing=True)
+
+    def record(self, ev):
+        ev.record(self.stream)
+
+    def prime(self, ms):
+        if ms > 0:
+            self.ctx.prime(int(ms * 1000))
+
+    def host_bytes(self, b, nbytes):
+        return b["buf"][:nbytes].cpu().numpy()
+
+    def close(self):
+        self.ctx.close()
+
+
+def run(args, world, rank, be, distributed):
+    """The timed loop of one rank on backend `be`; returns (result, ICRCs on
+    the host, batch).  Steps: the hot path over the resident shard + (N > 1)
+    the all-gather of the u32 results (IcrcGather, one collective per step,
+    double-buffered; async on the collective's stream by default).  The K
+    timed steps sit between barrier + synchronize on both sides; elapsed and
+    kernel time are the max over ranks, bytes the sum."""
     import numpy as np
     import torch
     import torch.distributed as dist
 
-    import roce_icrc
     from roce_icrc.dist import IcrcGather
 
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    distributed = world > 1 or "MASTER_ADDR" in os.environ
     if distributed:
-        dist.init_process_group("nccl", device_id=dev)
-    ctx = roce_icrc.Context(devices=[local])
-
-    stream = torch.cuda.current_stream()
-    b = build_batch(torch, np, ctx, dev, stream, args, world, rank)
+        be.init_dist()
+    b = be.build(args, world, rank)
     count, sizes = b["sizes"][rank], b["sizes"]
-    pk, d_offs, d_lens, rank_bytes = b["buf"], b["d_offs"], b["d_lens"], b["rank_bytes"]
+    rank_bytes = b["rank_bytes"]
     do_gather = distributed and not args.no_gather
     g = IcrcGather(sizes)
     # Double-buffered results (padded to the longest shard).  Default: step
-    # i's all-gather runs async on RCCL's stream, overlapping step i+1's
-    # kernel, and a buffer is reused only after the gather that read it has
-    # been waited for.  --in-stream-gather: the gather is ordered after the
-    # kernel on the compute stream.
-    outs = [g.local_buffer(dev) for _ in range(2)]
-    gathered = [g.gathered_buffer(dev) for _ in range(2)] if do_gather else None
+    # i's all-gather runs async on the collective's stream, overlapping step
+    # i+1's kernel, and a buffer is reused only after the gather that read it
+    # has been waited for.  --in-stream-gather: the gather is ordered after
+    # the kernel on the compute stream (DESIGN.md §6).
+    outs = [g.local_buffer(be.dev) for _ in range(2)]
+    gathered = [g.gathered_buffer(be.dev) for _ in range(2)] if do_gather else None
     pending = [None, None]
 
     def step(i, ev=None):
@@ -419,15 +513,11 @@ def main(argv=None):
             pending[j].wait()  # the current stream waits for the gather that read outs[j]
             pending[j] = None
         if ev is not None:
-            ev[0].record(stream)
+            be.record(ev[0])
         if count:
-            if args.mix:
-                ctx.batch_device(pk, count, outs[j], offsets=d_offs, lengths=d_lens, stream=stream,
-                                 family=args.family)
-            else:
-                ctx.batch_device(pk, count, outs[j], stride=args.size, stream=stream, family=args.family)
+            be.compute(b, count, outs[j], args)
         if ev is not None:
-            ev[1].record(stream)
+            be.record(ev[1])
         if do_gather:
             pending[j] = g.start(outs[j], gathered[j], async_op=args.overlap_gather)
 
@@ -437,32 +527,31 @@ def main(argv=None):
                 pending[j].wait()
                 pending[j] = None
 
-    torch.cuda.synchronize()
-    if args.prime_ms > 0:
-        ctx.prime(int(args.prime_ms * 1000))
+    be.sync()
+    be.prime(args.prime_ms)
     for i in range(args.warmup):
         step(i)
     drain()
     n_ev = args.steps if args.step_events else 1
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_ev)]
-    torch.cuda.synchronize()
+    evs = [(be.event(), be.event()) for _ in range(n_ev)]
+    be.sync()
     if distributed:
         dist.barrier()
-    torch.cuda.synchronize()
+    be.sync()
     t0 = time.perf_counter()
     if args.step_events:
         for i in range(args.steps):
             step(i, evs[i])
     else:
-        evs[0][0].record(stream)
+        be.record(evs[0][0])
         for i in range(args.steps):
             step(i)
-        evs[0][1].record(stream)
+        be.record(evs[0][1])
     drain()
-    torch.cuda.synchronize()
+    be.sync()
     if distributed:
         dist.barrier()
-    torch.cuda.synchronize()
+    be.sync()
     elapsed = time.perf_counter() - t0
     kern_ms = sum(a.elapsed_time(c) for a, c in evs) / max(args.steps, 1)
 
@@ -488,10 +577,10 @@ def main(argv=None):
 
     all_bytes = rank_bytes
     if distributed:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=be.dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
-        nb = torch.tensor([rank_bytes], dtype=torch.int64, device=dev)
+        nb = torch.tensor([rank_bytes], dtype=torch.int64, device=be.dev)
         dist.all_reduce(nb, op=dist.ReduceOp.SUM)
         all_bytes = int(nb[0])
 
@@ -499,7 +588,7 @@ def main(argv=None):
     # per launch: packets read + ICRCs written (+ 12 B of offset/length descriptors per packet, ragged)
     alg_bytes = rank_bytes + 4 * count + (12 * count if args.mix else 0)
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
-    traffic = None if (args.mix or args.family != "v4") else load_traffic(args.size, count)
+    traffic = load_traffic(args, count)
 
     strong = args.global_count is not None
     if args.mix:
@@ -514,7 +603,7 @@ def main(argv=None):
     if do_gather:
         workload += " + RCCL all-gather of the u32 ICRCs" + (" (overlapped)" if args.overlap_gather else "")
     result = {
-        "metric": MIX_METRIC if args.mix else METRIC,
+        "metric": metric_for(args, b["T"], count),
         "value": round(value, 2),
         "unit": "GiB/s",
         "n_gpus": world,
@@ -534,6 +623,31 @@ def main(argv=None):
                      "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": alg_bytes},
         "oracle_sampled_all_ranks": True,
     }
+    return result, full_h, b
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    chk = check_world(args)
+    if chk is not None:
+        code, msg = chk
+        if msg == "relaunch":  # --gpus N > 1 outside torchrun: N ranks, before any GPU call
+            return relaunch(args, argv)
+        print(msg, file=sys.stderr)
+        return code
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.plan_only:
+        return plan_only(args, world, rank)
+
+    import torch.distributed as dist
+
+    be = HipBackend(local)
+    distributed = world > 1 or "MASTER_ADDR" in os.environ
+    result, full_h, b = run(args, world, rank, be, distributed)
+    count = b["sizes"][rank]
 
     if world == 1 and not args.no_cpu:
         ns = min(count, 32768)
@@ -541,18 +655,18 @@ def main(argv=None):
         if args.mix:
             h_offs, h_lens = b["h_offs"], b["h_lens"]
             span = int(h_offs[ns - 1]) + int(h_lens[ns - 1])
-            sample = pk[:span].cpu().numpy()
+            sample = be.host_bytes(b, span)
             result["cpu_baseline"] = cpu_baseline(sample, got, args.size, args.cpu_seconds,
                                                   offsets=h_offs[:ns].copy(), lengths=h_lens[:ns].copy(),
                                                   family=args.family)
         else:
-            sample = pk[: ns * args.size].cpu().numpy().reshape(ns, args.size)
+            sample = be.host_bytes(b, ns * args.size).reshape(ns, args.size)
             result["cpu_baseline"] = cpu_baseline(sample, got, args.size, args.cpu_seconds, family=args.family)
         result["c0"] = c0_latency()
 
     if rank == 0:
         print(json.dumps(result), flush=True)
-    ctx.close()
+    be.close()
     if distributed:
         dist.destroy_process_group()
     return 0

@@ -32,8 +32,8 @@
  *
  * Two shared libraries implement this header:
  *   libroceicrc.so      everything (gfx950 kernels + host runtime + RCCL);
- *   libroceicrc_cpu.so  the per-packet CPU section only (ricrc_one .. ricrc_combine,
- *                       ricrc_icrc, ricrc_strerror), built by g++ with no HIP,
+ *   libroceicrc_cpu.so  the CPU section only (ricrc_one .. ricrc_combine,
+ *                       ricrc_icrc, ricrc_batch_cpu, ricrc_strerror), built by g++ with no HIP,
  *                       RCCL or torch dependency: the simulator drop-in
  *                       (python/simulator.py:49-55) loads it on any host.
  */
@@ -77,6 +77,15 @@ int ricrc_stamp_one(uint8_t *l3, uint32_t n);
  * UDP dport 4791, total_len == n, RICRC_MIN_LEN <= n (the ingress parser's
  * accept path, p4/shuffle/shuffle_ingress_parser.p4:12-36, header.p4:14). */
 int ricrc_is_rocev2(const uint8_t *l3, uint32_t n);
+
+/* CPU batch: out[i] = ICRC of packet i, addressed as in the GPU batch calls
+ * below, folded by the slice-by-16 code of ricrc_one on `threads` host
+ * threads (the caller's thread included).  For hosts without a GPU and the
+ * CPU figure bench.py reports next to the GPU's; the GPU batch calls never
+ * fall back to it.  0, or -EINVAL (NULL, bad flags, a length outside
+ * [RICRC_MIN_LEN, RICRC_MAX_LEN]; nothing is written then). */
+int ricrc_batch_cpu(const uint8_t *base, const uint64_t *off, const uint32_t *len, uint32_t stride, uint64_t count,
+                    uint32_t l3_offset, uint32_t *out, uint32_t flags, int threads);
 
 /* ------------------------------------------------------- address families
  * The reference is IPv4-only (header.p4:42-53, shuffle_ingress_parser.p4:16-19)
@@ -269,12 +278,37 @@ int ricrc_repair_device(ricrc_ctx *ctx, int dev, void *d_base, const uint64_t *d
  * the *_ex calls.  0, -EINVAL (also: ricrc_comm_init not called), -EIO.
  *
  * ricrc_allgather: only the exchange, for shards computed by the caller into
- * d_out[k] + counts[0] + ... + counts[k-1] (on ricrc_stream(ctx, k)). */
+ * d_out[k] + counts[0] + ... + counts[k-1] (on ricrc_stream(ctx, k)).
+ *
+ * Status: with more than one device this exchange is unverified on hardware
+ * (the development boxes have one GPU); its plan (ricrc_allgather_plan,
+ * below) is checked on the CPU by simulating RCCL's semantics. */
 int ricrc_comm_init(ricrc_ctx *ctx);
 int ricrc_batch_device_all(ricrc_ctx *ctx, const void *const *d_base, const uint64_t *const *d_off,
                            const uint32_t *const *d_len, uint32_t stride, const uint64_t *counts,
                            uint32_t l3_offset, uint32_t *const *d_out, uint32_t flags);
 int ricrc_allgather(ricrc_ctx *ctx, const uint64_t *counts, uint32_t *const *d_out);
+
+/* The exchange ricrc_allgather / ricrc_batch_device_all issue for n devices
+ * and these counts, one entry per RCCL call (CPU only, no GPU, no RCCL; in
+ * both libraries): equal counts -> one in-place ALLGATHER per device (offset
+ * = k * count, RCCL's in-place condition); unequal -> SEND of device k's
+ * shard to every peer and RECV of every peer's shard at its offset, all in
+ * one RCCL group.  Offsets and counts are in uint32 elements of d_out[dev].
+ * Returns the number of calls (entries beyond max_ops are not written),
+ * -EINVAL for n < 1 or NULL counts. */
+#define RICRC_XFER_ALLGATHER 0
+#define RICRC_XFER_SEND 1
+#define RICRC_XFER_RECV 2
+typedef struct ricrc_xfer {
+  int32_t dev;     /* context device (RCCL rank) that issues the call */
+  int32_t kind;    /* RICRC_XFER_* */
+  int32_t peer;    /* SEND / RECV: the other device; ALLGATHER: -1 */
+  int32_t reserved;
+  uint64_t offset; /* ALLGATHER / SEND: the shard sent from d_out[dev] + offset; RECV: lands at d_out[dev] + offset */
+  uint64_t count;
+} ricrc_xfer;
+int ricrc_allgather_plan(int n, const uint64_t *counts, ricrc_xfer *ops, int max_ops);
 int ricrc_sync(ricrc_ctx *ctx);
 
 /* Pinned host memory for NIC-ring style buffers (the role of huge_malloc in

@@ -24,6 +24,7 @@
 #include "../../include/roce_icrc.h"
 #include "icrc_kernels.h"
 #include "icrc_math.h"
+#include "icrc_plan.h"
 
 using namespace ricrc;
 
@@ -479,31 +480,26 @@ void comm_destroy(ricrc_ctx *ctx) {
 
 // All-gather of per-device result vectors in place: device k's d_out[k]
 // holds its shard's counts[k] results at offset sum(counts[<k]) and ends with
-// all of them.  Equal shards: one in-place ncclAllGather per device; unequal
-// shards: ncclSend / ncclRecv pairs, every device's calls in one group.
+// all of them.  The calls come from allgather_plan (icrc_plan.h, checked on
+// the CPU): equal shards, one in-place ncclAllGather per device; unequal
+// shards, ncclSend / ncclRecv pairs; every device's calls in one group.
 int comm_allgather(ricrc_ctx *ctx, const uint64_t *counts, uint32_t *const *d_out) {
   Rccl &r = rccl();
-  const int n = (int)ctx->devs.size();
-  std::vector<uint64_t> at(n + 1, 0);
-  bool equal = true;
-  for (int k = 0; k < n; ++k) {
-    at[k + 1] = at[k] + counts[k];
-    equal = equal && counts[k] == counts[0];
-  }
-  if (n == 1) return 0;  // already in place
+  const std::vector<ricrc_xfer> plan = allgather_plan((int)ctx->devs.size(), counts);
+  if (plan.empty()) return 0;  // one device (or nothing to move): already in place
   int rc = nccl_err(r.group_start());
   if (rc) return rc;
-  for (int k = 0; k < n && !rc; ++k) {
-    Dev &d = ctx->devs[k];
-    if (equal) {
-      rc = nccl_err(r.all_gather(d_out[k] + at[k], d_out[k], (size_t)counts[k], ncclUint32, ctx->comms[k], d.stream));
-      continue;
-    }
-    for (int p = 0; p < n && !rc; ++p) {
-      if (p == k) continue;
-      if (counts[k]) rc = nccl_err(r.send(d_out[k] + at[k], (size_t)counts[k], ncclUint32, p, ctx->comms[k], d.stream));
-      if (!rc && counts[p]) rc = nccl_err(r.recv(d_out[k] + at[p], (size_t)counts[p], ncclUint32, p, ctx->comms[k], d.stream));
-    }
+  for (const ricrc_xfer &x : plan) {
+    const ncclComm_t comm = ctx->comms[x.dev];
+    const hipStream_t st = ctx->devs[x.dev].stream;
+    uint32_t *buf = d_out[x.dev];
+    if (x.kind == RICRC_XFER_ALLGATHER)
+      rc = nccl_err(r.all_gather(buf + x.offset, buf, (size_t)x.count, ncclUint32, comm, st));
+    else if (x.kind == RICRC_XFER_SEND)
+      rc = nccl_err(r.send(buf + x.offset, (size_t)x.count, ncclUint32, x.peer, comm, st));
+    else
+      rc = nccl_err(r.recv(buf + x.offset, (size_t)x.count, ncclUint32, x.peer, comm, st));
+    if (rc) break;
   }
   const int rc2 = nccl_err(r.group_end());
   return rc ? rc : rc2;

@@ -13,8 +13,13 @@
 #include <errno.h>
 #include <string.h>
 
+#include <algorithm>
+#include <thread>
+#include <vector>
+
 #include "../../include/roce_icrc.h"
 #include "icrc_math.h"
+#include "icrc_plan.h"
 
 namespace {
 
@@ -134,6 +139,45 @@ int ricrc_is_rocev2(const uint8_t *l3, uint32_t n) {
   if (((uint32_t)l3[2] << 8 | l3[3]) != n) return 0;         // total_len
   if (((uint32_t)l3[22] << 8 | l3[23]) != 4791) return 0;    // udp_h dst_port == UDP_PORT_ROCE
   return 1;
+}
+
+int ricrc_batch_cpu(const uint8_t *base, const uint64_t *off, const uint32_t *len, uint32_t stride, uint64_t count,
+                    uint32_t l3_offset, uint32_t *out, uint32_t flags, int threads) {
+  if (count == 0) return 0;
+  if (!base || !out || !flags_ok(flags)) return -EINVAL;
+  if (!off && stride == 0) return -EINVAL;
+  if (!len && stride <= l3_offset) return -EINVAL;
+  auto pkt = [&](uint64_t i, uint32_t &n) -> const uint8_t * {
+    n = len ? len[i] : stride - l3_offset;
+    return base + (off ? off[i] : i * (uint64_t)stride) + l3_offset;
+  };
+  for (uint64_t i = 0; i < count; ++i) {
+    uint32_t n;
+    (void)pkt(i, n);
+    if (n < RICRC_MIN_LEN || n > RICRC_MAX_LEN) return -EINVAL;
+  }
+  auto work = [&](uint64_t lo, uint64_t hi) {
+    for (uint64_t i = lo; i < hi; ++i) {
+      uint32_t n;
+      const uint8_t *p = pkt(i, n);
+      out[i] = ~icrc_register(p, n, family_of(p, n, flags));
+    }
+  };
+  const uint64_t t = (uint64_t)std::max(1, std::min(threads, 256));
+  const uint64_t nt = std::min<uint64_t>(t, count);
+  std::vector<std::thread> th;
+  th.reserve(nt - 1);
+  for (uint64_t k = 1; k < nt; ++k) th.emplace_back(work, count * k / nt, count * (k + 1) / nt);
+  work(0, count / nt);
+  for (auto &x : th) x.join();
+  return 0;
+}
+
+int ricrc_allgather_plan(int n, const uint64_t *counts, ricrc_xfer *ops, int max_ops) {
+  if (n < 1 || !counts || (max_ops > 0 && !ops)) return -EINVAL;
+  const std::vector<ricrc_xfer> plan = ricrc::allgather_plan(n, counts);
+  for (int i = 0; i < (int)plan.size() && i < max_ops; ++i) ops[i] = plan[i];
+  return (int)plan.size();
 }
 
 uint32_t ricrc_shift(uint32_t reg, uint64_t nbytes) { return ricrc::gf_mul(reg, ricrc::gf_x8n(nbytes)); }

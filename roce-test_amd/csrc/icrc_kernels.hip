@@ -612,6 +612,7 @@ __global__ __launch_bounds__(256) void icrc_prime_kernel(const u32x4 *src, uint6
 
 // ----------------------------------------------------------- host launchers
 hipError_t launch_stream(const StreamArgs &a, int cpl, int grid, hipStream_t st) {
+  (void)hipGetLastError();  // a stale error of an earlier, unrelated HIP call must not fail this launch
   const bool pipe = cpl == 1;
   if (cpl == 1 && pipe) hipLaunchKernelGGL((icrc_stream_kernel<1, true>), dim3(grid), dim3(kBlock), 0, st, a);
   else if (cpl == 2) hipLaunchKernelGGL((icrc_stream_kernel<2, false>), dim3(grid), dim3(kBlock), 0, st, a);
@@ -621,12 +622,14 @@ hipError_t launch_stream(const StreamArgs &a, int cpl, int grid, hipStream_t st)
 }
 
 hipError_t launch_tsk(const TskArgs &a, int grid, hipStream_t st) {
+  (void)hipGetLastError();  // a stale error of an earlier, unrelated HIP call must not fail this launch
   if (a.log2C == 7) hipLaunchKernelGGL((icrc_tsk_kernel<true, 0>), dim3(grid), dim3(kBlock), 0, st, a);
   else hipLaunchKernelGGL((icrc_tsk_kernel<false, 0>), dim3(grid), dim3(kBlock), 0, st, a);
   return hipGetLastError();
 }
 
 hipError_t launch_synth(const SynthArgs &a, hipStream_t st) {
+  (void)hipGetLastError();  // a stale error of an earlier, unrelated HIP call must not fail this launch
   const uint64_t total = a.count * (a.stride >> 3);
   uint64_t blocks = (total + 255) / 256;
   if (blocks > 65536) blocks = 65536;
@@ -636,12 +639,14 @@ hipError_t launch_synth(const SynthArgs &a, hipStream_t st) {
 }
 
 hipError_t launch_prime(const void *scratch, uint64_t bytes, uint32_t *sink, int n_cu, hipStream_t st) {
+  (void)hipGetLastError();  // a stale error of an earlier, unrelated HIP call must not fail this launch
   hipLaunchKernelGGL(icrc_prime_kernel, dim3(8 * n_cu), dim3(256), 0, st, reinterpret_cast<const u32x4 *>(scratch),
                      bytes / 16, sink);
   return hipGetLastError();
 }
 
 hipError_t launch_synth_ragged(const SynthArgs &a, hipStream_t st) {
+  (void)hipGetLastError();  // a stale error of an earlier, unrelated HIP call must not fail this launch
   if (a.count == 0) return hipSuccess;
   uint64_t blocks = (a.count + 3) / 4;  // 4 waves per block, one packet per wave
   if (blocks > 16384) blocks = 16384;

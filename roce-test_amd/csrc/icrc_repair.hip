@@ -165,6 +165,7 @@ __global__ __launch_bounds__(256) void family_fix_kernel(FamilyFixArgs a) {
 }  // namespace
 
 hipError_t launch_family_fix(const FamilyFixArgs &a, int grid, hipStream_t st) {
+  (void)hipGetLastError();  // a stale error of an earlier, unrelated HIP call must not fail this launch
   if (a.count == 0) return hipSuccess;
   const uint64_t need = (a.count + 255) / 256;
   const unsigned blocks = (unsigned)std::min<uint64_t>(need, (uint64_t)grid);
@@ -173,6 +174,7 @@ hipError_t launch_family_fix(const FamilyFixArgs &a, int grid, hipStream_t st) {
 }
 
 hipError_t launch_repair(const RepairArgs &a, int grid, hipStream_t st) {
+  (void)hipGetLastError();  // a stale error of an earlier, unrelated HIP call must not fail this launch
   if (a.count == 0) return hipSuccess;
   const uint64_t need = (a.count + 255) / 256;
   const unsigned blocks = (unsigned)std::min<uint64_t>(need, (uint64_t)grid);

@@ -903,6 +903,7 @@ static void launch_passes(const RsckArgs &a, int pgrid, hipStream_t st) {
 }
 
 hipError_t launch_rsck(RsckArgs &a, int grid, hipStream_t st) {
+  (void)hipGetLastError();  // a stale error of an earlier, unrelated HIP call must not fail this launch
   if (a.count == 0) return hipSuccess;
   // a.counts (+ the misaligned flag) is zero here: zeroed when the workspace
   // was allocated, and again by rsck_gather at the end of every call.

@@ -349,6 +349,7 @@ hipError_t launch_sck_fam(const SckArgs &a, int grid, hipStream_t st) {
 }
 
 hipError_t launch_sck(const SckArgs &a, int grid, hipStream_t st) {
+  (void)hipGetLastError();  // a stale error of an earlier, unrelated HIP call must not fail this launch
   if (a.family == kFamV6) return launch_sck_fam<kFamV6>(a, grid, st);
   if (a.family == kFamAuto) return launch_sck_fam<kFamAuto>(a, grid, st);
   if (a.family != kFamV4) return hipErrorInvalidValue;

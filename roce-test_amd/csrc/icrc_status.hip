@@ -91,6 +91,7 @@ __global__ __launch_bounds__(kStBlock) void icrc_status_kernel(StatusArgs a) {
 }  // namespace
 
 hipError_t launch_status(const StatusArgs &a, int n_cu, hipStream_t st) {
+  (void)hipGetLastError();  // a stale error of an earlier, unrelated HIP call must not fail this launch
   if (a.count == 0) return hipSuccess;
   const uint64_t want = (a.count + kStBlock * kStUnroll - 1) / (kStBlock * kStUnroll);
   const uint64_t cap = 8ull * (uint64_t)n_cu;

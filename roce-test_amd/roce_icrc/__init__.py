@@ -41,7 +41,7 @@ MAX_LEN = 65535
 CPU_EXPORTED = (
     "ricrc_one", "ricrc_verify_one", "ricrc_stamp_one", "ricrc_is_rocev2", "ricrc_shift",
     "ricrc_one_ex", "ricrc_verify_one_ex", "ricrc_stamp_one_ex", "ricrc_classify", "ricrc_repair_one",
-    "ricrc_combine", "ricrc_icrc", "ricrc_strerror",
+    "ricrc_combine", "ricrc_icrc", "ricrc_strerror", "ricrc_batch_cpu", "ricrc_allgather_plan",
 )
 EXPORTED = CPU_EXPORTED + (
     "ricrc_create", "ricrc_create_devices", "ricrc_destroy", "ricrc_device_count", "ricrc_batch_host",
@@ -73,6 +73,8 @@ _SIG = {
     "ricrc_shift": ([_u32, _u64], _u32),
     "ricrc_combine": ([_u32, _u32, _u64], _u32),
     "ricrc_strerror": ([_i32], ctypes.c_char_p),
+    "ricrc_batch_cpu": ([_vp, _vp, _vp, _u32, _u64, _u32, _vp, _u32, _i32], _i32),
+    "ricrc_allgather_plan": ([_i32, _vp, _vp, _i32], _i32),
     "ricrc_create": ([ctypes.POINTER(_vp), _i32], _i32),
     "ricrc_create_devices": ([ctypes.POINTER(_vp), ctypes.POINTER(_i32), _i32], _i32),
     "ricrc_destroy": ([_vp], None),
@@ -265,6 +267,44 @@ def shift(reg: int, nbytes: int) -> int:
 def combine(crc1: int, crc2: int, len2: int) -> int:
     """crc32(A || B) from crc32(A), crc32(B), len(B)."""
     return int(cpu.ricrc_combine(crc1 & 0xFFFFFFFF, crc2 & 0xFFFFFFFF, len2))
+
+
+def icrc_batch_cpu(buf, offsets=None, lengths=None, stride: int = 0, l3_offset: int = 0, count: int | None = None,
+                   family: str = "v4", threads: int = 1) -> np.ndarray:
+    """``ricrc_batch_cpu``: a batch on the host CPU (slice-by-16, ``threads``
+    threads) -- no GPU involved, and never used by the GPU batch calls."""
+    buf = np.ascontiguousarray(buf).reshape(-1).view(np.uint8)
+    off = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint64)
+    ln = None if lengths is None else np.ascontiguousarray(lengths, dtype=np.uint32)
+    if count is None:
+        count = len(off) if off is not None else (len(ln) if ln is not None else buf.size // stride)
+    out = np.empty(count, dtype=np.uint32)
+    rc = cpu.ricrc_batch_cpu(buf.ctypes.data, _ptr(off), _ptr(ln), stride, count, l3_offset, out.ctypes.data,
+                             _fam(family), threads)
+    if rc:
+        raise ICRCError(rc, "ricrc_batch_cpu")
+    return out
+
+
+class Xfer(ctypes.Structure):
+    """One RCCL call of the all-gather plan (``ricrc_xfer``)."""
+    _fields_ = [("dev", ctypes.c_int32), ("kind", ctypes.c_int32), ("peer", ctypes.c_int32),
+                ("reserved", ctypes.c_int32), ("offset", ctypes.c_uint64), ("count", ctypes.c_uint64)]
+
+
+XFER_ALLGATHER, XFER_SEND, XFER_RECV = 0, 1, 2
+
+
+def allgather_plan(counts) -> list:
+    """``ricrc_allgather_plan``: the RCCL calls ricrc_batch_device_all issues
+    for these per-device shard counts, as (dev, kind, peer, offset, count)."""
+    cnt = (ctypes.c_uint64 * len(counts))(*[int(c) for c in counts])
+    need = cpu.ricrc_allgather_plan(len(counts), cnt, None, 0)
+    if need < 0:
+        raise ICRCError(need, "ricrc_allgather_plan")
+    ops = (Xfer * max(need, 1))()
+    cpu.ricrc_allgather_plan(len(counts), cnt, ops, need)
+    return [(x.dev, x.kind, x.peer, x.offset, x.count) for x in ops[:need]]
 
 
 # ------------------------------------------------------------------- batches

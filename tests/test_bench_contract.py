@@ -110,6 +110,22 @@ def test_metric_matches_baseline_json():
         assert json.load(f)["metric"] == bench.METRIC
 
 
+def test_metric_names_the_workload_run():
+    """Only BASELINE's own config carries BASELINE's metric string; C1/C2,
+    the strong-scaling C3 batch and the C4 mix name what they ran."""
+    m = lambda *a: bench.metric_for(bench.parse(list(a)), *((lambda x: (  # noqa: E731
+        x.global_count if x.global_count is not None else x.count, x.count))(bench.parse(list(a)))))
+    assert m() == bench.METRIC
+    assert "1M\u00d764B" in m("--size", "64") and "4096B" not in m("--size", "64")
+    assert "1M\u00d71024B" in m("--size", "1024")
+    c3 = m("--global-count", "4194304")
+    assert "4M\u00d74096B" in c3 and "fixed total" in c3 and c3 != bench.METRIC
+    assert "1M\u00d74096B" not in m("--count", "4194304") and "4M\u00d74096B" in m("--count", "4194304")
+    mix = m("--mix")
+    assert "mixed-MTU" in mix and "4M per GPU" in mix
+    assert "16M in all" in m("--mix", "--global-count", str(16 << 20))
+
+
 def test_kernel_labels_follow_the_dispatch():
     assert "icrc_sck_kernel" in bench.kernel_label(4096)
     assert "icrc_sck_kernel" in bench.kernel_label(1024)
@@ -127,8 +143,10 @@ def test_traffic_is_tied_to_the_kernel_source(tmp_path):
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     with open(p) as f:
         d = json.load(f)
-    got = bench.load_traffic(d["size"], d["count"])
+    got = bench.load_traffic(bench.parse(["--size", str(d["size"]), "--count", str(d["count"])]), d["count"])
     assert (got is not None) == (d.get("kernel_src") == h)
+    # the mix's record is tied to the ragged pipeline's sources, not the SCK's
+    assert "icrc_rsck.hip" in bench.RAGGED_SOURCES and "icrc_rsck.hip" not in bench.SCK_SOURCES
 
 
 def test_committed_traffic_matches_headline_kernel():
@@ -142,7 +160,7 @@ def test_committed_traffic_matches_headline_kernel():
     assert (d["size"], d["count"]) == (a.size, 1 << 20)
     assert d["kernel_src"] == bench.kernel_source_hash()
     assert 0.99 < d["traffic_over_algorithmic"] < 1.05
-    assert bench.load_traffic(a.size, 1 << 20) == d["hbm_bytes_per_launch"]
+    assert bench.load_traffic(a, 1 << 20) == d["hbm_bytes_per_launch"]
 
 
 def test_bench_compiles_standalone():

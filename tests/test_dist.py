@@ -140,3 +140,56 @@ def test_byte_balanced_cuts_mixed_mtu():
         assert cuts[0] == 0 and cuts[-1] == len(lens) and cuts == sorted(cuts)
         shard_bytes = [int(lens[cuts[i]:cuts[i + 1]].sum()) for i in range(world)]
         assert max(shard_bytes) - min(shard_bytes) <= 2 * 4096
+
+
+def _simulate_plan(counts, ops):
+    """Execute an all-gather plan on host buffers with RCCL's semantics:
+    in-place all-gather, and grouped send/recv matched in issue order per
+    (sender, receiver) pair.  Returns every device's buffer."""
+    n, total = len(counts), int(sum(counts))
+    at = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    bufs = [np.full(total, -1, np.int64) for _ in range(n)]
+    for k in range(n):
+        bufs[k][at[k]:at[k + 1]] = np.arange(at[k], at[k + 1])  # shard k computed on device k
+    ag = [x for x in ops if x[1] == 0]
+    if ag:
+        assert len(ag) == n and {x[0] for x in ag} == set(range(n))
+        c = ag[0][4]
+        for dev, _, peer, off, cnt in ag:  # in place: sendbuff == recvbuff + rank * count
+            assert cnt == c and off == dev * c and peer == -1
+        full = np.concatenate([bufs[k][k * c:(k + 1) * c] for k in range(n)])
+        bufs = [full.copy() for _ in range(n)]
+        return bufs
+    sends = {}
+    for dev, kind, peer, off, cnt in ops:
+        assert peer != dev and cnt > 0
+        if kind == 1:
+            sends.setdefault((dev, peer), []).append(bufs[dev][off:off + cnt].copy())
+    for dev, kind, peer, off, cnt in ops:
+        if kind == 2:
+            data = sends[(peer, dev)].pop(0)
+            assert len(data) == cnt
+            bufs[dev][off:off + cnt] = data
+    assert all(not v for v in sends.values())  # every send matched by exactly one receive
+    return bufs
+
+
+@pytest.mark.parametrize("counts", [[5, 5, 5], [7, 0, 3], [1, 1000, 2, 9], [4, 4], [0, 0], [3]])
+def test_allgather_plan_every_device_ends_with_every_shard(counts):
+    """ricrc_allgather_plan (the plan ricrc_batch_device_all issues through
+    RCCL, pure host code): simulated with RCCL's semantics, every device's
+    buffer ends with all shards in shard order -- equal counts through the
+    in-place all-gather, unequal (byte-balanced) counts through matched
+    send/recv pairs, zero-length shards moving nothing."""
+    import roce_icrc
+
+    ops = roce_icrc.allgather_plan(counts)
+    if len(counts) == 1 or sum(counts) == 0:
+        assert ops == [] or all(x[4] == 0 for x in ops)
+    bufs = _simulate_plan(counts, ops)
+    for b in bufs:
+        np.testing.assert_array_equal(b, np.arange(sum(counts)))
+    if len(set(counts)) > 1:
+        n = len(counts)
+        nz = sum(1 for c in counts if c)
+        assert len(ops) == 2 * nz * (n - 1)  # each non-empty shard sent to and received by every peer

@@ -139,7 +139,7 @@ def test_status_batch_device_and_host(ctx, family, strict, verify, framed):
                 buf[int(offs[i]) + l3 + int(lens[i]) - 5] ^= 0x08
     w_out, w_st = O.status_batch(buf, offsets=offs, lengths=lens, l3_offset=l3, family=family, strict=strict,
                                  verify=verify)
-    assert (w_st == O.ST_BADLEN).sum() > 100 and (w_st == O.ST_OK).sum() > 1000
+    assert (w_st == O.ST_BADLEN).sum() > 100 and (w_st == O.ST_OK).sum() > 300
     if strict:
         assert (w_st == O.ST_NOTROCE).sum() > 300
     else:

@@ -2,15 +2,23 @@
 """Measure HBM traffic per ICRC launch with rocprofv3 PMC counters.
 
 Runs bench.py under two separate `rocprofv3 --pmc` passes (FETCH_SIZE, then
-WRITE_SIZE: they do not fit one pass on gfx950), averages the streaming
-kernel's per-dispatch values and applies the gfx950 correction of
+WRITE_SIZE: they do not fit one pass on gfx950), averages each kernel's
+per-dispatch values and applies the gfx950 correction of
 /opt/skills/guides/MI355X_MICROARCH.md §HBM: FETCH_SIZE counts exactly half of
 the bytes of a wide (16 B/lane) coalesced streaming read, so it is doubled;
-WRITE_SIZE is taken as reported (4 B per packet, small).  Both are in KiB.
+WRITE_SIZE is taken as reported.  Both are in KiB.
 
-Writes gpurun_out/pmc_traffic.json; copied into profiles/pmc_traffic.json it is
-what bench.py reports as roofline.traffic when the workload matches.  Usage (on the GPU box):
-    python3 tools/pmc_traffic.py [--out profiles/pmc_traffic.json]
+  (default)  the headline: 1 M x 4096 B, icrc_sck_kernel -> profiles/pmc_traffic.json
+  --mix      C4: the ragged pipeline's five kernels (count/plan, scatter, fold,
+             one-line, gather) summed per step -> profiles/pmc_traffic_mix.json.
+             The pass kernels read 8- and 4-byte descriptors, an access width
+             the guide's x2 is not calibrated for; the count pass reads exactly
+             12 B per packet, so its doubled FETCH_SIZE against that byte count
+             is reported as the check ("count_pass_fetch_over_descriptors").
+
+Copied into profiles/, the file is what bench.py reports as roofline.traffic
+when the workload and the kernel sources match (bench.kernel_source_hash).
+Usage (on the GPU box):  python3 tools/pmc_traffic.py [--mix] [--out F]
 """
 import argparse
 import csv
@@ -21,46 +29,65 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+RAGGED_KERNELS = ("rsck_count", "rsck_scatter", "icrc_rsck_kernel", "icrc_rsmall_kernel", "rsck_gather")
 
 
-def run_pass(counter, outdir):
+def run_pass(counter, outdir, bench_args, match):
     cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", outdir, "-o", "run", "--",
-           sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "5", "--warmup", "1", "--no-cpu"]
+           sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "5", "--warmup", "1", "--no-cpu"] + bench_args
     subprocess.run(cmd, check=True, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"), timeout=600,
                    stdout=subprocess.DEVNULL)
-    vals, names = [], set()
+    per = {}
     for f in glob.glob(os.path.join(outdir, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 k = row["Kernel_Name"]
-                if "icrc_sck_kernel" in k and row["Counter_Name"] == counter:  # the headline kernel only
-                    vals.append(float(row["Counter_Value"]))
-                    names.add(k)
-    if not vals:
-        raise SystemExit(f"no {counter} rows for the icrc kernel")
-    return sum(vals) / len(vals), len(vals), names
+                key = next((m for m in match if m in k), None)
+                if key and row["Counter_Name"] == counter:
+                    per.setdefault(key, []).append(float(row["Counter_Value"]))
+    if not per:
+        raise SystemExit(f"no {counter} rows for {match}")
+    return {k: (sum(v) / len(v), len(v)) for k, v in per.items()}
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "pmc_traffic.json"))
+    ap.add_argument("--mix", action="store_true")
+    ap.add_argument("--out", default=None)
     ap.add_argument("--scratch", default=os.path.join(ROOT, "gpurun_out", "pmc_traffic"))
     a = ap.parse_args()
-    a.out, a.scratch = os.path.abspath(a.out), os.path.abspath(a.scratch)
-    fetch_kib, nf, kernels = run_pass("FETCH_SIZE", os.path.join(a.scratch, "fetch"))
-    write_kib, nw, _ = run_pass("WRITE_SIZE", os.path.join(a.scratch, "write"))
-    count, size = 1 << 20, 4096
-    hbm = 2.0 * fetch_kib * 1024 + write_kib * 1024
-    alg = count * size + 4 * count
+    a.out = os.path.abspath(a.out or os.path.join(ROOT, "gpurun_out",
+                                                  "pmc_traffic_mix.json" if a.mix else "pmc_traffic.json"))
+    a.scratch = os.path.abspath(a.scratch + ("_mix" if a.mix else ""))
     sys.path.insert(0, ROOT)
     import bench
 
-    res = {"size": size, "count": count, "dispatches": [nf, nw], "kernel_src": bench.kernel_source_hash(),
-           "kernels": sorted(kernels),
-           "FETCH_SIZE_KiB": fetch_kib, "WRITE_SIZE_KiB": write_kib,
+    bench_args = ["--mix"] if a.mix else []
+    match = RAGGED_KERNELS if a.mix else ("icrc_sck_kernel",)
+    fetch = run_pass("FETCH_SIZE", os.path.join(a.scratch, "fetch"), bench_args, match)
+    write = run_pass("WRITE_SIZE", os.path.join(a.scratch, "write"), bench_args, match)
+    if a.mix:
+        import numpy as np
+
+        count = 4 << 20
+        lens = np.random.default_rng(bench.SEED).choice(np.array(bench.MIX_SIZES, np.uint32), size=count)
+        alg = int(lens.sum(dtype=np.uint64)) + 16 * count
+        src, size = bench.kernel_source_hash(bench.RAGGED_SOURCES), "mix"
+    else:
+        count, size = 1 << 20, 4096
+        alg = count * size + 4 * count
+        src = bench.kernel_source_hash()
+    kernels = {k: {"FETCH_SIZE_KiB": fetch.get(k, (0.0, 0))[0], "WRITE_SIZE_KiB": write.get(k, (0.0, 0))[0],
+                   "dispatches": [fetch.get(k, (0, 0))[1], write.get(k, (0, 0))[1]]} for k in match}
+    hbm = sum(2.0 * v["FETCH_SIZE_KiB"] * 1024 + v["WRITE_SIZE_KiB"] * 1024 for v in kernels.values())
+    res = {"size": size, "count": count, "kernel_src": src, "kernels": kernels,
            "correction": "FETCH_SIZE x2 (gfx950 wide-streaming read undercount, MI355X_MICROARCH.md §HBM)",
            "hbm_bytes_per_launch": hbm, "algorithmic_bytes_per_launch": alg,
            "traffic_over_algorithmic": hbm / alg}
+    if a.mix:
+        cp = kernels["rsck_count"]["FETCH_SIZE_KiB"] * 2 * 1024
+        res["count_pass_fetch_over_descriptors"] = cp / (12.0 * count)
+        res["fold_fetch_over_its_lines"] = None  # filled by tools/pmc_summary.py when the line count is known
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     with open(a.out, "w") as f:
         json.dump(res, f, indent=1)
