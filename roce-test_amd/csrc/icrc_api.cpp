@@ -42,6 +42,7 @@ constexpr uint64_t kRsChunk = 1ull << 30;  // the ragged pipeline's positions ar
 struct Knobs {
   bool no_sck = false;     // RICRC_NO_SCK: fixed 1/2/4 KiB batches take the transposed kernel
   bool no_tsk = false;     // RICRC_NO_TSK: ... and 128-512 B batches the direct streaming kernel
+  bool no_quad = false;    // RICRC_NO_QUAD: 64 B batches take the direct streaming kernel
   int sck_grid = 0;        // RICRC_SCK_GRID: cap the strided-chain grid (tests: many groups per wave)
   int rsck_grid = 0;       // RICRC_RSCK_GRID: cap the ragged fold grid (tests)
   uint32_t gcost = 0;      // RICRC_RS_GCOST: the ragged fold's per-group cost, quarter lines (0: kRsGroupCost)
@@ -335,6 +336,17 @@ int launch_batch_v4(Dev &d, const uint8_t *base, const uint64_t *off, const uint
       return hip_err(launch_sck(k, sgrid, st));
     }
     const uint32_t M = fixed_len - 4;
+    // Back-to-back 64-byte packets (C1): the quad kernel, coalesced 1 KiB loads.
+    if (fixed_len == 64 && stride == 64 && l3_offset == 0 && (uintptr_t)base % 16 == 0 && !d.knobs.no_quad) {
+      QuadArgs q{};
+      q.base = base;
+      q.count = count;
+      q.out = out;
+      q.verify = verify ? 1u : 0u;
+      const uint64_t steps = (count * 64 + 4095) / 4096;
+      const int qgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)d.n_cu, (steps + 15) / 16));
+      return hip_err(launch_quad(q, qgrid, st));
+    }
     int cpl = 0;
     for (int c : {1, 2, 4})
       if ((M + 64u * c - 1) / (64u * c) <= 64) {
@@ -555,6 +567,7 @@ Knobs read_knobs() {
   };
   k.no_sck = getenv("RICRC_NO_SCK") != nullptr;
   k.no_tsk = getenv("RICRC_NO_TSK") != nullptr;
+  k.no_quad = getenv("RICRC_NO_QUAD") != nullptr;
   k.sck_grid = (int)std::max(0L, num("RICRC_SCK_GRID", 0));
   k.rsck_grid = (int)std::max(0L, num("RICRC_RSCK_GRID", 0));
   k.gcost = (uint32_t)std::max(0L, num("RICRC_RS_GCOST", 0));

@@ -33,14 +33,15 @@ __device__ __forceinline__ uint32_t or_xor(uint32_t a, uint32_t b, uint32_t c) {
 __device__ __forceinline__ uint32_t table_entry(const SliceTables<4> &tab) {
   return tab.t[threadIdx.x >> 8][threadIdx.x & 255];
 }
-__device__ __forceinline__ void table_store(uint32_t *lds, uint32_t v) {
-  const uint32_t t = threadIdx.x >> 8, e = threadIdx.x & 255;
+__device__ __forceinline__ void table_store_at(uint32_t *lds, uint32_t idx, uint32_t v) {  // entry idx & 255 of T_{idx >> 8}
+  const uint32_t t = idx >> 8, e = idx & 255;
   const uint32_t region = t <= 1 ? 1u : 0u, half = (t == 0 || t == 2) ? 1u : 0u;  // T3 T2 | T1 T0
   typedef uint32_t v4 __attribute__((ext_vector_type(4)));
   v4 *dst = reinterpret_cast<v4 *>(lds + ((region << 14) | (e << 6) | (half << 5)));
 #pragma unroll
   for (int k = 0; k < 8; ++k) dst[k] = v4{v, v, v, v};
 }
+__device__ __forceinline__ void table_store(uint32_t *lds, uint32_t v) { table_store_at(lds, threadIdx.x, v); }
 __device__ __forceinline__ void fill_tables(uint32_t *lds, const SliceTables<4> &tab = g_tab) {
   static_assert(kBlock == 1024, "one table entry per thread");
   table_store(lds, table_entry(tab));

@@ -159,6 +159,17 @@ struct FamilyFixArgs {
 };
 hipError_t launch_family_fix(const FamilyFixArgs &a, int grid, hipStream_t st);
 
+// Back-to-back 64-byte packets (C1), 16-byte aligned: the quad kernel
+// (coalesced 1 KiB loads, lane-quad transposes).
+struct QuadArgs {
+  const uint8_t *base;
+  uint64_t count;
+  uint32_t *out;
+  uint32_t verify;
+  uint64_t *stamps;   // diagnostic builds only (tools/microbench); null in the product
+};
+hipError_t launch_quad(const QuadArgs &a, int grid, hipStream_t st);
+
 hipError_t launch_stream(const StreamArgs &a, int cpl, int grid, hipStream_t st);
 hipError_t launch_tsk(const TskArgs &a, int grid, hipStream_t st);
 hipError_t launch_synth(const SynthArgs &a, hipStream_t st);

@@ -496,6 +496,173 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
 }
 
 // =======================================================================
+// Quad kernel: back-to-back 64-byte packets (C1), 16-byte aligned.  The
+// direct kernel above gives each lane a whole packet, so each of its load
+// instructions reads 16 bytes at a 64-byte lane stride: that access pattern
+// alone streams 64 MiB in 21-25 us (all loads in flight), against 12 us for
+// coalesced 1 KiB loads (tools/microbench/c1_probe.hip,
+// profiles/r03/c1_probe.txt).  Here load k of a 4 KiB wave step reads 1 KiB
+// at 1024 k + 16 l, so lane 4 p + c holds 16-byte chunk c of packet 16 k + p;
+// after the step's 4 loads a 4 x 4 transpose inside each lane quad (two
+// rounds of DPP swaps) gives lane 4 p + c all 64 bytes of packet 16 c + p,
+// which it folds as the direct kernel does (15 words, slice-by-4, one chain;
+// the masks and the seed are the same for every lane).  Two steps are folded
+// side by side (F = 2: two independent chains per lane); R steps of loads
+// stay in flight through a register ring (R x 16 VGPRs: R = 4 with F = 2
+// spilled at 1024 threads per workgroup).  The slice-by-4 tables are computed by the
+// workgroup (<= 32 bit steps per thread) instead of loaded, so building them
+// never waits behind the data loads in the memory queue.  Results go to
+// per-wave LDS slots in packet order and leave in one coalesced 1 KiB store
+// per 4 steps.
+// ABL (timing-only, tools/microbench): 64 per-wave s_memrealtime stamps.
+// =======================================================================
+__device__ __forceinline__ uint32_t crc_table_value(uint32_t t) {
+  // entry t & 255 of T_{t >> 8}: (8 + 8 (t >> 8)) bit steps from the byte value
+  uint32_t c = t & 255u;
+  const uint32_t steps = 8u + 8u * (t >> 8);
+  for (uint32_t i = 0; i < steps; ++i) c = (c >> 1) ^ (kPoly & (0u - (c & 1u)));
+  return c;
+}
+
+// Lane quad transpose of 16-byte chunks: on entry lane 4 p + c holds chunk c
+// of the packets in A[0..3] (A[k]: load k); on exit it holds chunks 0..3 of
+// the packet that was in A[c].  swap(v, 1): the value of lane l ^ 1.
+__device__ __forceinline__ uint32_t dpp_swap1(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+}
+__device__ __forceinline__ uint32_t dpp_swap2(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+}
+__device__ __forceinline__ void quad_transpose(u32x4 (&A)[4], uint32_t c) {
+  const bool o1 = (c & 1u) != 0, o2 = (c & 2u) != 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {  // round 1: registers k, k ^ 1 across lanes c, c ^ 1
+    const uint32_t t0 = dpp_swap1(A[0][i]), t1 = dpp_swap1(A[1][i]);
+    const uint32_t t2 = dpp_swap1(A[2][i]), t3 = dpp_swap1(A[3][i]);
+    A[0][i] = o1 ? t1 : A[0][i];
+    A[1][i] = o1 ? A[1][i] : t0;
+    A[2][i] = o1 ? t3 : A[2][i];
+    A[3][i] = o1 ? A[3][i] : t2;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {  // round 2: registers k, k ^ 2 across lanes c, c ^ 2
+    const uint32_t t0 = dpp_swap2(A[0][i]), t1 = dpp_swap2(A[1][i]);
+    const uint32_t t2 = dpp_swap2(A[2][i]), t3 = dpp_swap2(A[3][i]);
+    A[0][i] = o2 ? t2 : A[0][i];
+    A[2][i] = o2 ? A[2][i] : t0;
+    A[1][i] = o2 ? t3 : A[1][i];
+    A[3][i] = o2 ? A[3][i] : t1;
+  }
+}
+
+template <int ABL, int R = 2, int F = 2, int W = kWaves>
+__global__ __launch_bounds__(64 * W) void icrc_quad_kernel(QuadArgs a) {
+  static_assert((F == 1 || F == 2) && R % F == 0 && 4 % R == 0, "ring of R steps, folded F at a time");
+  constexpr uint32_t N = 64;
+  constexpr uint32_t kSlots = 256;         // results per wave per round (4 steps)
+  __shared__ uint32_t lds[kLdsWords + W * kSlots];
+  uint32_t *tab = lds;
+
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t c = lane & 3u;
+  const uint64_t t_start = (ABL & 64) ? __builtin_amdgcn_s_memrealtime() : 0u;
+
+  const uint64_t total = a.count * N;
+  const uint64_t nsteps = (total + 4095u) >> 12;
+  const uint64_t wave = (uint64_t)blockIdx.x * W + wid;
+  const uint64_t nwaves = (uint64_t)gridDim.x * W;
+  const uint64_t per = (nsteps + nwaves - 1) / nwaves;
+  const uint64_t s_begin = wave * per < nsteps ? wave * per : nsteps;
+  const uint64_t s_end = s_begin + per < nsteps ? s_begin + per : nsteps;
+
+  // load k of step s (steps outside the wave's range read zeros)
+  auto load = [&](uint64_t s, uint32_t k) -> u32x4 {
+    const uint64_t b = s << 12;
+    const uint32_t rem = s < s_end ? (uint32_t)(total - b < 4096u ? total - b : 4096u) : 0u;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(a.base + (s < s_end ? b : 0), rem);
+    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 1024u * k + 16u * lane, 0, 2));
+  };
+  u32x4 ring[4 * R];
+#pragma unroll
+  for (int u = 0; u < 4 * R; ++u) {
+    __builtin_amdgcn_sched_barrier(0);
+    ring[u] = load(s_begin + (uint32_t)(u >> 2), (uint32_t)(u & 3));
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (uint32_t t = threadIdx.x; t < 1024u; t += 64u * W) table_store_at(tab, t, crc_table_value(t));
+  __syncthreads();
+
+  const LaneTab lt{(lane & 31) << 2, ((lane & 31) << 2) | 0x10000u};
+  uint32_t *slots = tab + kLdsWords + wid * kSlots;
+  const uint32_t q = 16u * c + (lane >> 2);  // the lane's packet within a step after the transpose
+  const uint32_t vmask = __builtin_amdgcn_readfirstlane(a.verify ? 0xFFFFFFFFu : 0u);
+
+  auto flush = [&](uint64_t s_lo, uint64_t s_hi) {  // the round of steps [s_lo, s_hi)
+    const uint64_t pb = s_lo * 64u;
+    const uint64_t want = (s_hi - s_lo) * 64u;
+    const uint32_t nout = (uint32_t)(pb < a.count ? (a.count - pb < want ? a.count - pb : want) : 0u);
+    const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out + (pb < a.count ? pb : 0), 4u * nout);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the slot writes have landed
+    const u32x4 v = *reinterpret_cast<const u32x4 *>(slots + 4 * lane);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v), ro,
+                                           16u * lane, 0, 0);
+  };
+
+  // Fold steps s .. s + F - 1 (ring slots u ..) side by side; slot of step
+  // s's packet q: (s - round_lo) * 64 + q.  Steps past the wave's range write
+  // slots the flush does not store (no branch here).
+  auto fold = [&](int u, uint64_t s, uint64_t round_lo) {
+    u32x4 A[F][4];
+#pragma unroll
+    for (int f = 0; f < F; ++f)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        A[f][k] = ring[4 * (u + f) + k];
+        ring[4 * (u + f) + k] = load(s + f + R, (uint32_t)k);  // refill: step s + f + R
+      }
+    uint32_t x[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f) {
+      quad_transpose(A[f], c);
+      x[f] = or_xor(A[f][0][0], kMaskW0, kSeed);
+    }
+#pragma unroll
+    for (int w = 1; w < 15; ++w) {  // words 1..14; word 15 is the trailer
+      const uint32_t m = w == 2 ? kMaskW2 : w == 6 ? kMaskW6 : w == 8 ? kMaskW8 : 0u;
+#pragma unroll
+      for (int f = 0; f < F; ++f) x[f] = step4x(tab, lt, x[f], A[f][w >> 2][w & 3] | m);
+    }
+#pragma unroll
+    for (int f = 0; f < F; ++f) {
+      const uint32_t r = ~step4x(tab, lt, x[f], 0u);
+      // verify ? (trailer == ICRC) : ICRC
+      slots[(uint32_t)(s + f - round_lo) * 64u + q] = __builtin_amdgcn_bitop3_b32(vmask, A[f][3][3] == r ? 1u : 0u, r, 0xCA);
+    }
+  };
+
+  // Rounds of 4 steps (256 results, one store); the ring turns R steps at a time.
+  uint64_t round_lo = s_begin;
+  for (uint64_t s0 = s_begin; s0 < s_end; s0 += R) {  // wave-uniform
+#pragma unroll
+    for (int u = 0; u < R; u += F) {
+      __builtin_amdgcn_sched_barrier(0);
+      fold(u, s0 + u, round_lo);
+    }
+    const uint64_t s_hi = s0 + R < s_end ? s0 + R : s_end;
+    if (s_hi == s_end || s_hi - round_lo == 4) {  // wave-uniform: the round is complete
+      flush(round_lo, s_hi);
+      round_lo = s_hi;
+    }
+  }
+  if ((ABL & 64) && lane == 0) {
+    a.stamps[2 * wave] = t_start;
+    a.stamps[2 * wave + 1] = __builtin_amdgcn_s_memrealtime();
+  }
+}
+
+// =======================================================================
 // Synthetic SEND_ONLY generator (bench/tests; restated on the CPU by
 // oracle/icrc_oracle.c:oracle_synth_packet).  One thread per 8-byte block.
 // =======================================================================
@@ -618,6 +785,12 @@ hipError_t launch_stream(const StreamArgs &a, int cpl, int grid, hipStream_t st)
   else if (cpl == 2) hipLaunchKernelGGL((icrc_stream_kernel<2, false>), dim3(grid), dim3(kBlock), 0, st, a);
   else if (cpl == 4) hipLaunchKernelGGL((icrc_stream_kernel<4, false>), dim3(grid), dim3(kBlock), 0, st, a);
   else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t launch_quad(const QuadArgs &a, int grid, hipStream_t st) {
+  (void)hipGetLastError();  // a stale error of an earlier, unrelated HIP call must not fail this launch
+  hipLaunchKernelGGL((icrc_quad_kernel<0, 2, 2>), dim3(grid), dim3(kBlock), 0, st, a);
   return hipGetLastError();
 }
 

@@ -459,3 +459,29 @@ def test_ragged_workspace_reuse_across_sizes_and_streams(ctx):
                 ctx.batch_device(_dev(buf), len(lens), out, offsets=_dev(offs), lengths=_dev(lens), stream=st)
             st.synchronize()
             np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), want)
+
+
+@pytest.mark.parametrize("count", [1, 15, 16, 17, 63, 64, 65, 255, 256, 257, 4096 * 4 + 3, 1 << 20])
+def test_quad_kernel_64B(ctx, ctx_env, count):
+    """icrc_quad_kernel (back-to-back 64-byte packets, 4 lanes per packet,
+    coalesced 1 KiB loads): partial loads, partial 4 KiB steps, partial
+    rounds of result slots, waves with several rounds (C1's 1 M), verify
+    mode with corruptions; and the direct kernel (RICRC_NO_QUAD) agrees."""
+    n = 64
+    host = oracle_c.synth_batch(SEED + count, 5, count, n)
+    want = oracle_c.icrc_batch(host, stride=n, threads=16)
+    d = _dev(host)
+    out = _out(count)
+    ctx.batch_device(d, count, out, stride=n, stream=_stream())
+    np.testing.assert_array_equal(_host_u32(out), want)
+    if count in (257, 4096 * 4 + 3):
+        out2 = _out(count)
+        ctx_env(RICRC_NO_QUAD=1).batch_device(d, count, out2, stride=n, stream=_stream())
+        np.testing.assert_array_equal(_host_u32(out2), want)
+    host[:, n - 4:] = want.view(np.uint8).reshape(count, 4)
+    bad = np.arange(0, count, 5)
+    host[bad, 40 + bad % 20] ^= 0x04
+    ctx.batch_device(_dev(host), count, out, stride=n, stream=_stream(), verify=True)
+    w = np.ones(count, np.uint32)
+    w[bad] = 0
+    np.testing.assert_array_equal(_host_u32(out), w)

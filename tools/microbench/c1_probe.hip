@@ -6,7 +6,8 @@
 //   lane64     memory path, each lane loads its packet's 64 B (4 x 16 B at
 //              64 l + 16 k: the product's direct kernel pattern)
 //   coal       memory path, coalesced: load k of a wave reads 1 KiB at 1024 k + 16 l
-//   product    icrc_stream_kernel<1, true> as the library launches it
+//   direct     icrc_stream_kernel<1, true> (the round-2 C1 kernel)
+//   quad       icrc_quad_kernel<4> as the library launches it (round 3)
 // Memory variants request all of a wave's bytes before using any (the whole
 // batch is ~4 steps per wave), XOR them and write one word per wave.
 // Per-wave s_memrealtime start / end stamps for `coal` and `lane64`.
@@ -20,9 +21,9 @@
 using namespace ricrc;
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s line %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 
-template <int MODE, bool FILL, int STEPS>
+template <int MODE, bool FILL, int STEPS, bool LDS = true>
 __global__ __launch_bounds__(1024) void probe(const uint8_t *buf, uint64_t bytes, uint32_t *sink, uint64_t *stamps) {
-  __shared__ uint32_t lds[kLdsWords];
+  __shared__ uint32_t lds[LDS ? kLdsWords : 64];
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t wave = (uint64_t)blockIdx.x * 16 + (threadIdx.x >> 6);
@@ -115,6 +116,8 @@ int main() {
   a.P = 1; a.log2P2 = 0; a.nw_last = 15; a.n_iters = count / 64; a.verify = 0;
   a.K[0] = gf_x8n(0);
   const int pgrid = (int)std::min<uint64_t>(cu, (a.n_iters + 15) / 16);
+  QuadArgs q{};
+  q.base = buf; q.count = count; q.out = out;
   for (int r = 0; r < 3; ++r) {
     printf("round %d\n", r);
     printf("  empty         %7.2f us\n", timeit([&] { hipLaunchKernelGGL((probe<0, false, 4>), dim3(cu), dim3(1024), 0, 0, buf, bytes, sink, nullptr); }));
@@ -125,17 +128,30 @@ int main() {
     printf("  coal+fill     %7.2f us\n", timeit([&] { hipLaunchKernelGGL((probe<2, true, 4>), dim3(cu), dim3(1024), 0, 0, buf, bytes, sink, nullptr); }));
     printf("  coal 2xgrid   %7.2f us  (2 steps per wave)\n", timeit([&] { hipLaunchKernelGGL((probe<2, false, 2>), dim3(2 * cu), dim3(1024), 0, 0, buf, bytes, sink, nullptr); }));
     printf("  coal 4xgrid   %7.2f us  (1 step per wave)\n", timeit([&] { hipLaunchKernelGGL((probe<2, false, 1>), dim3(4 * cu), dim3(1024), 0, 0, buf, bytes, sink, nullptr); }));
-    printf("  product       %7.2f us  (icrc_stream_kernel<1,true>, grid %d)\n", timeit([&] { CK(launch_stream(a, 1, pgrid, 0)); }), pgrid);
+    printf("  direct        %7.2f us  (icrc_stream_kernel<1,true>, grid %d)\n", timeit([&] { CK(launch_stream(a, 1, pgrid, 0)); }), pgrid);
+    printf("  quad          %7.2f us  (icrc_quad_kernel<4>, grid %d)\n", timeit([&] { CK(launch_quad(q, cu, 0)); }), cu);
+    printf("  empty noLDS   %7.2f us\n", timeit([&] { hipLaunchKernelGGL((probe<0, false, 4, false>), dim3(cu), dim3(1024), 0, 0, buf, bytes, sink, nullptr); }));
+    printf("  empty 256thr  %7.2f us\n", timeit([&] { hipLaunchKernelGGL((probe<0, false, 4>), dim3(cu), dim3(256), 0, 0, buf, bytes, sink, nullptr); }));
+    printf("  empty 64 WGs  %7.2f us\n", timeit([&] { hipLaunchKernelGGL((probe<0, false, 4>), dim3(64), dim3(1024), 0, 0, buf, bytes, sink, nullptr); }));
+    printf("  quad W8       %7.2f us  (512-thread workgroups)\n", timeit([&] { hipLaunchKernelGGL((icrc_quad_kernel<0, 2, 2, 8>), dim3(cu), dim3(512), 0, 0, q); }));
+    printf("  quad W8 R4F2  %7.2f us  (512-thread workgroups)\n", timeit([&] { hipLaunchKernelGGL((icrc_quad_kernel<0, 4, 2, 8>), dim3(cu), dim3(512), 0, 0, q); }));
+    printf("  quad R4 F1    %7.2f us\n", timeit([&] { hipLaunchKernelGGL((icrc_quad_kernel<0, 4, 1>), dim3(cu), dim3(kBlock), 0, 0, q); }));
+    printf("  quad R2 F1    %7.2f us\n", timeit([&] { hipLaunchKernelGGL((icrc_quad_kernel<0, 2, 1>), dim3(cu), dim3(kBlock), 0, 0, q); }));
+    printf("  quad R1 F1    %7.2f us\n", timeit([&] { hipLaunchKernelGGL((icrc_quad_kernel<0, 1, 1>), dim3(cu), dim3(kBlock), 0, 0, q); }));
+    printf("  quad R4 F2    %7.2f us\n", timeit([&] { hipLaunchKernelGGL((icrc_quad_kernel<0, 4, 2>), dim3(cu), dim3(kBlock), 0, 0, q); }));
   }
-  for (int m : {1, 2}) {
+  for (int m : {1, 2, 3}) {
     std::vector<uint64_t> st(2 * 16 * cu);
+    QuadArgs qs = q;
+    qs.stamps = stamps;
     for (int i = 0; i < 5; ++i) {
       if (m == 1) hipLaunchKernelGGL((probe<1, true, 4>), dim3(cu), dim3(1024), 0, 0, buf, bytes, sink, stamps);
-      else hipLaunchKernelGGL((probe<2, true, 4>), dim3(cu), dim3(1024), 0, 0, buf, bytes, sink, stamps);
+      else if (m == 2) hipLaunchKernelGGL((probe<2, true, 4>), dim3(cu), dim3(1024), 0, 0, buf, bytes, sink, stamps);
+      else hipLaunchKernelGGL((icrc_quad_kernel<64, 2, 2>), dim3(cu), dim3(kBlock), 0, 0, qs);
     }
     CK(hipDeviceSynchronize());
     CK(hipMemcpy(st.data(), stamps, st.size() * 8, hipMemcpyDeviceToHost));
-    timeline(m == 1 ? "lane64" : "coal", st, 16 * cu);
+    timeline(m == 1 ? "lane64" : m == 2 ? "coal" : "quad", st, 16 * cu);
   }
   return 0;
 }
