@@ -14,3 +14,6 @@ done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c1" -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu --size 64 > "$OUT/prof_c1.log" 2>&1 || exit 5
 python3 tools/prof_summary.py --last 20 "$OUT/prof_c1/run_kernel_trace.csv" | grep -A1 quad
 TAG=${TAG:-r3c}_insts bash tools/pmc_insts.sh || exit 6
+timeout -k 10 600 python3 tools/pmc_traffic.py --out "$OUT/pmc_traffic.json" --scratch "$OUT/pmc" > "$OUT/pmc.log" 2>&1 || exit 7
+timeout -k 10 600 python3 tools/pmc_traffic.py --mix --out "$OUT/pmc_traffic_mix.json" --scratch "$OUT/pmc" > "$OUT/pmc_mix.log" 2>&1 || exit 8
+python3 -c "import json; [print(f, json.load(open('$OUT/'+f))['traffic_over_algorithmic']) for f in ('pmc_traffic.json','pmc_traffic_mix.json')]"
