@@ -495,6 +495,9 @@ def run(args, world, rank, be, distributed):
         be.init_dist()
     b = be.build(args, world, rank)
     count, sizes = b["sizes"][rank], b["sizes"]
+    if os.environ.get("RICRC_DEBUG") and hasattr(b["buf"], "data_ptr"):  # placement studies
+        print("bench: buf %#x offs %#x lens %#x" % (b["buf"].data_ptr(), getattr(b.get("d_offs"), "data_ptr", int)(),
+                                                    getattr(b.get("d_lens"), "data_ptr", int)()), file=sys.stderr)
     rank_bytes = b["rank_bytes"]
     do_gather = distributed and not args.no_gather
     g = IcrcGather(sizes)

@@ -253,6 +253,8 @@ int ragged_ws(Dev &d, hipStream_t st, uint64_t bytes, Dev::Ws **out) {
     HIP_TRY(hipMallocAsync(&w->p, grow, st));
     w->bytes = grow;
     w->dirty = true;
+    if (g_debug) fprintf(stderr, "libroceicrc: ragged workspace %p (%llu B) for stream %p\n", w->p,
+                         (unsigned long long)grow, (void *)st);
   }
   if (w->dirty) {
     HIP_TRY(rs_zero_counters(w->p, st));

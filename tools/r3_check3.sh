@@ -17,3 +17,4 @@ TAG=${TAG:-r3c}_insts bash tools/pmc_insts.sh || exit 6
 timeout -k 10 600 python3 tools/pmc_traffic.py --out "$OUT/pmc_traffic.json" --scratch "$OUT/pmc" > "$OUT/pmc.log" 2>&1 || exit 7
 timeout -k 10 600 python3 tools/pmc_traffic.py --mix --out "$OUT/pmc_traffic_mix.json" --scratch "$OUT/pmc" > "$OUT/pmc_mix.log" 2>&1 || exit 8
 python3 -c "import json; [print(f, json.load(open('$OUT/'+f))['traffic_over_algorithmic']) for f in ('pmc_traffic.json','pmc_traffic_mix.json')]"
+TAG=${TAG:-r3c}_modes RUNS=6 bash tools/c4_modes.sh
