@@ -355,7 +355,11 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   constexpr uint32_t kSlots = (ABL & 512) ? 192 : 64, kRound = kSlots / 8;
   constexpr uint32_t kBlk = 128;                          // words per descriptor block (8 groups x 8 x 8 B)
   constexpr uint32_t kWaveWords = kSlots + 2 * kBlk + 64;  // slots | 2-block ring | 8-group info FIFO
-  constexpr int D = 8;                                    // lines in flight per wave
+  // lines in flight per wave: 6 (with the quiet blocks below, 8 lines in
+  // flight left no registers for them: 128 VGPRs and spills; fold of a
+  // C4-shaped 5.3 GiB batch 953 -> 930 us, tools/microbench/fold_var.hip,
+  // profiles/r03/fold_var.txt)
+  constexpr int D = 6;
   // Finish tables first, so every lookup's constant part fits a ds_read's
   // 16-bit offset: x^-32 nibble table (128 words) | x^(-128 s) nibble tables
   // (8 x 132 words: rows padded by 4 words so the 8 lane slots spread over
@@ -516,6 +520,8 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   // short-circuit || on a ballot-derived bool compiled to five branches per
   // step, and C4's fold ran 1.5 % slower)
   uint32_t fd_hl = __ballot(fd_a > 88u) != 0 ? 2u : 1u;
+  // edge line <=> fd_k < fd_hl or fd_k == fd_L - 1 <=> (fd_k - fd_hl) >= fd_span, unsigned
+  uint32_t fd_span = fd_L - 1u > fd_hl ? fd_L - 1u - fd_hl : 0u;  // 0: every line is an edge line
 
   auto ld_advance = [&]() {
     if (++ld_k == ld_L) {  // wave-uniform
@@ -611,14 +617,34 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   // w ^ masked(w) on its own step; a group's last line leaves the next
   // group's first word alone in xr (its chains start from zero).
   uint32_t xr[4] = {ring[0][0], ring[0][1], ring[0][2], ring[0][3]};
-  auto fold_loop = [&](auto words) {
-  bool done = false;
-  while (!done) {
+  // Quiet steps.  Per-step cursor control cost the fold 16 SALU and 4.5
+  // branches per wave step against 1.7 and 0.1 in the SCK (rocprofv3 --pmc,
+  // profiles/r03/pmc_insts.txt).  A run of steps in which neither cursor
+  // changes group and the fold cursor's line is no edge line (not a head
+  // line, not the group's last) needs none of it: a step is then the 16
+  // lookups, the XORs and a load.  Every full step computes the length of
+  // the run that follows it (quiet); a block of D steps that starts with a
+  // run of >= D ahead is D quiet steps with no per-step test at all, and
+  // shorter runs go through full steps (a per-step quiet / full branch
+  // measured 17 % slower: 1115 against 953 us, tools/microbench/fold_var.hip).
+  uint32_t quiet = 0;
+  auto quiet_step = [&](int u, uint32_t ahead) {  // ahead: lines the load cursor is past ld_k within the block
+    const u32x4 wn = ring[(u + 1) % D];
 #pragma unroll
-    for (int u = 0; u < D; ++u) {
-      __builtin_amdgcn_sched_barrier(0);
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t t0 = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0400u));
+      const uint32_t t1 = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0500u) + 128);
+      const uint32_t t2 = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo1, 0x0C020600u));
+      const uint32_t t3 = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo1, 0x0C020700u) + 128);
+      xr[i] = xor3(t0, t1, xor3(t2, t3, wn[i]));
+    }
+    ring[u] = gload16_nt(ld.line0 + 128ull * (ld_k + ahead));
+  };
+  auto fold_loop = [&](auto words) {
+  // One full step: edge masks, group finish and both cursors' group changes.
+  auto full_step = [&](int u, bool &done) {
       const u32x4 wn = ring[(u + 1) % D];  // the next line, raw
-      if (!(ABL & 8) && ((fd_k < fd_hl) | (fd_k + 1 == fd_L))) {  // wave-uniform
+      if (!(ABL & 8) && fd_k - fd_hl >= fd_span) {  // wave-uniform: an edge line
         const u32x4 wc = ring[u];
         const int rel0 = (int)(128u * fd_k + 16u * s) - (int)fd_a;
         if constexpr (decltype(words)::value) {
@@ -665,6 +691,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
           ++fd_q;
           fd_enter(fd_q);
           fd_hl = __ballot(fd_a > 88u) != 0 ? 2u : 1u;
+          fd_span = fd_L - 1u > fd_hl ? fd_L - 1u - fd_hl : 0u;
         } else {
           done = true;
           fd_L = 0xFFFFFFFFu;
@@ -677,6 +704,30 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
       // rewritten by this step's load-cursor advance.
       ring[u] = ld_issue();
       ld_advance();
+      // The quiet run that follows: fold lines fd_k .. fd_L - 2 past the head
+      // lines, loads up to the line before the load cursor's group change
+      // (ld_L = 1 once every group is loaded: no run).
+      const uint32_t nf = (fd_k >= fd_hl && fd_k + 1 < fd_L) ? fd_L - 1u - fd_k : 0u;
+      const uint32_t nl = ld_L - 1u - ld_k;
+      quiet = nf < nl ? nf : nl;
+  };
+  bool done = false;
+  while (!done) {
+    if (!(ABL & 8) && quiet >= (uint32_t)D) {  // wave-uniform: D quiet steps, no per-step control
+#pragma unroll
+      for (int u = 0; u < D; ++u) {
+        __builtin_amdgcn_sched_barrier(0);
+        quiet_step(u, (uint32_t)u);
+      }
+      quiet -= D;
+      fd_k += D;
+      ld_k += D;
+      continue;
+    }
+#pragma unroll
+    for (int u = 0; u < D; ++u) {  // full steps (correct in any state; each one measures the next run)
+      __builtin_amdgcn_sched_barrier(0);
+      full_step(u, done);
     }
   }
   };
