@@ -507,11 +507,13 @@ __global__ __launch_bounds__(kBlock) void icrc_tsk_kernel(TskArgs a) {
 // rounds of DPP swaps) gives lane 4 p + c all 64 bytes of packet 16 c + p,
 // which it folds as the direct kernel does (15 words, slice-by-4, one chain;
 // the masks and the seed are the same for every lane).  Two steps are folded
-// side by side (F = 2: two independent chains per lane); R steps of loads
-// stay in flight through a register ring (R x 16 VGPRs: R = 4 with F = 2
-// spilled at 1024 threads per workgroup).  The slice-by-4 tables are computed by the
-// workgroup (<= 32 bit steps per thread) instead of loaded, so building them
-// never waits behind the data loads in the memory queue.  Results go to
+// side by side (F = 2: two independent chains per lane), transposed and
+// folded in the ring registers themselves (IP), which are refilled after the
+// fold; R = 2 steps of loads stay in flight.  The slice-by-4 tables are
+// computed by the workgroup (<= 32 bit steps per thread) instead of loaded,
+// so building them never waits behind the data loads in the memory queue
+// (a table load queued behind the data loads cost ~3 us of the C1 launch in
+// c1_probe's memory-path variant).  Results go to
 // per-wave LDS slots in packet order and leave in one coalesced 1 KiB store
 // per 4 steps.
 // ABL (timing-only, tools/microbench): 64 per-wave s_memrealtime stamps.
@@ -555,7 +557,7 @@ __device__ __forceinline__ void quad_transpose(u32x4 (&A)[4], uint32_t c) {
   }
 }
 
-template <int ABL, int R = 2, int F = 2, int W = kWaves>
+template <int ABL, int R = 2, int F = 2, int W = kWaves, bool IP = false>
 __global__ __launch_bounds__(64 * W) void icrc_quad_kernel(QuadArgs a) {
   static_assert((F == 1 || F == 2) && R % F == 0 && 4 % R == 0, "ring of R steps, folded F at a time");
   constexpr uint32_t N = 64;
@@ -613,15 +615,20 @@ __global__ __launch_bounds__(64 * W) void icrc_quad_kernel(QuadArgs a) {
   // Fold steps s .. s + F - 1 (ring slots u ..) side by side; slot of step
   // s's packet q: (s - round_lo) * 64 + q.  Steps past the wave's range write
   // slots the flush does not store (no branch here).
+  // IP: transposed and folded in the ring registers themselves, refilled
+  // after the fold (no copies: R = 4 with F = 2 then fits without spills).
   auto fold = [&](int u, uint64_t s, uint64_t round_lo) {
-    u32x4 A[F][4];
+    u32x4 Acp[IP ? 1 : F][4];
+    u32x4(&A)[F][4] = *reinterpret_cast<u32x4(*)[F][4]>(IP ? &ring[4 * u] : &Acp[0][0]);
+    if (!IP) {
 #pragma unroll
-    for (int f = 0; f < F; ++f)
+      for (int f = 0; f < F; ++f)
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        A[f][k] = ring[4 * (u + f) + k];
-        ring[4 * (u + f) + k] = load(s + f + R, (uint32_t)k);  // refill: step s + f + R
-      }
+        for (int k = 0; k < 4; ++k) {
+          A[f][k] = ring[4 * (u + f) + k];
+          ring[4 * (u + f) + k] = load(s + f + R, (uint32_t)k);  // refill: step s + f + R
+        }
+    }
     uint32_t x[F];
 #pragma unroll
     for (int f = 0; f < F; ++f) {
@@ -639,6 +646,12 @@ __global__ __launch_bounds__(64 * W) void icrc_quad_kernel(QuadArgs a) {
       const uint32_t r = ~step4x(tab, lt, x[f], 0u);
       // verify ? (trailer == ICRC) : ICRC
       slots[(uint32_t)(s + f - round_lo) * 64u + q] = __builtin_amdgcn_bitop3_b32(vmask, A[f][3][3] == r ? 1u : 0u, r, 0xCA);
+    }
+    if (IP) {
+#pragma unroll
+      for (int f = 0; f < F; ++f)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ring[4 * (u + f) + k] = load(s + f + R, (uint32_t)k);  // refill: step s + f + R
     }
   };
 
@@ -790,7 +803,11 @@ hipError_t launch_stream(const StreamArgs &a, int cpl, int grid, hipStream_t st)
 
 hipError_t launch_quad(const QuadArgs &a, int grid, hipStream_t st) {
   (void)hipGetLastError();  // a stale error of an earlier, unrelated HIP call must not fail this launch
-  hipLaunchKernelGGL((icrc_quad_kernel<0, 2, 2>), dim3(grid), dim3(kBlock), 0, st, a);
+  // two steps folded side by side, in place, two steps of loads in flight:
+  // 14.0-14.3 us on 1 M x 64 B; all four of C1's steps per wave in flight at
+  // once measured slower (16.8-17.2 us), one chain per lane too (15.7-17.1 us)
+  // (tools/microbench/c1_probe.hip, profiles/r03/c1_probe_quad_variants.txt)
+  hipLaunchKernelGGL((icrc_quad_kernel<0, 2, 2, kWaves, true>), dim3(grid), dim3(kBlock), 0, st, a);
   return hipGetLastError();
 }
 

@@ -135,6 +135,12 @@ int main() {
     printf("  empty 64 WGs  %7.2f us\n", timeit([&] { hipLaunchKernelGGL((probe<0, false, 4>), dim3(64), dim3(1024), 0, 0, buf, bytes, sink, nullptr); }));
     printf("  quad W8       %7.2f us  (512-thread workgroups)\n", timeit([&] { hipLaunchKernelGGL((icrc_quad_kernel<0, 2, 2, 8>), dim3(cu), dim3(512), 0, 0, q); }));
     printf("  quad W8 R4F2  %7.2f us  (512-thread workgroups)\n", timeit([&] { hipLaunchKernelGGL((icrc_quad_kernel<0, 4, 2, 8>), dim3(cu), dim3(512), 0, 0, q); }));
+    printf("  quad R4F2 IP  %7.2f us  (in-place ring)\n", timeit([&] { hipLaunchKernelGGL((icrc_quad_kernel<0, 4, 2, 16, true>), dim3(cu), dim3(kBlock), 0, 0, q); }));
+    printf("  quad R2F2 IP  %7.2f us  (in-place ring)\n", timeit([&] { hipLaunchKernelGGL((icrc_quad_kernel<0, 2, 2, 16, true>), dim3(cu), dim3(kBlock), 0, 0, q); }));
+    printf("  quad R4F1 IP  %7.2f us  (in-place ring)\n", timeit([&] { hipLaunchKernelGGL((icrc_quad_kernel<0, 4, 1, 16, true>), dim3(cu), dim3(kBlock), 0, 0, q); }));
+    printf("  quad R2F1 IP  %7.2f us  (in-place ring)\n", timeit([&] { hipLaunchKernelGGL((icrc_quad_kernel<0, 2, 1, 16, true>), dim3(cu), dim3(kBlock), 0, 0, q); }));
+    printf("  quad R1F1 IP  %7.2f us  (in-place ring)\n", timeit([&] { hipLaunchKernelGGL((icrc_quad_kernel<0, 1, 1, 16, true>), dim3(cu), dim3(kBlock), 0, 0, q); }));
+    printf("  quad R2F2 IP W8 %5.2f us  (in-place ring, 512 threads)\n", timeit([&] { hipLaunchKernelGGL((icrc_quad_kernel<0, 2, 2, 8, true>), dim3(cu), dim3(512), 0, 0, q); }));
     printf("  quad R4 F1    %7.2f us\n", timeit([&] { hipLaunchKernelGGL((icrc_quad_kernel<0, 4, 1>), dim3(cu), dim3(kBlock), 0, 0, q); }));
     printf("  quad R2 F1    %7.2f us\n", timeit([&] { hipLaunchKernelGGL((icrc_quad_kernel<0, 2, 1>), dim3(cu), dim3(kBlock), 0, 0, q); }));
     printf("  quad R1 F1    %7.2f us\n", timeit([&] { hipLaunchKernelGGL((icrc_quad_kernel<0, 1, 1>), dim3(cu), dim3(kBlock), 0, 0, q); }));
@@ -147,7 +153,7 @@ int main() {
     for (int i = 0; i < 5; ++i) {
       if (m == 1) hipLaunchKernelGGL((probe<1, true, 4>), dim3(cu), dim3(1024), 0, 0, buf, bytes, sink, stamps);
       else if (m == 2) hipLaunchKernelGGL((probe<2, true, 4>), dim3(cu), dim3(1024), 0, 0, buf, bytes, sink, stamps);
-      else hipLaunchKernelGGL((icrc_quad_kernel<64, 2, 2>), dim3(cu), dim3(kBlock), 0, 0, qs);
+      else hipLaunchKernelGGL((icrc_quad_kernel<64, 2, 2, 16, true>), dim3(cu), dim3(kBlock), 0, 0, qs);
     }
     CK(hipDeviceSynchronize());
     CK(hipMemcpy(st.data(), stamps, st.size() * 8, hipMemcpyDeviceToHost));
