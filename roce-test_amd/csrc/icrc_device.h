@@ -187,4 +187,42 @@ __device__ __forceinline__ uint32_t gload4_unaligned(uintptr_t addr) {
   return *reinterpret_cast<gptr_u32_unaligned>(addr);
 }
 
+// ---------------------------------------------------------- lane quads (DPP)
+// Lane quad transpose of 16-byte chunks: on entry lane 4 p + c holds chunk c
+// of the packets in A[0..3] (A[k]: load k); on exit it holds chunks 0..3 of
+// the packet that was in A[c].  swap(v, 1): the value of lane l ^ 1.
+__device__ __forceinline__ uint32_t dpp_swap1(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+}
+__device__ __forceinline__ uint32_t dpp_swap2(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+}
+__device__ __forceinline__ void quad_transpose(u32x4 (&A)[4], uint32_t c) {
+  const bool o1 = (c & 1u) != 0, o2 = (c & 2u) != 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {  // round 1: registers k, k ^ 1 across lanes c, c ^ 1
+    const uint32_t t0 = dpp_swap1(A[0][i]), t1 = dpp_swap1(A[1][i]);
+    const uint32_t t2 = dpp_swap1(A[2][i]), t3 = dpp_swap1(A[3][i]);
+    A[0][i] = o1 ? t1 : A[0][i];
+    A[1][i] = o1 ? A[1][i] : t0;
+    A[2][i] = o1 ? t3 : A[2][i];
+    A[3][i] = o1 ? A[3][i] : t2;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {  // round 2: registers k, k ^ 2 across lanes c, c ^ 2
+    const uint32_t t0 = dpp_swap2(A[0][i]), t1 = dpp_swap2(A[1][i]);
+    const uint32_t t2 = dpp_swap2(A[2][i]), t3 = dpp_swap2(A[3][i]);
+    A[0][i] = o2 ? t2 : A[0][i];
+    A[2][i] = o2 ? A[2][i] : t0;
+    A[1][i] = o2 ? t3 : A[1][i];
+    A[3][i] = o2 ? A[3][i] : t1;
+  }
+}
+
+// The value v of lane 4 (l / 4) + c (c a constant 0..3): a quad broadcast.
+template <int C>
+__device__ __forceinline__ uint32_t dpp_quad_bcast(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, C * 0x55, 0xF, 0xF, false);  // quad_perm [C,C,C,C]
+}
+
 }  // namespace ricrc

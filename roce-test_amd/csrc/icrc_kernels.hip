@@ -526,37 +526,6 @@ __device__ __forceinline__ uint32_t crc_table_value(uint32_t t) {
   return c;
 }
 
-// Lane quad transpose of 16-byte chunks: on entry lane 4 p + c holds chunk c
-// of the packets in A[0..3] (A[k]: load k); on exit it holds chunks 0..3 of
-// the packet that was in A[c].  swap(v, 1): the value of lane l ^ 1.
-__device__ __forceinline__ uint32_t dpp_swap1(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-}
-__device__ __forceinline__ uint32_t dpp_swap2(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
-}
-__device__ __forceinline__ void quad_transpose(u32x4 (&A)[4], uint32_t c) {
-  const bool o1 = (c & 1u) != 0, o2 = (c & 2u) != 0;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {  // round 1: registers k, k ^ 1 across lanes c, c ^ 1
-    const uint32_t t0 = dpp_swap1(A[0][i]), t1 = dpp_swap1(A[1][i]);
-    const uint32_t t2 = dpp_swap1(A[2][i]), t3 = dpp_swap1(A[3][i]);
-    A[0][i] = o1 ? t1 : A[0][i];
-    A[1][i] = o1 ? A[1][i] : t0;
-    A[2][i] = o1 ? t3 : A[2][i];
-    A[3][i] = o1 ? A[3][i] : t2;
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {  // round 2: registers k, k ^ 2 across lanes c, c ^ 2
-    const uint32_t t0 = dpp_swap2(A[0][i]), t1 = dpp_swap2(A[1][i]);
-    const uint32_t t2 = dpp_swap2(A[2][i]), t3 = dpp_swap2(A[3][i]);
-    A[0][i] = o2 ? t2 : A[0][i];
-    A[2][i] = o2 ? A[2][i] : t0;
-    A[1][i] = o2 ? t3 : A[1][i];
-    A[3][i] = o2 ? A[3][i] : t1;
-  }
-}
-
 template <int ABL, int R = 2, int F = 2, int W = kWaves, bool IP = false>
 __global__ __launch_bounds__(64 * W) void icrc_quad_kernel(QuadArgs a) {
   static_assert((F == 1 || F == 2) && R % F == 0 && 4 % R == 0, "ring of R steps, folded F at a time");

@@ -829,6 +829,11 @@ struct SmallPk {
     u32x4 U[KB + 1];
 #pragma unroll
     for (int k = 0; k <= KB; ++k) U[k] = unit(j0 + k);
+    blocks<KB, WA, MASK>(lds, lt, U);
+  }
+  // Fold blocks 0 .. KB-1 of units U (block j from units j, j + 1).
+  template <int KB, bool WA, int MASK>
+  __device__ __forceinline__ void blocks(const uint32_t *lds, const LaneTab &lt, const u32x4 (&U)[KB + 1]) {
 #pragma unroll
     for (int j = 0; j < KB; ++j) {
       // Block j's 4 words from units j, j + 1: X[k] = W[(t >> 2) + k] by
@@ -885,9 +890,45 @@ __global__ __launch_bounds__(kBlock) void icrc_rsmall_kernel(RsckArgs a) {
     const bool wa = __builtin_amdgcn_ballot_w64(((d.lo | (d.hi >> 16)) & 3u) != 0) == 0;
     // heads in blocks 0..3: rel_4 = M - 16 Kmax + 64 >= 40 for every lane
     const bool uk = __builtin_amdgcn_ballot_w64((d.hi >> 16) - 4u + 24u < 16u * Kmax) == 0;
+    // Half-line packets: every covered byte in one aligned 64-byte half
+    // line hb .. hb + 63 whose last 16-byte unit holds the covered end, not
+    // at the half line's end (C4's 64-byte packets: 64-byte aligned, 60
+    // covered bytes).  For a wave of them the 5 units of the 4 blocks are
+    // the half line's units 0, 0, 1, 2, 3, and they are read coalesced: in
+    // load c the 4 lanes of quad p read units 0..3 of lane 4 p + c's half
+    // line (64 contiguous bytes), and a 4 x 4 quad transpose hands every lane
+    // its own -- instead of every lane reading its packet's units alone, 64
+    // lines apart (the access pattern that costs C1's direct kernel, see the
+    // quad kernel in icrc_kernels.hip).
+    const uint64_t pa = ((uint64_t)(d.hi & 0xFFFFu) << 32) | d.lo;
+    const uint64_t pe = pa + ((d.hi >> 16) - 4u);
+    const uint64_t hb = (pe - 1u) & ~63ull;
+    const bool half = pa >= hb && ((uint32_t)pe & 63u) > 48u;
+    const bool halfw = Kmax == 4u && __builtin_amdgcn_ballot_w64(!half) == 0;
+    auto half_line_units = [&](u32x4 (&U)[5]) {
+      const uint32_t hlo = (uint32_t)hb, hhi = (uint32_t)(hb >> 32), q = lane & 3u;
+      u32x4 H[4];
+      auto at = [&](uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32 | lo) + 16u * q; };
+      H[0] = gload16(at(dpp_quad_bcast<0>(hlo), dpp_quad_bcast<0>(hhi)));
+      H[1] = gload16(at(dpp_quad_bcast<1>(hlo), dpp_quad_bcast<1>(hhi)));
+      H[2] = gload16(at(dpp_quad_bcast<2>(hlo), dpp_quad_bcast<2>(hhi)));
+      H[3] = gload16(at(dpp_quad_bcast<3>(hlo), dpp_quad_bcast<3>(hhi)));
+      quad_transpose(H, q);
+      U[0] = H[0];
+      U[1] = H[0];
+      U[2] = H[1];
+      U[3] = H[2];
+      U[4] = H[3];
+    };
     auto run = [&](auto words, auto uniform) {
       constexpr bool WA = decltype(words)::value;
       constexpr int M1 = decltype(uniform)::value ? 1 : 2, M2 = decltype(uniform)::value ? 0 : 2;
+      if (halfw) {  // wave-uniform
+        u32x4 U[5];
+        half_line_units(U);
+        P.blocks<4, WA, M1>(lds, lt, U);
+        return;
+      }
       uint32_t j = 0;
       switch (Kmax & 15u) {
         case 4: P.chunk<4, WA, M1>(lds, lt, 0); j = 4; break;

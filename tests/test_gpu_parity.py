@@ -485,3 +485,35 @@ def test_quad_kernel_64B(ctx, ctx_env, count):
     w = np.ones(count, np.uint32)
     w[bad] = 0
     np.testing.assert_array_equal(_host_u32(out), w)
+
+
+@pytest.mark.parametrize("case", ["c4_64B_aligned", "mixed_starts", "one_spoiler_per_wave", "end_at_half_line_end"])
+def test_one_line_packets_half_line_path(ctx, case):
+    """The one-line kernel's coalesced half-line path (C4's 64-byte packets,
+    64-byte aligned: every covered byte in one aligned 64-byte half line whose
+    last unit holds the covered end) against the oracle, and waves where that
+    condition fails for some lanes (start 4 bytes in, covered end exactly at
+    the half line's end, one packet per 64 spoiling its wave) taking the
+    per-lane path -- mixed with bigger packets so the classes interleave."""
+    rng = np.random.default_rng(hash(case) & 0xFFFF)
+    count = 40_000
+    lens = rng.choice(np.array([64, 64, 64, 1024, 256], np.uint32), size=count)
+    starts = np.zeros(count, np.uint64)
+    if case == "mixed_starts":
+        lens = np.where(lens == 64, rng.choice(np.array([53, 56, 60, 64], np.uint32), size=count), lens)
+        starts = rng.choice(np.array([0, 0, 4], np.uint64), size=count)
+    elif case == "one_spoiler_per_wave":
+        starts[::64] = 2
+    elif case == "end_at_half_line_end":
+        lens = np.where(lens == 64, np.uint32(68), lens)  # covered end 64: the half line's last byte
+    offs = np.zeros(count, np.uint64)
+    pos = 0
+    for i in range(count):  # each packet at a 64-byte boundary (+ its start offset)
+        pos = (pos + 63) // 64 * 64
+        offs[i] = pos + int(starts[i])
+        pos = int(offs[i]) + int(lens[i])
+    buf = rng.integers(0, 256, size=pos + 128, dtype=np.uint8)
+    want = oracle_c.icrc_batch(buf, offsets=offs, lengths=lens, threads=16)
+    out = _out(count)
+    ctx.batch_device(_dev(buf), count, out, offsets=_dev(offs), lengths=_dev(lens), stream=_stream())
+    np.testing.assert_array_equal(_host_u32(out), want)
