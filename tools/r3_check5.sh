@@ -17,3 +17,6 @@ for cfg in "c1:--size 64" "c4:--mix"; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$name" -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu $args > "$OUT/prof_$name.log" 2>&1 || exit 6
   python3 tools/prof_summary.py --last 20 "$OUT/prof_$name/run_kernel_trace.csv" | grep -A1 "quad\|rsck\|rsmall\|gather\|count\|scatter"
 done
+timeout -k 10 600 python3 tools/pmc_traffic.py --out "$OUT/pmc_traffic.json" --scratch "$OUT/pmc" > "$OUT/pmc.log" 2>&1 || exit 7
+timeout -k 10 600 python3 tools/pmc_traffic.py --mix --out "$OUT/pmc_traffic_mix.json" --scratch "$OUT/pmc" > "$OUT/pmc_mix.log" 2>&1 || exit 8
+python3 -c "import json; [print(f, json.load(open('$OUT/'+f))['traffic_over_algorithmic']) for f in ('pmc_traffic.json','pmc_traffic_mix.json')]"
