@@ -630,17 +630,16 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   uint32_t xr[4] = {ring[0][0], ring[0][1], ring[0][2], ring[0][3]};
   // Quiet steps.  Per-step cursor control cost the fold 16 SALU and 4.5
   // branches per wave step against 1.7 and 0.1 in the SCK (rocprofv3 --pmc,
-  // profiles/r03/pmc_insts.txt).  A run of lines in which the fold cursor
-  // stays in its group and meets no edge line (not a head line, not the
-  // group's last) needs no edge test and no finish.  Every full step
-  // computes the length of that run (qf); a block of D steps that starts with
-  // qf >= D folds with no per-step test at all, and its loads skip the load
-  // cursor's control too when that cursor stays in its group for the whole
-  // block (then a step is the 16 lookups, the XORs and a load); shorter runs
-  // go through full steps (a per-step quiet / full branch measured 17 %
-  // slower: 1115 against 953 us, tools/microbench/fold_var.hip).
-  uint32_t qf = 0;  // quiet fold lines ahead, measured by the last full step
-  auto quiet_fold = [&](int u) {
+  // profiles/r03/pmc_insts.txt).  A run of steps in which neither cursor
+  // changes group and the fold cursor's line is no edge line (not a head
+  // line, not the group's last) needs none of it: a step is then the 16
+  // lookups, the XORs and a load.  Every full step computes the length of
+  // the run that follows it (quiet); a block of D steps that starts with a
+  // run of >= D ahead is D quiet steps with no per-step test at all, and
+  // shorter runs go through full steps (a per-step quiet / full branch
+  // measured 17 % slower: 1115 against 953 us, tools/microbench/fold_var.hip).
+  uint32_t quiet = 0;
+  auto quiet_step = [&](int u, uint32_t ahead) {  // ahead: lines the load cursor is past ld_k within the block
     const u32x4 wn = ring[(u + 1) % D];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -650,6 +649,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
       const uint32_t t3 = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo1, 0x0C020700u) + 128);
       xr[i] = xor3(t0, t1, xor3(t2, t3, wn[i]));
     }
+    ring[u] = gload16_nt(ld.line0 + 128ull * (ld_k + ahead));
   };
   auto fold_loop = [&](auto words) {
   // One full step: edge masks, group finish and both cursors' group changes.
@@ -715,31 +715,24 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
       // rewritten by this step's load-cursor advance.
       ring[u] = ld_issue();
       ld_advance();
-      // The quiet run that follows: fold lines fd_k .. fd_L - 2 past the head lines.
-      qf = (fd_k >= fd_hl && fd_k + 1 < fd_L) ? fd_L - 1u - fd_k : 0u;
+      // The quiet run that follows: fold lines fd_k .. fd_L - 2 past the head
+      // lines, loads up to the line before the load cursor's group change
+      // (ld_L = 1 once every group is loaded: no run).
+      const uint32_t nf = (fd_k >= fd_hl && fd_k + 1 < fd_L) ? fd_L - 1u - fd_k : 0u;
+      const uint32_t nl = ld_L - 1u - ld_k;
+      quiet = nf < nl ? nf : nl;
   };
   bool done = false;
   while (!done) {
-    if (!(ABL & 8) && qf >= (uint32_t)D) {  // wave-uniform: D quiet fold steps
-      qf -= D;
-      fd_k += D;
-      if (ld_L - 1u - ld_k >= (uint32_t)D) {  // and the load cursor stays in its group: no per-step control
+    if (!(ABL & 8) && quiet >= (uint32_t)D) {  // wave-uniform: D quiet steps, no per-step control
 #pragma unroll
-        for (int u = 0; u < D; ++u) {
-          __builtin_amdgcn_sched_barrier(0);
-          quiet_fold(u);
-          ring[u] = gload16_nt(ld.line0 + 128ull * (ld_k + u));
-        }
-        ld_k += D;
-        continue;
-      }
-#pragma unroll
-      for (int u = 0; u < D; ++u) {  // the load cursor enters a group inside the block
+      for (int u = 0; u < D; ++u) {
         __builtin_amdgcn_sched_barrier(0);
-        ring[u] = ld_issue();  // line u is already in xr: its register is free
-        ld_advance();
-        quiet_fold(u);
+        quiet_step(u, (uint32_t)u);
       }
+      quiet -= D;
+      fd_k += D;
+      ld_k += D;
       continue;
     }
 #pragma unroll
