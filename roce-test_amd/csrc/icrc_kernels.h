@@ -115,7 +115,7 @@ void rs_bind_workspace(RsckArgs &a, void *ws);
 hipError_t rs_zero_counters(void *ws, hipStream_t st);
 // The whole ragged pipeline on `st`: count/classify, plan, scatter, fold, gather.
 // count < 2^31 (the host cuts larger batches).
-hipError_t launch_rsck(RsckArgs &a, int grid, hipStream_t st);
+hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, int gather_cap, hipStream_t st);  // caps: 0 = default
 
 struct SynthArgs {
   uint8_t *buf;

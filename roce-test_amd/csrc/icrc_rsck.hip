@@ -1005,18 +1005,21 @@ static void launch_passes(const RsckArgs &a, int pgrid, hipStream_t st) {
   else launch_passes_t<false, false>(a, pgrid, st);
 }
 
-hipError_t launch_rsck(RsckArgs &a, int grid, hipStream_t st) {
+hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, int gather_cap, hipStream_t st) {
   (void)hipGetLastError();  // a stale error of an earlier, unrelated HIP call must not fail this launch
   if (a.count == 0) return hipSuccess;
   // a.counts (+ the misaligned flag) is zero here: zeroed when the workspace
   // was allocated, and again by rsck_gather at the end of every call.
   const uint64_t want = (a.count + kPassBlock - 1) / kPassBlock;
-  const int pgrid = (int)(want < kPassBlocks ? want : kPassBlocks);
+  int pgrid = (int)(want < kPassBlocks ? want : kPassBlocks);
+  if (pass_cap > 0 && pass_cap < pgrid) pgrid = pass_cap;
   launch_passes(a, pgrid, st);
   hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, st, a);
   // the small region [0, *small_pos): one lane per packet
   hipLaunchKernelGGL(icrc_rsmall_kernel, dim3(grid), dim3(kBlock), 0, st, a);
-  hipLaunchKernelGGL(rsck_gather, dim3(gather_grid(a.count)), dim3(256), 0, st, a);
+  int ggrid = gather_grid(a.count);
+  if (gather_cap > 0 && gather_cap < ggrid) ggrid = gather_cap;
+  hipLaunchKernelGGL(rsck_gather, dim3(ggrid), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
