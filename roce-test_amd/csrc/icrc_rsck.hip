@@ -382,13 +382,8 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t s = lane & 7, g = lane >> 3;
 
-  // The tables are filled after this wave's first descriptor blocks and
-  // line loads are in flight (fill_tables below): the chain plan -> groups
-  // -> descriptors -> lines is four dependent memory latencies, which the
-  // fill now hides.  Every wave fills its part, busy or not.
   const uint32_t tab_v = table_entry(g_tab128);
   const uint32_t tz_v = a.tzb[threadIdx.x < kTzWords ? threadIdx.x : 0];
-  auto fill_tables = [&]() {
   table_store(tab, tab_v);
   if (!(ABL & 512) && threadIdx.x < kTzWords) tzl[threadIdx.x] = tz_v;
   if (!(ABL & 512)) {  // entry (s, w, v) = (nibble v at bits 4w..4w+3) * x^(-128 s), where bit
@@ -427,7 +422,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
     x2tl[threadIdx.x] = t2;
     x3tl[threadIdx.x] = t3;
   }
-  };
+  __syncthreads();
 
   // This wave's groups: those whose first line lies in its share of steps.
   const RsPlan *P = a.plan;
@@ -451,11 +446,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   };
   const uint64_t x0 = wave * share < S ? wave * share : S;
   const uint32_t q_begin = first_group_at(x0), q_end = first_group_at(x0 + share);
-  if (q_begin >= q_end) {  // no work: fill this wave's part of the tables (no barrier below)
-    fill_tables();
-    __syncthreads();
-    return;
-  }
+  if (q_begin >= q_end) return;  // no barrier below
 
   const LaneTab lt{(lane & 31) << 2, ((lane & 31) << 2) | 0x10000u};
   const uint32_t *qrow = qtl + s * kQtStride;
@@ -557,8 +548,6 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
     ld_advance();
   }
   __builtin_amdgcn_sched_barrier(0);
-  fill_tables();
-  __syncthreads();
 
   uint32_t r[4] = {0u, 0u, 0u, 0u};
   uint32_t round_q0 = q_begin;  // first group of the current round of result slots
@@ -875,6 +864,8 @@ __global__ __launch_bounds__(kBlock) void icrc_rsmall_kernel(RsckArgs a) {
   __shared__ uint32_t lds[kLdsWords];
   const uint32_t tab_v = table_entry(g_tab);
   const uint32_t count = *a.small_pos;
+  table_store(lds, tab_v);
+  __syncthreads();
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const LaneTab lt{(lane & 31) << 2, ((lane & 31) << 2) | 0x10000u};
@@ -882,9 +873,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rsmall_kernel(RsckArgs a) {
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.res, 4u * count);
   auto desc_at = [&](uint32_t pos) -> RsDesc { return a.desc[pos < count ? pos : (count ? count - 1u : 0u)]; };
   uint32_t base = (blockIdx.x * kWaves + wid) * 64u;
-  RsDesc dn = desc_at(base + lane);  // in flight during the table fill
-  table_store(lds, tab_v);
-  __syncthreads();
+  RsDesc dn = desc_at(base + lane);
   for (; base < count; base += step) {
     const uint32_t pos = base + lane;
     const RsDesc d = dn;
