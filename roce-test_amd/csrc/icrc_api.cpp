@@ -35,7 +35,7 @@ constexpr uint64_t kStagePkts = 1ull << 20;     // per staging slot (packets)
 // Ragged-path workspaces per device, one per recently used stream: batch_host's
 // two slot streams + the context stream + callers' streams.
 constexpr size_t kMaxWorkspaces = 8;
-constexpr uint64_t kRsChunk = 1ull << 30;  // the ragged pipeline's positions are 32-bit: longer batches are cut
+constexpr uint64_t kRsChunk = kRsMaxCount;  // the ragged pipeline's group counter is 26-bit: longer batches are cut
 
 // Environment knobs, read ONCE by ricrc_create (diagnostics, tests and
 // schedule studies; the launch path never calls getenv).
@@ -574,7 +574,7 @@ Knobs read_knobs() {
   k.no_quad = getenv("RICRC_NO_QUAD") != nullptr;
   k.sck_grid = (int)std::max(0L, num("RICRC_SCK_GRID", 0));
   k.rsck_grid = (int)std::max(0L, num("RICRC_RSCK_GRID", 0));
-  k.gcost = (uint32_t)std::max(0L, num("RICRC_RS_GCOST", 0));
+  k.gcost = (uint32_t)std::min(1024L, std::max(0L, num("RICRC_RS_GCOST", 0)));  // the packed work counter's range
   k.pass_grid = (int)std::max(0L, num("RICRC_RS_PASS_GRID", 0));
   k.gather_grid = (int)std::max(0L, num("RICRC_RS_GATHER_GRID", 0));
   k.fail_chunk = num("RICRC_FAIL_CHUNK", -1);

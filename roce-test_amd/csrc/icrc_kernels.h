@@ -48,7 +48,7 @@ struct RsDesc {
 // Ragged strided-chain path (icrc_rsck.hip): any packet addresses and
 // lengths, packets bucketed by their number of 128-byte lines on the device,
 // 8 packets of equal line count per group, folded as in the SCK.
-// Classes: 0 = not bucketed (n < 44 or n > 65535: done in the count pass);
+// Classes: 0 = not bucketed (n < 44 or n > 65535: done in the bucket pass);
 // 1 + P for packets spanning <= kRsSmallL lines, by their 64-byte piece count P
 // (one lane per packet, icrc_rsmall_kernel: 8 lanes per packet is too coarse
 // for them); kRsBigBase + L for the rest, by line count L (the strided-chain
@@ -59,14 +59,28 @@ struct RsDesc {
 constexpr int kRsSmallL = RICRC_RS_SMALL_L;
 constexpr int kRsBigBase = 8;                  // small classes 2..8 (P <= 7 for L <= 3)
 constexpr int kRsClasses = kRsBigBase + 514;   // L <= 513 (n <= 65535, any start offset)
+constexpr int kRsRuns = kRsClasses - kRsBigBase;  // big classes a pass block can hold
 constexpr int kTzWords = 264;                  // tz bases: m = 2 tz + q <= 2 * 127 + 7
-struct RsPlan {
-  uint32_t nc;        // non-empty big classes
-  uint32_t ngroups;   // 8-packet groups over all classes
-  uint64_t nsteps;    // weighted work over all groups: lines + a per-group finish cost
-  uint32_t L[kRsClasses];   // compact, ascending
-  uint32_t g0[kRsClasses];  // first group of the class
-  uint64_t s0[kRsClasses];  // weighted work before the class's first group
+// Bucket layout (block-local, one pass): pass block b lays its packets out
+// by class -- the small ones in a range of the small pool, the big ones as
+// "runs" of whole 8-packet groups in a range of the big pool (each run is one
+// class, its last group padded with copies of its last packet) -- and
+// reserves both ranges with one atomic each.  The big pool's counter packs
+// groups (bits 0..25) and weighted work (bits 26..63) so a block's groups and
+// its work prefix come from ONE atomic: group order and work order agree.
+constexpr int kRsGroupBits = 26;
+struct RsCounters {
+  uint32_t odd;                // a big packet not starting or ending on a 4-byte word
+  uint32_t small;              // small-pool packets
+  unsigned long long pool;     // big pool: groups | work << kRsGroupBits
+};
+struct RsBlock {               // pass block b's big-pool range (runs == 0: none)
+  uint32_t g0, groups, runs, pad;
+  uint64_t s0, work;
+};
+struct RsRun {                 // one class of one pass block: groups [g0, g0 + groups) of L lines
+  uint32_t g0, groups, L, pad;
+  uint64_t s0;                 // weighted work before the run's first group
 };
 struct RsckArgs {
   const uint8_t *base;
@@ -80,15 +94,16 @@ struct RsckArgs {
   uint32_t group_cost;  // a group's finish in line-steps of the fold's work split (launch_rsck sets it)
   uint32_t *out;
   // device workspace (icrc_api.cpp sizes it: rs_workspace_bytes)
-  uint32_t *counts;   // [kRsClasses + 2], zeroed before the count pass: class counts, "misaligned" flag, count-pass ticket
-  uint32_t *cursor;   // [kRsClasses], zeroed by the plan pass
-  uint32_t *bucket;   // [kRsClasses] first position of each class
-  RsPlan *plan;
-  RsDesc *desc;       // [count + 8 kRsClasses] in class order
-  uint32_t *pos_of;   // [count] position of packet i, or ~0 (written by the scatter pass)
-  uint32_t *res;      // [count + 8 kRsClasses] results in class order
-  uint32_t *hist;     // [pass blocks][kRsClasses] per-block class counts
-  uint32_t *small_pos;  // positions of the small region [0, *small_pos) (device count)
+  RsCounters *ctr;      // zeroed on allocation and by the gather pass of every call
+  RsBlock *blk;         // [pass blocks]
+  RsRun *runs;          // [pass blocks][kRsRuns]
+  RsDesc *desc;         // small pool [0, count) | big pool [small_cap, ...) (positions)
+  RsDesc *bdesc;        // desc + small_cap: the big pool, group q at 8 q
+  uint32_t *pos_of;     // [count] position of packet i, or ~0 (written by the bucket pass)
+  uint32_t *res;        // results by position, like desc
+  uint32_t *bres;       // res + small_cap
+  uint32_t small_cap;   // count rounded up to 8
+  uint32_t nblk;        // pass blocks of this call (launch_rsck sets it)
   const uint32_t *tzb;  // [kTzWords]: entry m = x^(31 - 4 m), i.e. basis word 4 q of x^(-8 tz) at m = 2 tz + q
   uint32_t XB[32];      // basis of x^-32
   uint32_t XB2[32];     // basis of x^-64
@@ -110,11 +125,13 @@ constexpr uint32_t kRsGroupCost = 12;  // quarter line-steps (3 lines)
 uint64_t rs_workspace_bytes(uint64_t count);
 // Carves the workspace (rs_workspace_bytes(count) bytes at ws) into a.
 void rs_bind_workspace(RsckArgs &a, void *ws);
-// Zeroes a workspace's class counters (on allocation; afterwards every call
+// Zeroes a workspace's counters (on allocation; afterwards every call
 // leaves them zero).
 hipError_t rs_zero_counters(void *ws, hipStream_t st);
-// The whole ragged pipeline on `st`: count/classify, plan, scatter, fold, gather.
-// count < 2^31 (the host cuts larger batches).
+// The whole ragged pipeline on `st`: bucket, fold, one-line fold, gather.
+// count <= kRsMaxCount (the host cuts larger batches: the big pool's group
+// count must fit kRsGroupBits).
+constexpr uint64_t kRsMaxCount = 1ull << 28;
 hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, int gather_cap, hipStream_t st);  // caps: 0 = default
 
 struct SynthArgs {

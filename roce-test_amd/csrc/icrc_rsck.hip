@@ -7,26 +7,24 @@
 // of 8 packets per load and folds them without any transpose.  This path
 // gives ragged batches the same inner loop:
 //
-//  1. rsck_count    classify every packet by its number of 128-byte lines on
+//  1. rsck_bucket   classify every packet by its number of 128-byte lines on
 //                   the ABSOLUTE line grid, L = ceil(((addr & 127) + n - 4) /
-//                   128), histogram the classes; packets too short for a
-//                   RoCEv2 header (4 <= n < 44) are computed right there by a
-//                   scalar loop, invalid lengths yield 0 (as the ragged kernel
-//                   always did).  Its last workgroup runs
-//  2. rsck_plan     a scan of the class counts: each class gets a bucket
-//                   padded to whole 8-packet groups, a first group and a
-//                   first step (line);
-//  3. rsck_scatter  writes each packet's descriptor {addr, n} into its class
-//                   bucket (block-aggregated atomics) and its position;
-//  4. icrc_rsck_kernel  folds groups of 8 equal-L packets (L > kRsSmallL)
+//                   128), and lay each pass block's packets out by class:
+//                   small ones in a range of the small pool, big ones as runs
+//                   of whole 8-packet groups of one L in a range of the big
+//                   pool (block-local: no grid-wide count or plan, see the
+//                   kernel); packets too short for a RoCEv2 header
+//                   (4 <= n < 44) are computed right there by a scalar loop,
+//                   invalid lengths yield 0;
+//  2. icrc_rsck_kernel  folds groups of 8 equal-L packets (L > kRsSmallL)
 //                   exactly like the SCK -- lane 8g+s owns slot s of every
 //                   line of packet g, four chains per lane, T_124..T_127
-//                   tables in LDS -- with a load cursor running 8 lines ahead
-//                   of the fold cursor across group boundaries, descriptors
-//                   read 64 at a time;
-//     icrc_rsmall_kernel folds the one-line packets (C4's 64 B; 8 lanes per
+//                   tables in LDS -- with a load cursor running ahead of the
+//                   fold cursor across group boundaries, descriptors read 64
+//                   at a time, waves splitting the big pool by weighted work;
+//  3. icrc_rsmall_kernel folds the one-line packets (C4's 64 B; 8 lanes per
 //                   packet is too coarse for them) one lane per packet;
-//  5. rsck_gather   out[i] = res[pos(i)] (verify mode: the trailer compared
+//  4. rsck_gather   out[i] = res[pos(i)] (verify mode: the trailer compared
 //                   with it).
 //
 // Lines are 128-byte aligned in memory (misaligned line grids measured 20 %
@@ -91,16 +89,10 @@ __device__ uint32_t icrc_small(uint64_t addr, uint32_t n) {
   return ~r;
 }
 
-// Pass blocks own contiguous packet ranges (the same in the count and the
-// scatter pass), so each block reserves its bucket ranges with ONE global
-// atomic per class (per-chunk reservations serialised on the few hot class
-// counters: 50 us per million packets).
+// Pass blocks own contiguous packet ranges.
 constexpr int kPassBlock = 1024;
-constexpr int kPassBlocks = 512;  // pass grid cap (per-block class histograms: 1 MiB)
+constexpr int kPassBlocks = 512;  // pass grid cap
 constexpr int kPassUnroll = 8;    // packets per thread whose descriptors are read at once
-// a.counts: [0, kRsClasses) class counts, [kRsClasses] misaligned flag,
-// [kRsTicket] count-pass workgroups done
-constexpr int kRsTicket = kRsClasses + 1;
 __device__ __forceinline__ void pass_range(uint64_t count, uint64_t &lo, uint64_t &hi) {
   const uint64_t per = ((count + gridDim.x - 1) / gridDim.x + kPassBlock - 1) / kPassBlock * kPassBlock;
   lo = (uint64_t)blockIdx.x * per;
@@ -120,187 +112,161 @@ __device__ __forceinline__ T wave_scan(T v) {
   return v;
 }
 
-// One workgroup: exclusive scans over the classes of groups (bucket
-// positions), of weighted work and of the non-empty big classes (the fold's
-// class table).
-// Run by the count pass's last workgroup (1024 threads), after every
-// workgroup's class counts have landed in a.counts.  One barrier: each wave
-// scans its 64 classes, then adds the totals of the waves before it (the
-// 10-round LDS scan before it cost ~0.2 % of C4's step, tools/ab_env.sh).
-__device__ void rsck_plan(const RsckArgs &a) {
-  __shared__ uint32_t wg[16], wf[16];
-  __shared__ uint64_t wsum[16];
-  const uint32_t t = threadIdx.x, wid = t >> 6;
-  const uint32_t cnt = (t >= 1 && t < (uint32_t)kRsClasses)
-                           ? __hip_atomic_load(&a.counts[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                           : 0u;
-  const bool big = t > (uint32_t)kRsBigBase;
-  const uint32_t G = (cnt + 7u) >> 3, f = (big && cnt) ? 1u : 0u;
-  const uint32_t L = big ? t - (uint32_t)kRsBigBase : 0u;
-  const uint64_t S = big ? (uint64_t)G * (4u * L + a.group_cost) : 0u;  // quarter line-steps
-  uint32_t ig = wave_scan(G), jf = wave_scan(f);
-  uint64_t is = wave_scan(S);
-  if ((t & 63u) == 63u) {
-    wg[wid] = ig;
-    wf[wid] = jf;
-    wsum[wid] = is;
-  }
-  __syncthreads();
-  for (uint32_t w = 0; w < wid; ++w) {  // wave-uniform
-    ig += wg[w];
-    jf += wf[w];
-    is += wsum[w];
-  }
-  const uint32_t g0 = ig - G, ci = jf - f;
-  const uint64_t s0 = is - S;
-  RsPlan *P = a.plan;
-  if (f) {
-    P->L[ci] = L;
-    P->g0[ci] = g0;
-    P->s0[ci] = s0;
-  }
-  if (t < (uint32_t)kRsClasses) {
-    a.bucket[t] = 8u * g0;
-    a.cursor[t] = 0u;
-  }
-  if (t == (uint32_t)kRsBigBase + 1) *a.small_pos = 8u * g0;
-  if (t == 1023) {
-    P->nc = jf;
-    P->ngroups = ig;
-    P->nsteps = is;
-  }
-}
-
+// The bucket pass: ONE kernel, no grid-wide dependency.  Round 2 counted
+// the classes over the whole batch first (a count pass, then a plan in its
+// last workgroup: class-contiguous buckets), so every packet's descriptors
+// were read twice and the pipeline paid a launch and a serial plan tail.
+// The fold does not need classes to be contiguous over the batch, only
+// groups of 8 equal-L packets and a work prefix in group order: so each
+// block buckets its own packets --
+//   1. read the descriptors (kept in registers when the block's packets fit
+//      one round of kPassUnroll per thread: C4's 4 M packets on 512 blocks),
+//      classify, rank each packet in its class by an LDS atomic; packets
+//      that are not bucketed (n < 44: Sarwate loop; invalid lengths: 0) are
+//      done right here;
+//   2. scan the block's class counts (one class per thread): small classes
+//      are laid out back to back, big classes as runs of whole groups;
+//   3. reserve the block's small range and its big range -- groups and
+//      weighted work packed in ONE 64-bit atomic, so the big pool's group
+//      order and work order agree -- and publish the block's runs (RsBlock,
+//      RsRun) for the fold's work split;
+//   4. write each descriptor to its position (and pos_of[i]); the packet
+//      ranked last in its class pads the run's last group with copies of
+//      itself.
+// Blocks whose packets take several rounds re-read them for step 4 (ranks
+// from a second LDS cursor: any order of ranks is a valid layout).
 template <bool OFF, bool LEN>
-__global__ __launch_bounds__(kPassBlock) void rsck_count(RsckArgs a) {
-  __shared__ uint32_t h[kRsClasses];
-  for (int t = threadIdx.x; t < kRsClasses; t += blockDim.x) h[t] = 0;
+__global__ __launch_bounds__(kPassBlock) void rsck_bucket(RsckArgs a) {
+  __shared__ uint32_t h[kRsClasses], at[kRsClasses], cur[kRsClasses];
+  __shared__ uint32_t wg[16], wsm[16], wf[16];
+  __shared__ uint64_t ww[16];
+  __shared__ uint32_t blk_g0, blk_small;
+  __shared__ uint64_t blk_s0;
+  for (int t = threadIdx.x; t < kRsClasses; t += blockDim.x) {
+    h[t] = 0;
+    cur[t] = 0;
+  }
   __syncthreads();
   uint64_t lo, hi;
   pass_range(a.count, lo, hi);
-  int odd = 0;  // a strided-chain packet not starting or ending on a 4-byte word
-  // kPassUnroll packets per thread in flight at once: one at a time, the
-  // pass was a chain of dependent memory latencies.
-  for (uint64_t i0 = lo + threadIdx.x; i0 < hi; i0 += kPassUnroll * blockDim.x) {
+  const bool one = hi - lo <= (uint64_t)kPassUnroll * blockDim.x;  // block-uniform
+  int odd = 0;  // a big packet not starting or ending on a 4-byte word
+  uint64_t addr[kPassUnroll];
+  uint32_t n[kPassUnroll], c[kPassUnroll], rank[kPassUnroll];
+  auto load = [&](uint64_t r0) {
     // Raw loads first, unconditional (index clamped), arithmetic after: an
     // add on a loaded value inside a per-packet branch made the compiler wait
     // for each load before issuing the next.
-    uint64_t addr[kPassUnroll];
-    uint32_t n[kPassUnroll];
 #pragma unroll
     for (int k = 0; k < kPassUnroll; ++k) {
-      uint64_t i = i0 + (uint64_t)k * blockDim.x;
+      uint64_t i = r0 + (uint64_t)k * blockDim.x + threadIdx.x;
       i = i < hi ? i : hi - 1;
       addr[k] = OFF ? a.off[i] : i * a.stride;
       n[k] = LEN ? a.len[i] : a.fixed_len;
     }
 #pragma unroll
     for (int k = 0; k < kPassUnroll; ++k) addr[k] += (uint64_t)(uintptr_t)a.base + a.l3_offset;
-#pragma unroll
-    for (int k = 0; k < kPassUnroll; ++k) {
-      const uint64_t i = i0 + (uint64_t)k * blockDim.x;
-      if (i >= hi) break;
-      const uint32_t c = rs_class(addr[k], n[k]);
-      if (c) {
-        atomicAdd(&h[c], 1u);
-        odd |= (c >= (uint32_t)kRsBigBase && ((addr[k] | n[k]) & 3u)) ? 1 : 0;
-      } else {
-        uint32_t v = 0u;
-        if (n[k] >= 4u && n[k] <= kMaxLen) {
-          v = icrc_small(addr[k], n[k]);
-          if (a.verify) v = gload4_unaligned((uintptr_t)(addr[k] + n[k] - 4u)) == v ? 1u : 0u;
-        }
-        a.out[i] = v;
-      }
-    }
-  }
-  if (__syncthreads_or(odd) && threadIdx.x == 0) atomicOr(&a.counts[kRsClasses], 1u);
-  for (int t = threadIdx.x; t < kRsClasses; t += blockDim.x) {
-    a.hist[(uint64_t)blockIdx.x * kRsClasses + t] = h[t];
-    if (h[t]) atomicAdd(&a.counts[t], h[t]);
-  }
-  // The last workgroup to finish plans the buckets (one launch fewer).  Only
-  // the class-count atomics need ordering before the ticket: each thread
-  // waits for its own to be acknowledged (vmcnt(0)), not a __threadfence (an
-  // agent-scope release writes the XCD's L2 back: 130 us over the pass).
-  __shared__ uint32_t last;
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-  __syncthreads();
-  if (threadIdx.x == 0)
-    last = __hip_atomic_fetch_add(&a.counts[kRsTicket], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                   gridDim.x - 1
-               ? 1u
-               : 0u;
-  __syncthreads();
-  if (last) rsck_plan(a);
-}
-
-template <bool OFF, bool LEN>
-__global__ __launch_bounds__(kPassBlock) void rsck_scatter(RsckArgs a) {
-  // The class tables in LDS: per-round global reads of them were a
-  // dependent latency in every round.
-  __shared__ uint32_t base[kRsClasses], sbk[kRsClasses], send[kRsClasses];
-  for (int t = threadIdx.x; t < kRsClasses; t += blockDim.x) {
-    const uint32_t hb = a.hist[(uint64_t)blockIdx.x * kRsClasses + t];
-    const uint32_t bk = a.bucket[t];
-    base[t] = hb ? bk + atomicAdd(&a.cursor[t], hb) : 0u;
-    sbk[t] = bk;
-    send[t] = bk + a.counts[t];
-  }
-  uint64_t lo, hi;
-  pass_range(a.count, lo, hi);
-  // Rounds of kPassUnroll packets per thread (descriptors read at once),
-  // positions by returning LDS atomics on the block's class cursors: no
-  // barrier per round (per-round ranks with two barriers each measured 0.3 %
-  // slower on C4's step, tools/ab_env.sh); the order of packets within a
-  // class does not matter.
-  __syncthreads();
+  };
   for (uint64_t r0 = lo; r0 < hi; r0 += kPassUnroll * blockDim.x) {  // block-uniform
-    uint64_t addr[kPassUnroll];
-    uint32_t n[kPassUnroll];
-#pragma unroll
-    for (int k = 0; k < kPassUnroll; ++k) {
-      uint64_t i = r0 + (uint64_t)k * blockDim.x + threadIdx.x;
-      i = i < hi ? i : hi - 1;
-      addr[k] = OFF ? __builtin_nontemporal_load(&a.off[i]) : i * a.stride;  // last read of the descriptors: nt
-      n[k] = LEN ? __builtin_nontemporal_load(&a.len[i]) : a.fixed_len;
-    }
-#pragma unroll
-    for (int k = 0; k < kPassUnroll; ++k) addr[k] += (uint64_t)(uintptr_t)a.base + a.l3_offset;
-    uint32_t c[kPassUnroll], pos[kPassUnroll];
+    load(r0);
 #pragma unroll
     for (int k = 0; k < kPassUnroll; ++k) {
       const uint64_t i = r0 + (uint64_t)k * blockDim.x + threadIdx.x;
       c[k] = i < hi ? rs_class(addr[k], n[k]) : 0u;
-      pos[k] = c[k] ? atomicAdd(&base[c[k]], 1u) : 0u;
+      rank[k] = c[k] ? atomicAdd(&h[c[k]], 1u) : 0u;
+      odd |= (c[k] > (uint32_t)kRsBigBase && ((addr[k] | n[k]) & 3u)) ? 1 : 0;
     }
 #pragma unroll
     for (int k = 0; k < kPassUnroll; ++k) {
       const uint64_t i = r0 + (uint64_t)k * blockDim.x + threadIdx.x;
-      if (i >= hi) continue;
-      if (!c[k]) {
-        a.pos_of[i] = 0xFFFFFFFFu;
-        continue;
+      if (i >= hi || c[k]) continue;
+      uint32_t v = 0u;
+      if (n[k] >= 4u && n[k] <= kMaxLen) {
+        v = icrc_small(addr[k], n[k]);
+        if (a.verify) v = gload4_unaligned((uintptr_t)(addr[k] + n[k] - 4u)) == v ? 1u : 0u;
       }
-      const RsDesc d{(uint32_t)addr[k], (uint32_t)(addr[k] >> 32) | (n[k] << 16)};
-      const uint32_t bk = sbk[c[k]];
-      // streaming stores: the fold that follows reads these once, and dirty
-      // lines left in the caches would be written back into its read stream
-      __builtin_nontemporal_store(d.lo, &a.desc[pos[k]].lo);
-      __builtin_nontemporal_store(d.hi, &a.desc[pos[k]].hi);
-      __builtin_nontemporal_store(pos[k], &a.pos_of[i]);
-      const uint32_t end = send[c[k]];
-      if (pos[k] + 1 == end)  // the class's last packet pads its group with copies of itself
-        for (uint32_t p = end; (p - bk) & 7u; ++p) a.desc[p] = d;
+      a.out[i] = v;
+      a.pos_of[i] = 0xFFFFFFFFu;
     }
+  }
+  if (__syncthreads_or(odd) && threadIdx.x == 0) atomicOr(&a.ctr->odd, 1u);
+
+  // Block scan over the classes, one per thread (one barrier: each wave
+  // scans its 64 classes, then adds the totals of the waves before it).
+  const uint32_t t = threadIdx.x, wid = t >> 6;
+  const uint32_t cnt = t < (uint32_t)kRsClasses ? h[t] : 0u;
+  const bool big = t > (uint32_t)kRsBigBase && t < (uint32_t)kRsClasses;
+  const uint32_t L = big ? t - (uint32_t)kRsBigBase : 0u;
+  const uint32_t G = big ? (cnt + 7u) >> 3 : 0u;
+  const uint32_t Sm = big ? 0u : cnt;  // class 0 is never counted
+  const uint32_t f = (big && cnt) ? 1u : 0u;
+  const uint64_t W = (uint64_t)G * (4u * L + a.group_cost);
+  uint32_t ig = wave_scan(G), is = wave_scan(Sm), jf = wave_scan(f);
+  uint64_t iw = wave_scan(W);
+  if ((t & 63u) == 63u) {
+    wg[wid] = ig;
+    wsm[wid] = is;
+    wf[wid] = jf;
+    ww[wid] = iw;
+  }
+  __syncthreads();
+  for (uint32_t w = 0; w < wid; ++w) {  // wave-uniform
+    ig += wg[w];
+    is += wsm[w];
+    jf += wf[w];
+    iw += ww[w];
+  }
+  if (t == blockDim.x - 1) {  // block totals: reserve the ranges
+    const unsigned long long old =
+        ig ? atomicAdd(&a.ctr->pool, ((unsigned long long)iw << kRsGroupBits) | ig) : 0ull;
+    blk_g0 = (uint32_t)(old & ((1ull << kRsGroupBits) - 1u));
+    blk_s0 = old >> kRsGroupBits;
+    blk_small = is ? atomicAdd(&a.ctr->small, is) : 0u;
+    a.blk[blockIdx.x] = RsBlock{blk_g0, ig, ig ? jf : 0u, 0u, blk_s0, iw};
+  }
+  __syncthreads();
+  if (t < (uint32_t)kRsClasses) at[t] = big ? 8u * (blk_g0 + ig - G) : blk_small + is - Sm;
+  if (f) a.runs[(uint64_t)blockIdx.x * kRsRuns + (jf - 1u)] = RsRun{blk_g0 + ig - G, G, L, 0u, blk_s0 + iw - W};
+  __syncthreads();
+
+  auto place = [&](uint64_t r0) {
+#pragma unroll
+    for (int k = 0; k < kPassUnroll; ++k) {
+      const uint64_t i = r0 + (uint64_t)k * blockDim.x + threadIdx.x;
+      if (i >= hi || !c[k]) continue;
+      const RsDesc d{(uint32_t)addr[k], (uint32_t)(addr[k] >> 32) | (n[k] << 16)};
+      const bool bc = c[k] > (uint32_t)kRsBigBase;
+      const uint32_t p = at[c[k]] + rank[k];
+      RsDesc *D = bc ? a.bdesc : a.desc;
+      // streaming stores: the folds that follow read these once, and dirty
+      // lines left in the caches would be written back into their read stream
+      __builtin_nontemporal_store(d.lo, &D[p].lo);
+      __builtin_nontemporal_store(d.hi, &D[p].hi);
+      __builtin_nontemporal_store(bc ? a.small_cap + p : p, &a.pos_of[i]);
+      if (bc && rank[k] + 1u == h[c[k]])  // the class's last packet pads its run's last group with copies of itself
+        for (uint32_t q = p + 1u; q & 7u; ++q) a.bdesc[q] = d;
+    }
+  };
+  if (one) {  // block-uniform: the round's descriptors are still in registers
+    place(lo);
+    return;
+  }
+  for (uint64_t r0 = lo; r0 < hi; r0 += kPassUnroll * blockDim.x) {
+    load(r0);
+#pragma unroll
+    for (int k = 0; k < kPassUnroll; ++k) {
+      const uint64_t i = r0 + (uint64_t)k * blockDim.x + threadIdx.x;
+      c[k] = i < hi ? rs_class(addr[k], n[k]) : 0u;
+      rank[k] = c[k] ? atomicAdd(&cur[c[k]], 1u) : 0u;
+    }
+    place(r0);
   }
 }
 
 __global__ __launch_bounds__(256) void rsck_gather(RsckArgs a) {
-  // The class counters are dead now (plan, scatter and both folds have read
+  // The counters are dead now (the bucket pass and both folds have read
   // them): zero them for the next call on this workspace.
-  if (blockIdx.x == 0)
-    for (uint32_t t = threadIdx.x; t <= (uint32_t)kRsTicket; t += blockDim.x) a.counts[t] = 0u;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *a.ctr = RsCounters{0u, 0u, 0ull};
   constexpr int U = 4;  // packets per thread in flight at once
   const uint64_t T = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < a.count; i0 += U * T) {
@@ -425,23 +391,56 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   __syncthreads();
 
   // This wave's groups: those whose first line lies in its share of steps.
-  const RsPlan *P = a.plan;
-  const uint32_t nc = P->nc, NG = P->ngroups;
-  const uint64_t S = P->nsteps;
+  // The big pool: NG groups, S weighted work (the bucket pass's packed
+  // counter); block b's groups [g0, g0 + groups) hold work [s0, s0 + work),
+  // its runs split that range by class.
+  const unsigned long long pool = a.ctr->pool;
+  const uint32_t NG = (uint32_t)(pool & ((1ull << kRsGroupBits) - 1u));
+  const uint64_t S = pool >> kRsGroupBits;
   const uint64_t wave = (uint64_t)blockIdx.x * kWaves + wid;
   const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
   const uint64_t share = (S + nwaves - 1) / nwaves;
+  // First group whose work starts at or after x (within the run holding x):
+  // the pass block whose work range holds x (one ballot per 64 blocks), then
+  // its run (one ballot per 64 runs).
   auto first_group_at = [&](uint64_t x) -> uint32_t {
     if (x >= S) return NG;
-    uint32_t cnt = 0;
-    for (uint32_t b = 0; b < nc; b += 64) {
-      const uint32_t c = b + lane;
-      cnt += (uint32_t)__builtin_popcountll(__ballot(c < nc && P->s0[c < nc ? c : 0] <= x));
+    uint32_t b = 0;
+    for (uint32_t b0 = 0; b0 < a.nblk; b0 += 64) {
+      const uint32_t bb = b0 + lane;
+      bool in = false;
+      if (bb < a.nblk) {
+        const RsBlock B = a.blk[bb];
+        in = B.runs != 0u && B.s0 <= x && x - B.s0 < B.work;
+      }
+      const uint64_t m = __ballot(in);
+      if (m) {  // wave-uniform
+        b = b0 + (uint32_t)__builtin_ctzll(m);
+        break;
+      }
     }
-    const uint32_t c = __builtin_amdgcn_readfirstlane(cnt - 1u);  // s0[0] = 0 <= x
-    const uint32_t L = P->L[c], g0 = P->g0[c], gend = c + 1 < nc ? P->g0[c + 1] : NG;
-    const uint64_t w = 4u * L + a.group_cost;  // quarter line-steps
-    const uint64_t q = g0 + (x - P->s0[c] + w - 1) / w;
+    b = __builtin_amdgcn_readfirstlane(b);
+    const uint32_t nr = a.blk[b].runs;
+    const RsRun *R = a.runs + (uint64_t)b * kRsRuns;
+    uint32_t r = 0;
+    for (uint32_t r0 = 0; r0 < nr; r0 += 64) {
+      const uint32_t rr = r0 + lane;
+      bool in = false;
+      if (rr < nr) {
+        const RsRun Q = R[rr];
+        in = Q.s0 <= x && x - Q.s0 < (uint64_t)Q.groups * (4u * Q.L + a.group_cost);
+      }
+      const uint64_t m = __ballot(in);
+      if (m) {  // wave-uniform
+        r = r0 + (uint32_t)__builtin_ctzll(m);
+        break;
+      }
+    }
+    r = __builtin_amdgcn_readfirstlane(r);
+    const RsRun Q = R[r];
+    const uint64_t w = 4u * Q.L + a.group_cost;  // quarter line-steps
+    const uint64_t q = Q.g0 + (x - Q.s0 + w - 1) / w;
+    const uint32_t gend = Q.g0 + Q.groups < NG ? Q.g0 + Q.groups : NG;  // (never past the pool)
     return q < gend ? (uint32_t)q : gend;
   };
   const uint64_t x0 = wave * share < S ? wave * share : S;
@@ -470,7 +469,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
     uint64_t e = (uint64_t)b * 64u + lane;
     e = e < npos ? e : npos - 1;
     return *reinterpret_cast<const u32x2 __attribute__((address_space(1))) *>(
-        (uintptr_t)reinterpret_cast<const uint32_t *>(a.desc + e));
+        (uintptr_t)reinterpret_cast<const uint32_t *>(a.bdesc + e));
   };
   auto put_block = [&](uint32_t b, const u32x2 &v) {
     *reinterpret_cast<u32x2 *>(dring + (b & 1u) * kBlk + 2u * lane) = v;
@@ -553,7 +552,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   uint32_t round_q0 = q_begin;  // first group of the current round of result slots
   auto flush = [&](uint32_t q_stop) {  // groups [round_q0, q_stop) of the round
     const uint32_t valid = 8u * (q_stop - round_q0);
-    const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.res + 8ull * round_q0, 4u * valid);
+    const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.bres + 8ull * round_q0, 4u * valid);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the slot writes have landed
     if (ABL & 32) {
       r[1] ^= slots[lane] ^ slots[kSlots - 64 + lane];  // keep the slot reads
@@ -731,18 +730,18 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
     }
   }
   };
-  if (a.counts[kRsClasses] == 0)
+  if (a.ctr->odd == 0)
     fold_loop(std::true_type{});
   else
     fold_loop(std::false_type{});
   if (!(ABL & 16) && q_end != round_q0) flush(q_end);
-  if ((ABL & 48) && r[0] == 0x12345678u) a.res[0] = r[1];
+  if ((ABL & 48) && r[0] == 0x12345678u) a.bres[0] = r[1];
 }
 
 
 // =======================================================================
 // Small packets of the ragged path (<= kRsSmallL lines: the 64 / 256-byte
-// share of C4): ONE LANE PER PACKET, descriptors [0, *small_pos) of the
+// share of C4): ONE LANE PER PACKET, descriptors [0, ctr->small) of the
 // buckets.  8 lanes per packet (the fold above) is too coarse for them, and
 // the round-1 piece kernel (one 64-byte piece per lane; git history) paid a
 // GF(2) re-alignment, prefix XOR and end multiply per packet.  Here a lane folds its
@@ -863,7 +862,7 @@ struct SmallPk {
 __global__ __launch_bounds__(kBlock) void icrc_rsmall_kernel(RsckArgs a) {
   __shared__ uint32_t lds[kLdsWords];
   const uint32_t tab_v = table_entry(g_tab);
-  const uint32_t count = *a.small_pos;
+  const uint32_t count = a.ctr->small;
   table_store(lds, tab_v);
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63;
@@ -948,30 +947,39 @@ __global__ __launch_bounds__(kBlock) void icrc_rsmall_kernel(RsckArgs a) {
   }
 }
 
-uint64_t rs_workspace_bytes(uint64_t count) {
-  const uint64_t npos = count + 8ull * kRsClasses;
-  auto al = [](uint64_t b) { return (b + 255) & ~255ull; };
-  return 3 * al(4ull * kRsClasses) + al(sizeof(RsPlan)) + al(sizeof(RsDesc) * npos) + al(4 * count) + al(4 * npos) +
-         al(4ull * kRsClasses * kPassBlocks) + al(4);
+// Positions: the small pool [0, small_cap), the big pool after it; the big
+// pool holds every big packet plus at most 7 padding copies per run (a run
+// needs a packet: at most min(count, kRsRuns x pass blocks) runs).
+static uint64_t rs_small_cap(uint64_t count) { return (count + 7) & ~7ull; }
+static uint64_t rs_npos(uint64_t count) {
+  const uint64_t runs = count < (uint64_t)kRsRuns * kPassBlocks ? count : (uint64_t)kRsRuns * kPassBlocks;
+  return rs_small_cap(count) + ((count + 7 * runs + 7) & ~7ull);
 }
 
-hipError_t rs_zero_counters(void *ws, hipStream_t st) {  // counts is the workspace's first region
-  return hipMemsetAsync(ws, 0, 4ull * (kRsTicket + 1), st);
+uint64_t rs_workspace_bytes(uint64_t count) {
+  const uint64_t npos = rs_npos(count);
+  auto al = [](uint64_t b) { return (b + 255) & ~255ull; };
+  return al(sizeof(RsCounters)) + al(sizeof(RsBlock) * kPassBlocks) + al(sizeof(RsRun) * kRsRuns * kPassBlocks) +
+         al(sizeof(RsDesc) * npos) + al(4 * count) + al(4 * npos);
+}
+
+hipError_t rs_zero_counters(void *ws, hipStream_t st) {  // the counters are the workspace's first region
+  return hipMemsetAsync(ws, 0, sizeof(RsCounters), st);
 }
 
 void rs_bind_workspace(RsckArgs &a, void *ws) {
-  const uint64_t npos = a.count + 8ull * kRsClasses;
+  const uint64_t npos = rs_npos(a.count);
   auto al = [](uint64_t b) { return (b + 255) & ~255ull; };
   char *p = static_cast<char *>(ws);
-  a.counts = reinterpret_cast<uint32_t *>(p), p += al(4ull * kRsClasses);
-  a.cursor = reinterpret_cast<uint32_t *>(p), p += al(4ull * kRsClasses);
-  a.bucket = reinterpret_cast<uint32_t *>(p), p += al(4ull * kRsClasses);
-  a.plan = reinterpret_cast<RsPlan *>(p), p += al(sizeof(RsPlan));
+  a.ctr = reinterpret_cast<RsCounters *>(p), p += al(sizeof(RsCounters));
+  a.blk = reinterpret_cast<RsBlock *>(p), p += al(sizeof(RsBlock) * kPassBlocks);
+  a.runs = reinterpret_cast<RsRun *>(p), p += al(sizeof(RsRun) * kRsRuns * kPassBlocks);
   a.desc = reinterpret_cast<RsDesc *>(p), p += al(sizeof(RsDesc) * npos);
   a.pos_of = reinterpret_cast<uint32_t *>(p), p += al(4 * a.count);
-  a.res = reinterpret_cast<uint32_t *>(p), p += al(4 * npos);
-  a.hist = reinterpret_cast<uint32_t *>(p), p += al(4ull * kRsClasses * kPassBlocks);
-  a.small_pos = reinterpret_cast<uint32_t *>(p);
+  a.res = reinterpret_cast<uint32_t *>(p);
+  a.small_cap = (uint32_t)rs_small_cap(a.count);
+  a.bdesc = a.desc + a.small_cap;
+  a.bres = a.res + a.small_cap;
 }
 
 // Gather: one round of 4 packets per thread where the grid allows.
@@ -980,31 +988,27 @@ static int gather_grid(uint64_t count) {
   return (int)(want < 16384 ? (want ? want : 1) : 16384);
 }
 
-template <bool OFF, bool LEN>
-static void launch_passes_t(const RsckArgs &a, int pgrid, hipStream_t st) {
-  static_assert(kPassBlock == 1024, "the count pass's last workgroup runs the 1024-thread plan");
-  hipLaunchKernelGGL((rsck_count<OFF, LEN>), dim3(pgrid), dim3(kPassBlock), 0, st, a);
-  hipLaunchKernelGGL((rsck_scatter<OFF, LEN>), dim3(pgrid), dim3(kPassBlock), 0, st, a);
-}
-// count, plan, scatter
-static void launch_passes(const RsckArgs &a, int pgrid, hipStream_t st) {
-  if (a.off && a.len) launch_passes_t<true, true>(a, pgrid, st);
-  else if (a.off) launch_passes_t<true, false>(a, pgrid, st);
-  else if (a.len) launch_passes_t<false, true>(a, pgrid, st);
-  else launch_passes_t<false, false>(a, pgrid, st);
+static void launch_bucket(const RsckArgs &a, int pgrid, hipStream_t st) {
+  static_assert(kPassBlock == 1024 && kRsClasses <= kPassBlock, "one class per thread in the bucket pass's scan");
+  if (a.off && a.len) hipLaunchKernelGGL((rsck_bucket<true, true>), dim3(pgrid), dim3(kPassBlock), 0, st, a);
+  else if (a.off) hipLaunchKernelGGL((rsck_bucket<true, false>), dim3(pgrid), dim3(kPassBlock), 0, st, a);
+  else if (a.len) hipLaunchKernelGGL((rsck_bucket<false, true>), dim3(pgrid), dim3(kPassBlock), 0, st, a);
+  else hipLaunchKernelGGL((rsck_bucket<false, false>), dim3(pgrid), dim3(kPassBlock), 0, st, a);
 }
 
 hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, int gather_cap, hipStream_t st) {
   (void)hipGetLastError();  // a stale error of an earlier, unrelated HIP call must not fail this launch
   if (a.count == 0) return hipSuccess;
-  // a.counts (+ the misaligned flag) is zero here: zeroed when the workspace
-  // was allocated, and again by rsck_gather at the end of every call.
+  if (a.count > kRsMaxCount) return hipErrorInvalidValue;
+  // a.ctr is zero here: zeroed when the workspace was allocated, and again
+  // by rsck_gather at the end of every call.
   const uint64_t want = (a.count + kPassBlock - 1) / kPassBlock;
   int pgrid = (int)(want < kPassBlocks ? want : kPassBlocks);
   if (pass_cap > 0 && pass_cap < pgrid) pgrid = pass_cap;
-  launch_passes(a, pgrid, st);
+  a.nblk = (uint32_t)pgrid;
+  launch_bucket(a, pgrid, st);
   hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, st, a);
-  // the small region [0, *small_pos): one lane per packet
+  // the small pool [0, ctr->small): one lane per packet
   hipLaunchKernelGGL(icrc_rsmall_kernel, dim3(grid), dim3(kBlock), 0, st, a);
   int ggrid = gather_grid(a.count);
   if (gather_cap > 0 && gather_cap < ggrid) ggrid = gather_cap;

@@ -173,6 +173,44 @@ def test_ragged_work_split_does_not_change_results(ctx, ctx_env, gcost):
         np.testing.assert_array_equal(_host_u32(out), want)
 
 
+@pytest.mark.parametrize("pass_grid", [1, 3, 7])
+def test_ragged_bucket_pass_blocks_of_several_rounds(ctx, ctx_env, pass_grid):
+    """The bucket pass lays each pass block's packets out by class; a block
+    whose packets take several rounds (more than 8 per thread) counts them
+    first and re-reads them to place them.  Few pass blocks
+    (RICRC_RS_PASS_GRID) force that path: every size class (one-line, 2-3
+    line, long), short packets computed in the pass itself (n < 44), invalid
+    lengths, odd starts, in verify mode too -- and the session context after
+    (the counters must be left clean)."""
+    rng = np.random.default_rng(100 + pass_grid)
+    count = 30_000
+    lens = rng.choice(np.array([4, 20, 43, 44, 64, 100, 256, 1024, 1500, 4096, 9000], np.uint32), size=count)
+    gaps = rng.integers(0, 9, size=count).astype(np.uint64)
+    offs = np.zeros(count, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + gaps[:-1], dtype=np.uint64)
+    buf = rng.integers(0, 256, size=int(offs[-1] + lens[-1]) + 64, dtype=np.uint8)
+    bad = rng.choice(count, size=50, replace=False)
+    lens_dev = lens.copy()
+    lens_dev[bad] = 70000  # invalid: 0, as the status-less call documents
+    want = oracle_c.icrc_batch(buf, offsets=offs, lengths=lens, threads=16)
+    want[bad] = 0
+    d_buf, d_offs, d_lens = _dev(buf), _dev(offs), _dev(lens_dev)
+    for c in (ctx_env(RICRC_RS_PASS_GRID=pass_grid), ctx):
+        out = _out(count)
+        c.batch_device(d_buf, count, out, offsets=d_offs, lengths=d_lens, stream=_stream())
+        np.testing.assert_array_equal(_host_u32(out), want)
+    stamped, want_v, badset = buf.copy(), np.zeros(count, np.uint32), set(bad.tolist())
+    for i in range(0, count, 97):
+        if i not in badset:
+            stamped[int(offs[i]) + int(lens[i]) - 4:int(offs[i]) + int(lens[i])] = np.frombuffer(
+                int(want[i]).to_bytes(4, "little"), np.uint8)
+            want_v[i] = 1
+    out = _out(count)
+    ctx_env(RICRC_RS_PASS_GRID=pass_grid).batch_device(_dev(stamped), count, out, offsets=d_offs, lengths=d_lens,
+                                                       stream=_stream(), verify=True)
+    np.testing.assert_array_equal(_host_u32(out), want_v)
+
+
 def test_ragged_kernel_offsets_only_and_lengths_only(ctx):
     """Descriptor modes: offsets with a fixed length (stride - l3_offset), and
     per-packet lengths at a fixed stride."""

@@ -54,9 +54,9 @@ int main() {
   CK(rs_zero_counters(ws, 0));
   rs_bind_workspace(a, ws);
   const uint64_t want = (count + kPassBlock - 1) / kPassBlock;
-  launch_passes(a, (int)(want < kPassBlocks ? want : kPassBlocks), 0);
+  { a.nblk = (uint32_t)((int)(want < kPassBlocks ? want : kPassBlocks)); launch_bucket(a, (int)((int)(want < kPassBlocks ? want : kPassBlocks)), 0); }
   CK(hipDeviceSynchronize());
-  const uint64_t npos = count + 8ull * kRsClasses;
+  const uint64_t npos = rs_npos(count);
   std::vector<uint32_t> ref(npos), got(npos);
   auto check = [&](const char *nm) {
     CK(hipDeviceSynchronize());

@@ -46,7 +46,7 @@ int main(int argc, char **argv) {
     rs_bind_workspace(a, ws);
     const uint64_t want = (count + kPassBlock - 1) / kPassBlock;
     const int pgrid = (int)(want < kPassBlocks ? want : kPassBlocks);
-    launch_passes(a, pgrid, 0);
+    { a.nblk = (uint32_t)(pgrid); launch_bucket(a, (int)(pgrid), 0); }
     CK(hipDeviceSynchronize());
     char nm[128];
     for (int r = 0; r < 2; ++r) {
@@ -91,7 +91,7 @@ int main(int argc, char **argv) {
           // the counters (and the count pass's ticket) must start at zero: the
           // product's gather zeroes them, the variants above never ran it
           CK(rs_zero_counters(ws, 0));
-          launch_passes(a, pgrid, 0);
+          { a.nblk = (uint32_t)(pgrid); launch_bucket(a, (int)(pgrid), 0); }
           CK(hipEventRecord(f0, 0));
           hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, 0, a);
           CK(hipEventRecord(f1, 0));
@@ -130,7 +130,7 @@ int main(int argc, char **argv) {
       CK(rs_zero_counters(ws, 0));
       rs_bind_workspace(a, ws);
       const uint64_t want = (a.count + kPassBlock - 1) / kPassBlock;
-      launch_passes(a, (int)(want < kPassBlocks ? want : kPassBlocks), 0);
+      { a.nblk = (uint32_t)((int)(want < kPassBlocks ? want : kPassBlocks)); launch_bucket(a, (int)((int)(want < kPassBlocks ? want : kPassBlocks)), 0); }
       CK(hipDeviceSynchronize());
       for (int r = 0; r < 3; ++r) {
         rep("1 KiB full", timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, 0, a); }, 5), (double)bytes);

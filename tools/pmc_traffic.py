@@ -9,12 +9,12 @@ the bytes of a wide (16 B/lane) coalesced streaming read, so it is doubled;
 WRITE_SIZE is taken as reported.  Both are in KiB.
 
   (default)  the headline: 1 M x 4096 B, icrc_sck_kernel -> profiles/pmc_traffic.json
-  --mix      C4: the ragged pipeline's five kernels (count/plan, scatter, fold,
-             one-line, gather) summed per step -> profiles/pmc_traffic_mix.json.
-             The pass kernels read 8- and 4-byte descriptors, an access width
-             the guide's x2 is not calibrated for; the count pass reads exactly
-             12 B per packet, so its doubled FETCH_SIZE against that byte count
-             is reported as the check ("count_pass_fetch_over_descriptors").
+  --mix      C4: the ragged pipeline's four kernels (bucket, fold, one-line,
+             gather) summed per step -> profiles/pmc_traffic_mix.json.  The
+             bucket pass reads its 12 descriptor bytes per packet once, so its
+             doubled FETCH_SIZE against that byte count is reported as a check
+             of the x2 correction on scattered traffic
+             ("bucket_pass_fetch_over_descriptors").
 
 Copied into profiles/, the file is what bench.py reports as roofline.traffic
 when the workload and the kernel sources match (bench.kernel_source_hash).
@@ -29,7 +29,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-RAGGED_KERNELS = ("rsck_count", "rsck_scatter", "icrc_rsck_kernel", "icrc_rsmall_kernel", "rsck_gather")
+RAGGED_KERNELS = ("rsck_bucket", "icrc_rsck_kernel", "icrc_rsmall_kernel", "rsck_gather")
 
 
 def run_pass(counter, outdir, bench_args, match):
@@ -85,8 +85,8 @@ def main():
            "hbm_bytes_per_launch": hbm, "algorithmic_bytes_per_launch": alg,
            "traffic_over_algorithmic": hbm / alg}
     if a.mix:
-        cp = kernels["rsck_count"]["FETCH_SIZE_KiB"] * 2 * 1024
-        res["count_pass_fetch_over_descriptors"] = cp / (12.0 * count)
+        cp = kernels["rsck_bucket"]["FETCH_SIZE_KiB"] * 2 * 1024
+        res["bucket_pass_fetch_over_descriptors"] = cp / (12.0 * count)
         res["fold_fetch_over_its_lines"] = None  # filled by tools/pmc_summary.py when the line count is known
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     with open(a.out, "w") as f:
