@@ -13,9 +13,7 @@
 //                   small ones in a range of the small pool, big ones as runs
 //                   of whole 8-packet groups of one L in a range of the big
 //                   pool (block-local: no grid-wide count or plan, see the
-//                   kernel); packets too short for a RoCEv2 header
-//                   (4 <= n < 44) are computed right there by a scalar loop,
-//                   invalid lengths yield 0;
+//                   kernel);
 //  2. icrc_rsck_kernel  folds groups of 8 equal-L packets (L > kRsSmallL)
 //                   exactly like the SCK -- lane 8g+s owns slot s of every
 //                   line of packet g, four chains per lane, T_124..T_127
@@ -25,7 +23,9 @@
 //  3. icrc_rsmall_kernel folds the one-line packets (C4's 64 B; 8 lanes per
 //                   packet is too coarse for them) one lane per packet;
 //  4. rsck_gather   out[i] = res[pos(i)] (verify mode: the trailer compared
-//                   with it).
+//                   with it); packets too short for a RoCEv2 header
+//                   (4 <= n < 44) are computed here by a scalar loop, invalid
+//                   lengths yield 0.
 //
 // Lines are 128-byte aligned in memory (misaligned line grids measured 20 %
 // slower, tools/microbench/mb_lines.hip), so a packet's first and last line
@@ -91,8 +91,8 @@ __device__ uint32_t icrc_small(uint64_t addr, uint32_t n) {
 
 // Pass blocks own contiguous packet ranges.
 constexpr int kPassBlock = 1024;
-constexpr int kPassBlocks = 512;  // pass grid cap
-constexpr int kPassUnroll = 8;    // packets per thread whose descriptors are read at once
+constexpr int kPassBlocks = 256;  // pass grid cap: one 1024-thread block per CU, all resident at once
+constexpr int kPassUnroll = 16;   // packets per thread whose descriptors are read at once (C4: one round)
 __device__ __forceinline__ void pass_range(uint64_t count, uint64_t &lo, uint64_t &hi) {
   const uint64_t per = ((count + gridDim.x - 1) / gridDim.x + kPassBlock - 1) / kPassBlock * kPassBlock;
   lo = (uint64_t)blockIdx.x * per;
@@ -121,9 +121,9 @@ __device__ __forceinline__ T wave_scan(T v) {
 // block buckets its own packets --
 //   1. read the descriptors (kept in registers when the block's packets fit
 //      one round of kPassUnroll per thread: C4's 4 M packets on 512 blocks),
-//      classify, rank each packet in its class by an LDS atomic; packets
-//      that are not bucketed (n < 44: Sarwate loop; invalid lengths: 0) are
-//      done right here;
+//      classify, rank each packet in its class by an LDS atomic (packets
+//      that are not bucketed -- n < 44, invalid lengths -- are left to the
+//      gather pass);
 //   2. scan the block's class counts (one class per thread): small classes
 //      are laid out back to back, big classes as runs of whole groups;
 //   3. reserve the block's small range and its big range -- groups and
@@ -147,48 +147,48 @@ __global__ __launch_bounds__(kPassBlock) void rsck_bucket(RsckArgs a) {
     cur[t] = 0;
   }
   __syncthreads();
-  uint64_t lo, hi;
-  pass_range(a.count, lo, hi);
-  const bool one = hi - lo <= (uint64_t)kPassUnroll * blockDim.x;  // block-uniform
+  // 32-bit packet indexes (count <= kRsMaxCount): fewer registers per packet in flight
+  uint32_t lo, hi;
+  {
+    uint64_t l, h_;
+    pass_range(a.count, l, h_);
+    lo = (uint32_t)l;
+    hi = (uint32_t)h_;
+  }
+  const bool one = hi - lo <= (uint32_t)kPassUnroll * blockDim.x;  // block-uniform
   int odd = 0;  // a big packet not starting or ending on a 4-byte word
-  uint64_t addr[kPassUnroll];
-  uint32_t n[kPassUnroll], c[kPassUnroll], rank[kPassUnroll];
-  auto load = [&](uint64_t r0) {
-    // Raw loads first, unconditional (index clamped), arithmetic after: an
-    // add on a loaded value inside a per-packet branch made the compiler wait
-    // for each load before issuing the next.
+  // Per packet, packed (3 VGPRs): the descriptor words and class | rank << 10.
+  uint32_t dlo[kPassUnroll], dhi[kPassUnroll], cr[kPassUnroll];
+  // One round: descriptors of kPassUnroll packets per thread read at once
+  // (raw loads first, unconditional with the index clamped, arithmetic after:
+  // an add on a loaded value inside a per-packet branch made the compiler
+  // wait for each load before issuing the next), then classified and ranked
+  // in their class by an LDS atomic on `ctr` (h in the first sweep, cur in
+  // the second); packets that are not bucketed are marked for the gather.
+  auto round = [&](uint32_t r0, uint32_t *ctr, bool first) {
+    uint64_t addr[kPassUnroll];
+    uint32_t n[kPassUnroll];
 #pragma unroll
     for (int k = 0; k < kPassUnroll; ++k) {
-      uint64_t i = r0 + (uint64_t)k * blockDim.x + threadIdx.x;
+      uint32_t i = r0 + (uint32_t)k * blockDim.x + threadIdx.x;
       i = i < hi ? i : hi - 1;
-      addr[k] = OFF ? a.off[i] : i * a.stride;
+      addr[k] = OFF ? a.off[i] : (uint64_t)i * a.stride;
       n[k] = LEN ? a.len[i] : a.fixed_len;
     }
 #pragma unroll
-    for (int k = 0; k < kPassUnroll; ++k) addr[k] += (uint64_t)(uintptr_t)a.base + a.l3_offset;
+    for (int k = 0; k < kPassUnroll; ++k) {
+      const uint32_t i = r0 + (uint32_t)k * blockDim.x + threadIdx.x;
+      const uint64_t ad = addr[k] + (uint64_t)(uintptr_t)a.base + a.l3_offset;
+      const uint32_t c = i < hi ? rs_class(ad, n[k]) : 0u;
+      const uint32_t rk = c ? atomicAdd(&ctr[c], 1u) : 0u;
+      odd |= (c > (uint32_t)kRsBigBase && ((ad | n[k]) & 3u)) ? 1 : 0;
+      if (first && i < hi && !c) a.pos_of[i] = 0xFFFFFFFFu;  // the gather pass computes it
+      dlo[k] = (uint32_t)ad;
+      dhi[k] = (uint32_t)(ad >> 32) | (n[k] << 16);
+      cr[k] = c | (rk << 10);
+    }
   };
-  for (uint64_t r0 = lo; r0 < hi; r0 += kPassUnroll * blockDim.x) {  // block-uniform
-    load(r0);
-#pragma unroll
-    for (int k = 0; k < kPassUnroll; ++k) {
-      const uint64_t i = r0 + (uint64_t)k * blockDim.x + threadIdx.x;
-      c[k] = i < hi ? rs_class(addr[k], n[k]) : 0u;
-      rank[k] = c[k] ? atomicAdd(&h[c[k]], 1u) : 0u;
-      odd |= (c[k] > (uint32_t)kRsBigBase && ((addr[k] | n[k]) & 3u)) ? 1 : 0;
-    }
-#pragma unroll
-    for (int k = 0; k < kPassUnroll; ++k) {
-      const uint64_t i = r0 + (uint64_t)k * blockDim.x + threadIdx.x;
-      if (i >= hi || c[k]) continue;
-      uint32_t v = 0u;
-      if (n[k] >= 4u && n[k] <= kMaxLen) {
-        v = icrc_small(addr[k], n[k]);
-        if (a.verify) v = gload4_unaligned((uintptr_t)(addr[k] + n[k] - 4u)) == v ? 1u : 0u;
-      }
-      a.out[i] = v;
-      a.pos_of[i] = 0xFFFFFFFFu;
-    }
-  }
+  for (uint32_t r0 = lo; r0 < hi; r0 += kPassUnroll * blockDim.x) round(r0, h, true);  // block-uniform
   if (__syncthreads_or(odd) && threadIdx.x == 0) atomicOr(&a.ctr->odd, 1u);
 
   // Block scan over the classes, one per thread (one barrier: each wave
@@ -229,21 +229,22 @@ __global__ __launch_bounds__(kPassBlock) void rsck_bucket(RsckArgs a) {
   if (f) a.runs[(uint64_t)blockIdx.x * kRsRuns + (jf - 1u)] = RsRun{blk_g0 + ig - G, G, L, 0u, blk_s0 + iw - W};
   __syncthreads();
 
-  auto place = [&](uint64_t r0) {
+  auto place = [&](uint32_t r0) {
 #pragma unroll
     for (int k = 0; k < kPassUnroll; ++k) {
-      const uint64_t i = r0 + (uint64_t)k * blockDim.x + threadIdx.x;
-      if (i >= hi || !c[k]) continue;
-      const RsDesc d{(uint32_t)addr[k], (uint32_t)(addr[k] >> 32) | (n[k] << 16)};
-      const bool bc = c[k] > (uint32_t)kRsBigBase;
-      const uint32_t p = at[c[k]] + rank[k];
+      const uint32_t i = r0 + (uint32_t)k * blockDim.x + threadIdx.x;
+      const uint32_t c = cr[k] & 1023u, rk = cr[k] >> 10;
+      if (i >= hi || !c) continue;
+      const RsDesc d{dlo[k], dhi[k]};
+      const bool bc = c > (uint32_t)kRsBigBase;
+      const uint32_t p = at[c] + rk;
       RsDesc *D = bc ? a.bdesc : a.desc;
       // streaming stores: the folds that follow read these once, and dirty
       // lines left in the caches would be written back into their read stream
       __builtin_nontemporal_store(d.lo, &D[p].lo);
       __builtin_nontemporal_store(d.hi, &D[p].hi);
       __builtin_nontemporal_store(bc ? a.small_cap + p : p, &a.pos_of[i]);
-      if (bc && rank[k] + 1u == h[c[k]])  // the class's last packet pads its run's last group with copies of itself
+      if (bc && rk + 1u == h[c])  // the class's last packet pads its run's last group with copies of itself
         for (uint32_t q = p + 1u; q & 7u; ++q) a.bdesc[q] = d;
     }
   };
@@ -251,14 +252,8 @@ __global__ __launch_bounds__(kPassBlock) void rsck_bucket(RsckArgs a) {
     place(lo);
     return;
   }
-  for (uint64_t r0 = lo; r0 < hi; r0 += kPassUnroll * blockDim.x) {
-    load(r0);
-#pragma unroll
-    for (int k = 0; k < kPassUnroll; ++k) {
-      const uint64_t i = r0 + (uint64_t)k * blockDim.x + threadIdx.x;
-      c[k] = i < hi ? rs_class(addr[k], n[k]) : 0u;
-      rank[k] = c[k] ? atomicAdd(&cur[c[k]], 1u) : 0u;
-    }
+  for (uint32_t r0 = lo; r0 < hi; r0 += kPassUnroll * blockDim.x) {
+    round(r0, cur, false);
     place(r0);
   }
 }
@@ -278,7 +273,19 @@ __global__ __launch_bounds__(256) void rsck_gather(RsckArgs a) {
 #pragma unroll
     for (int k = 0; k < U; ++k) {
       const uint64_t i = i0 + k * T;
-      if (p[k] == 0xFFFFFFFFu) continue;  // past the end, or done by the count pass
+      if (i >= a.count) break;
+      if (p[k] == 0xFFFFFFFFu) {  // not bucketed: n < 44 (Sarwate loop here) or an invalid length (0)
+        uint64_t addr;
+        uint32_t n;
+        rs_packet(a, i, addr, n);
+        uint32_t v = 0u;
+        if (n >= 4u && n <= kMaxLen) {
+          v = icrc_small(addr, n);
+          if (a.verify) v = gload4_unaligned((uintptr_t)(addr + n - 4u)) == v ? 1u : 0u;
+        }
+        a.out[i] = v;
+        continue;
+      }
       if (a.verify) {  // out = trailer holds the ICRC
         uint64_t addr;
         uint32_t n;
