@@ -46,8 +46,7 @@ struct Knobs {
   int sck_grid = 0;        // RICRC_SCK_GRID: cap the strided-chain grid (tests: many groups per wave)
   int rsck_grid = 0;       // RICRC_RSCK_GRID: cap the ragged fold grid (tests)
   uint32_t gcost = 0;      // RICRC_RS_GCOST: the ragged fold's per-group cost, quarter lines (0: kRsGroupCost)
-  int pass_grid = 0;       // RICRC_RS_PASS_GRID: cap the ragged count / scatter pass grid (schedule studies)
-  int gather_grid = 0;     // RICRC_RS_GATHER_GRID: cap the ragged gather pass grid (schedule studies)
+  int pass_grid = 0;       // RICRC_RS_PASS_GRID: cap the ragged bucket / gather pass grid (schedule studies)
   long fail_chunk = -1;    // RICRC_FAIL_CHUNK: the next ricrc_batch_host fails after queueing chunk k (tests; once)
   int host_threads = 16;   // RICRC_HOST_THREADS: CPU copy threads of ricrc_batch_host
 };
@@ -311,7 +310,7 @@ int launch_rsck_range(Dev &d, const uint8_t *base, const uint64_t *off, const ui
   rs_bind_workspace(k, ws->p);
   int rgrid = d.n_cu;
   if (d.knobs.rsck_grid > 0) rgrid = std::min(rgrid, d.knobs.rsck_grid);
-  const hipError_t e = launch_rsck(k, rgrid, d.knobs.pass_grid, d.knobs.gather_grid, st);
+  const hipError_t e = launch_rsck(k, rgrid, d.knobs.pass_grid, st);
   if (e != hipSuccess) ws->dirty = true;
   const hipError_t e2 = hipEventRecord(ws->done, st);
   return hip_err(e != hipSuccess ? e : e2);
@@ -576,7 +575,6 @@ Knobs read_knobs() {
   k.rsck_grid = (int)std::max(0L, num("RICRC_RSCK_GRID", 0));
   k.gcost = (uint32_t)std::min(1024L, std::max(0L, num("RICRC_RS_GCOST", 0)));  // the packed work counter's range
   k.pass_grid = (int)std::max(0L, num("RICRC_RS_PASS_GRID", 0));
-  k.gather_grid = (int)std::max(0L, num("RICRC_RS_GATHER_GRID", 0));
   k.fail_chunk = num("RICRC_FAIL_CHUNK", -1);
   const unsigned hw = std::thread::hardware_concurrency();
   k.host_threads = (int)std::max(1L, std::min(64L, num("RICRC_HOST_THREADS", (long)std::min(16u, std::max(1u, hw)))));

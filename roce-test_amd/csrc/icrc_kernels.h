@@ -74,9 +74,11 @@ struct RsCounters {
   uint32_t small;              // small-pool packets
   unsigned long long pool;     // big pool: groups | work << kRsGroupBits
 };
-struct RsBlock {               // pass block b's big-pool range (runs == 0: none)
-  uint32_t g0, groups, runs, pad;
-  uint64_t s0, work;
+struct RsBlock {               // pass block b's ranges (runs == 0: no big packets)
+  uint32_t g0, groups, runs;   // big pool: groups [g0, g0 + groups), its runs
+  uint32_t small0, small;      // small pool: positions [small0, small0 + small)
+  uint32_t staged;             // 1: pos_of holds positions in the block's layout (small range | big range)
+  uint64_t s0, work;           // big pool: weighted work [s0, s0 + work)
 };
 struct RsRun {                 // one class of one pass block: groups [g0, g0 + groups) of L lines
   uint32_t g0, groups, L, pad;
@@ -99,7 +101,8 @@ struct RsckArgs {
   RsRun *runs;          // [pass blocks][kRsRuns]
   RsDesc *desc;         // small pool [0, count) | big pool [small_cap, ...) (positions)
   RsDesc *bdesc;        // desc + small_cap: the big pool, group q at 8 q
-  uint32_t *pos_of;     // [count] position of packet i, or ~0 (written by the bucket pass)
+  uint32_t *pos_of;     // [count] position of packet i (in its pool, or in its block's layout when the
+                        // block is staged), or ~0 (written by the bucket pass)
   uint32_t *res;        // results by position, like desc
   uint32_t *bres;       // res + small_cap
   uint32_t small_cap;   // count rounded up to 8
@@ -132,7 +135,7 @@ hipError_t rs_zero_counters(void *ws, hipStream_t st);
 // count <= kRsMaxCount (the host cuts larger batches: the big pool's group
 // count must fit kRsGroupBits).
 constexpr uint64_t kRsMaxCount = 1ull << 28;
-hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, int gather_cap, hipStream_t st);  // caps: 0 = default
+hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, hipStream_t st);  // pass_cap: 0 = default
 
 struct SynthArgs {
   uint8_t *buf;

@@ -120,7 +120,7 @@ __device__ __forceinline__ T wave_scan(T v) {
 // groups of 8 equal-L packets and a work prefix in group order: so each
 // block buckets its own packets --
 //   1. read the descriptors (kept in registers when the block's packets fit
-//      one round of kPassUnroll per thread: C4's 4 M packets on 512 blocks),
+//      one round of kPassUnroll per thread: C4's 4 M packets on 256 blocks),
 //      classify, rank each packet in its class by an LDS atomic (packets
 //      that are not bucketed -- n < 44, invalid lengths -- are left to the
 //      gather pass);
@@ -132,16 +132,28 @@ __device__ __forceinline__ T wave_scan(T v) {
 //      RsRun) for the fold's work split;
 //   4. write each descriptor to its position (and pos_of[i]); the packet
 //      ranked last in its class pads the run's last group with copies of
-//      itself.
+//      itself.  When the block's packets fit one round, the block's layout
+//      is built in LDS first and leaves in coalesced 8-byte stores: its
+//      small range and its big range are each contiguous in the pools, so
+//      LDS entry j maps to a pool position by one offset.  (Stored straight
+//      from the registers, every wave scattered 4-byte stores over its
+//      classes' ranges: 25 of the pass's 46 us on C4, against 5 us
+//      coalesced; tools/microbench/bucket_abl.hip.)
 // Blocks whose packets take several rounds re-read them for step 4 (ranks
-// from a second LDS cursor: any order of ranks is a valid layout).
-template <bool OFF, bool LEN>
+// from a second LDS cursor: any order of ranks is a valid layout) and store
+// from the registers.
+// ABL (timing-only ablations, tools/microbench/bucket_abl.hip): 1 stop after
+// the ranking round, 2 no LDS atomics (rank 0), 4 stop after the reservation,
+// 8 no pos_of stores, 16 no descriptor stores, 32 no LDS staging.
+constexpr uint32_t kStage = kPassUnroll * kPassBlock + 512;  // a round's packets + room for group padding
+template <bool OFF, bool LEN, int ABL = 0>
 __global__ __launch_bounds__(kPassBlock) void rsck_bucket(RsckArgs a) {
   __shared__ uint32_t h[kRsClasses], at[kRsClasses], cur[kRsClasses];
   __shared__ uint32_t wg[16], wsm[16], wf[16];
   __shared__ uint64_t ww[16];
-  __shared__ uint32_t blk_g0, blk_small;
+  __shared__ uint32_t blk_g0, blk_small, blk_stot, blk_total;
   __shared__ uint64_t blk_s0;
+  __shared__ uint64_t stage[kStage];  // the block's layout: small range | big range (132 KiB)
   for (int t = threadIdx.x; t < kRsClasses; t += blockDim.x) {
     h[t] = 0;
     cur[t] = 0;
@@ -180,7 +192,7 @@ __global__ __launch_bounds__(kPassBlock) void rsck_bucket(RsckArgs a) {
       const uint32_t i = r0 + (uint32_t)k * blockDim.x + threadIdx.x;
       const uint64_t ad = addr[k] + (uint64_t)(uintptr_t)a.base + a.l3_offset;
       const uint32_t c = i < hi ? rs_class(ad, n[k]) : 0u;
-      const uint32_t rk = c ? atomicAdd(&ctr[c], 1u) : 0u;
+      const uint32_t rk = (c && !(ABL & 2)) ? atomicAdd(&ctr[c], 1u) : 0u;
       odd |= (c > (uint32_t)kRsBigBase && ((ad | n[k]) & 3u)) ? 1 : 0;
       if (first && i < hi && !c) a.pos_of[i] = 0xFFFFFFFFu;  // the gather pass computes it
       dlo[k] = (uint32_t)ad;
@@ -190,6 +202,13 @@ __global__ __launch_bounds__(kPassBlock) void rsck_bucket(RsckArgs a) {
   };
   for (uint32_t r0 = lo; r0 < hi; r0 += kPassUnroll * blockDim.x) round(r0, h, true);  // block-uniform
   if (__syncthreads_or(odd) && threadIdx.x == 0) atomicOr(&a.ctr->odd, 1u);
+  if (ABL & 1) {  // keep the round's results live
+    uint32_t x = 0;
+#pragma unroll
+    for (int k = 0; k < kPassUnroll; ++k) x ^= cr[k] ^ dlo[k] ^ dhi[k];
+    if (x == 0x9E3779B9u) a.pos_of[threadIdx.x] = x;
+    return;
+  }
 
   // Block scan over the classes, one per thread (one barrier: each wave
   // scans its 64 classes, then adds the totals of the waves before it).
@@ -222,12 +241,26 @@ __global__ __launch_bounds__(kPassBlock) void rsck_bucket(RsckArgs a) {
     blk_g0 = (uint32_t)(old & ((1ull << kRsGroupBits) - 1u));
     blk_s0 = old >> kRsGroupBits;
     blk_small = is ? atomicAdd(&a.ctr->small, is) : 0u;
-    a.blk[blockIdx.x] = RsBlock{blk_g0, ig, ig ? jf : 0u, 0u, blk_s0, iw};
+    blk_stot = is;
+    blk_total = is + 8u * ig;
+    const bool st = !(ABL & 32) && one && is + 8u * ig <= kStage;
+    a.blk[blockIdx.x] = RsBlock{blk_g0, ig, ig ? jf : 0u, blk_small, is, st ? 1u : 0u, blk_s0, iw};
   }
   __syncthreads();
-  if (t < (uint32_t)kRsClasses) at[t] = big ? 8u * (blk_g0 + ig - G) : blk_small + is - Sm;
+  const uint32_t Stot = blk_stot, total = blk_total;
+  const bool staged = !(ABL & 32) && one && total <= kStage;  // block-uniform
+  // at[c]: the class's first position -- in the LDS layout when staged, else in its pool
+  if (t < (uint32_t)kRsClasses)
+    at[t] = staged ? (big ? Stot + 8u * (ig - G) : is - Sm) : big ? 8u * (blk_g0 + ig - G) : blk_small + is - Sm;
   if (f) a.runs[(uint64_t)blockIdx.x * kRsRuns + (jf - 1u)] = RsRun{blk_g0 + ig - G, G, L, 0u, blk_s0 + iw - W};
   __syncthreads();
+  if (ABL & 4) {
+    uint32_t x = 0;
+#pragma unroll
+    for (int k = 0; k < kPassUnroll; ++k) x ^= cr[k] ^ dlo[k] ^ dhi[k];
+    if (x == 0x9E3779B9u) a.pos_of[threadIdx.x] = x;
+    return;
+  }
 
   auto place = [&](uint32_t r0) {
 #pragma unroll
@@ -241,13 +274,41 @@ __global__ __launch_bounds__(kPassBlock) void rsck_bucket(RsckArgs a) {
       RsDesc *D = bc ? a.bdesc : a.desc;
       // streaming stores: the folds that follow read these once, and dirty
       // lines left in the caches would be written back into their read stream
-      __builtin_nontemporal_store(d.lo, &D[p].lo);
-      __builtin_nontemporal_store(d.hi, &D[p].hi);
-      __builtin_nontemporal_store(bc ? a.small_cap + p : p, &a.pos_of[i]);
+      if (!(ABL & 16)) {
+        __builtin_nontemporal_store(d.lo, &D[p].lo);
+        __builtin_nontemporal_store(d.hi, &D[p].hi);
+      }
+      if (!(ABL & 8)) __builtin_nontemporal_store(bc ? a.small_cap + p : p, &a.pos_of[i]);
       if (bc && rk + 1u == h[c])  // the class's last packet pads its run's last group with copies of itself
         for (uint32_t q = p + 1u; q & 7u; ++q) a.bdesc[q] = d;
     }
   };
+  if (staged) {  // block-uniform: the round's descriptors are still in registers
+    const uint32_t big0 = 8u * blk_g0, small0 = blk_small;
+#pragma unroll
+    for (int k = 0; k < kPassUnroll; ++k) {
+      const uint32_t i = lo + (uint32_t)k * blockDim.x + threadIdx.x;
+      const uint32_t c = cr[k] & 1023u, rk = cr[k] >> 10;
+      if (i >= hi || !c) continue;
+      const uint64_t d = ((uint64_t)dhi[k] << 32) | dlo[k];
+      const bool bc = c > (uint32_t)kRsBigBase;
+      const uint32_t lp = at[c] + rk;
+      stage[lp] = d;
+      if (!(ABL & 8)) __builtin_nontemporal_store(lp, &a.pos_of[i]);  // the gather maps the block's layout back
+      if (bc && rk + 1u == h[c])  // the class's last packet pads its run's last group with copies of itself
+        for (uint32_t q = lp + 1u; (q - Stot) & 7u; ++q) stage[q] = d;
+    }
+    __syncthreads();
+    if (ABL & 16) return;
+    uint64_t *sm = reinterpret_cast<uint64_t *>(a.desc) + small0;
+    uint64_t *bg = reinterpret_cast<uint64_t *>(a.bdesc) + big0 - Stot;
+    // streaming stores: the folds that follow read these once, and dirty
+    // lines left in the caches would be written back into their read stream
+#pragma unroll 4
+    for (uint32_t j = threadIdx.x; j < total; j += blockDim.x)
+      __builtin_nontemporal_store(stage[j], (j < Stot ? sm : bg) + j);
+    return;
+  }
   if (one) {  // block-uniform: the round's descriptors are still in registers
     place(lo);
     return;
@@ -258,41 +319,90 @@ __global__ __launch_bounds__(kPassBlock) void rsck_bucket(RsckArgs a) {
   }
 }
 
-__global__ __launch_bounds__(256) void rsck_gather(RsckArgs a) {
+// out[i] for packet i, which the bucket pass left to the gather (n < 44:
+// Sarwate loop here; an invalid length: 0), or from its result v.
+__device__ __forceinline__ uint32_t gather_one(const RsckArgs &a, uint64_t i, uint32_t p, uint32_t v) {
+  if (p == 0xFFFFFFFFu) {
+    uint64_t addr;
+    uint32_t n;
+    rs_packet(a, i, addr, n);
+    v = 0u;
+    if (n >= 4u && n <= kMaxLen) {
+      v = icrc_small(addr, n);
+      if (a.verify) v = gload4_unaligned((uintptr_t)(addr + n - 4u)) == v ? 1u : 0u;
+    }
+    return v;
+  }
+  if (a.verify) {  // out = trailer holds the ICRC
+    uint64_t addr;
+    uint32_t n;
+    rs_packet(a, i, addr, n);
+    v = gload4_unaligned((uintptr_t)(addr + n - 4u)) == v ? 1u : 0u;
+  }
+  return v;
+}
+
+// Gather: block b serves pass block b's packets.  A staged block's results
+// sit in two contiguous ranges (its small range, its big range): they are
+// read coalesced into LDS in the block's layout order and pos_of indexes
+// that copy, instead of one 4-byte read per packet scattered over the class
+// runs of the pools.
+__global__ __launch_bounds__(kPassBlock) void rsck_gather(RsckArgs a) {
+  __shared__ uint32_t lres[kStage];
   // The counters are dead now (the bucket pass and both folds have read
   // them): zero them for the next call on this workspace.
   if (blockIdx.x == 0 && threadIdx.x == 0) *a.ctr = RsCounters{0u, 0u, 0ull};
+  uint32_t lo, hi;
+  {
+    uint64_t l, h_;
+    pass_range(a.count, l, h_);
+    lo = (uint32_t)l;
+    hi = (uint32_t)h_;
+  }
+  const RsBlock B = a.blk[blockIdx.x];
   constexpr int U = 4;  // packets per thread in flight at once
-  const uint64_t T = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < a.count; i0 += U * T) {
+  if (B.staged) {  // block-uniform (a staged block's packets fit one round: hi - lo <= kPassUnroll x blockDim)
+    // every load of the block issued before the barrier: the positions, then
+    // the results into LDS
+    uint32_t p[kPassUnroll];
+#pragma unroll
+    for (int k = 0; k < kPassUnroll; ++k) {
+      const uint32_t i = lo + (uint32_t)k * blockDim.x + threadIdx.x;
+      p[k] = i < hi ? __builtin_nontemporal_load(a.pos_of + i) : 0xFFFFFFFFu;
+    }
+    const uint32_t total = B.small + 8u * B.groups;
+    const uint32_t *rs = a.res + B.small0, *rb = a.bres + 8ull * B.g0 - B.small;
+    constexpr int R = (kStage + kPassBlock - 1) / kPassBlock;
+    uint32_t v[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      const uint32_t j = (uint32_t)k * blockDim.x + threadIdx.x;
+      v[k] = j < total ? __builtin_nontemporal_load((j < B.small ? rs : rb) + j) : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      const uint32_t j = (uint32_t)k * blockDim.x + threadIdx.x;
+      if (j < total) lres[j] = v[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kPassUnroll; ++k) {
+      const uint32_t i = lo + (uint32_t)k * blockDim.x + threadIdx.x;
+      if (i < hi) __builtin_nontemporal_store(gather_one(a, i, p[k], p[k] != 0xFFFFFFFFu ? lres[p[k]] : 0u), a.out + i);
+    }
+    return;
+  }
+  for (uint32_t i0 = lo + threadIdx.x; i0 < hi; i0 += U * blockDim.x) {
     uint32_t p[U], v[U];
 #pragma unroll
-    for (int k = 0; k < U; ++k) p[k] = i0 + k * T < a.count ? a.pos_of[i0 + k * T] : 0xFFFFFFFFu;
+    for (int k = 0; k < U; ++k) p[k] = i0 + k * blockDim.x < hi ? a.pos_of[i0 + k * blockDim.x] : 0xFFFFFFFFu;
 #pragma unroll
     for (int k = 0; k < U; ++k) v[k] = p[k] != 0xFFFFFFFFu ? a.res[p[k]] : 0u;
 #pragma unroll
     for (int k = 0; k < U; ++k) {
-      const uint64_t i = i0 + k * T;
-      if (i >= a.count) break;
-      if (p[k] == 0xFFFFFFFFu) {  // not bucketed: n < 44 (Sarwate loop here) or an invalid length (0)
-        uint64_t addr;
-        uint32_t n;
-        rs_packet(a, i, addr, n);
-        uint32_t v = 0u;
-        if (n >= 4u && n <= kMaxLen) {
-          v = icrc_small(addr, n);
-          if (a.verify) v = gload4_unaligned((uintptr_t)(addr + n - 4u)) == v ? 1u : 0u;
-        }
-        a.out[i] = v;
-        continue;
-      }
-      if (a.verify) {  // out = trailer holds the ICRC
-        uint64_t addr;
-        uint32_t n;
-        rs_packet(a, i, addr, n);
-        v[k] = gload4_unaligned((uintptr_t)(addr + n - 4u)) == v[k] ? 1u : 0u;
-      }
-      a.out[i] = v[k];
+      const uint32_t i = i0 + k * blockDim.x;
+      if (i >= hi) break;
+      a.out[i] = gather_one(a, i, p[k], v[k]);
     }
   }
 }
@@ -989,12 +1099,6 @@ void rs_bind_workspace(RsckArgs &a, void *ws) {
   a.bres = a.res + a.small_cap;
 }
 
-// Gather: one round of 4 packets per thread where the grid allows.
-static int gather_grid(uint64_t count) {
-  const uint64_t want = (count + 1023) / 1024;
-  return (int)(want < 16384 ? (want ? want : 1) : 16384);
-}
-
 static void launch_bucket(const RsckArgs &a, int pgrid, hipStream_t st) {
   static_assert(kPassBlock == 1024 && kRsClasses <= kPassBlock, "one class per thread in the bucket pass's scan");
   if (a.off && a.len) hipLaunchKernelGGL((rsck_bucket<true, true>), dim3(pgrid), dim3(kPassBlock), 0, st, a);
@@ -1003,7 +1107,7 @@ static void launch_bucket(const RsckArgs &a, int pgrid, hipStream_t st) {
   else hipLaunchKernelGGL((rsck_bucket<false, false>), dim3(pgrid), dim3(kPassBlock), 0, st, a);
 }
 
-hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, int gather_cap, hipStream_t st) {
+hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, hipStream_t st) {
   (void)hipGetLastError();  // a stale error of an earlier, unrelated HIP call must not fail this launch
   if (a.count == 0) return hipSuccess;
   if (a.count > kRsMaxCount) return hipErrorInvalidValue;
@@ -1017,9 +1121,8 @@ hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, int gather_cap, hipS
   hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, st, a);
   // the small pool [0, ctr->small): one lane per packet
   hipLaunchKernelGGL(icrc_rsmall_kernel, dim3(grid), dim3(kBlock), 0, st, a);
-  int ggrid = gather_grid(a.count);
-  if (gather_cap > 0 && gather_cap < ggrid) ggrid = gather_cap;
-  hipLaunchKernelGGL(rsck_gather, dim3(ggrid), dim3(256), 0, st, a);
+  // the gather's blocks are the bucket pass's (block b serves pass block b's packets)
+  hipLaunchKernelGGL(rsck_gather, dim3(pgrid), dim3(kPassBlock), 0, st, a);
   return hipGetLastError();
 }
 
