@@ -296,14 +296,22 @@ int launch_rsck_range(Dev &d, const uint8_t *base, const uint64_t *off, const ui
   k.group_cost = d.knobs.gcost ? d.knobs.gcost : kRsGroupCost;
   k.out = out;
   k.tzb = d.d_tzb;
-  const uint32_t xi = gf_xinv8n(4);
-  const uint32_t xi2 = gf_xinv8n(8), xi3 = gf_xinv8n(12);
-  for (int j = 0; j < 32; ++j) {
-    k.XB[j] = gf_mul(xi, 1u << j);
-    k.XB2[j] = gf_mul(xi2, 1u << j);
-    k.XB3[j] = gf_mul(xi3, 1u << j);
-  }
-  for (int s = 0; s < 8; ++s) k.QS[s] = gf_xinv8n(16ull * s);
+  // GF(2) constants of the fold's finish (the same for every call)
+  static const RsckArgs kc = [] {
+    RsckArgs c{};
+    const uint32_t xi = gf_xinv8n(4), xi2 = gf_xinv8n(8), xi3 = gf_xinv8n(12);
+    for (int j = 0; j < 32; ++j) {
+      c.XB[j] = gf_mul(xi, 1u << j);
+      c.XB2[j] = gf_mul(xi2, 1u << j);
+      c.XB3[j] = gf_mul(xi3, 1u << j);
+    }
+    for (int s = 0; s < 8; ++s) c.QS[s] = gf_xinv8n(16ull * s);
+    return c;
+  }();
+  memcpy(k.XB, kc.XB, sizeof k.XB);
+  memcpy(k.XB2, kc.XB2, sizeof k.XB2);
+  memcpy(k.XB3, kc.XB3, sizeof k.XB3);
+  memcpy(k.QS, kc.QS, sizeof k.QS);
   Dev::Ws *ws = nullptr;
   const int wrc = ragged_ws(d, st, rs_workspace_bytes(count), &ws);
   if (wrc) return wrc;

@@ -428,7 +428,9 @@ __device__ __forceinline__ uint32_t edge_word(uint32_t w, int rel, int M) {
 // fold, 2 no finish, 4 descriptors by arithmetic (uniform batch in natural
 // order: packet 8 q + g at base + (8 q + g) stride, no descriptor ring),
 // 8 no edge masks, 16 no result slots / stores, 32 no global stores (slots kept),
-// 512 (with 2) 192 result slots, 1024 / 2048 / 4096 result stores nt / default / sc0 sc1.
+// 512 (with 2) 192 result slots, 1024 / 2048 / 4096 result stores nt / default / sc0 sc1,
+// 8192 per-wave s_memrealtime start / end stamps, groups and first group into a.out
+// (4 words per wave; tools/microbench/bucket_abl.hip).
 template <int ABL>
 __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   // Result slots per wave (a round of 8 groups leaves in one store; a store
@@ -562,6 +564,13 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   };
   const uint64_t x0 = wave * share < S ? wave * share : S;
   const uint32_t q_begin = first_group_at(x0), q_end = first_group_at(x0 + share);
+  if ((ABL & 8192) && lane == 0) {  // timing only: per-wave start stamp, groups, first group
+    const uint32_t t_start = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    a.out[4 * wave] = t_start;
+    a.out[4 * wave + 1] = t_start;
+    a.out[4 * wave + 2] = q_end > q_begin ? q_end - q_begin : 0u;
+    a.out[4 * wave + 3] = q_begin;
+  }
   if (q_begin >= q_end) return;  // no barrier below
 
   const LaneTab lt{(lane & 31) << 2, ((lane & 31) << 2) | 0x10000u};
@@ -853,6 +862,10 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
     fold_loop(std::false_type{});
   if (!(ABL & 16) && q_end != round_q0) flush(q_end);
   if ((ABL & 48) && r[0] == 0x12345678u) a.bres[0] = r[1];
+  if ((ABL & 8192) && lane == 0) {  // timing only: end stamp after every store has left
+    __builtin_amdgcn_s_waitcnt(0);
+    a.out[4 * wave + 1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+  }
 }
 
 

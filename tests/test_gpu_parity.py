@@ -176,8 +176,9 @@ def test_ragged_work_split_does_not_change_results(ctx, ctx_env, gcost):
 @pytest.mark.parametrize("pass_grid", [1, 3, 7])
 def test_ragged_bucket_pass_blocks_of_several_rounds(ctx, ctx_env, pass_grid):
     """The bucket pass lays each pass block's packets out by class; a block
-    whose packets take several rounds (more than 8 per thread) counts them
-    first and re-reads them to place them.  Few pass blocks
+    whose packets take several rounds (more than 16 per thread) counts them
+    first and re-reads them to place them (stores from the registers; blocks
+    of one round build their layout in LDS).  Few pass blocks
     (RICRC_RS_PASS_GRID) force that path: every size class (one-line, 2-3
     line, long), short packets computed in the pass itself (n < 44), invalid
     lengths, odd starts, in verify mode too -- and the session context after
@@ -209,6 +210,28 @@ def test_ragged_bucket_pass_blocks_of_several_rounds(ctx, ctx_env, pass_grid):
     ctx_env(RICRC_RS_PASS_GRID=pass_grid).batch_device(_dev(stamped), count, out, offsets=d_offs, lengths=d_lens,
                                                        stream=_stream(), verify=True)
     np.testing.assert_array_equal(_host_u32(out), want_v)
+
+
+@pytest.mark.parametrize("hi", [6000, 30000])
+def test_ragged_bucket_layout_lds_or_overflow(ctx, ctx_env, hi):
+    """A pass block of one round builds its layout in LDS when the layout
+    fits (its packets + the padding of each class's last group <= 16384 +
+    512 entries): lengths up to 6000 B span <= 48 line classes (padding <=
+    336, LDS); up to 30000 B, ~235 classes whose padding overflows the LDS
+    room, so the block stores from its registers and the gather reads pool
+    positions.  One pass block of 16384 packets (RICRC_RS_PASS_GRID=1)."""
+    rng = np.random.default_rng(hi)
+    count = 16384
+    lens = rng.integers(44, hi + 1, size=count).astype(np.uint32)
+    offs = np.zeros(count, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + 3, dtype=np.uint64)
+    buf = rng.integers(0, 256, size=int(offs[-1] + lens[-1]) + 64, dtype=np.uint8)
+    want = oracle_c.icrc_batch(buf, offsets=offs, lengths=lens, threads=16)
+    d_buf, d_offs, d_lens = _dev(buf), _dev(offs), _dev(lens)
+    for c in (ctx_env(RICRC_RS_PASS_GRID=1), ctx):
+        out = _out(count)
+        c.batch_device(d_buf, count, out, offsets=d_offs, lengths=d_lens, stream=_stream())
+        np.testing.assert_array_equal(_host_u32(out), want)
 
 
 def test_ragged_kernel_offsets_only_and_lengths_only(ctx):
