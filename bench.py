@@ -53,6 +53,23 @@ SEED = 0x1CEC0DE
 SCK_SOURCES = ("icrc_sck.hip", "icrc_sck.h", "icrc_device.h", "icrc_math.h")
 # The ragged pipeline's (C4, --mix): passes, fold, one-line kernel, gather.
 RAGGED_SOURCES = ("icrc_rsck.hip", "icrc_kernels.h", "icrc_sck.h", "icrc_device.h", "icrc_math.h")
+# The quad kernel's (C1: back-to-back 64-byte packets).
+QUAD_SOURCES = ("icrc_kernels.hip", "icrc_kernels.h", "icrc_device.h", "icrc_math.h")
+
+
+def traffic_record(mix, size):
+    """(profiles/ file, kernel sources, kernel names) of the PMC traffic
+    record for a workload (tools/pmc_traffic.py writes it), or None."""
+    if mix:
+        return "pmc_traffic_mix.json", RAGGED_SOURCES, ("rsck_bucket", "icrc_rsck_kernel", "icrc_rsmall_kernel",
+                                                        "rsck_gather")
+    if size == 4096:
+        return "pmc_traffic.json", SCK_SOURCES, ("icrc_sck_kernel",)
+    if size in (1024, 2048):
+        return f"pmc_traffic_{size}.json", SCK_SOURCES, ("icrc_sck_kernel",)
+    if size == 64:
+        return "pmc_traffic_64.json", QUAD_SOURCES, ("icrc_quad_kernel",)
+    return None
 
 
 def parse(argv=None):
@@ -134,10 +151,10 @@ def load_traffic(args, count):
     """HBM bytes per launch measured by separate rocprofv3 --pmc passes
     (profiles/pmc_traffic*.json, from tools/pmc_traffic.py) on this very
     workload and kernel source, or None."""
-    if args.family != "v4":
+    rec = traffic_record(args.mix, args.size)
+    if args.family != "v4" or rec is None:
         return None
-    name = "pmc_traffic_mix.json" if args.mix else "pmc_traffic.json"
-    srcs = RAGGED_SOURCES if args.mix else SCK_SOURCES
+    name, srcs, _ = rec
     p = os.path.join(ROOT, "profiles", name)
     try:
         with open(p) as f:

@@ -9,6 +9,8 @@ the bytes of a wide (16 B/lane) coalesced streaming read, so it is doubled;
 WRITE_SIZE is taken as reported.  Both are in KiB.
 
   (default)  the headline: 1 M x 4096 B, icrc_sck_kernel -> profiles/pmc_traffic.json
+  --size N   1 M x N B back to back (64: the quad kernel, C1; 1024 / 2048:
+             the SCK, C2) -> profiles/pmc_traffic_N.json
   --mix      C4: the ragged pipeline's four kernels (bucket, fold, one-line,
              gather) summed per step -> profiles/pmc_traffic_mix.json.  The
              bucket pass reads its 12 descriptor bytes per packet once, so its
@@ -18,7 +20,7 @@ WRITE_SIZE is taken as reported.  Both are in KiB.
 
 Copied into profiles/, the file is what bench.py reports as roofline.traffic
 when the workload and the kernel sources match (bench.kernel_source_hash).
-Usage (on the GPU box):  python3 tools/pmc_traffic.py [--mix] [--out F]
+Usage (on the GPU box):  python3 tools/pmc_traffic.py [--mix | --size N] [--out F]
 """
 import argparse
 import csv
@@ -29,7 +31,6 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-RAGGED_KERNELS = ("rsck_bucket", "icrc_rsck_kernel", "icrc_rsmall_kernel", "rsck_gather")
 
 
 def run_pass(counter, outdir, bench_args, match):
@@ -53,17 +54,20 @@ def run_pass(counter, outdir, bench_args, match):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mix", action="store_true")
+    ap.add_argument("--size", type=int, default=4096)
     ap.add_argument("--out", default=None)
     ap.add_argument("--scratch", default=os.path.join(ROOT, "gpurun_out", "pmc_traffic"))
     a = ap.parse_args()
-    a.out = os.path.abspath(a.out or os.path.join(ROOT, "gpurun_out",
-                                                  "pmc_traffic_mix.json" if a.mix else "pmc_traffic.json"))
-    a.scratch = os.path.abspath(a.scratch + ("_mix" if a.mix else ""))
     sys.path.insert(0, ROOT)
     import bench
 
-    bench_args = ["--mix"] if a.mix else []
-    match = RAGGED_KERNELS if a.mix else ("icrc_sck_kernel",)
+    rec = bench.traffic_record(a.mix, a.size)
+    if rec is None:
+        raise SystemExit(f"no traffic record is kept for --size {a.size}")
+    name, srcs, match = rec
+    a.out = os.path.abspath(a.out or os.path.join(ROOT, "gpurun_out", name))
+    a.scratch = os.path.abspath(a.scratch + ("_mix" if a.mix else f"_{a.size}"))
+    bench_args = ["--mix"] if a.mix else ["--size", str(a.size)]
     fetch = run_pass("FETCH_SIZE", os.path.join(a.scratch, "fetch"), bench_args, match)
     write = run_pass("WRITE_SIZE", os.path.join(a.scratch, "write"), bench_args, match)
     if a.mix:
@@ -72,11 +76,11 @@ def main():
         count = 4 << 20
         lens = np.random.default_rng(bench.SEED).choice(np.array(bench.MIX_SIZES, np.uint32), size=count)
         alg = int(lens.sum(dtype=np.uint64)) + 16 * count
-        src, size = bench.kernel_source_hash(bench.RAGGED_SOURCES), "mix"
+        src, size = bench.kernel_source_hash(srcs), "mix"
     else:
-        count, size = 1 << 20, 4096
+        count, size = 1 << 20, a.size
         alg = count * size + 4 * count
-        src = bench.kernel_source_hash()
+        src = bench.kernel_source_hash(srcs)
     kernels = {k: {"FETCH_SIZE_KiB": fetch.get(k, (0.0, 0))[0], "WRITE_SIZE_KiB": write.get(k, (0.0, 0))[0],
                    "dispatches": [fetch.get(k, (0, 0))[1], write.get(k, (0, 0))[1]]} for k in match}
     hbm = sum(2.0 * v["FETCH_SIZE_KiB"] * 1024 + v["WRITE_SIZE_KiB"] * 1024 for v in kernels.values())
