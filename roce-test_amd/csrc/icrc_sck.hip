@@ -42,7 +42,7 @@ namespace ricrc {
 //
 // ABL (timing-only ablations for tools/microbench; the product uses 0):
 // 1 no table fold, 2 no finish, 8 no global loads, 16 no stores, 64 per-wave
-// start/end s_memrealtime stamps into a.stamps.
+// start/end s_memrealtime stamps into a.stamps, 128 no LDS table build.
 // D: lines in flight per wave.  Every finish multiply goes through nibble
 // tables, ONE copy each (the 16 entries of a nibble position sit in 16 banks:
 // any lane pattern is conflict-free) -- x^-32 (128 words) and, per lane slot
@@ -121,8 +121,8 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
     ring[k] = load(k < L ? qcur : qnext, (uint32_t)(k % L));
   }
   __builtin_amdgcn_sched_barrier(0);
-  table_store(tab, tab_v);
-  {
+  if (!(ABL & 128)) table_store(tab, tab_v);
+  if (!(ABL & 128)) {
     if (threadIdx.x < 128) {  // entry 16 w + v: (nibble v at bits 4w..4w+3) * x^-32
       const uint32_t w = threadIdx.x >> 4, v = threadIdx.x & 15u;
       uint32_t t = 0;

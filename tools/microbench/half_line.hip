@@ -8,22 +8,31 @@
 // same line.  Time per launch here; FETCH_SIZE per kernel under
 // rocprofv3 --pmc FETCH_SIZE.  Build:
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 half_line.hip -o half_line
-#include <hip/hip_runtime.h>
+#include "../../roce-test_amd/csrc/icrc_kernels.hip"
+#include "../../roce-test_amd/csrc/icrc_sck.hip"
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+using namespace ricrc;
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s\n", hipGetErrorString(e)); exit(1); } } while (0)
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef const u32x4 __attribute__((address_space(1))) *gp_t;
 
-template <int MODE>  // 0 all slots, 1 upper half only (masked), 2 lower half redirected to the upper half
+// MODE 0 all slots, 1 upper half only (masked), 2 lower half redirected to
+// the upper half; group order (all slots): 0 group q = wave + i nw
+// (interleaved), 3 a contiguous block of groups per wave (the SCK's order),
+// 4 / 5 chunks of 8 / 2 consecutive groups interleaved over the waves.
+template <int MODE>
 __global__ __launch_bounds__(1024) void stream_kernel(const uint8_t *buf, uint64_t groups, uint32_t *sink) {
   const uint32_t lane = threadIdx.x & 63, s = lane & 7, g = lane >> 3;
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
   u32x4 acc = {0u, 0u, 0u, 0u};
-  for (uint64_t q = wave; q < groups; q += nw) {
+  const uint64_t per = (groups + nw - 1) / nw;
+  constexpr uint64_t CH = MODE == 4 ? 8 : MODE == 5 ? 2 : 1;
+  for (uint64_t i = 0; i < per; ++i) {
+    uint64_t q = MODE == 3 ? wave * per + i : ((i / CH) * nw + wave) * CH + i % CH;
+    if (q >= groups) break;
     const uint8_t *pk = buf + (8 * q + g) * 4096;
 #pragma unroll 8
     for (int k = 0; k < 32; ++k) {
@@ -51,16 +60,43 @@ template <typename F> float timeit(F launch, int reps) {
 }
 
 int main() {
-  const uint64_t bytes = 2ull << 30, groups = bytes / (8 * 4096);
-  uint8_t *buf; CK(hipMalloc(&buf, bytes)); CK(hipMemset(buf, 0x3C, bytes));
+  const uint64_t bytes = 4ull << 30, groups = bytes / (8 * 4096);
+  uint8_t *buf; CK(hipMalloc(&buf, bytes));
+  {  // random bytes (constant data runs at a higher clock than real traffic)
+    uint64_t *h = (uint64_t *)malloc(bytes);
+    uint64_t x = 0x9E3779B97F4A7C15ull;
+    for (uint64_t i = 0; i < bytes / 8; ++i) { x ^= x << 13; x ^= x >> 7; x ^= x << 17; h[i] = x; }
+    CK(hipMemcpy(buf, h, bytes, hipMemcpyHostToDevice));
+    free(h);
+  }
+  uint32_t *out; CK(hipMalloc(&out, 4ull << 22));
+  SckArgs sa{}; sa.base = buf; sa.count = bytes / 4096; sa.out = out; sa.n = 4096;
+  for (int j = 0; j < 32; ++j) sa.XB[j] = 0x85EBCA6Bu * (j + 3);
+  for (int k = 0; k < 8; ++k) sa.QS[k] = 0x9E3779B9u * (k + 1);
   uint32_t *sink; CK(hipMalloc(&sink, 4096));
   const int grid = 256;
   for (int r = 0; r < 3; ++r) {
     const float a = timeit([&] { hipLaunchKernelGGL((stream_kernel<0>), dim3(grid), dim3(1024), 0, 0, buf, groups, sink); }, 10);
     const float b = timeit([&] { hipLaunchKernelGGL((stream_kernel<1>), dim3(grid), dim3(1024), 0, 0, buf, groups, sink); }, 10);
     const float c = timeit([&] { hipLaunchKernelGGL((stream_kernel<2>), dim3(grid), dim3(1024), 0, 0, buf, groups, sink); }, 10);
-    printf("2 GiB of lines: all slots %.1f us (%.0f GB/s of lines) | upper half, masked %.1f us | lower half redirected %.1f us\n",
+    printf("4 GiB of lines: all slots %.1f us (%.0f GB/s of lines) | upper half, masked %.1f us | lower half redirected %.1f us\n",
            a * 1e3, bytes / (a * 1e-3) / 1e9, b * 1e3, c * 1e3);
+    const float d = timeit([&] { hipLaunchKernelGGL((stream_kernel<3>), dim3(grid), dim3(1024), 0, 0, buf, groups, sink); }, 10);
+    const float e = timeit([&] { hipLaunchKernelGGL((stream_kernel<4>), dim3(grid), dim3(1024), 0, 0, buf, groups, sink); }, 10);
+    const float f = timeit([&] { hipLaunchKernelGGL((stream_kernel<5>), dim3(grid), dim3(1024), 0, 0, buf, groups, sink); }, 10);
+    printf("group order: interleaved %.1f us | contiguous block per wave (SCK) %.1f us (%.0f GB/s) | chunks of 8 %.1f us | chunks of 2 %.1f us\n",
+           a * 1e3, d * 1e3, bytes / (d * 1e-3) / 1e9, e * 1e3, f * 1e3);
+    const float sf = timeit([&] { hipLaunchKernelGGL((icrc_sck_kernel<32, 0>), dim3(grid), dim3(kBlock), 0, 0, sa); }, 10);
+    const float sm = timeit([&] { hipLaunchKernelGGL((icrc_sck_kernel<32, 1 | 2>), dim3(grid), dim3(kBlock), 0, 0, sa); }, 10);
+    const float sn = timeit([&] { hipLaunchKernelGGL((icrc_sck_kernel<32, 1 | 2 | 16>), dim3(grid), dim3(kBlock), 0, 0, sa); }, 10);
+    printf("same bytes: SCK full %.1f us (%.0f GB/s) | SCK memory path (no fold, no finish) %.1f us | memory path, no stores %.1f us\n",
+           sf * 1e3, bytes / (sf * 1e-3) / 1e9, sm * 1e3, sn * 1e3);
+    const float st = timeit([&] { hipLaunchKernelGGL((icrc_sck_kernel<32, 1 | 2 | 16 | 128>), dim3(grid), dim3(kBlock), 0, 0, sa); }, 10);
+    const float s8 = timeit([&] { hipLaunchKernelGGL((icrc_sck_kernel<32, 8>), dim3(grid), dim3(kBlock), 0, 0, sa); }, 10);
+    const float s1 = timeit([&] { hipLaunchKernelGGL((icrc_sck_kernel<32, 1>), dim3(grid), dim3(kBlock), 0, 0, sa); }, 10);
+    const float s2 = timeit([&] { hipLaunchKernelGGL((icrc_sck_kernel<32, 2>), dim3(grid), dim3(kBlock), 0, 0, sa); }, 10);
+    printf("  SCK memory path, no stores, no table build %.1f us | no loads (compute only) %.1f us | no fold %.1f us | no finish %.1f us\n",
+           st * 1e3, s8 * 1e3, s1 * 1e3, s2 * 1e3);
   }
   return 0;
 }
