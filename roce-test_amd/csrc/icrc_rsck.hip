@@ -430,7 +430,8 @@ __device__ __forceinline__ uint32_t edge_word(uint32_t w, int rel, int M) {
 // 8 no edge masks, 16 no result slots / stores, 32 no global stores (slots kept),
 // 512 (with 2) 192 result slots, 1024 / 2048 / 4096 result stores nt / default / sc0 sc1,
 // 8192 per-wave s_memrealtime start / end stamps, groups and first group into a.out
-// (4 words per wave; tools/microbench/bucket_abl.hip).
+// (4 words per wave; tools/microbench/bucket_abl.hip), 16384 no line loads, 32768 every
+// edge line through the head-line path (the round-3 session-23 fold).
 template <int ABL>
 __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   // Result slots per wave (a round of 8 groups leaves in one store; a store
@@ -663,7 +664,12 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
       }
     }
   };
-  auto ld_issue = [&]() -> u32x4 { return gload16_nt(ld.line0 + 128ull * ld_k); };
+  // (ABL 16384, timing only: no line loads, a value derived from the address)
+  auto line_load = [&](uint64_t addr) -> u32x4 {
+    if (ABL & 16384) return u32x4{(uint32_t)addr, (uint32_t)(addr >> 7), lane, (uint32_t)addr * 3u};
+    return gload16_nt(addr);
+  };
+  auto ld_issue = [&]() -> u32x4 { return line_load(ld.line0 + 128ull * ld_k); };
 
   u32x4 ring[D];
 #pragma unroll
@@ -732,7 +738,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
     }
   };
 
-  // Two copies of the fold loop: one with whole-word edges when the count
+  // Two copies of the fold loop: one with whole-word edges when the bucket
   // pass found every strided-chain packet word-aligned in start and length
   // (a per-group choice inside the loop made the compiler rotate the load
   // ring through copies and drain vmcnt(0) at the loop head).
@@ -763,7 +769,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
       const uint32_t t3 = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo1, 0x0C020700u) + 128);
       xr[i] = xor3(t0, t1, xor3(t2, t3, wn[i]));
     }
-    ring[u] = gload16_nt(ld.line0 + 128ull * (ld_k + ahead));
+    ring[u] = line_load(ld.line0 + 128ull * (ld_k + ahead));
   };
   auto fold_loop = [&](auto words) {
   // One full step: edge masks, group finish and both cursors' group changes.
@@ -773,17 +779,26 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
         const u32x4 wc = ring[u];
         const int rel0 = (int)(128u * fd_k + 16u * s) - (int)fd_a;
         if constexpr (decltype(words)::value) {
+          if ((ABL & 32768) || fd_k < fd_hl) {  // wave-uniform: a head line
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            // whole words: keep 0 <= rel < M by sign arithmetic (compare +
-            // select pairs needed hazard NOPs), head masks from a 16-entry
-            // table (rel >= 40 and rel < 0 index the zero entry 15)
-            const int rel = rel0 + 4 * i;
-            const uint32_t keep = (uint32_t)(((rel - (int)fd_M) & ~rel) >> 31);
-            const uint32_t k = __builtin_elementwise_min((uint32_t)rel >> 2, 15u);
-            typedef uint32_t u32x2e __attribute__((ext_vector_type(2)));
-            const u32x2e e = *reinterpret_cast<const u32x2e *>(etl + 2 * k);
-            xr[i] = xor3(xr[i], wc[i], ((wc[i] & keep) | e[0]) ^ e[1]);
+            for (int i = 0; i < 4; ++i) {
+              // whole words: keep 0 <= rel < M by sign arithmetic (compare +
+              // select pairs needed hazard NOPs), head masks from a 16-entry
+              // table (rel >= 40 and rel < 0 index the zero entry 15)
+              const int rel = rel0 + 4 * i;
+              const uint32_t keep = (uint32_t)(((rel - (int)fd_M) & ~rel) >> 31);
+              const uint32_t k = __builtin_elementwise_min((uint32_t)rel >> 2, 15u);
+              typedef uint32_t u32x2e __attribute__((ext_vector_type(2)));
+              const u32x2e e = *reinterpret_cast<const u32x2e *>(etl + 2 * k);
+              xr[i] = xor3(xr[i], wc[i], ((wc[i] & keep) | e[0]) ^ e[1]);
+            }
+          } else {
+            // the group's last line past its head lines: rel >= 40 (no head
+            // masks), only the bytes at rel >= M dropped -- 3 VALU a word
+            // instead of 10 and a table read
+            const int lim = (int)fd_M - 1 - rel0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) xr[i] ^= wc[i] & (uint32_t)((lim - 4 * i) >> 31);
           }
         } else {
 #pragma unroll

@@ -47,6 +47,14 @@ __global__ __launch_bounds__(1024) void copy_floor(const uint64_t *off, const ui
   }
 }
 
+__global__ void fill_random(uint64_t *p, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t x = (i + 1) * 0x9E3779B97F4A7C15ull;
+    x ^= x >> 31; x *= 0xBF58476D1CE4E5B9ull; x ^= x >> 27;
+    p[i] = x;
+  }
+}
+
 int main(int argc, char **argv) {
   hipDeviceProp_t p; CK(hipGetDeviceProperties(&p, 0));
   const int grid = p.multiProcessorCount;
@@ -59,7 +67,9 @@ int main(int argc, char **argv) {
     off[i] = pos; len[i] = sizes[x & 3]; pos += len[i];
   }
   uint8_t *buf; CK(hipMalloc(&buf, pos + 4096));
-  CK(hipMemset(buf, 0x5A, pos));
+  // random bytes (constant data can run at another clock than real traffic)
+  hipLaunchKernelGGL(fill_random, dim3(4096), dim3(256), 0, 0, reinterpret_cast<uint64_t *>(buf), (pos + 4096) / 8);
+  CK(hipDeviceSynchronize());
   uint64_t *d_off; uint32_t *d_len;
   CK(hipMalloc(&d_off, 8 * count)); CK(hipMalloc(&d_len, 4 * count));
   CK(hipMemcpy(d_off, off.data(), 8 * count, hipMemcpyHostToDevice));
@@ -145,6 +155,16 @@ int main(int argc, char **argv) {
     };
     if (r == 0) for (uint32_t gc : {4u, 8u, 16u}) fold_report(gc);
     fold_report(kRsGroupCost);
+    for (int ab = 0; ab < 3; ++ab) {  // same-process A/B of the edge paths, alternating
+      rep("fold A/B: last lines through the head-line path (before)", timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<32768>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10));
+      rep("fold A/B: cheap last-line path (product)", timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10));
+    }
+    rep("fold, no line loads (compute only)", timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<16384>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10));
+    rep("fold, no line loads, head-line path for every edge", timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<16384 | 32768>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10));
+    rep("fold, memory path (no table fold, no finish)", timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<3>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10));
+    rep("fold, no edge masks", timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<8>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10));
+    rep("fold, no finish", timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<2>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10));
+    rep("fold, memory path, no edges, no stores", timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<3 | 8 | 16>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10));
     rep("one-line (icrc_rsmall_kernel)", timeit([&] { hipLaunchKernelGGL(icrc_rsmall_kernel, dim3(grid), dim3(kBlock), 0, 0, a); }, 20));
     {  // the gather zeroes the counters: restore them before each timed launch
       RsCounters *saved; CK(hipMalloc(&saved, sizeof(RsCounters)));
