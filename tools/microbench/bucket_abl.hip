@@ -183,5 +183,23 @@ int main(int argc, char **argv) {
       CK(hipFree(saved));
     }
   }
+  {  // placement: the same batch at a second address (a second 5.7 GB allocation), fold on each, alternating
+    uint8_t *buf2; CK(hipMalloc(&buf2, pos + 4096));
+    CK(hipMemcpy(buf2, buf, pos + 4096, hipMemcpyDeviceToDevice));
+    printf("placement: batch A at %p, batch B at %p\n", (void *)buf, (void *)buf2);
+    for (int r = 0; r < 4; ++r) {
+      for (int which = 0; which < 2; ++which) {
+        a.base = which ? buf2 : buf;
+        a.group_cost = kRsGroupCost;
+        CK(rs_zero_counters(ws, 0));
+        hipLaunchKernelGGL((rsck_bucket<true, true, 0>), dim3(pgrid), dim3(kPassBlock), 0, 0, a);
+        CK(hipDeviceSynchronize());
+        rep(which ? "placement: fold on batch B" : "placement: fold on batch A",
+            timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10));
+      }
+    }
+    a.base = buf;
+    CK(hipFree(buf2));
+  }
   return 0;
 }
