@@ -274,7 +274,18 @@ int sck_grid(const Dev &d, const uint8_t *base, const uint64_t *off, const uint3
   if (off || len || l3_offset != 0 || ((uintptr_t)base % 16) != 0 || d.knobs.no_sck || count == 0) return 0;
   if (stride != 1024 && stride != 2048 && stride != 4096) return 0;
   const uint64_t groups = (count + 7) / 8;
-  int g = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)d.n_cu, (groups + 15) / 16));
+  // One workgroup per CU.  Batches of up to 48 groups per wave (6 GiB of
+  // 4 KiB packets on 256 CUs) run on 15/16 of the CUs (240 of 256): the grid
+  // on every CU took 1-3 % longer there (1 M x 4 KiB: 641 against 626 us,
+  // 1.5 M: 972-992 against 957-980; 1 M x 1 KiB: 163-165 against 162; grids
+  // of 248 / 244 read 670) and left no CU to a collective kernel on another
+  // stream (bench.py's overlapped RCCL all-gather at N > 1); from 2 M x 4 KiB
+  // on, every CU is as fast or faster (profiles/r03/s31_sck_grid_sweep.txt,
+  // s32_sck_grid_sweep_4k_1k.txt, s33_ab_sck_grid_15_16.txt,
+  // s34_sck_grid_by_batch_size.txt, s30_sck_overlap_standin.txt).
+  const uint64_t full = (uint64_t)d.n_cu;
+  const uint64_t cus = groups <= 48ull * 16ull * full ? (uint64_t)std::max(1, d.n_cu - d.n_cu / 16) : full;
+  int g = (int)std::max<uint64_t>(1, std::min<uint64_t>(cus, (groups + 15) / 16));
   if (d.knobs.sck_grid > 0) g = std::min(g, d.knobs.sck_grid);
   return g;
 }

@@ -75,6 +75,41 @@ int main() {
   for (int k = 0; k < 8; ++k) sa.QS[k] = 0x9E3779B9u * (k + 1);
   uint32_t *sink; CK(hipMalloc(&sink, 4096));
   const int grid = 256;
+  if (getenv("SIZE_SWEEP")) {  // SCK at 256 vs 240 workgroups by batch size (4 KiB packets), alternating
+    uint8_t *big; CK(hipMalloc(&big, 16ull << 30));
+    CK(hipMemset(big, 0x6B, 16ull << 30));
+    for (uint64_t cnt : {1ull << 20, 3ull << 19, 2ull << 20, 3ull << 20, 4ull << 20}) {
+      SckArgs b = sa; b.base = big; b.count = cnt;
+      uint32_t *o2; CK(hipMalloc(&o2, 4 * cnt)); b.out = o2;
+      printf("%llu x 4 KiB:", (unsigned long long)cnt);
+      for (int r = 0; r < 3; ++r)
+        for (int g : {256, 240}) {
+          const float t = timeit([&] { hipLaunchKernelGGL((icrc_sck_kernel<32, 0>), dim3(g), dim3(kBlock), 0, 0, b); }, 10);
+          printf(" %d:%.1f", g, t * 1e3);
+        }
+      printf(" us\n");
+      CK(hipFree(o2));
+    }
+    return 0;
+  }
+  if (getenv("GRID_SWEEP")) {  // SCK grid sweep, alternating (one 1024-thread workgroup per CU used)
+    SckArgs s2 = sa; s2.n = 1024; s2.count = 1 << 20;  // C2: 1 M x 1 KiB (super-groups)
+    for (int r = 0; r < 3; ++r) {
+      printf("SCK 4 KiB grid sweep round %d:", r);
+      for (int g : {256, 252, 248, 244, 240, 236, 232, 228, 224, 216}) {
+        const float t = timeit([&] { hipLaunchKernelGGL((icrc_sck_kernel<32, 0>), dim3(g), dim3(kBlock), 0, 0, sa); }, 20);
+        printf(" %d:%.1f", g, t * 1e3);
+      }
+      printf(" us\n");
+      printf("SCK 1 KiB (C2) grid sweep round %d:", r);
+      for (int g : {256, 248, 240, 232, 224, 216, 208, 192}) {
+        const float t = timeit([&] { hipLaunchKernelGGL((icrc_sck_kernel<32, 0, kFamV4, 8>), dim3(g), dim3(kBlock), 0, 0, s2); }, 20);
+        printf(" %d:%.1f", g, t * 1e3);
+      }
+      printf(" us\n");
+    }
+    return 0;
+  }
   for (int r = 0; r < 3; ++r) {
     const float a = timeit([&] { hipLaunchKernelGGL((stream_kernel<0>), dim3(grid), dim3(1024), 0, 0, buf, groups, sink); }, 10);
     const float b = timeit([&] { hipLaunchKernelGGL((stream_kernel<1>), dim3(grid), dim3(1024), 0, 0, buf, groups, sink); }, 10);
