@@ -93,6 +93,10 @@ __device__ uint32_t icrc_small(uint64_t addr, uint32_t n) {
 constexpr int kPassBlock = 1024;
 constexpr int kPassBlocks = 256;  // pass grid cap: one 1024-thread block per CU, all resident at once
 constexpr int kPassUnroll = 16;   // packets per thread whose descriptors are read at once (C4: one round)
+// Batches of more than kPassBlocks x kPassBlock x 16 packets (4 M; C4's
+// byte-balanced shards at N > 1 hold up to 4.2 M) read 17 per thread, so
+// their blocks stay on the one-round, LDS-staged path up to 4.46 M.
+constexpr int kPassUnrollBig = 17;
 __device__ __forceinline__ void pass_range(uint64_t count, uint64_t &lo, uint64_t &hi) {
   const uint64_t per = ((count + gridDim.x - 1) / gridDim.x + kPassBlock - 1) / kPassBlock * kPassBlock;
   lo = (uint64_t)blockIdx.x * per;
@@ -145,15 +149,17 @@ __device__ __forceinline__ T wave_scan(T v) {
 // ABL (timing-only ablations, tools/microbench/bucket_abl.hip): 1 stop after
 // the ranking round, 2 no LDS atomics (rank 0), 4 stop after the reservation,
 // 8 no pos_of stores, 16 no descriptor stores, 32 no LDS staging.
-constexpr uint32_t kStage = kPassUnroll * kPassBlock + 512;  // a round's packets + room for group padding
-template <bool OFF, bool LEN, int ABL = 0>
+// LDS layout entries of a block: a round's packets + room for group padding
+__host__ __device__ constexpr uint32_t stage_entries(int U) { return (uint32_t)U * kPassBlock + 512u; }
+template <bool OFF, bool LEN, int ABL = 0, int U = kPassUnroll>
 __global__ __launch_bounds__(kPassBlock) void rsck_bucket(RsckArgs a) {
+  constexpr uint32_t kStage = stage_entries(U);
   __shared__ uint32_t h[kRsClasses], at[kRsClasses], cur[kRsClasses];
   __shared__ uint32_t wg[16], wsm[16], wf[16];
   __shared__ uint64_t ww[16];
   __shared__ uint32_t blk_g0, blk_small, blk_stot, blk_total;
   __shared__ uint64_t blk_s0;
-  __shared__ uint64_t stage[kStage];  // the block's layout: small range | big range (132 KiB)
+  __shared__ uint64_t stage[kStage];  // the block's layout: small range | big range (132 / 140 KiB)
   for (int t = threadIdx.x; t < kRsClasses; t += blockDim.x) {
     h[t] = 0;
     cur[t] = 0;
@@ -167,28 +173,28 @@ __global__ __launch_bounds__(kPassBlock) void rsck_bucket(RsckArgs a) {
     lo = (uint32_t)l;
     hi = (uint32_t)h_;
   }
-  const bool one = hi - lo <= (uint32_t)kPassUnroll * blockDim.x;  // block-uniform
+  const bool one = hi - lo <= (uint32_t)U * blockDim.x;  // block-uniform
   int odd = 0;  // a big packet not starting or ending on a 4-byte word
   // Per packet, packed (3 VGPRs): the descriptor words and class | rank << 10.
-  uint32_t dlo[kPassUnroll], dhi[kPassUnroll], cr[kPassUnroll];
-  // One round: descriptors of kPassUnroll packets per thread read at once
+  uint32_t dlo[U], dhi[U], cr[U];
+  // One round: descriptors of U packets per thread read at once
   // (raw loads first, unconditional with the index clamped, arithmetic after:
   // an add on a loaded value inside a per-packet branch made the compiler
   // wait for each load before issuing the next), then classified and ranked
   // in their class by an LDS atomic on `ctr` (h in the first sweep, cur in
   // the second); packets that are not bucketed are marked for the gather.
   auto round = [&](uint32_t r0, uint32_t *ctr, bool first) {
-    uint64_t addr[kPassUnroll];
-    uint32_t n[kPassUnroll];
+    uint64_t addr[U];
+    uint32_t n[U];
 #pragma unroll
-    for (int k = 0; k < kPassUnroll; ++k) {
+    for (int k = 0; k < U; ++k) {
       uint32_t i = r0 + (uint32_t)k * blockDim.x + threadIdx.x;
       i = i < hi ? i : hi - 1;
       addr[k] = OFF ? a.off[i] : (uint64_t)i * a.stride;
       n[k] = LEN ? a.len[i] : a.fixed_len;
     }
 #pragma unroll
-    for (int k = 0; k < kPassUnroll; ++k) {
+    for (int k = 0; k < U; ++k) {
       const uint32_t i = r0 + (uint32_t)k * blockDim.x + threadIdx.x;
       const uint64_t ad = addr[k] + (uint64_t)(uintptr_t)a.base + a.l3_offset;
       const uint32_t c = i < hi ? rs_class(ad, n[k]) : 0u;
@@ -200,12 +206,12 @@ __global__ __launch_bounds__(kPassBlock) void rsck_bucket(RsckArgs a) {
       cr[k] = c | (rk << 10);
     }
   };
-  for (uint32_t r0 = lo; r0 < hi; r0 += kPassUnroll * blockDim.x) round(r0, h, true);  // block-uniform
+  for (uint32_t r0 = lo; r0 < hi; r0 += U * blockDim.x) round(r0, h, true);  // block-uniform
   if (__syncthreads_or(odd) && threadIdx.x == 0) atomicOr(&a.ctr->odd, 1u);
   if (ABL & 1) {  // keep the round's results live
     uint32_t x = 0;
 #pragma unroll
-    for (int k = 0; k < kPassUnroll; ++k) x ^= cr[k] ^ dlo[k] ^ dhi[k];
+    for (int k = 0; k < U; ++k) x ^= cr[k] ^ dlo[k] ^ dhi[k];
     if (x == 0x9E3779B9u) a.pos_of[threadIdx.x] = x;
     return;
   }
@@ -257,14 +263,14 @@ __global__ __launch_bounds__(kPassBlock) void rsck_bucket(RsckArgs a) {
   if (ABL & 4) {
     uint32_t x = 0;
 #pragma unroll
-    for (int k = 0; k < kPassUnroll; ++k) x ^= cr[k] ^ dlo[k] ^ dhi[k];
+    for (int k = 0; k < U; ++k) x ^= cr[k] ^ dlo[k] ^ dhi[k];
     if (x == 0x9E3779B9u) a.pos_of[threadIdx.x] = x;
     return;
   }
 
   auto place = [&](uint32_t r0) {
 #pragma unroll
-    for (int k = 0; k < kPassUnroll; ++k) {
+    for (int k = 0; k < U; ++k) {
       const uint32_t i = r0 + (uint32_t)k * blockDim.x + threadIdx.x;
       const uint32_t c = cr[k] & 1023u, rk = cr[k] >> 10;
       if (i >= hi || !c) continue;
@@ -286,7 +292,7 @@ __global__ __launch_bounds__(kPassBlock) void rsck_bucket(RsckArgs a) {
   if (staged) {  // block-uniform: the round's descriptors are still in registers
     const uint32_t big0 = 8u * blk_g0, small0 = blk_small;
 #pragma unroll
-    for (int k = 0; k < kPassUnroll; ++k) {
+    for (int k = 0; k < U; ++k) {
       const uint32_t i = lo + (uint32_t)k * blockDim.x + threadIdx.x;
       const uint32_t c = cr[k] & 1023u, rk = cr[k] >> 10;
       if (i >= hi || !c) continue;
@@ -313,7 +319,7 @@ __global__ __launch_bounds__(kPassBlock) void rsck_bucket(RsckArgs a) {
     place(lo);
     return;
   }
-  for (uint32_t r0 = lo; r0 < hi; r0 += kPassUnroll * blockDim.x) {
+  for (uint32_t r0 = lo; r0 < hi; r0 += U * blockDim.x) {
     round(r0, cur, false);
     place(r0);
   }
@@ -347,7 +353,9 @@ __device__ __forceinline__ uint32_t gather_one(const RsckArgs &a, uint64_t i, ui
 // read coalesced into LDS in the block's layout order and pos_of indexes
 // that copy, instead of one 4-byte read per packet scattered over the class
 // runs of the pools.
+template <int PU>  // the bucket pass's packets per thread
 __global__ __launch_bounds__(kPassBlock) void rsck_gather(RsckArgs a) {
+  constexpr uint32_t kStage = stage_entries(PU);
   __shared__ uint32_t lres[kStage];
   // The counters are dead now (the bucket pass and both folds have read
   // them): zero them for the next call on this workspace.
@@ -361,12 +369,12 @@ __global__ __launch_bounds__(kPassBlock) void rsck_gather(RsckArgs a) {
   }
   const RsBlock B = a.blk[blockIdx.x];
   constexpr int U = 4;  // packets per thread in flight at once
-  if (B.staged) {  // block-uniform (a staged block's packets fit one round: hi - lo <= kPassUnroll x blockDim)
+  if (B.staged) {  // block-uniform (a staged block's packets fit one round: hi - lo <= PU x blockDim)
     // every load of the block issued before the barrier: the positions, then
     // the results into LDS
-    uint32_t p[kPassUnroll];
+    uint32_t p[PU];
 #pragma unroll
-    for (int k = 0; k < kPassUnroll; ++k) {
+    for (int k = 0; k < PU; ++k) {
       const uint32_t i = lo + (uint32_t)k * blockDim.x + threadIdx.x;
       p[k] = i < hi ? __builtin_nontemporal_load(a.pos_of + i) : 0xFFFFFFFFu;
     }
@@ -386,7 +394,7 @@ __global__ __launch_bounds__(kPassBlock) void rsck_gather(RsckArgs a) {
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < kPassUnroll; ++k) {
+    for (int k = 0; k < PU; ++k) {
       const uint32_t i = lo + (uint32_t)k * blockDim.x + threadIdx.x;
       if (i < hi) __builtin_nontemporal_store(gather_one(a, i, p[k], p[k] != 0xFFFFFFFFu ? lres[p[k]] : 0u), a.out + i);
     }
@@ -1127,12 +1135,21 @@ void rs_bind_workspace(RsckArgs &a, void *ws) {
   a.bres = a.res + a.small_cap;
 }
 
-static void launch_bucket(const RsckArgs &a, int pgrid, hipStream_t st) {
+template <int U>
+static void launch_bucket_u(const RsckArgs &a, int pgrid, hipStream_t st) {
   static_assert(kPassBlock == 1024 && kRsClasses <= kPassBlock, "one class per thread in the bucket pass's scan");
-  if (a.off && a.len) hipLaunchKernelGGL((rsck_bucket<true, true>), dim3(pgrid), dim3(kPassBlock), 0, st, a);
-  else if (a.off) hipLaunchKernelGGL((rsck_bucket<true, false>), dim3(pgrid), dim3(kPassBlock), 0, st, a);
-  else if (a.len) hipLaunchKernelGGL((rsck_bucket<false, true>), dim3(pgrid), dim3(kPassBlock), 0, st, a);
-  else hipLaunchKernelGGL((rsck_bucket<false, false>), dim3(pgrid), dim3(kPassBlock), 0, st, a);
+  if (a.off && a.len) hipLaunchKernelGGL((rsck_bucket<true, true, 0, U>), dim3(pgrid), dim3(kPassBlock), 0, st, a);
+  else if (a.off) hipLaunchKernelGGL((rsck_bucket<true, false, 0, U>), dim3(pgrid), dim3(kPassBlock), 0, st, a);
+  else if (a.len) hipLaunchKernelGGL((rsck_bucket<false, true, 0, U>), dim3(pgrid), dim3(kPassBlock), 0, st, a);
+  else hipLaunchKernelGGL((rsck_bucket<false, false, 0, U>), dim3(pgrid), dim3(kPassBlock), 0, st, a);
+}
+// Packets per thread of the bucket and gather passes for a batch on pgrid blocks.
+static bool pass_big(const RsckArgs &a, int pgrid) {
+  return a.count > (uint64_t)pgrid * kPassBlock * kPassUnroll;
+}
+static void launch_bucket(const RsckArgs &a, int pgrid, hipStream_t st) {
+  if (pass_big(a, pgrid)) launch_bucket_u<kPassUnrollBig>(a, pgrid, st);
+  else launch_bucket_u<kPassUnroll>(a, pgrid, st);
 }
 
 hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, hipStream_t st) {
@@ -1150,7 +1167,8 @@ hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, hipStream_t st) {
   // the small pool [0, ctr->small): one lane per packet
   hipLaunchKernelGGL(icrc_rsmall_kernel, dim3(grid), dim3(kBlock), 0, st, a);
   // the gather's blocks are the bucket pass's (block b serves pass block b's packets)
-  hipLaunchKernelGGL(rsck_gather, dim3(pgrid), dim3(kPassBlock), 0, st, a);
+  if (pass_big(a, pgrid)) hipLaunchKernelGGL(rsck_gather<kPassUnrollBig>, dim3(pgrid), dim3(kPassBlock), 0, st, a);
+  else hipLaunchKernelGGL(rsck_gather<kPassUnroll>, dim3(pgrid), dim3(kPassBlock), 0, st, a);
   return hipGetLastError();
 }
 

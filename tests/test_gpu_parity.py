@@ -436,6 +436,24 @@ def test_c4_full_size_bit_exact(ctx):
     assert int(_host_u32(out).astype(np.uint64).sum()) == count
 
 
+@pytest.mark.slow
+def test_ragged_more_than_4m_packets(ctx):
+    """More than 256 x 1024 x 16 packets (C4's byte-balanced shards at N > 1
+    hold up to 4.2 M): the bucket and gather passes read 17 packets per
+    thread so every block stays one staged round -- mixed classes, every ICRC
+    against the oracle."""
+    rng = np.random.default_rng(4242)
+    count = 4_200_000
+    lens = rng.choice(np.array([64, 100, 256, 1024], np.uint32), size=count, p=[0.4, 0.3, 0.25, 0.05])
+    offs = np.zeros(count, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    buf = rng.integers(0, 256, size=int(offs[-1] + lens[-1]) + 64, dtype=np.uint8)
+    want = oracle_c.icrc_batch(buf, offsets=offs, lengths=lens, threads=16)
+    out = _out(count)
+    ctx.batch_device(_dev(buf), count, out, offsets=_dev(offs), lengths=_dev(lens), stream=_stream())
+    np.testing.assert_array_equal(_host_u32(out), want)
+
+
 @pytest.mark.parametrize("n", [1024, 2048, 4096])
 @pytest.mark.parametrize("count,grid", [(1, None), (7, None), (9, None), (8 * 16 * 64 + 3, 1),
                                          (8 * 16 * 130 + 5, 1), (8 * 16 * 200, 2), (70001, None)])

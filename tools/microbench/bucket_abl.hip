@@ -174,7 +174,7 @@ int main(int argc, char **argv) {
       for (int it = 0; it < 23; ++it) {
         CK(hipMemcpyAsync(a.ctr, saved, sizeof(RsCounters), hipMemcpyDeviceToDevice, 0));
         CK(hipEventRecord(e0, 0));
-        hipLaunchKernelGGL(rsck_gather, dim3(pgrid), dim3(kPassBlock), 0, 0, a);
+        hipLaunchKernelGGL(rsck_gather<kPassUnroll>, dim3(pgrid), dim3(kPassBlock), 0, 0, a);
         CK(hipEventRecord(e1, 0)); CK(hipEventSynchronize(e1));
         float ms; CK(hipEventElapsedTime(&ms, e0, e1));
         if (it >= 3) tot += ms;

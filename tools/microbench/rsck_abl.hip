@@ -96,7 +96,7 @@ int main(int argc, char **argv) {
           hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, 0, a);
           CK(hipEventRecord(f1, 0));
           hipLaunchKernelGGL(icrc_rsmall_kernel, dim3(grid), dim3(kBlock), 0, 0, a);
-          hipLaunchKernelGGL(rsck_gather, dim3(pgrid), dim3(kPassBlock), 0, 0, a);
+          hipLaunchKernelGGL(rsck_gather<kPassUnroll>, dim3(pgrid), dim3(kPassBlock), 0, 0, a);
           CK(hipEventSynchronize(f1));
           float ms; CK(hipEventElapsedTime(&ms, f0, f1));
           if (it >= 3) tot += ms;
