@@ -49,26 +49,34 @@ MIX_SIZES = (64, 256, 1024, 4096)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 SEED = 0x1CEC0DE
 # Headline kernel's sources: PMC traffic (profiles/pmc_traffic.json) is only
-# reported for the exact sources it was measured on.
-SCK_SOURCES = ("icrc_sck.hip", "icrc_sck.h", "icrc_device.h", "icrc_math.h")
+# reported for the exact sources it was measured on -- the kernel's own and
+# icrc_api.cpp, which picks its launch configuration (grids, pass sizes).
+SCK_SOURCES = ("icrc_sck.hip", "icrc_sck.h", "icrc_device.h", "icrc_math.h", "icrc_api.cpp")
 # The ragged pipeline's (C4, --mix): passes, fold, one-line kernel, gather.
-RAGGED_SOURCES = ("icrc_rsck.hip", "icrc_kernels.h", "icrc_sck.h", "icrc_device.h", "icrc_math.h")
+RAGGED_SOURCES = ("icrc_rsck.hip", "icrc_kernels.h", "icrc_sck.h", "icrc_device.h", "icrc_math.h", "icrc_api.cpp")
 # The quad kernel's (C1: back-to-back 64-byte packets).
-QUAD_SOURCES = ("icrc_kernels.hip", "icrc_kernels.h", "icrc_device.h", "icrc_math.h")
+QUAD_SOURCES = ("icrc_kernels.hip", "icrc_kernels.h", "icrc_device.h", "icrc_math.h", "icrc_api.cpp")
 
 
-def traffic_record(mix, size):
+RAGGED_KERNELS = ("rsck_bucket", "icrc_rsck_kernel", "icrc_rsmall_kernel", "rsck_gather")
+
+
+def traffic_record(mix, size, count=None):
     """(profiles/ file, kernel sources, kernel names) of the PMC traffic
-    record for a workload (tools/pmc_traffic.py writes it), or None."""
+    record for a workload of `count` packets on this rank (tools/pmc_traffic.py
+    writes it), or None.  The BASELINE counts (1 M fixed-size packets, 4 M
+    mixed) keep their round-3 names; other counts (C3's 16 GiB batch, the
+    8-GPU shard stand-ins) carry the count in the name."""
+    std = (4 << 20) if mix else (1 << 20)
+    tag = "" if count in (None, std) else f"_{count}"
     if mix:
-        return "pmc_traffic_mix.json", RAGGED_SOURCES, ("rsck_bucket", "icrc_rsck_kernel", "icrc_rsmall_kernel",
-                                                        "rsck_gather")
+        return f"pmc_traffic_mix{tag}.json", RAGGED_SOURCES, RAGGED_KERNELS
     if size == 4096:
-        return "pmc_traffic.json", SCK_SOURCES, ("icrc_sck_kernel",)
+        return (f"pmc_traffic_4096{tag}.json" if tag else "pmc_traffic.json"), SCK_SOURCES, ("icrc_sck_kernel",)
     if size in (1024, 2048):
-        return f"pmc_traffic_{size}.json", SCK_SOURCES, ("icrc_sck_kernel",)
+        return f"pmc_traffic_{size}{tag}.json", SCK_SOURCES, ("icrc_sck_kernel",)
     if size == 64:
-        return "pmc_traffic_64.json", QUAD_SOURCES, ("icrc_quad_kernel",)
+        return f"pmc_traffic_64{tag}.json", QUAD_SOURCES, ("icrc_quad_kernel",)
     return None
 
 
@@ -151,7 +159,7 @@ def load_traffic(args, count):
     """HBM bytes per launch measured by separate rocprofv3 --pmc passes
     (profiles/pmc_traffic*.json, from tools/pmc_traffic.py) on this very
     workload and kernel source, or None."""
-    rec = traffic_record(args.mix, args.size)
+    rec = traffic_record(args.mix, args.size, count)
     if args.family != "v4" or rec is None:
         return None
     name, srcs, _ = rec
@@ -168,13 +176,45 @@ def load_traffic(args, count):
     return None
 
 
-def kernel_label(size):
-    """The kernel libroceicrc's dispatch picks for back-to-back packets of `size` bytes."""
-    if size in (1024, 2048, 4096):
-        return "strided-chain ICRC kernel (icrc_sck_kernel)"
-    if 128 <= size <= 4096 and size & (size - 1) == 0:
-        return "transposed streaming ICRC kernel (icrc_tsk_kernel)"
-    return "streaming ICRC kernel"
+# What each kernel of the dispatch is, for the workload string.
+KERNEL_ROLES = {
+    "icrc_sck_kernel": "strided-chain ICRC kernel",
+    "icrc_quad_kernel": "quad ICRC kernel (64-byte packets, lane-quad transposes)",
+    "icrc_tsk_kernel": "transposed streaming ICRC kernel",
+    "icrc_stream_kernel": "direct streaming ICRC kernel",
+    "rsck_bucket": "bucket pass",
+    "icrc_rsck_kernel": "strided-chain fold of packets of >= 2 lines",
+    "icrc_rsmall_kernel": "one-line packets",
+    "rsck_gather": "gather",
+    "family_fix_kernel": "address-family fix-up",
+}
+
+
+def kernel_path(args, base=0x100000, count=1):
+    """The kernels libroceicrc's dispatch launches for this workload, straight
+    from the library (ricrc_kernel_path: the same code that launches them),
+    with ``base`` the batch's device address (only its alignment matters)."""
+    import roce_icrc
+
+    if args.mix:
+        return roce_icrc.kernel_path(base, count, offsets=8, lengths=8, family=args.family)
+    return roce_icrc.kernel_path(base, count, stride=args.size, family=args.family)
+
+
+def kernel_label(args, base=0x100000, count=1):
+    """Human-readable label of kernel_path: 'role (kernel) -> role (kernel)'."""
+    return " -> ".join(f"{KERNEL_ROLES.get(k, k)} ({k})" for k in kernel_path(args, base, count).split("+"))
+
+
+def rccl_version():
+    """RCCL's version as torch reports it ("nccl" is RCCL on ROCm), or None."""
+    try:
+        import torch
+
+        v = torch.cuda.nccl.version()
+        return ".".join(map(str, v)) if isinstance(v, tuple) else str(v)
+    except Exception:
+        return None
 
 
 def cpu_share():
@@ -290,19 +330,25 @@ def cpu_baseline(sample_host, got_sample, size, budget_s, offsets=None, lengths=
             icrc_oracle.icrc(p, family)
             zb += len(p)
     zdt = time.perf_counter() - zt0
+    oracle_gibs = sample_bytes * reps / dt / 2**30
+    prod = product_cpu(sample_host, got_sample, size, min(5.0, budget_s), threads, offsets, lengths, family)
+    if not isinstance(prod, float):
+        raise SystemExit(f"bench: the product CPU path disagrees with the GPU on the CPU-baseline sample ({prod})")
+    # value: the build's own CPU batch path (SURVEY.md 8(d)(3) names it the CPU
+    # baseline); the C oracle's time on the same sample is a side key.
     return {
-        "value": sample_bytes * reps / dt / 2**30,
+        "value": round(prod, 2),
         "unit": "GiB/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{what} of the same synthetic batch, {reps} passes in {dt:.1f} s; oracle/icrc_oracle.c "
-                  f"slice-by-8 on {threads} threads (this GPU's CPU share of {os.cpu_count()} visible host CPUs)",
+        "sample": f"{what} of the same synthetic batch; ricrc_batch_cpu (libroceicrc_cpu.so: the slice-by-16 fold of "
+                  f"ricrc_one, the build's CPU path restating calc_icrc) on {threads} threads (this GPU's CPU share of "
+                  f"{os.cpu_count()} visible host CPUs), ICRCs checked equal to the GPU's first",
         "cpu_model": cpu_model(),
+        "oracle_port_GiBs": round(oracle_gibs, 2),
+        "oracle_port": f"oracle/icrc_oracle.c slice-by-8 on the same sample and {threads} threads, {reps} passes in "
+                       f"{dt:.1f} s (test infrastructure; the checker)",
         "zlib_1core_GiBs": round(zb / zdt / 2**30, 3),
-        "product_cpu_GiBs": (lambda v: round(v, 2) if isinstance(v, float) else v)(
-            product_cpu(sample_host, got_sample, size, min(3.0, budget_s), threads, offsets, lengths, family)),
-        "product_cpu": f"ricrc_batch_cpu (libroceicrc_cpu.so, slice-by-16 fold of ricrc_one) on the same sample "
-                       f"and {threads} threads -- the build's own CPU path, not the reference's",
     }
 
 
@@ -575,6 +621,33 @@ def run(args, world, rank, be, distributed):
     elapsed = time.perf_counter() - t0
     kern_ms = sum(a.elapsed_time(c) for a, c in evs) / max(args.steps, 1)
 
+    # ---- N > 1, after the timed region: the step's two parts timed apart
+    # (compute-only and with-gather scaling reported
+    # separately), each as K more iterations between barrier + synchronize,
+    # max over ranks -- so a shortfall of the driver's scaling run can be
+    # pinned on the kernels or on the collective.
+    split = None
+    if distributed:
+        def timed(fn):
+            be.sync()
+            dist.barrier()
+            be.sync()
+            t = time.perf_counter()
+            for i in range(args.steps):
+                fn(i)
+            be.sync()
+            dist.barrier()
+            be.sync()
+            return (time.perf_counter() - t) * 1e3 / max(args.steps, 1)
+
+        def compute_only(i):
+            if count:
+                be.compute(b, count, outs[i & 1], args)
+
+        split = {"compute_only_ms_per_step": timed(compute_only)}
+        if do_gather:
+            split["gather_ms"] = timed(lambda i: g.start(outs[0], gathered[0], async_op=False))
+
     # ---- after the timed region: correctness on every rank
     last = (args.steps - 1) & 1
     out = outs[last][:count]
@@ -597,9 +670,11 @@ def run(args, world, rank, be, distributed):
 
     all_bytes = rank_bytes
     if distributed:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=be.dev)
+        keys = sorted(split)
+        t = torch.tensor([elapsed, kern_ms] + [split[k] for k in keys], dtype=torch.float64, device=be.dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
+        split = {k: round(float(v), 4) for k, v in zip(keys, t[2:])}
         nb = torch.tensor([rank_bytes], dtype=torch.int64, device=be.dev)
         dist.all_reduce(nb, op=dist.ReduceOp.SUM)
         all_bytes = int(nb[0])
@@ -611,15 +686,16 @@ def run(args, world, rank, be, distributed):
     traffic = load_traffic(args, count)
 
     strong = args.global_count is not None
+    base = b["buf"].data_ptr() if hasattr(b["buf"], "data_ptr") else 0x100000
+    label = kernel_label(args, base, max(count, 1))  # from the library's own dispatch (ricrc_kernel_path)
     if args.mix:
         workload = (f"{b['T']} RoCEv2 packets in all ({'fixed total' if strong else f'{args.count} per GPU'}), "
                     "lengths uniform over 64/256/1024/4096 B, packed, uint64 offsets + uint32 lengths, "
                     f"shards cut at equal bytes; rank 0: {sizes[0]} packets, {rank_bytes if rank == 0 else '?'} B; "
-                    "device-resident, ragged strided-chain path (count/plan + scatter passes, icrc_rsck_kernel "
-                    "for packets of >= 2 lines, icrc_rsmall_kernel for one-line packets, gather)")
+                    f"device-resident, ragged path: {label}")
     else:
         workload = (f"{b['T']} x {args.size} B RoCEv2 packets in all ({count} on rank 0), device-resident, "
-                    + kernel_label(args.size))
+                    + label)
     if do_gather:
         workload += " + RCCL all-gather of the u32 ICRCs" + (" (overlapped)" if args.overlap_gather else "")
     result = {
@@ -643,6 +719,11 @@ def run(args, world, rank, be, distributed):
                      "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": alg_bytes},
         "oracle_sampled_all_ranks": True,
     }
+    if distributed:
+        result["world_size"] = dist.get_world_size()
+        result["collective_backend"] = dist.get_backend()
+        result["rccl_version"] = rccl_version()
+        result.update(split)
     return result, full_h, b
 
 

@@ -102,6 +102,18 @@ int ricrc_batch_cpu(const uint8_t *base, const uint64_t *off, const uint32_t *le
 #define RICRC_F_IPV6 1u
 #define RICRC_F_AUTO 2u
 #define RICRC_F_STRICT 0x100u /* ricrc_icrc / *_st calls: reject packets that do not classify */
+/* ricrc_icrc / ricrc_batch_cpu / *_st calls: the length a descriptor gives
+ * (n, len[i], or stride - l3_offset) is the FRAME's extent past the L3
+ * start, which on an Ethernet NIC ring may include minimum-frame padding (a
+ * 44-byte SEND_ONLY in a 60-byte frame: 2 bytes) and a kept FCS (4 bytes).
+ * The packet's L3 length is then its IP header's -- IPv4 total_len, IPv6
+ * payload length + 40 -- whenever that lies in [RICRC_MIN_LEN, the
+ * descriptor length]; otherwise the descriptor length stands (and
+ * RICRC_F_STRICT rejects the packet, its total_len not matching).  The
+ * reference's parser takes each header's fields from the packet and never
+ * uses a descriptor length (shuffle_ingress_parser.p4:12-36; total_len at
+ * header.p4:45).  Without this flag the descriptor length is the L3 length. */
+#define RICRC_F_FRAMELEN 0x400u
 
 uint32_t ricrc_one_ex(const uint8_t *l3, uint32_t n, uint32_t flags);
 int ricrc_verify_one_ex(const uint8_t *l3, uint32_t n, uint32_t flags);
@@ -349,6 +361,19 @@ int ricrc_prime(ricrc_ctx *ctx, int dev, uint32_t usec);
 
 /* The context's own stream (a hipStream_t) for context device dev. */
 void *ricrc_stream(ricrc_ctx *ctx, int dev);
+
+/* The gfx950 kernel(s) ricrc_batch_device(_ex) launches for a batch of this
+ * shape, from the same dispatch code: a static string of '+'-joined kernel
+ * names as rocprofv3 reports them, e.g. "icrc_sck_kernel" (back-to-back 1, 2,
+ * 4 KiB packets), "icrc_quad_kernel" (back-to-back 64 B) or
+ * "rsck_bucket+icrc_rsck_kernel+icrc_rsmall_kernel+rsck_gather" (the ragged
+ * pipeline), "+family_fix_kernel" for IPv6 / AUTO where the kernel applies
+ * IPv4 masks.  No GPU is touched: d_base is inspected only for its alignment;
+ * ctx may be NULL (the dispatch without the context's RICRC_NO_* test knobs).
+ * NULL for a call ricrc_batch_device would reject (flags as the *_ex calls).
+ * Bench and test labels come from here, so they name what actually ran. */
+const char *ricrc_kernel_path(const ricrc_ctx *ctx, const void *d_base, const uint64_t *d_off, const uint32_t *d_len,
+                              uint32_t stride, uint64_t count, uint32_t l3_offset, uint32_t flags);
 
 const char *ricrc_strerror(int err);
 

@@ -203,13 +203,35 @@ def classify(l3: bytes, ethertype: int | None = None) -> int:
 ST_OK, ST_BADLEN, ST_NOTROCE = 0, 1, 2
 
 
+def frame_l3_len(frame: bytes) -> int:
+    """RICRC_F_FRAMELEN: the L3 length of a packet given the bytes from its L3
+    header to the end of its frame, which on an Ethernet NIC ring may carry
+    minimum-frame padding and the FCS after the datagram.  The reference's
+    parser keys only on EtherType / protocol / dport
+    (shuffle_ingress_parser.p4:12-36) and never uses a descriptor length; the
+    datagram's own extent is ipv4_h.total_len (header.p4:45), or, for IPv6,
+    payload length + 40.  That length is taken whenever it lies in
+    [MIN_PKT, len(frame)]; otherwise the frame length stands (and a strict
+    classification then rejects the packet).  A frame extent outside
+    [MIN_PKT, MAX_PKT] is a bad length whatever its header says."""
+    n = len(frame)
+    if n < MIN_PKT or n > MAX_PKT:
+        return n
+    v = frame[0] >> 4
+    t = ((frame[2] << 8) | frame[3]) if v == 4 else (((frame[4] << 8) | frame[5]) + 40 if v == 6 else 0)
+    return t if MIN_PKT <= t <= n else n
+
+
 def status_batch(buf: np.ndarray, offsets=None, lengths=None, stride: int = 0, count: int | None = None,
-                 l3_offset: int = 0, family: str = "v4", strict: bool = False, verify: bool = False):
+                 l3_offset: int = 0, family: str = "v4", strict: bool = False, verify: bool = False,
+                 framelen: bool = False):
     """(out, status) of ricrc_batch_*_st on a packed batch: per packet
     ST_BADLEN for a length outside [MIN_PKT, MAX_PKT], ST_NOTROCE under
     ``strict`` for a packet :func:`classify` rejects (EtherType checked when
     l3_offset >= 14) or of a family not asked for, else ST_OK with the ICRC
-    (``verify``: 1/0 trailer check); out = 0 where status != ST_OK."""
+    (``verify``: 1/0 trailer check); out = 0 where status != ST_OK.
+    ``framelen`` (RICRC_F_FRAMELEN): the descriptor length is the frame's
+    extent past L3 and the packet's is :func:`frame_l3_len` of it."""
     mv = memoryview(np.ascontiguousarray(buf).reshape(-1).view(np.uint8))
     if count is None:
         count = len(offsets) if offsets is not None else len(mv) // stride
@@ -219,6 +241,8 @@ def status_batch(buf: np.ndarray, offsets=None, lengths=None, stride: int = 0, c
     for i in range(count):
         o = int(offsets[i]) if offsets is not None else i * stride
         n = int(lengths[i]) if lengths is not None else stride - l3_offset
+        if framelen and MIN_PKT <= n <= MAX_PKT:
+            n = frame_l3_len(mv[o + l3_offset: o + l3_offset + n].tobytes())
         if n < MIN_PKT or n > MAX_PKT:
             st[i] = ST_BADLEN
             continue

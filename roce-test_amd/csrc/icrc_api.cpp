@@ -15,6 +15,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <new>
 #include <type_traits>
@@ -35,6 +36,10 @@ constexpr uint64_t kStagePkts = 1ull << 20;     // per staging slot (packets)
 // Ragged-path workspaces per device, one per recently used stream: batch_host's
 // two slot streams + the context stream + callers' streams.
 constexpr size_t kMaxWorkspaces = 8;
+// ... and at most this many bytes of them per device (one workspace for a
+// 2^28-packet chunk is ~7.5 GB): least recently used ones are freed first
+// when a workspace grows; the one in use is never evicted.
+constexpr uint64_t kMaxWorkspaceBytes = 12ull << 30;
 constexpr uint64_t kRsChunk = kRsMaxCount;  // the ragged pipeline's group counter is 26-bit: longer batches are cut
 
 // Environment knobs, read ONCE by ricrc_create (diagnostics, tests and
@@ -93,6 +98,7 @@ struct Dev {
     hipEvent_t done;
   };
   std::vector<Ws> ws;
+  std::vector<hipEvent_t> spare;  // events of workspaces evicted for bytes, reused by the next new one
 };
 
 int hip_err(hipError_t e) {
@@ -135,6 +141,9 @@ struct ricrc_ctx {
   std::vector<Dev> devs;
   std::vector<HostRange> pinned;  // host ranges the DMA engines may read directly
   Knobs knobs;
+  // RICRC_FAIL_CHUNK's one-shot state (tests): consumed by a compare-exchange,
+  // so two host threads sharing a context cannot both fire it.
+  std::atomic<long> fail_once{-1};
   std::vector<ncclComm_t> comms;  // ricrc_comm_init: one RCCL communicator per device
 };
 
@@ -204,6 +213,8 @@ void free_dev(Dev &d) {
     (void)hipFree(w.p);
   }
   d.ws.clear();
+  for (hipEvent_t e : d.spare) (void)hipEventSynchronize(e), (void)hipEventDestroy(e);
+  d.spare.clear();
   (void)hipFree(d.d_tzb);
   (void)hipFree(d.d_x8n);
   if (d.stream) (void)hipStreamDestroy(d.stream);
@@ -240,6 +251,9 @@ int ragged_ws(Dev &d, hipStream_t st, uint64_t bytes, Dev::Ws **out) {
       HIP_TRY(hipStreamWaitEvent(st, old.done, 0));
       if (old.p) HIP_TRY(hipFreeAsync(old.p, st));
       w.done = old.done;  // re-recorded after this call
+    } else if (!d.spare.empty()) {
+      w.done = d.spare.back();
+      d.spare.pop_back();
     } else {
       HIP_TRY(hipEventCreateWithFlags(&w.done, hipEventDisableTiming));
     }
@@ -251,6 +265,19 @@ int ragged_ws(Dev &d, hipStream_t st, uint64_t bytes, Dev::Ws **out) {
     w->p = nullptr;
     w->bytes = 0;
     const uint64_t grow = std::max<uint64_t>(bytes, bytes + bytes / 4);
+    // Byte cap: free least recently used workspaces (in stream order on st,
+    // after their last use) until this one fits beside the rest.
+    uint64_t others = 0;
+    for (size_t k = 0; k + 1 < d.ws.size(); ++k) others += d.ws[k].bytes;
+    while (d.ws.size() > 1 && others + grow > kMaxWorkspaceBytes) {
+      Dev::Ws old = d.ws.front();
+      d.ws.erase(d.ws.begin());
+      HIP_TRY(hipStreamWaitEvent(st, old.done, 0));
+      if (old.p) HIP_TRY(hipFreeAsync(old.p, st));
+      others -= old.bytes;
+      d.spare.push_back(old.done);
+    }
+    w = &d.ws.back();
     HIP_TRY(hipMallocAsync(&w->p, grow, st));
     w->bytes = grow;
     w->dirty = true;
@@ -335,16 +362,62 @@ int launch_rsck_range(Dev &d, const uint8_t *base, const uint64_t *off, const ui
   return hip_err(e != hipSuccess ? e : e2);
 }
 
+// The kernel path of a batch: ONE decision, used by launch_batch_v4 and by
+// ricrc_kernel_path (which bench.py and the tests query, so the labels of a
+// run cannot drift from what ran).
+enum class Path { kSck, kQuad, kTsk, kStream, kRagged };
+
+// Chunks of a fixed-length batch per lane of the direct streaming kernel
+// (1, 2 or 4), or 0 if its packets are too long for it.
+int stream_cpl(uint32_t fixed_len) {
+  const uint32_t M = fixed_len - 4;
+  for (int c : {1, 2, 4})
+    if ((M + 64u * c - 1) / (64u * c) <= 64) return c;
+  return 0;
+}
+
+Path choose_path(const Knobs &kn, const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
+                 uint32_t l3_offset) {
+  const uint8_t *first = base + l3_offset;
+  const uint32_t fixed_len = stride > l3_offset ? (uint32_t)std::min<uint64_t>(stride - l3_offset, 0xFFFFFFFFu) : 0u;
+  const bool aligned = ((uintptr_t)first % 16 == 0) && (stride % 16 == 0);
+  if (off || len || !aligned || fixed_len < kMinLen || fixed_len > kMaxLen || fixed_len % 4 != 0) return Path::kRagged;
+  // Back-to-back 1, 2 or 4 KiB packets: the strided-chain kernel (no LDS transpose).
+  if (l3_offset == 0 && (uintptr_t)base % 16 == 0 && !kn.no_sck && (stride == 1024 || stride == 2048 || stride == 4096))
+    return Path::kSck;
+  // Back-to-back 64-byte packets (C1): the quad kernel, coalesced 1 KiB loads.
+  if (fixed_len == 64 && stride == 64 && l3_offset == 0 && (uintptr_t)base % 16 == 0 && !kn.no_quad) return Path::kQuad;
+  const int cpl = stream_cpl(fixed_len);
+  // Back-to-back packets of 32 * 2^j bytes: coalesced + LDS-transposed kernel.
+  // (64-byte packets: the direct streaming kernel is faster, 20.1 vs 23.8 us on 1 M x 64 B.)
+  if (cpl && l3_offset == 0 && stride == fixed_len && fixed_len >= 128 && fixed_len <= 4096 &&
+      (fixed_len & (fixed_len - 1)) == 0 && ((uintptr_t)base % 16 == 0) && !kn.no_tsk)
+    return Path::kTsk;
+  // any other fixed length up to 16 KiB: lanes fold 64 CPL-byte chunks
+  return cpl ? Path::kStream : Path::kRagged;
+}
+
+const char *path_kernels(Path p) {
+  switch (p) {
+    case Path::kSck: return "icrc_sck_kernel";
+    case Path::kQuad: return "icrc_quad_kernel";
+    case Path::kTsk: return "icrc_tsk_kernel";
+    case Path::kStream: return "icrc_stream_kernel";
+    default: return "rsck_bucket+icrc_rsck_kernel+icrc_rsmall_kernel+rsck_gather";
+  }
+}
+
 int launch_batch_v4(Dev &d, const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
                     uint64_t count, uint32_t l3_offset, uint32_t *out, hipStream_t st, bool verify,
                     uint32_t family = kFamV4) {
   if (count == 0) return 0;
   const uint8_t *first = base + l3_offset;
   const uint32_t fixed_len = stride > l3_offset ? (uint32_t)std::min<uint64_t>(stride - l3_offset, 0xFFFFFFFFu) : 0u;
-  const bool aligned = ((uintptr_t)first % 16 == 0) && (stride % 16 == 0);
-  if (!off && !len && aligned && fixed_len >= kMinLen && fixed_len <= kMaxLen && fixed_len % 4 == 0) {
+  const Path path = choose_path(d.knobs, base, off, len, stride, l3_offset);
+  if (path != Path::kRagged) {
     // Back-to-back 1, 2 or 4 KiB packets: the strided-chain kernel (no LDS transpose).
-    if (const int sgrid = sck_grid(d, base, off, len, stride, count, l3_offset)) {
+    if (path == Path::kSck) {
+      const int sgrid = sck_grid(d, base, off, len, stride, count, l3_offset);
       SckArgs k{};
       k.family = family;
       k.base = base;
@@ -358,8 +431,7 @@ int launch_batch_v4(Dev &d, const uint8_t *base, const uint64_t *off, const uint
       return hip_err(launch_sck(k, sgrid, st));
     }
     const uint32_t M = fixed_len - 4;
-    // Back-to-back 64-byte packets (C1): the quad kernel, coalesced 1 KiB loads.
-    if (fixed_len == 64 && stride == 64 && l3_offset == 0 && (uintptr_t)base % 16 == 0 && !d.knobs.no_quad) {
+    if (path == Path::kQuad) {
       QuadArgs q{};
       q.base = base;
       q.count = count;
@@ -369,16 +441,8 @@ int launch_batch_v4(Dev &d, const uint8_t *base, const uint64_t *off, const uint
       const int qgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)d.n_cu, (steps + 15) / 16));
       return hip_err(launch_quad(q, qgrid, st));
     }
-    int cpl = 0;
-    for (int c : {1, 2, 4})
-      if ((M + 64u * c - 1) / (64u * c) <= 64) {
-        cpl = c;
-        break;
-      }
-    // Back-to-back packets of 32 * 2^j bytes: coalesced + LDS-transposed kernel.
-    // (64-byte packets: the direct streaming kernel is faster, 20.1 vs 23.8 us on 1 M x 64 B.)
-    if (cpl && l3_offset == 0 && stride == fixed_len && fixed_len >= 128 && fixed_len <= 4096 &&
-        (fixed_len & (fixed_len - 1)) == 0 && ((uintptr_t)base % 16 == 0) && !d.knobs.no_tsk) {
+    const int cpl = stream_cpl(fixed_len);
+    if (path == Path::kTsk) {
       TskArgs t{};
       t.base = base;
       t.stride = stride;
@@ -397,7 +461,7 @@ int launch_batch_v4(Dev &d, const uint8_t *base, const uint64_t *off, const uint
       const int tgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)d.n_cu, tw));
       return hip_err(launch_tsk(t, tgrid, st));
     }
-    if (cpl) {  // any other fixed length up to 16 KiB: lanes fold 64 CPL-byte chunks
+    {  // Path::kStream: any other fixed length up to 16 KiB, lanes fold 64 CPL-byte chunks
       StreamArgs a{};
       const uint32_t chunk = 64u * cpl;
       a.base = first;
@@ -440,7 +504,7 @@ int launch_batch(Dev &d, const uint8_t *base, const uint64_t *off, const uint32_
                  uint32_t family = kFamV4) {
   if (family == kFamV4 || count == 0)
     return launch_batch_v4(d, base, off, len, stride, count, l3_offset, out, st, verify);
-  if (sck_grid(d, base, off, len, stride, count, l3_offset))  // masks native in the kernel
+  if (choose_path(d.knobs, base, off, len, stride, l3_offset) == Path::kSck)  // masks native in the kernel
     return launch_batch_v4(d, base, off, len, stride, count, l3_offset, out, st, verify, family);
   const int rc = launch_batch_v4(d, base, off, len, stride, count, l3_offset, out, st, false);
   if (rc) return rc;
@@ -565,18 +629,19 @@ int launch_status_pass(Dev &d, const uint8_t *base, const uint64_t *off, const u
   return hip_err(launch_status(a, d.n_cu, st));
 }
 
-// flags of the *_st calls: a family | RICRC_F_STRICT | RICRC_F_VERIFY.
+// flags of the *_st calls: a family | RICRC_F_STRICT | RICRC_F_VERIFY | RICRC_F_FRAMELEN.
 struct StFlags {
   uint32_t fam;
-  bool strict, verify;
+  bool strict, verify, framelen;
   uint32_t accept;  // StatusArgs::accept
 };
 bool decode_st_flags(uint32_t flags, StFlags &f) {
-  if (flags & ~(3u | RICRC_F_STRICT | RICRC_F_VERIFY)) return false;
+  if (flags & ~(3u | RICRC_F_STRICT | RICRC_F_VERIFY | RICRC_F_FRAMELEN)) return false;
   f.fam = flags & 3u;
   if (f.fam > RICRC_F_AUTO) return false;
   f.strict = (flags & RICRC_F_STRICT) != 0;
   f.verify = (flags & RICRC_F_VERIFY) != 0;
+  f.framelen = (flags & RICRC_F_FRAMELEN) != 0;
   f.accept = !f.strict ? 0u : f.fam == RICRC_F_IPV4 ? 1u : f.fam == RICRC_F_IPV6 ? 2u : 3u;
   return true;
 }
@@ -617,6 +682,7 @@ int ricrc_create_devices(ricrc_ctx **ctx, const int *devices, int n) {
   ricrc_ctx *c = new (std::nothrow) ricrc_ctx;
   if (!c) return -ENOMEM;
   c->knobs = read_knobs();
+  c->fail_once.store(c->knobs.fail_chunk);
   g_debug = getenv("RICRC_DEBUG") != nullptr;
   c->devs.resize(n);
   for (int i = 0; i < n; ++i) {
@@ -663,6 +729,21 @@ int ricrc_device_count(const ricrc_ctx *ctx) { return ctx ? (int)ctx->devs.size(
 void *ricrc_stream(ricrc_ctx *ctx, int dev) {
   if (!ctx || dev < 0 || dev >= (int)ctx->devs.size()) return nullptr;
   return ctx->devs[dev].stream;
+}
+
+const char *ricrc_kernel_path(const ricrc_ctx *ctx, const void *d_base, const uint64_t *d_off, const uint32_t *d_len,
+                              uint32_t stride, uint64_t count, uint32_t l3_offset, uint32_t flags) {
+  if (!d_base || flags > RICRC_F_AUTO || count == 0) return nullptr;
+  if ((!d_off && stride == 0) || (!d_len && stride <= l3_offset)) return nullptr;
+  const Knobs kn = ctx ? ctx->knobs : Knobs{};
+  const Path p = choose_path(kn, (const uint8_t *)d_base, d_off, d_len, stride, l3_offset);
+  if (flags == RICRC_F_IPV4 || p == Path::kSck) return path_kernels(p);  // the SCK applies every family natively
+  switch (p) {  // IPv6 / AUTO: the IPv4-mask kernels, then the linear header fix-up
+    case Path::kQuad: return "icrc_quad_kernel+family_fix_kernel";
+    case Path::kTsk: return "icrc_tsk_kernel+family_fix_kernel";
+    case Path::kStream: return "icrc_stream_kernel+family_fix_kernel";
+    default: return "rsck_bucket+icrc_rsck_kernel+icrc_rsmall_kernel+rsck_gather+family_fix_kernel";
+  }
 }
 
 static int batch_device_impl(ricrc_ctx *ctx, int dev, const void *d_base, const uint64_t *d_off,
@@ -720,10 +801,34 @@ int ricrc_batch_device_st(ricrc_ctx *ctx, int dev, const void *d_base, const uin
   if (!g.ok()) return -ENODEV;
   hipStream_t st = (hipStream_t)stream;
   const uint8_t *base = (const uint8_t *)d_base;
-  const int rc = launch_batch(d, base, d_off, d_len, stride, count, l3_offset, d_out, st, f.verify, f.fam);
-  if (rc) return rc;
-  return launch_status_pass(d, base, d_off, d_len, stride, count, l3_offset, f.accept,
-                            f.strict && l3_offset >= 14, d_out, d_status, nullptr, st);
+  uint32_t *eff = nullptr;  // RICRC_F_FRAMELEN: the packets' L3 lengths from their IP headers
+  if (f.framelen) {
+    HIP_TRY(hipMallocAsync((void **)&eff, count * sizeof(uint32_t), st));
+    FrameLenArgs fa{};
+    fa.base = base;
+    fa.off = d_off;
+    fa.len = d_len;
+    fa.stride = stride;
+    fa.count = count;
+    fa.fixed_len = d_len ? 0u : stride - l3_offset;
+    fa.l3_offset = l3_offset;
+    fa.eff = eff;
+    int rc = hip_err(launch_framelen(fa, d.n_cu, st));
+    if (rc) {
+      (void)hipFreeAsync(eff, st);
+      return rc;
+    }
+    d_len = eff;  // every later pass runs on the packets' own lengths
+  }
+  int rc = launch_batch(d, base, d_off, d_len, stride, count, l3_offset, d_out, st, f.verify, f.fam);
+  if (!rc)
+    rc = launch_status_pass(d, base, d_off, d_len, stride, count, l3_offset, f.accept, f.strict && l3_offset >= 14,
+                            d_out, d_status, nullptr, st);
+  if (eff) {
+    const int rc2 = hip_err(hipFreeAsync(eff, st));  // stream-ordered: after the passes that read it
+    if (!rc) rc = rc2;
+  }
+  return rc;
 }
 
 int ricrc_classify_device(ricrc_ctx *ctx, int dev, const void *d_base, const uint64_t *d_off,
@@ -1004,12 +1109,17 @@ static int batch_host_impl(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *
   if (!off && stride == 0) return -EINVAL;
   if (!len && stride <= l3_offset) return -EINVAL;
   auto len_ok = [](uint64_t n) { return n >= kMinLen && n <= kMaxLen; };
-  // Bytes staged for packet i (0 for a bad length under a status array).
+  auto frame = [&](uint64_t i) -> uint64_t { return off ? off[i] : i * (uint64_t)stride; };
+  // Bytes staged for packet i (0 for a bad length under a status array);
+  // RICRC_F_FRAMELEN: its L3 length from its IP header (frame_l3_len).
   auto pkt_len = [&](uint64_t i) -> uint64_t {
-    const uint64_t n = len ? len[i] : (uint64_t)stride - l3_offset;
+    uint64_t n = len ? len[i] : (uint64_t)stride - l3_offset;
+    if (f.framelen && frame_len_applies((uint32_t)n)) {
+      const uint8_t *l3 = base + frame(i) + l3_offset;
+      n = frame_l3_len((uint32_t)n, l3[0], (uint32_t)l3[2] << 8 | l3[3], (uint32_t)l3[4] << 8 | l3[5]);
+    }
     return (status && !len_ok(n)) ? 0 : n;
   };
-  auto frame = [&](uint64_t i) -> uint64_t { return off ? off[i] : i * (uint64_t)stride; };
   if (!len && !len_ok((uint64_t)stride - l3_offset)) return -EINVAL;  // the batch's one length
   uint64_t total = 0;
   for (uint64_t i = 0; i < count; ++i) {
@@ -1056,7 +1166,7 @@ static int batch_host_impl(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *
   // Debug knob (tests): RICRC_FAIL_CHUNK=k fails the context's next host
   // call with -EIO right after chunk k (0-based, counted over devices) has
   // been queued; later calls run normally.
-  const long fail_chunk = ctx->knobs.fail_chunk;
+  const long fail_chunk = ctx->fail_once.load();
   long chunk_no = 0;
 
   auto run = [&]() -> int {
@@ -1104,7 +1214,7 @@ static int batch_host_impl(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *
             par_for(bytes, T, 4u << 20, [&](uint64_t a, uint64_t b) { memcpy(sl.h_buf + a, src + a, b - a); });
             HIP_TRY(hipMemcpyAsync(sl.d_buf + pad, sl.h_buf, bytes, hipMemcpyHostToDevice, sl.st));
           }
-          if (off || len)
+          if (off || len || f.framelen)
             for (uint64_t i = lo; i < hi; ++i) sl.h_off[i - lo] = frame(i) - s_lo + pad;
         } else {
           // Gather: packed L3 packets, 16-byte aligned each (after `pre`
@@ -1129,7 +1239,7 @@ static int batch_host_impl(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *
           HIP_TRY(hipMemcpyAsync(sl.d_buf, sl.h_buf, bytes, hipMemcpyHostToDevice, sl.st));
           kl3 = pre;
         }
-        const bool fixed = span && !off && !len;  // frames at i*stride from d_buf + pad
+        const bool fixed = span && !off && !len && !f.framelen;  // frames at i*stride from d_buf + pad
         const uint8_t *dbase = fixed ? sl.d_buf + pad : sl.d_buf;
         const uint64_t *doff = nullptr;
         const uint32_t *dlen = nullptr;
@@ -1155,8 +1265,8 @@ static int batch_host_impl(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *
         c.next = hi;
         c.slot ^= 1;
         if (chunk_no++ == fail_chunk) {
-          ctx->knobs.fail_chunk = -1;
-          return -EIO;
+          long armed = fail_chunk;
+          if (ctx->fail_once.compare_exchange_strong(armed, -1)) return -EIO;
         }
       }
     }

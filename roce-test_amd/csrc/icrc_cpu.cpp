@@ -64,6 +64,12 @@ uint32_t icrc_register(const uint8_t *l3, uint32_t n, uint32_t fam) {
 
 bool flags_ok(uint32_t flags) { return flags <= ricrc::kFamAuto; }
 
+// RICRC_F_FRAMELEN: the L3 length of the packet whose frame extends n bytes past l3.
+uint32_t frame_len(const uint8_t *l3, uint32_t n) {
+  if (!ricrc::frame_len_applies(n)) return n;
+  return ricrc::frame_l3_len(n, l3[0], (uint32_t)l3[2] << 8 | l3[3], (uint32_t)l3[4] << 8 | l3[5]);
+}
+
 }  // namespace
 
 extern "C" {
@@ -76,8 +82,10 @@ uint32_t ricrc_one_ex(const uint8_t *l3, uint32_t n, uint32_t flags) {
 uint32_t ricrc_one(const uint8_t *l3, uint32_t n) { return ricrc_one_ex(l3, n, RICRC_F_IPV4); }
 
 int ricrc_icrc(const uint8_t *l3, uint32_t n, uint32_t flags, uint32_t *out) {
-  const uint32_t fam = flags & ~RICRC_F_STRICT;
-  if (!l3 || !out || !flags_ok(fam) || n < RICRC_MIN_LEN || n > RICRC_MAX_LEN) return -EINVAL;
+  const uint32_t fam = flags & ~(RICRC_F_STRICT | RICRC_F_FRAMELEN);
+  if (!l3 || !out || !flags_ok(fam)) return -EINVAL;
+  if (flags & RICRC_F_FRAMELEN) n = frame_len(l3, n);
+  if (n < RICRC_MIN_LEN || n > RICRC_MAX_LEN) return -EINVAL;
   if (flags & RICRC_F_STRICT) {
     const int c = ricrc_classify(l3, n);
     const uint32_t want = fam == RICRC_F_AUTO ? 0u : (fam == RICRC_F_IPV6 ? 6u : 4u);
@@ -144,12 +152,16 @@ int ricrc_is_rocev2(const uint8_t *l3, uint32_t n) {
 int ricrc_batch_cpu(const uint8_t *base, const uint64_t *off, const uint32_t *len, uint32_t stride, uint64_t count,
                     uint32_t l3_offset, uint32_t *out, uint32_t flags, int threads) {
   if (count == 0) return 0;
+  const bool framelen = (flags & RICRC_F_FRAMELEN) != 0;
+  flags &= ~RICRC_F_FRAMELEN;
   if (!base || !out || !flags_ok(flags)) return -EINVAL;
   if (!off && stride == 0) return -EINVAL;
   if (!len && stride <= l3_offset) return -EINVAL;
   auto pkt = [&](uint64_t i, uint32_t &n) -> const uint8_t * {
     n = len ? len[i] : stride - l3_offset;
-    return base + (off ? off[i] : i * (uint64_t)stride) + l3_offset;
+    const uint8_t *p = base + (off ? off[i] : i * (uint64_t)stride) + l3_offset;
+    if (framelen) n = frame_len(p, n);
+    return p;
   };
   for (uint64_t i = 0; i < count; ++i) {
     uint32_t n;
@@ -165,10 +177,17 @@ int ricrc_batch_cpu(const uint8_t *base, const uint64_t *off, const uint32_t *le
   };
   const uint64_t t = (uint64_t)std::max(1, std::min(threads, 256));
   const uint64_t nt = std::min<uint64_t>(t, count);
+  // A thread that cannot be created must not throw across the C ABI: its
+  // range (and every later one) runs on the caller's thread instead.
   std::vector<std::thread> th;
-  th.reserve(nt - 1);
-  for (uint64_t k = 1; k < nt; ++k) th.emplace_back(work, count * k / nt, count * (k + 1) / nt);
+  uint64_t k = 1;
+  try {
+    th.reserve(nt - 1);
+    for (; k < nt; ++k) th.emplace_back(work, count * k / nt, count * (k + 1) / nt);
+  } catch (...) {
+  }
   work(0, count / nt);
+  if (k < nt) work(count * k / nt, count);
   for (auto &x : th) x.join();
   return 0;
 }

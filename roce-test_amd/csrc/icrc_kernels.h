@@ -210,6 +210,18 @@ struct StatusArgs {
   uint8_t *cls;     // classify mode (non-null): per-packet 4 / 6 / 0 instead of a status
 };
 hipError_t launch_status(const StatusArgs &a, int n_cu, hipStream_t st);
+// RICRC_F_FRAMELEN (icrc_status.hip): eff[i] = the L3 length of packet i
+// from its IP header when its descriptor length is the frame's extent past
+// L3 (frame_l3_len, icrc_math.h); the batch then runs on eff as lengths.
+struct FrameLenArgs {
+  const uint8_t *base;
+  const uint64_t *off;  // may be null (then i * stride)
+  const uint32_t *len;  // may be null (then fixed_len)
+  uint64_t stride, count;
+  uint32_t fixed_len, l3_offset;
+  uint32_t *eff;
+};
+hipError_t launch_framelen(const FrameLenArgs &a, int n_cu, hipStream_t st);
 hipError_t launch_synth_ragged(const SynthArgs &a, hipStream_t st);
 // ricrc_prime's streaming read of `bytes` (a multiple of 16) of scratch.
 hipError_t launch_prime(const void *scratch, uint64_t bytes, uint32_t *sink, int n_cu, hipStream_t st);

@@ -61,6 +61,22 @@ RICRC_HD constexpr uint32_t mask_byte(uint32_t fam, uint32_t i) {
   return i < kMaskSpan ? (mask_word(fam, i >> 2) >> (8 * (i & 3))) & 0xFFu : 0u;
 }
 
+// RICRC_F_FRAMELEN (include/roce_icrc.h): the L3 length of a packet whose
+// frame extends n bytes past its L3 start (an Ethernet NIC ring's frame may
+// carry minimum-frame padding and the FCS after the datagram).  b0 = L3 byte
+// 0, h2 / h4 = the big-endian 16-bit fields at L3 bytes 2 and 4 (read only
+// when kMinLen <= n <= kMaxLen; a longer or shorter descriptor is a bad
+// length whatever the header says): IPv4 total_len (header.p4:45), IPv6
+// payload length + 40.  That length when it lies in [kMinLen, n], else n (a
+// strict classification rejects such a packet).  Same rule:
+// oracle/icrc_oracle.py frame_l3_len.
+RICRC_HD constexpr bool frame_len_applies(uint32_t n) { return n >= kMinLen && n <= kMaxLen; }
+RICRC_HD constexpr uint32_t frame_l3_len(uint32_t n, uint32_t b0, uint32_t h2, uint32_t h4) {
+  const uint32_t v = b0 >> 4;
+  const uint32_t t = v == 4u ? h2 : (v == 6u ? h4 + 40u : 0u);
+  return (frame_len_applies(n) && t >= kMinLen && t <= n) ? t : n;
+}
+
 RICRC_HD constexpr uint32_t gf_mulx(uint32_t a) { return (a >> 1) ^ ((a & 1u) ? kPoly : 0u); }
 
 // a * b mod P, both reflected.

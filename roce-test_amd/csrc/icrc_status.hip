@@ -88,7 +88,49 @@ __global__ __launch_bounds__(kStBlock) void icrc_status_kernel(StatusArgs a) {
   }
 }
 
+// RICRC_F_FRAMELEN: one thread per packet, four packets per thread with the
+// descriptor loads, then the 6 header bytes, issued before any is used.
+__global__ __launch_bounds__(kStBlock) void icrc_framelen_kernel(FrameLenArgs a) {
+  const uint64_t T = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < a.count; i0 += kStUnroll * T) {
+    uint64_t addr[kStUnroll];
+    uint32_t n[kStUnroll], b0[kStUnroll], h2[kStUnroll], h4[kStUnroll];
+#pragma unroll
+    for (int k = 0; k < kStUnroll; ++k) {
+      uint64_t i = i0 + k * T;
+      i = i < a.count ? i : a.count - 1;
+      addr[k] = (uint64_t)(uintptr_t)a.base + (a.off ? a.off[i] : i * a.stride) + a.l3_offset;
+      n[k] = a.len ? a.len[i] : a.fixed_len;
+    }
+#pragma unroll
+    for (int k = 0; k < kStUnroll; ++k) {
+      b0[k] = h2[k] = h4[k] = 0u;
+      if (frame_len_applies(n[k])) {  // the frame holds at least the IPv4 / BTH headers: bytes 0..5 are in it
+        const gbyte l3 = reinterpret_cast<gbyte>((uintptr_t)addr[k]);
+        b0[k] = l3[0];
+        h2[k] = be16(l3 + 2);
+        h4[k] = be16(l3 + 4);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kStUnroll; ++k) {
+      const uint64_t i = i0 + k * T;
+      if (i < a.count) a.eff[i] = frame_l3_len(n[k], b0[k], h2[k], h4[k]);
+    }
+  }
+}
+
 }  // namespace
+
+hipError_t launch_framelen(const FrameLenArgs &a, int n_cu, hipStream_t st) {
+  (void)hipGetLastError();
+  if (a.count == 0) return hipSuccess;
+  const uint64_t want = (a.count + kStBlock * kStUnroll - 1) / (kStBlock * kStUnroll);
+  const uint64_t cap = 8ull * (uint64_t)n_cu;
+  const int grid = (int)(want < cap ? (want ? want : 1) : cap);
+  hipLaunchKernelGGL(icrc_framelen_kernel, dim3(grid), dim3(kStBlock), 0, st, a);
+  return hipGetLastError();
+}
 
 hipError_t launch_status(const StatusArgs &a, int n_cu, hipStream_t st) {
   (void)hipGetLastError();  // a stale error of an earlier, unrelated HIP call must not fail this launch

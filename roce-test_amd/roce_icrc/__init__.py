@@ -49,12 +49,12 @@ EXPORTED = CPU_EXPORTED + (
     "ricrc_batch_device_ex", "ricrc_verify_device_ex", "ricrc_host_alloc", "ricrc_host_free",
     "ricrc_host_register", "ricrc_host_unregister", "ricrc_synth_device", "ricrc_synth_ragged_device",
     "ricrc_prime", "ricrc_stream", "ricrc_comm_init", "ricrc_batch_device_all", "ricrc_allgather", "ricrc_sync",
-    "ricrc_batch_device_st", "ricrc_batch_host_st", "ricrc_classify_device",
+    "ricrc_batch_device_st", "ricrc_batch_host_st", "ricrc_classify_device", "ricrc_kernel_path",
 )
 
 # Per-packet status of the *_st batch calls (include/roce_icrc.h).
 ST_OK, ST_BADLEN, ST_NOTROCE = 0, 1, 2
-F_STRICT, F_VERIFY = 0x100, 0x200
+F_STRICT, F_VERIFY, F_FRAMELEN = 0x100, 0x200, 0x400
 
 _vp = ctypes.c_void_p
 _u32, _u64, _i32 = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
@@ -102,6 +102,7 @@ _SIG = {
     "ricrc_batch_device_st": ([_vp, _i32, _vp, _vp, _vp, _u32, _u64, _u32, _vp, _vp, _vp, _u32], _i32),
     "ricrc_batch_host_st": ([_vp, _vp, _vp, _vp, _u32, _u64, _u32, _vp, _vp, _u32], _i32),
     "ricrc_classify_device": ([_vp, _i32, _vp, _vp, _vp, _u32, _u64, _u32, _vp, _vp], _i32),
+    "ricrc_kernel_path": ([_vp, _vp, _vp, _vp, _u32, _u64, _u32, _u32], ctypes.c_char_p),
 }
 
 
@@ -242,13 +243,16 @@ def repair(pkt, off: int, old_bytes, old_icrc: int, family: str = "v4") -> int:
     return int(out.value)
 
 
-def icrc_checked(pkt, family: str = "v4", strict: bool = False) -> int:
+def icrc_checked(pkt, family: str = "v4", strict: bool = False, framelen: bool = False) -> int:
     """``ricrc_icrc``: like :func:`icrc` but with the length contract
     (MIN_LEN..MAX_LEN, else ValueError) and, with ``strict``, the RoCEv2
-    classifier (not RoCEv2 of that family -> ValueError)."""
+    classifier (not RoCEv2 of that family -> ValueError).  ``framelen``
+    (RICRC_F_FRAMELEN): ``pkt`` runs from the L3 header to the end of its
+    Ethernet frame (padding, FCS) and the packet's length is its IP header's."""
     p, n, _keep = _buf(pkt)
     out = ctypes.c_uint32()
-    rc = cpu.ricrc_icrc(p, n, _fam(family) | (0x100 if strict else 0), ctypes.byref(out))
+    flags = _fam(family) | (F_STRICT if strict else 0) | (F_FRAMELEN if framelen else 0)
+    rc = cpu.ricrc_icrc(p, n, flags, ctypes.byref(out))
     if rc < 0:
         raise ValueError(f"ricrc_icrc: {rc} ({_strerror(rc)})")
     return int(out.value)
@@ -270,7 +274,7 @@ def combine(crc1: int, crc2: int, len2: int) -> int:
 
 
 def icrc_batch_cpu(buf, offsets=None, lengths=None, stride: int = 0, l3_offset: int = 0, count: int | None = None,
-                   family: str = "v4", threads: int = 1) -> np.ndarray:
+                   family: str = "v4", threads: int = 1, framelen: bool = False) -> np.ndarray:
     """``ricrc_batch_cpu``: a batch on the host CPU (slice-by-16, ``threads``
     threads) -- no GPU involved, and never used by the GPU batch calls."""
     buf = np.ascontiguousarray(buf).reshape(-1).view(np.uint8)
@@ -280,7 +284,7 @@ def icrc_batch_cpu(buf, offsets=None, lengths=None, stride: int = 0, l3_offset: 
         count = len(off) if off is not None else (len(ln) if ln is not None else buf.size // stride)
     out = np.empty(count, dtype=np.uint32)
     rc = cpu.ricrc_batch_cpu(buf.ctypes.data, _ptr(off), _ptr(ln), stride, count, l3_offset, out.ctypes.data,
-                             _fam(family), threads)
+                             _fam(family) | (F_FRAMELEN if framelen else 0), threads)
     if rc:
         raise ICRCError(rc, "ricrc_batch_cpu")
     return out
@@ -393,7 +397,7 @@ class Context:
 
     def batch_host_st(self, buf, offsets=None, lengths=None, stride: int = 0, l3_offset: int = 0,
                       count: int | None = None, family: str = "v4", strict: bool = False,
-                      verify: bool = False):
+                      verify: bool = False, framelen: bool = False):
         """``ricrc_batch_host_st``: ``(out, status)`` -- a status per packet
         (:data:`ST_OK`, :data:`ST_BADLEN`, :data:`ST_NOTROCE`) instead of
         failing the call on a bad descriptor length; with ``strict`` only
@@ -406,7 +410,7 @@ class Context:
             count = len(off) if off is not None else (len(ln) if ln is not None else buf.size // stride)
         out = np.empty(count, dtype=np.uint32)
         st = np.empty(count, dtype=np.uint8)
-        flags = _fam(family) | (F_STRICT if strict else 0) | (F_VERIFY if verify else 0)
+        flags = _fam(family) | (F_STRICT if strict else 0) | (F_VERIFY if verify else 0) | (F_FRAMELEN if framelen else 0)
         rc = self._lib.ricrc_batch_host_st(self._h, buf.ctypes.data, _ptr(off), _ptr(ln), stride, count,
                                            l3_offset, out.ctypes.data, st.ctypes.data, flags)
         if rc:
@@ -425,11 +429,12 @@ class Context:
 
     def batch_device_st(self, base, count: int, out, status, stride: int = 0, offsets=None, lengths=None,
                         l3_offset: int = 0, dev: int = 0, stream=None, family: str = "v4",
-                        strict: bool = False, verify: bool = False) -> None:
+                        strict: bool = False, verify: bool = False, framelen: bool = False) -> None:
         """``ricrc_batch_device_st``: as :meth:`batch_device`, plus ``status``
         (``count`` uint8 on the device, :data:`ST_OK` / :data:`ST_BADLEN` /
-        :data:`ST_NOTROCE`)."""
-        flags = _fam(family) | (F_STRICT if strict else 0) | (F_VERIFY if verify else 0)
+        :data:`ST_NOTROCE`).  ``framelen``: RICRC_F_FRAMELEN (descriptor
+        lengths are frame extents past L3; packet lengths from the IP headers)."""
+        flags = _fam(family) | (F_STRICT if strict else 0) | (F_VERIFY if verify else 0) | (F_FRAMELEN if framelen else 0)
         rc = self._lib.ricrc_batch_device_st(self._h, dev, _ptr(base), _ptr(offsets), _ptr(lengths), stride, count,
                                              l3_offset, _ptr(out), _ptr(status), _stream_ptr(stream), flags)
         if rc:
@@ -536,6 +541,19 @@ class Context:
         rc = self._lib.ricrc_host_unregister(self._h, arr.ctypes.data)
         if rc:
             raise ICRCError(rc, "ricrc_host_unregister")
+
+
+def kernel_path(base, count: int, stride: int = 0, offsets=None, lengths=None, l3_offset: int = 0,
+                family: str = "v4", ctx: Context | None = None) -> str:
+    """``ricrc_kernel_path``: the '+'-joined gfx950 kernel names the batch
+    dispatch launches for a batch of this shape (``base`` only for its
+    alignment: a tensor, array or integer address).  No GPU needed."""
+    addr = _ptr(base)
+    r = hip_lib().ricrc_kernel_path(ctx.handle if ctx else None, addr, _ptr(offsets), _ptr(lengths), stride, count,
+                                    l3_offset, _fam(family))
+    if r is None:
+        raise ValueError("ricrc_kernel_path: not a valid batch")
+    return r.decode()
 
 
 def icrc_batch(buf, offsets=None, lengths=None, stride: int = 0, l3_offset: int = 0,

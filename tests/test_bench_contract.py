@@ -12,6 +12,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
+import pytest
+
 import bench  # noqa: E402
 
 
@@ -127,10 +129,36 @@ def test_metric_names_the_workload_run():
 
 
 def test_kernel_labels_follow_the_dispatch():
-    assert "icrc_sck_kernel" in bench.kernel_label(4096)
-    assert "icrc_sck_kernel" in bench.kernel_label(1024)
-    assert "icrc_tsk_kernel" in bench.kernel_label(256)
-    assert "icrc_tsk_kernel" not in bench.kernel_label(64)
+    """Labels come from the library's own dispatch (ricrc_kernel_path, no GPU
+    needed): the kernels rocprofv3 shows for each BASELINE config."""
+    lab = lambda *a: bench.kernel_label(bench.parse(list(a)))  # noqa: E731
+    assert "(icrc_sck_kernel)" in lab() and "(icrc_sck_kernel)" in lab("--size", "1024")
+    assert lab("--size", "64") == "quad ICRC kernel (64-byte packets, lane-quad transposes) (icrc_quad_kernel)"
+    assert "(icrc_tsk_kernel)" in lab("--size", "256")
+    mix = lab("--mix")  # the ragged pipeline's passes, in launch order
+    assert mix.split(" -> ") == ["bucket pass (rsck_bucket)",
+                                 "strided-chain fold of packets of >= 2 lines (icrc_rsck_kernel)",
+                                 "one-line packets (icrc_rsmall_kernel)", "gather (rsck_gather)"]
+    assert "family_fix_kernel" in lab("--size", "64", "--family", "v6")
+    assert "family_fix_kernel" not in lab("--family", "v6")  # the SCK applies IPv6 masks natively
+    assert "count/plan" not in mix and "scatter" not in mix
+
+
+def test_cpu_baseline_value_is_the_product_cpu_path():
+    """cpu_baseline.value is the build's own slice-by-16 CPU batch path
+    (SURVEY.md 8(d)(3)); the oracle port's figure is a side key."""
+    import oracle_c
+
+    host = oracle_c.synth_batch(bench.SEED, 0, 64, 1024)
+    want = oracle_c.icrc_batch(host, stride=1024)
+    cb = bench.cpu_baseline(host, want, 1024, 0.05)
+    assert cb["kind"] == "port" and cb["unit"] == "GiB/s" and cb["cores"] >= 1
+    assert "ricrc_batch_cpu" in cb["sample"] and cb["value"] > 0
+    assert cb["oracle_port_GiBs"] > 0 and "icrc_oracle.c" in cb["oracle_port"]
+    with pytest.raises(SystemExit):  # a GPU result the CPU paths disagree with
+        bad = want.copy()
+        bad[3] ^= 1
+        bench.cpu_baseline(host, bad, 1024, 0.05)
 
 
 def test_traffic_is_tied_to_the_kernel_source(tmp_path):

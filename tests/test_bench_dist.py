@@ -158,6 +158,10 @@ def test_bench_run_world2_gloo(argv, scaling, total):
     assert res["config"]["packets_total"] == total and res["config"]["parallelism"] == "dp2 (all-gather u32 results)"
     assert res["value"] > 0 and res["ms_per_step"] > 0 and res["oracle_sampled_all_ranks"]
     assert "cpu_baseline" not in res
+    # the step's parts timed apart (compute-only, the collective alone), the
+    # group's own world size, the collective library's version (None on gloo)
+    assert res["world_size"] == 2 and res["collective_backend"] == "gloo" and "rccl_version" in res
+    assert res["compute_only_ms_per_step"] > 0 and res["gather_ms"] > 0
     sizes = got[0][2]
     assert sum(sizes) == total
     if "--mix" in argv:
@@ -174,5 +178,6 @@ def test_bench_run_world2_no_gather():
     got = run2(BASE + argv)
     want = _want(argv)
     assert got[0][0]["config"]["parallelism"] == "dp2"
+    assert got[0][0]["compute_only_ms_per_step"] > 0 and "gather_ms" not in got[0][0]
     np.testing.assert_array_equal(got[0][1], want[:1500])
     np.testing.assert_array_equal(got[1][1], want[1500:])

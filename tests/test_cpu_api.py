@@ -223,3 +223,48 @@ def test_icrc_checked_length_and_classifier_contract():
     assert roce_icrc.cpu.ricrc_icrc(None, 100, 0, ctypes.byref(out)) == -errno.EINVAL
     assert roce_icrc.cpu.ricrc_icrc(pkt, len(pkt), 9, ctypes.byref(out)) == -errno.EINVAL
     assert out.value == 7
+
+
+def test_framelen_padded_and_fcs_frames_cpu():
+    """RICRC_F_FRAMELEN on the CPU entry points (ricrc_icrc, ricrc_batch_cpu)
+    against the oracle's frame_l3_len restatement: the ACK known answer
+    padded, with an FCS, both; RoCEv2/IPv6 with an FCS; frames whose IP
+    header gives no usable length keep the descriptor's (ARP, total_len past
+    the frame, total_len < 44), and a strict call still rejects those."""
+    ack = bytes.fromhex("450200301234400040110000c0a80164c0a80101457b12b7001c00001140ffff"
+                        "0000001100000005000000016c1f7922")
+    fcs = bytes.fromhex("deadbeef")
+    for tail in (bytes(2), fcs, bytes(2) + fcs, bytes(12)):
+        frame = ack + tail
+        assert O.frame_l3_len(frame) == len(ack)
+        assert roce_icrc.icrc_checked(frame, strict=True, framelen=True) == 0x22791F6C
+        with pytest.raises(ValueError, match="-71"):  # without the flag: total_len != descriptor length
+            roce_icrc.icrc_checked(frame, strict=True)
+    rng = np.random.default_rng(11)
+    v6 = bytearray(rng.integers(0, 256, 100, dtype=np.uint8).tobytes())
+    v6[0] = 0x60
+    v6[4:6] = (60).to_bytes(2, "big")
+    v6[6] = 17
+    v6[42:44] = (4791).to_bytes(2, "big")
+    assert O.frame_l3_len(bytes(v6) + fcs) == 100
+    assert roce_icrc.icrc_checked(bytes(v6) + fcs, family="v6", strict=True, framelen=True) == O.icrc(bytes(v6), "v6")
+    arp = bytes.fromhex("0001080006040001") + bytes(52)
+    assert O.frame_l3_len(arp) == 60 and roce_icrc.icrc_checked(arp, framelen=True) == O.icrc(arp)
+    long_t = bytearray(ack + fcs)
+    long_t[2:4] = (200).to_bytes(2, "big")  # total_len past the frame
+    short_t = bytearray(ack + fcs)
+    short_t[2:4] = (40).to_bytes(2, "big")  # shorter than a RoCEv2 header
+    for f in (bytes(long_t), bytes(short_t)):
+        assert O.frame_l3_len(f) == len(f) and roce_icrc.icrc_checked(f, framelen=True) == O.icrc(f)
+        with pytest.raises(ValueError, match="-71"):
+            roce_icrc.icrc_checked(f, strict=True, framelen=True)
+    # a batch of frames: lengths from the IP headers, slots of 128 bytes
+    frames = [ack + bytes(2), ack + fcs, bytes(v6) + fcs, arp, bytes(long_t)]
+    buf = np.zeros(128 * len(frames), np.uint8)
+    for i, f in enumerate(frames):
+        buf[128 * i:128 * i + len(f)] = np.frombuffer(f, np.uint8)
+    lens = np.array([len(f) for f in frames], np.uint32)
+    offs = np.arange(len(frames), dtype=np.uint64) * 128
+    got = roce_icrc.icrc_batch_cpu(buf, offs, lens, framelen=True, family="auto")
+    want = [O.icrc(f[:O.frame_l3_len(f)], "auto") for f in frames]
+    np.testing.assert_array_equal(got, np.array(want, np.uint32))

@@ -50,22 +50,41 @@ def _l3(kind, n, rng, i):
     raise ValueError(kind)
 
 
-def mixed_ring(count, seed, framed=True):
+# RICRC_F_FRAMELEN rings: Ethernet frames whose descriptor length is the
+# frame's extent past L3 -- a 44-byte SEND_ONLY (no payload) padded to the
+# 60-byte minimum frame (2 bytes of padding), frames that keep their 4-byte
+# FCS, both at once, and RoCEv2/IPv6 with an FCS.
+FRAME_KINDS = ("pad44", "fcs", "pad44_fcs", "roce6_fcs")
+
+
+def mixed_ring(count, seed, framed=True, frame_kinds=False):
     """Frames back to back with small gaps: (buf, offsets, lengths, kinds,
     EtherTypes).  Offsets point at the frame; L3 starts 14 bytes later when
-    framed (else at the offset, no Ethernet header)."""
+    framed (else at the offset, no Ethernet header).  frame_kinds: a quarter
+    of the frames carry Ethernet padding and / or an FCS after the datagram
+    (FRAME_KINDS), their descriptor length covering it."""
     rng = np.random.default_rng(seed)
     sizes = np.array([64, 100, 256, 1024, 1500, 4096], np.uint32)
-    kinds = rng.choice(len(KINDS), size=count, p=[.35, .15, .05, .08, .07, .05, .05, .05, .05, .10])
+    kinds = [KINDS[k] for k in rng.choice(len(KINDS), size=count, p=[.35, .15, .05, .08, .07, .05, .05, .05, .05, .10])]
+    if frame_kinds:
+        fk = rng.choice(len(FRAME_KINDS), size=count)
+        kinds = [FRAME_KINDS[f] if rng.random() < 0.25 else k for k, f in zip(kinds, fk)]
     parts, offs, lens, ets, pos = [], [], [], [], 0
-    for i, k in enumerate(kinds):
-        kind = KINDS[k]
+    for i, kind in enumerate(kinds):
         gap = int(rng.integers(0, 12))
         parts.append(np.zeros(gap, np.uint8))
         pos += gap
         if kind == "badlen":
             n_desc = int(rng.choice([0, 3, 20, 43, 70000, 0xFFFFFFFF]))
             body, et = _l3("roce4", 64, rng, i)
+        elif kind in FRAME_KINDS:
+            n = 44 if kind.startswith("pad44") else int(rng.choice(sizes))
+            body, et = _l3("roce6" if kind == "roce6_fcs" else "roce4", max(n, 64) if kind == "roce6_fcs" else n,
+                           rng, i)
+            tail = (bytes(2) if kind.startswith("pad44") else b"") + \
+                (rng.integers(0, 256, 4, dtype=np.uint8).tobytes() if kind.endswith("fcs") else b"")
+            body += tail
+            n_desc = len(body)
         else:
             n = int(rng.choice(sizes[sizes >= (64 if "roce6" in kind else 46)]))
             body, et = _l3(kind, n, rng, i)
@@ -78,8 +97,7 @@ def mixed_ring(count, seed, framed=True):
         ets.append(et)
         pos += frame.size
     parts.append(np.zeros(128, np.uint8))
-    return (np.concatenate(parts), np.array(offs, np.uint64), np.array(lens, np.uint32),
-            [KINDS[k] for k in kinds], ets)
+    return (np.concatenate(parts), np.array(offs, np.uint64), np.array(lens, np.uint32), kinds, ets)
 
 
 def _dev(a):
@@ -207,5 +225,85 @@ def test_status_call_errors(ctx):
     with pytest.raises(roce_icrc.ICRCError):  # no status array
         ctx.batch_device_st(d, 1, out, None, stride=64)
     rc = ctx._lib.ricrc_batch_device_st(ctx.handle, 0, d.data_ptr(), None, None, 64, 1, 0, out.data_ptr(),
-                                        st.data_ptr(), None, 0x400)
+                                        st.data_ptr(), None, 0x800)
     assert rc == -errno.EINVAL  # unknown flag bit
+
+
+@pytest.mark.parametrize("family,strict,verify", [("v4", True, False), ("auto", True, False), ("auto", False, False),
+                                                  ("auto", True, True)])
+def test_framelen_padded_and_fcs_frames(ctx, family, strict, verify):
+    """RICRC_F_FRAMELEN on an Ethernet NIC ring whose descriptor lengths are
+    frame extents: 44-byte SEND_ONLY packets padded to the 60-byte minimum
+    frame, frames that keep their FCS, both, RoCEv2/IPv6 with an FCS, next to
+    every reject case of the mixed ring.  The packet's length comes from its IP
+    header (the reference's parser never uses a descriptor length,
+    shuffle_ingress_parser.p4:12-36; total_len at header.p4:45); status and out
+    equal the oracle's status_batch(framelen=True) on the device and on both
+    host routes (span, gather)."""
+    buf, offs, lens, kinds, ets = mixed_ring(3000, 41, True, frame_kinds=True)
+    l3 = 14
+    k = np.array(kinds)
+    for kind in FRAME_KINDS:
+        assert (k == kind).sum() > 50, kind
+    if verify:  # corrupt one covered byte of every 9th packet: the IP length decides where the trailer is
+        for i in range(0, len(lens), 9):
+            if roce_icrc.MIN_LEN <= lens[i] <= roce_icrc.MAX_LEN:
+                buf[int(offs[i]) + l3 + 40] ^= 0x08
+    w_out, w_st = O.status_batch(buf, offsets=offs, lengths=lens, l3_offset=l3, family=family, strict=strict,
+                                 verify=verify, framelen=True)
+    fr = np.isin(k, FRAME_KINDS) & ~((k == "roce6_fcs") & strict & (family == "v4"))
+    assert (w_st[fr] == O.ST_OK).all()  # every padded / FCS frame (of an accepted family) is accepted and computed
+    if not verify:
+        for i in np.flatnonzero(fr)[:200]:  # over the datagram only: the IP length, not the descriptor's
+            o, n = int(offs[i]) + l3, int(lens[i])
+            pkt = buf[o:o + n].tobytes()
+            m = O.frame_l3_len(pkt)
+            assert m < n and w_out[i] == O.icrc(pkt[:m], family)
+    if strict:  # without the flag the same frames are rejected (total_len != descriptor length)
+        _, st0 = O.status_batch(buf, offsets=offs, lengths=lens, l3_offset=l3, family=family, strict=True)
+        assert (st0[fr] == O.ST_NOTROCE).all()
+        assert (w_st == O.ST_NOTROCE).sum() > 300
+    count = len(lens)
+    out = torch.full((count,), -1, dtype=torch.int32, device="cuda")
+    st = torch.full((count,), 0xEE, dtype=torch.uint8, device="cuda")
+    ctx.batch_device_st(_dev(buf), count, out, st, offsets=_dev(offs), lengths=_dev(lens), l3_offset=l3,
+                        family=family, strict=strict, verify=verify, framelen=True, stream=torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(st.cpu().numpy(), w_st)
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), w_out)
+    h_out, h_st = ctx.batch_host_st(buf, offs, lens, l3_offset=l3, family=family, strict=strict, verify=verify,
+                                    framelen=True)
+    np.testing.assert_array_equal(h_st, w_st)
+    np.testing.assert_array_equal(h_out, w_out)
+    perm = np.random.default_rng(3).permutation(count)  # the gather route
+    h_out, h_st = ctx.batch_host_st(buf, offs[perm], lens[perm], l3_offset=l3, family=family, strict=strict,
+                                    verify=verify, framelen=True)
+    np.testing.assert_array_equal(h_st, w_st[perm])
+    np.testing.assert_array_equal(h_out, w_out[perm])
+
+
+def test_framelen_fixed_stride_ring(ctx):
+    """A fixed-slot ring (no per-packet lengths: every descriptor is the slot)
+    of 44..1500-byte packets under RICRC_F_FRAMELEN: the device pre-pass gives
+    each packet its IP length, so the batch runs as a ragged one."""
+    rng = np.random.default_rng(5)
+    count, slot, l3 = 2048, 1536, 14
+    buf = rng.integers(0, 256, count * slot + 64, dtype=np.uint8)
+    for i in range(count):
+        n = int(rng.choice([44, 60, 256, 1000, 1500 - l3]))
+        body, et = _l3("roce4", n, rng, i)
+        o = i * slot
+        buf[o + 12:o + 14] = np.frombuffer(et.to_bytes(2, "big"), np.uint8)
+        buf[o + l3:o + l3 + n] = np.frombuffer(body, np.uint8)
+    w_out, w_st = O.status_batch(buf, stride=slot, count=count, l3_offset=l3, strict=True, framelen=True)
+    assert (w_st == O.ST_OK).all()
+    out = torch.empty(count, dtype=torch.int32, device="cuda")
+    st = torch.empty(count, dtype=torch.uint8, device="cuda")
+    ctx.batch_device_st(_dev(buf), count, out, st, stride=slot, l3_offset=l3, strict=True, framelen=True,
+                        stream=torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(st.cpu().numpy(), w_st)
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), w_out)
+    h_out, h_st = ctx.batch_host_st(buf, stride=slot, count=count, l3_offset=l3, strict=True, framelen=True)
+    np.testing.assert_array_equal(h_st, w_st)
+    np.testing.assert_array_equal(h_out, w_out)

@@ -17,6 +17,10 @@ WRITE_SIZE is taken as reported.  Both are in KiB.
              doubled FETCH_SIZE against that byte count is reported as a check
              of the x2 correction on scattered traffic
              ("bucket_pass_fetch_over_descriptors").
+  --count N  packets on the (one) GPU instead of the BASELINE count (1 M, or
+             4 M with --mix): C3's 16 GiB batch (--count 4194304) and the
+             8-GPU shard stand-ins; the record's name carries N
+             (bench.traffic_record).
 
 Copied into profiles/, the file is what bench.py reports as roofline.traffic
 when the workload and the kernel sources match (bench.kernel_source_hash).
@@ -55,30 +59,32 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mix", action="store_true")
     ap.add_argument("--size", type=int, default=4096)
+    ap.add_argument("--count", type=int, default=None)
     ap.add_argument("--out", default=None)
     ap.add_argument("--scratch", default=os.path.join(ROOT, "gpurun_out", "pmc_traffic"))
     a = ap.parse_args()
     sys.path.insert(0, ROOT)
     import bench
 
-    rec = bench.traffic_record(a.mix, a.size)
+    std = (4 << 20) if a.mix else (1 << 20)
+    count = a.count or std
+    rec = bench.traffic_record(a.mix, a.size, count)
     if rec is None:
         raise SystemExit(f"no traffic record is kept for --size {a.size}")
     name, srcs, match = rec
     a.out = os.path.abspath(a.out or os.path.join(ROOT, "gpurun_out", name))
-    a.scratch = os.path.abspath(a.scratch + ("_mix" if a.mix else f"_{a.size}"))
-    bench_args = ["--mix"] if a.mix else ["--size", str(a.size)]
+    a.scratch = os.path.abspath(a.scratch + ("_mix" if a.mix else f"_{a.size}") + f"_{count}")
+    bench_args = (["--mix"] if a.mix else ["--size", str(a.size)]) + ["--count", str(count)]
     fetch = run_pass("FETCH_SIZE", os.path.join(a.scratch, "fetch"), bench_args, match)
     write = run_pass("WRITE_SIZE", os.path.join(a.scratch, "write"), bench_args, match)
     if a.mix:
         import numpy as np
 
-        count = 4 << 20
         lens = np.random.default_rng(bench.SEED).choice(np.array(bench.MIX_SIZES, np.uint32), size=count)
         alg = int(lens.sum(dtype=np.uint64)) + 16 * count
         src, size = bench.kernel_source_hash(srcs), "mix"
     else:
-        count, size = 1 << 20, a.size
+        size = a.size
         alg = count * size + 4 * count
         src = bench.kernel_source_hash(srcs)
     kernels = {k: {"FETCH_SIZE_KiB": fetch.get(k, (0.0, 0))[0], "WRITE_SIZE_KiB": write.get(k, (0.0, 0))[0],
