@@ -41,6 +41,7 @@
 #include <stdint.h>
 
 #include <type_traits>
+#include <utility>
 
 #include "icrc_device.h"
 #include "icrc_kernels.h"
@@ -359,7 +360,7 @@ __global__ __launch_bounds__(kPassBlock) void rsck_gather(RsckArgs a) {
   __shared__ uint32_t lres[kStage];
   // The counters are dead now (the bucket pass and both folds have read
   // them): zero them for the next call on this workspace.
-  if (blockIdx.x == 0 && threadIdx.x == 0) *a.ctr = RsCounters{0u, 0u, 0ull};
+  if (blockIdx.x == 0 && threadIdx.x == 0) *a.ctr = RsCounters{0u, 0u, 0ull, 0u, 0u};
   uint32_t lo, hi;
   {
     uint64_t l, h_;
@@ -431,6 +432,17 @@ __device__ __forceinline__ uint32_t edge_word(uint32_t w, int rel, int M) {
 
 
 }  // namespace
+
+constexpr uint32_t cgcd(uint32_t a, uint32_t b) { return b == 0u ? a : cgcd(b, a % b); }
+// f(integral_constant<0>), ..., f(integral_constant<N - 1>), unrolled.
+template <class F, uint32_t... I>
+__device__ __forceinline__ void static_for_impl(F &&f, std::integer_sequence<uint32_t, I...>) {
+  (f(std::integral_constant<uint32_t, I>{}), ...);
+}
+template <uint32_t N, class F>
+__device__ __forceinline__ void static_for(F &&f) {
+  static_for_impl(f, std::make_integer_sequence<uint32_t, N>{});
+}
 
 // ABL (timing-only ablations, tools/microbench/rsck_abl.hip): 1 no table
 // fold, 2 no finish, 4 descriptors by arithmetic (uniform batch in natural
@@ -609,93 +621,14 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   auto put_block = [&](uint32_t b, const u32x2 &v) {
     *reinterpret_cast<u32x2 *>(dring + (b & 1u) * kBlk + 2u * lane) = v;
   };
-  u32x2 NB = {0u, 0u};
-  if (!(ABL & 4)) {
-    const uint32_t b = q_begin >> 3;
-    put_block(b, load_block(b));
-    put_block(b + 1, load_block(b + 1));
-    NB = load_block(b + 2);
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-  }
-
-  struct LInfo {
-    uint64_t line0;  // lane's slot in the packet's first line
-  };
-  // Load cursor enters group q: line base, L, and (a, M) into the FIFO.
-  auto ld_enter = [&](uint32_t q, LInfo &li) -> uint32_t {
-    uint64_t addr;
-    uint32_t gM;
-    if (ABL & 4) {
-      addr = (uint64_t)(uintptr_t)a.base + (8ull * q + g) * a.stride;
-      gM = a.fixed_len - 4u;
-    } else {
-      const u32x2 d = *reinterpret_cast<const u32x2 *>(dring + ((q >> 3) & 1u) * kBlk + 2u * (8u * (q & 7u) + g));
-      addr = ((uint64_t)(d[1] & 0xFFFFu) << 32) | d[0];
-      gM = (d[1] >> 16) - 4u;
-    }
-    const uint32_t ga = (uint32_t)addr & 127u;
-    li.line0 = (addr & ~127ull) + 16u * s;
-    fifo[((q & 7u) << 3) | g] = (gM << 7) | ga;
-    return __builtin_amdgcn_readfirstlane((ga + gM + 127u) >> 7);  // equal within a group
-  };
-
-  LInfo ld;
-  uint32_t ld_q = q_begin, ld_k = 0, ld_L = ld_enter(ld_q, ld);
-  uint32_t fd_q = q_begin, fd_k = 0, fd_L = ld_L, fd_a, fd_M;
-  auto fd_enter = [&](uint32_t q) {
-    const uint32_t v = fifo[((q & 7u) << 3) | g];
-    fd_a = v & 127u;
-    fd_M = v >> 7;
-    fd_L = __builtin_amdgcn_readfirstlane((fd_a + fd_M + 127u) >> 7);
-  };
-  fd_enter(fd_q);
-  // head lines of the group: 2 when some packet's header runs into line 1 (a
-  // plain uint32 so the edge test below is SALU arithmetic and one branch:
-  // short-circuit || on a ballot-derived bool compiled to five branches per
-  // step, and C4's fold ran 1.5 % slower)
-  uint32_t fd_hl = __ballot(fd_a > 88u) != 0 ? 2u : 1u;
-  // edge line <=> fd_k < fd_hl or fd_k == fd_L - 1 <=> (fd_k - fd_hl) >= fd_span, unsigned
-  uint32_t fd_span = fd_L - 1u > fd_hl ? fd_L - 1u - fd_hl : 0u;  // 0: every line is an edge line
-
-  auto ld_advance = [&]() {
-    if (++ld_k == ld_L) {  // wave-uniform
-      ld_k = 0;
-      if (ld_q + 1 < q_end) {
-        ++ld_q;
-        if (!(ABL & 4) && (ld_q & 7u) == 0) {
-          put_block((ld_q >> 3) + 1, NB);
-          NB = load_block((ld_q >> 3) + 2);
-        }
-        ld_L = ld_enter(ld_q, ld);
-      } else {
-        ld_L = 1;  // done: re-read line 0 of the last group (ld_k wraps to 0 every step)
-      }
-    }
-  };
-  // (ABL 16384, timing only: no line loads, a value derived from the address)
-  auto line_load = [&](uint64_t addr) -> u32x4 {
-    if (ABL & 16384) return u32x4{(uint32_t)addr, (uint32_t)(addr >> 7), lane, (uint32_t)addr * 3u};
-    return gload16_nt(addr);
-  };
-  auto ld_issue = [&]() -> u32x4 { return line_load(ld.line0 + 128ull * ld_k); };
-
-  u32x4 ring[D];
-#pragma unroll
-  for (int u = 0; u < D; ++u) {
-    __builtin_amdgcn_sched_barrier(0);
-    ring[u] = ld_issue();
-    ld_advance();
-  }
-  __builtin_amdgcn_sched_barrier(0);
-
-  uint32_t r[4] = {0u, 0u, 0u, 0u};
   uint32_t round_q0 = q_begin;  // first group of the current round of result slots
+  uint32_t sink = 0;             // timing ablations: values kept live
   auto flush = [&](uint32_t q_stop) {  // groups [round_q0, q_stop) of the round
     const uint32_t valid = 8u * (q_stop - round_q0);
     const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.bres + 8ull * round_q0, 4u * valid);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the slot writes have landed
     if (ABL & 32) {
-      r[1] ^= slots[lane] ^ slots[kSlots - 64 + lane];  // keep the slot reads
+      sink ^= slots[lane] ^ slots[kSlots - 64 + lane];  // keep the slot reads
       return;
     }
 #pragma unroll
@@ -703,10 +636,13 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
       __builtin_amdgcn_raw_buffer_store_b32(slots[64 * h + lane], ro, 4u * (64 * h + lane), 0,
                                             (ABL & 1024) ? 2 : (ABL & 2048) ? 0 : (ABL & 4096) ? 17 : 16);
   };
-  auto finish = [&]() {
+  // A group's finish: its chain registers rr (after its last line), L lines,
+  // first-byte offsets ga and covered lengths gM of its 8 packets (per lane
+  // group), its position q in the big pool -> the ICRC into the wave's slot.
+  auto finish_group = [&](uint32_t (&rr)[4], uint32_t Lg, uint32_t ga, uint32_t gM, uint32_t q) {
     uint32_t R;
     if (ABL & 2) {
-      R = group_xor(r[0] ^ r[1] ^ r[2] ^ r[3], 3);
+      R = group_xor(rr[0] ^ rr[1] ^ rr[2] ^ rr[3], 3);
     } else {
       // Horner by x^-32 through the nibble table: 8 lookups per multiply
       // (one copy: the 16 entries of a nibble position sit in 16 banks, so
@@ -721,11 +657,11 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
       // r3 x^-96 + r2 x^-64 + r1 x^-32 + r0: three independent multiplies
       // (Horner chained them: four dependent LDS round trips per finish,
       // which the 2-3-line groups of 256-byte packets could not hide)
-      const uint32_t u = nib_mul(x3tl, r[3], nib_mul(x2tl, r[2], nib_mul(xtl, r[1], r[0])));
+      const uint32_t u = nib_mul(x3tl, rr[3], nib_mul(x2tl, rr[2], nib_mul(xtl, rr[1], rr[0])));
       R = group_xor(nib_mul(qrow, u, 0u), 3);  // u * x^(-128 s): lane slot s's nibble table
       // x^(-8 tz), distributed: lane s takes bits 4s..4s+3 of R; basis word
       // 4s from LDS, 4s+1..4s+3 by successive x^-1.
-      const uint32_t tz = 128u * fd_L - fd_a - fd_M;
+      const uint32_t tz = 128u * Lg - ga - gM;
       uint32_t bw = tzl[2u * tz + s], p = 0;
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -736,155 +672,421 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
       R = group_xor(p, 3);
     }
     if (ABL & 16) {
-      r[0] ^= R;  // keep the value live
+      sink ^= R;  // keep the value live
       return;
     }
-    slots[((fd_q - round_q0) << 3) | g] = ~R;
-    if (fd_q + 1 - round_q0 == kRound) {  // wave-uniform
-      flush(fd_q + 1);
-      round_q0 = fd_q + 1;
+    slots[((q - round_q0) << 3) | g] = ~R;
+    if (q + 1 - round_q0 == kRound) {  // wave-uniform
+      flush(q + 1);
+      round_q0 = q + 1;
     }
   };
 
-  // Two copies of the fold loop: one with whole-word edges when the bucket
-  // pass found every strided-chain packet word-aligned in start and length
-  // (a per-group choice inside the loop made the compiler rotate the load
-  // ring through copies and drain vmcnt(0) at the loop head).
-  // The fold keeps xr = r ^ (the current line's word), the lookup input: the
-  // XOR with the next line's word rides in the step's last 3-input XOR (as in
-  // the SCK), 4 VALU per line fewer.  An edge line corrects xr by
-  // w ^ masked(w) on its own step; a group's last line leaves the next
-  // group's first word alone in xr (its chains start from zero).
-  uint32_t xr[4] = {ring[0][0], ring[0][1], ring[0][2], ring[0][3]};
-  // Quiet steps.  Per-step cursor control cost the fold 16 SALU and 4.5
-  // branches per wave step against 1.7 and 0.1 in the SCK (rocprofv3 --pmc,
-  // profiles/r03/pmc_insts.txt).  A run of steps in which neither cursor
-  // changes group and the fold cursor's line is no edge line (not a head
-  // line, not the group's last) needs none of it: a step is then the 16
-  // lookups, the XORs and a load.  Every full step computes the length of
-  // the run that follows it (quiet); a block of D steps that starts with a
-  // run of >= D ahead is D quiet steps with no per-step test at all, and
-  // shorter runs go through full steps (a per-step quiet / full branch
-  // measured 17 % slower: 1115 against 953 us, tools/microbench/fold_var.hip).
-  uint32_t quiet = 0;
-  auto quiet_step = [&](int u, uint32_t ahead) {  // ahead: lines the load cursor is past ld_k within the block
-    const u32x4 wn = ring[(u + 1) % D];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t t0 = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0400u));
-      const uint32_t t1 = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0500u) + 128);
-      const uint32_t t2 = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo1, 0x0C020600u));
-      const uint32_t t3 = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo1, 0x0C020700u) + 128);
-      xr[i] = xor3(t0, t1, xor3(t2, t3, wn[i]));
+
+  // The generic fold over groups [qb, qe): any mix of line counts, byte- or
+  // word-granular edges (round 3's fold: two cursors, quiet blocks).
+  auto generic = [&](uint32_t qb, uint32_t qe) {
+    u32x2 NB = {0u, 0u};
+    if (!(ABL & 4)) {
+      const uint32_t b = qb >> 3;
+      put_block(b, load_block(b));
+      put_block(b + 1, load_block(b + 1));
+      NB = load_block(b + 2);
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
     }
-    ring[u] = line_load(ld.line0 + 128ull * (ld_k + ahead));
-  };
-  auto fold_loop = [&](auto words) {
-  // One full step: edge masks, group finish and both cursors' group changes.
-  auto full_step = [&](int u, bool &done) {
-      const u32x4 wn = ring[(u + 1) % D];  // the next line, raw
-      if (!(ABL & 8) && fd_k - fd_hl >= fd_span) {  // wave-uniform: an edge line
-        const u32x4 wc = ring[u];
-        const int rel0 = (int)(128u * fd_k + 16u * s) - (int)fd_a;
-        if constexpr (decltype(words)::value) {
-          if ((ABL & 32768) || fd_k < fd_hl) {  // wave-uniform: a head line
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              // whole words: keep 0 <= rel < M by sign arithmetic (compare +
-              // select pairs needed hazard NOPs), head masks from a 16-entry
-              // table (rel >= 40 and rel < 0 index the zero entry 15)
-              const int rel = rel0 + 4 * i;
-              const uint32_t keep = (uint32_t)(((rel - (int)fd_M) & ~rel) >> 31);
-              const uint32_t k = __builtin_elementwise_min((uint32_t)rel >> 2, 15u);
-              typedef uint32_t u32x2e __attribute__((ext_vector_type(2)));
-              const u32x2e e = *reinterpret_cast<const u32x2e *>(etl + 2 * k);
-              xr[i] = xor3(xr[i], wc[i], ((wc[i] & keep) | e[0]) ^ e[1]);
-            }
-          } else {
-            // the group's last line past its head lines: rel >= 40 (no head
-            // masks), only the bytes at rel >= M dropped -- 3 VALU a word
-            // instead of 10 and a table read
-            const int lim = (int)fd_M - 1 - rel0;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) xr[i] ^= wc[i] & (uint32_t)((lim - 4 * i) >> 31);
+
+    struct LInfo {
+      uint64_t line0;  // lane's slot in the packet's first line
+    };
+    // Load cursor enters group q: line base, L, and (a, M) into the FIFO.
+    auto ld_enter = [&](uint32_t q, LInfo &li) -> uint32_t {
+      uint64_t addr;
+      uint32_t gM;
+      if (ABL & 4) {
+        addr = (uint64_t)(uintptr_t)a.base + (8ull * q + g) * a.stride;
+        gM = a.fixed_len - 4u;
+      } else {
+        const u32x2 d = *reinterpret_cast<const u32x2 *>(dring + ((q >> 3) & 1u) * kBlk + 2u * (8u * (q & 7u) + g));
+        addr = ((uint64_t)(d[1] & 0xFFFFu) << 32) | d[0];
+        gM = (d[1] >> 16) - 4u;
+      }
+      const uint32_t ga = (uint32_t)addr & 127u;
+      li.line0 = (addr & ~127ull) + 16u * s;
+      fifo[((q & 7u) << 3) | g] = (gM << 7) | ga;
+      return __builtin_amdgcn_readfirstlane((ga + gM + 127u) >> 7);  // equal within a group
+    };
+
+    LInfo ld;
+    uint32_t ld_q = qb, ld_k = 0, ld_L = ld_enter(ld_q, ld);
+    uint32_t fd_q = qb, fd_k = 0, fd_L = ld_L, fd_a, fd_M;
+    auto fd_enter = [&](uint32_t q) {
+      const uint32_t v = fifo[((q & 7u) << 3) | g];
+      fd_a = v & 127u;
+      fd_M = v >> 7;
+      fd_L = __builtin_amdgcn_readfirstlane((fd_a + fd_M + 127u) >> 7);
+    };
+    fd_enter(fd_q);
+    // head lines of the group: 2 when some packet's header runs into line 1 (a
+    // plain uint32 so the edge test below is SALU arithmetic and one branch:
+    // short-circuit || on a ballot-derived bool compiled to five branches per
+    // step, and C4's fold ran 1.5 % slower)
+    uint32_t fd_hl = __ballot(fd_a > 88u) != 0 ? 2u : 1u;
+    // edge line <=> fd_k < fd_hl or fd_k == fd_L - 1 <=> (fd_k - fd_hl) >= fd_span, unsigned
+    uint32_t fd_span = fd_L - 1u > fd_hl ? fd_L - 1u - fd_hl : 0u;  // 0: every line is an edge line
+
+    auto ld_advance = [&]() {
+      if (++ld_k == ld_L) {  // wave-uniform
+        ld_k = 0;
+        if (ld_q + 1 < qe) {
+          ++ld_q;
+          if (!(ABL & 4) && (ld_q & 7u) == 0) {
+            put_block((ld_q >> 3) + 1, NB);
+            NB = load_block((ld_q >> 3) + 2);
           }
+          ld_L = ld_enter(ld_q, ld);
         } else {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) xr[i] = xor3(xr[i], wc[i], edge_word(wc[i], rel0 + 4 * i, (int)fd_M));
+          ld_L = 1;  // done: re-read line 0 of the last group (ld_k wraps to 0 every step)
         }
       }
-      uint32_t t[4][4];
-#pragma unroll
+    };
+    // (ABL 16384, timing only: no line loads, a value derived from the address)
+    auto line_load = [&](uint64_t addr) -> u32x4 {
+      if (ABL & 16384) return u32x4{(uint32_t)addr, (uint32_t)(addr >> 7), lane, (uint32_t)addr * 3u};
+      return gload16_nt(addr);
+    };
+    auto ld_issue = [&]() -> u32x4 { return line_load(ld.line0 + 128ull * ld_k); };
+
+    u32x4 ring[D];
+  #pragma unroll
+    for (int u = 0; u < D; ++u) {
+      __builtin_amdgcn_sched_barrier(0);
+      ring[u] = ld_issue();
+      ld_advance();
+    }
+    __builtin_amdgcn_sched_barrier(0);
+
+    uint32_t r[4] = {0u, 0u, 0u, 0u};
+    // Two copies of the fold loop: one with whole-word edges when the bucket
+    // pass found every strided-chain packet word-aligned in start and length
+    // (a per-group choice inside the loop made the compiler rotate the load
+    // ring through copies and drain vmcnt(0) at the loop head).
+    // The fold keeps xr = r ^ (the current line's word), the lookup input: the
+    // XOR with the next line's word rides in the step's last 3-input XOR (as in
+    // the SCK), 4 VALU per line fewer.  An edge line corrects xr by
+    // w ^ masked(w) on its own step; a group's last line leaves the next
+    // group's first word alone in xr (its chains start from zero).
+    uint32_t xr[4] = {ring[0][0], ring[0][1], ring[0][2], ring[0][3]};
+    // Quiet steps.  Per-step cursor control cost the fold 16 SALU and 4.5
+    // branches per wave step against 1.7 and 0.1 in the SCK (rocprofv3 --pmc,
+    // profiles/r03/pmc_insts.txt).  A run of steps in which neither cursor
+    // changes group and the fold cursor's line is no edge line (not a head
+    // line, not the group's last) needs none of it: a step is then the 16
+    // lookups, the XORs and a load.  Every full step computes the length of
+    // the run that follows it (quiet); a block of D steps that starts with a
+    // run of >= D ahead is D quiet steps with no per-step test at all, and
+    // shorter runs go through full steps (a per-step quiet / full branch
+    // measured 17 % slower: 1115 against 953 us, tools/microbench/fold_var.hip).
+    uint32_t quiet = 0;
+    auto quiet_step = [&](int u, uint32_t ahead) {  // ahead: lines the load cursor is past ld_k within the block
+      const u32x4 wn = ring[(u + 1) % D];
+  #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        if (ABL & 1) {
-          t[i][0] = __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0400u);
-          t[i][1] = xr[i] >> 7;
-          t[i][2] = 0u;
-          t[i][3] = 0u;
+        const uint32_t t0 = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0400u));
+        const uint32_t t1 = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0500u) + 128);
+        const uint32_t t2 = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo1, 0x0C020600u));
+        const uint32_t t3 = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo1, 0x0C020700u) + 128);
+        xr[i] = xor3(t0, t1, xor3(t2, t3, wn[i]));
+      }
+      ring[u] = line_load(ld.line0 + 128ull * (ld_k + ahead));
+    };
+    auto fold_loop = [&](auto words) {
+    // One full step: edge masks, group finish and both cursors' group changes.
+    auto full_step = [&](int u, bool &done) {
+        const u32x4 wn = ring[(u + 1) % D];  // the next line, raw
+        if (!(ABL & 8) && fd_k - fd_hl >= fd_span) {  // wave-uniform: an edge line
+          const u32x4 wc = ring[u];
+          const int rel0 = (int)(128u * fd_k + 16u * s) - (int)fd_a;
+          if constexpr (decltype(words)::value) {
+            if ((ABL & 32768) || fd_k < fd_hl) {  // wave-uniform: a head line
+  #pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                // whole words: keep 0 <= rel < M by sign arithmetic (compare +
+                // select pairs needed hazard NOPs), head masks from a 16-entry
+                // table (rel >= 40 and rel < 0 index the zero entry 15)
+                const int rel = rel0 + 4 * i;
+                const uint32_t keep = (uint32_t)(((rel - (int)fd_M) & ~rel) >> 31);
+                const uint32_t k = __builtin_elementwise_min((uint32_t)rel >> 2, 15u);
+                typedef uint32_t u32x2e __attribute__((ext_vector_type(2)));
+                const u32x2e e = *reinterpret_cast<const u32x2e *>(etl + 2 * k);
+                xr[i] = xor3(xr[i], wc[i], ((wc[i] & keep) | e[0]) ^ e[1]);
+              }
+            } else {
+              // the group's last line past its head lines: rel >= 40 (no head
+              // masks), only the bytes at rel >= M dropped -- 3 VALU a word
+              // instead of 10 and a table read
+              const int lim = (int)fd_M - 1 - rel0;
+  #pragma unroll
+              for (int i = 0; i < 4; ++i) xr[i] ^= wc[i] & (uint32_t)((lim - 4 * i) >> 31);
+            }
+          } else {
+  #pragma unroll
+            for (int i = 0; i < 4; ++i) xr[i] = xor3(xr[i], wc[i], edge_word(wc[i], rel0 + 4 * i, (int)fd_M));
+          }
+        }
+        uint32_t t[4][4];
+  #pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (ABL & 1) {
+            t[i][0] = __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0400u);
+            t[i][1] = xr[i] >> 7;
+            t[i][2] = 0u;
+            t[i][3] = 0u;
+          } else {
+            t[i][0] = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0400u));
+            t[i][1] = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0500u) + 128);
+            t[i][2] = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo1, 0x0C020600u));
+            t[i][3] = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo1, 0x0C020700u) + 128);
+          }
+        }
+        if (++fd_k == fd_L) {  // wave-uniform: group fd_q folded
+  #pragma unroll
+          for (int i = 0; i < 4; ++i) r[i] = xor3(t[i][0], t[i][1], t[i][2] ^ t[i][3]);
+          finish_group(r, fd_L, fd_a, fd_M, fd_q);
+  #pragma unroll
+          for (int i = 0; i < 4; ++i) xr[i] = wn[i];
+          fd_k = 0;
+          if (fd_q + 1 < qe) {
+            ++fd_q;
+            fd_enter(fd_q);
+            fd_hl = __ballot(fd_a > 88u) != 0 ? 2u : 1u;
+            fd_span = fd_L - 1u > fd_hl ? fd_L - 1u - fd_hl : 0u;
+          } else {
+            done = true;
+            fd_L = 0xFFFFFFFFu;
+          }
         } else {
+  #pragma unroll
+          for (int i = 0; i < 4; ++i) xr[i] = xor3(t[i][0], t[i][1], xor3(t[i][2], t[i][3], wn[i]));
+        }
+        // Refill after folding: the FIFO entry the fold just read may be
+        // rewritten by this step's load-cursor advance.
+        ring[u] = ld_issue();
+        ld_advance();
+        // The quiet run that follows: fold lines fd_k .. fd_L - 2 past the head
+        // lines, loads up to the line before the load cursor's group change
+        // (ld_L = 1 once every group is loaded: no run).
+        const uint32_t nf = (fd_k >= fd_hl && fd_k + 1 < fd_L) ? fd_L - 1u - fd_k : 0u;
+        const uint32_t nl = ld_L - 1u - ld_k;
+        quiet = nf < nl ? nf : nl;
+    };
+    bool done = false;
+    while (!done) {
+      if (!(ABL & 8) && quiet >= (uint32_t)D) {  // wave-uniform: D quiet steps, no per-step control
+  #pragma unroll
+        for (int u = 0; u < D; ++u) {
+          __builtin_amdgcn_sched_barrier(0);
+          quiet_step(u, (uint32_t)u);
+        }
+        quiet -= D;
+        fd_k += D;
+        ld_k += D;
+        continue;
+      }
+  #pragma unroll
+      for (int u = 0; u < D; ++u) {  // full steps (correct in any state; each one measures the next run)
+        __builtin_amdgcn_sched_barrier(0);
+        full_step(u, done);
+      }
+    }
+    };
+    if (a.ctr->odd == 0)
+      fold_loop(std::true_type{});
+    else
+      fold_loop(std::false_type{});
+  };
+
+  // The fold specialized on the line count (round 4).  A run of groups of
+  // one class L (C4: L = 2, 3 for 256 B, 8, 9 for 1 KiB, 32, 33 for 4 KiB
+  // packets at 128- / 64-byte alignment) with every packet word-aligned runs
+  // like the SCK: the schedule is static -- step k of a group folds its line
+  // k, its head line (k = 0, and 1 when a header runs into line 1) and last
+  // line (k = L - 1) take the edge masks, the finish follows step L - 1, and
+  // the load of step k + D is line (k + D) % L of group (k + D) / L ahead --
+  // so a step has no cursor arithmetic, no quiet-run bookkeeping and no
+  // per-step branch (round 3's generic fold: 16.4 SALU and 4.5 branches per
+  // wave step against the SCK's 1.7 and 0.1, profiles/r03/pmc_insts.txt).
+  // The ring index of step k must be a constant: P = D / gcd(L, D) groups
+  // are unrolled together (L = 33, D = 6: two groups, 66 steps).  Group
+  // descriptors: groups q .. q + J (J = the farthest group a load reaches)
+  // are kept per lane (first-line slot address, a, M); group q + J + 1's
+  // descriptor is loaded P groups (one unrolled period) before the group
+  // change that needs it, into the register that change consumes -- every
+  // period issues the same loads, so the compiler counts vmcnt exactly across
+  // the loop (a descriptor block refilled every 8 groups, as the generic fold
+  // does, cost a vmcnt(0) drain of the line ring each time); groups past the
+  // repeat the run's last group (their loads are never folded).
+  auto fixed = [&](auto Lc, uint32_t qb, uint32_t qs) {
+    constexpr uint32_t L = decltype(Lc)::value;
+    constexpr uint32_t D = (L % 8u == 0u) ? 8u : 6u;        // lines in flight
+    constexpr uint32_t P = D / cgcd(L, D);                    // groups per unrolled period
+    static_assert((P * L) % D == 0u, "the ring index must repeat every period");
+    constexpr uint32_t J = (L - 1u + D) / L;                  // the farthest group a load reaches
+    uint64_t l0[J + 1];
+    uint32_t ga[J + 1], gm[J + 1];
+    auto set_info = [&](const u32x2 &d, uint32_t j) {
+      const uint64_t addr = ((uint64_t)(d[1] & 0xFFFFu) << 32) | d[0];
+      l0[j] = (addr & ~127ull) + 16u * s;
+      ga[j] = (uint32_t)addr & 127u;
+      gm[j] = (d[1] >> 16) - 4u;
+    };
+    auto gdesc = [&](uint32_t x) -> u32x2 {  // group x's descriptor of this lane's packet
+      return *reinterpret_cast<const u32x2 __attribute__((address_space(1))) *>(
+          (uintptr_t)reinterpret_cast<const uint32_t *>(a.bdesc + 8ull * x + g));
+    };
+#pragma unroll
+    for (uint32_t j = 0; j <= J; ++j) {
+      if (j == 0u || qb + j < qs) {  // wave-uniform
+        set_info(gdesc(qb + j), j);
+      } else {
+        l0[j] = l0[j - 1u];
+        ga[j] = ga[j - 1u];
+        gm[j] = gm[j - 1u];
+      }
+    }
+    // nd[p]: the descriptor the group change after unrolled group p needs
+    // (group x = q + J + 1 when entering q + 1), clamped into the run
+    auto clamp_q = [&](uint32_t x) { return x < qs ? x : qs - 1u; };
+    u32x2 nd[P];
+#pragma unroll
+    for (uint32_t p = 0; p < P; ++p) nd[p] = gdesc(clamp_q(qb + J + 1u + p));
+    u32x4 ring[D];
+#pragma unroll
+    for (uint32_t k = 0; k < D; ++k) {
+      __builtin_amdgcn_sched_barrier(0);
+      ring[k] = gload16_nt(l0[k / L] + 128ull * (k % L));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    uint32_t xr[4] = {ring[0][0], ring[0][1], ring[0][2], ring[0][3]};
+    uint32_t hl2 = __ballot(ga[0] > 88u) != 0 ? 1u : 0u;  // some header runs into line 1
+    uint32_t q = qb;
+    // One group at position p of the period (the ring slots of its steps).
+    auto group_at = [&](auto pc) {
+      constexpr uint32_t p = decltype(pc)::value;
+#pragma unroll
+      for (uint32_t k = 0; k < L; ++k) {
+        const uint32_t u = (p * L + k) % D;
+        __builtin_amdgcn_sched_barrier(0);
+        const u32x4 wc = ring[u];
+        const u32x4 wn = ring[(u + 1u) % D];
+        if (k == 0u || (k == 1u && hl2)) {  // a head line: keep [0, M), invariant masks, seed
+          const int rel0 = (int)(128u * k + 16u * s) - (int)ga[0];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int rel = rel0 + 4 * i;
+            const uint32_t keep = (uint32_t)(((rel - (int)gm[0]) & ~rel) >> 31);
+            const uint32_t kk = __builtin_elementwise_min((uint32_t)rel >> 2, 15u);
+            typedef uint32_t u32x2e __attribute__((ext_vector_type(2)));
+            const u32x2e e = *reinterpret_cast<const u32x2e *>(etl + 2 * kk);
+            xr[i] = xor3(xr[i], wc[i], ((wc[i] & keep) | e[0]) ^ e[1]);
+          }
+        } else if (k == L - 1u) {  // the last line: the bytes at rel >= M dropped
+          const int lim = (int)gm[0] - 1 - ((int)(128u * k + 16u * s) - (int)ga[0]);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) xr[i] ^= wc[i] & (uint32_t)((lim - 4 * i) >> 31);
+        }
+        uint32_t t[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
           t[i][0] = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0400u));
           t[i][1] = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0500u) + 128);
           t[i][2] = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo1, 0x0C020600u));
           t[i][3] = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo1, 0x0C020700u) + 128);
         }
-      }
-      if (++fd_k == fd_L) {  // wave-uniform: group fd_q folded
+        if (k == L - 1u) {
+          uint32_t rr[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) r[i] = xor3(t[i][0], t[i][1], t[i][2] ^ t[i][3]);
-        finish();
+          for (int i = 0; i < 4; ++i) rr[i] = xor3(t[i][0], t[i][1], t[i][2] ^ t[i][3]);
+          finish_group(rr, L, ga[0], gm[0], q);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) xr[i] = wn[i];
-        fd_k = 0;
-        if (fd_q + 1 < q_end) {
-          ++fd_q;
-          fd_enter(fd_q);
-          fd_hl = __ballot(fd_a > 88u) != 0 ? 2u : 1u;
-          fd_span = fd_L - 1u > fd_hl ? fd_L - 1u - fd_hl : 0u;
+          for (int i = 0; i < 4; ++i) xr[i] = wn[i];  // the next group's line 0: its chains start from zero
         } else {
-          done = true;
-          fd_L = 0xFFFFFFFFu;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) xr[i] = xor3(t[i][0], t[i][1], xor3(t[i][2], t[i][3], wn[i]));
         }
+        // refill: the line of step k + D (after the fold read this slot)
+        ring[u] = gload16_nt(l0[(k + D) / L] + 128ull * ((k + D) % L));
+      }
+      // group q is folded; the next one's info moves to the front
+      ++q;
+#pragma unroll
+      for (uint32_t j = 0; j < J; ++j) {
+        l0[j] = l0[j + 1u];
+        ga[j] = ga[j + 1u];
+        gm[j] = gm[j + 1u];
+      }
+      if (q + J < qs) {  // wave-uniform: group q + J exists
+        set_info(nd[p], J);
       } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) xr[i] = xor3(t[i][0], t[i][1], xor3(t[i][2], t[i][3], wn[i]));
+        l0[J] = l0[J - 1u];
+        ga[J] = ga[J - 1u];
+        gm[J] = gm[J - 1u];
       }
-      // Refill after folding: the FIFO entry the fold just read may be
-      // rewritten by this step's load-cursor advance.
-      ring[u] = ld_issue();
-      ld_advance();
-      // The quiet run that follows: fold lines fd_k .. fd_L - 2 past the head
-      // lines, loads up to the line before the load cursor's group change
-      // (ld_L = 1 once every group is loaded: no run).
-      const uint32_t nf = (fd_k >= fd_hl && fd_k + 1 < fd_L) ? fd_L - 1u - fd_k : 0u;
-      const uint32_t nl = ld_L - 1u - ld_k;
-      quiet = nf < nl ? nf : nl;
-  };
-  bool done = false;
-  while (!done) {
-    if (!(ABL & 8) && quiet >= (uint32_t)D) {  // wave-uniform: D quiet steps, no per-step control
-#pragma unroll
-      for (int u = 0; u < D; ++u) {
-        __builtin_amdgcn_sched_barrier(0);
-        quiet_step(u, (uint32_t)u);
-      }
-      quiet -= D;
-      fd_k += D;
-      ld_k += D;
-      continue;
+      nd[p] = gdesc(clamp_q(q + J + P));  // the same change one period later
+      hl2 = __ballot(ga[0] > 88u) != 0 ? 1u : 0u;
+    };
+    // Whole periods in a loop with one exit; the last n % P groups after it
+    // (an exit after any group of an unrolled period made the compiler carry
+    // the group counter through a VGPR phi -- a readfirstlane and a vmcnt(0)
+    // drain of the line ring at every period).
+    uint32_t n = qs - qb;
+    while (n >= P) {  // wave-uniform
+      static_for<P>(group_at);
+      n -= P;
     }
-#pragma unroll
-    for (int u = 0; u < D; ++u) {  // full steps (correct in any state; each one measures the next run)
-      __builtin_amdgcn_sched_barrier(0);
-      full_step(u, done);
+    static_for<P - 1>([&](auto pc) {
+      if (decltype(pc)::value < n) group_at(pc);  // wave-uniform
+    });
+  };
+  // Specialized line counts (C4's classes); other classes and byte-granular
+  // batches take the generic fold.
+  auto special = [](uint32_t L) { return L == 2u || L == 3u || L == 8u || L == 9u || L == 32u || L == 33u; };
+
+  if (ABL != 0 || a.ctr->odd != 0) {
+    generic(q_begin, q_end);
+  } else {
+    // Segments of the wave's groups: a run of one specialized L, or a run of
+    // other classes (up to 64 groups of look-ahead per segment).
+    uint32_t q = q_begin;
+    while (q < q_end) {  // wave-uniform
+      const uint32_t x = q + lane;
+      uint32_t Lx = 0xFFFFFFFFu;
+      if (x < q_end) {
+        const u32x2 d = *reinterpret_cast<const u32x2 __attribute__((address_space(1))) *>(
+            (uintptr_t)reinterpret_cast<const uint32_t *>(a.bdesc + 8ull * x));
+        Lx = ((d[0] & 127u) + (d[1] >> 16) - 4u + 127u) >> 7;
+      }
+      uint32_t L0 = __builtin_amdgcn_readfirstlane(Lx);
+      const bool sp = special(L0);
+      const uint64_t stop = __ballot(sp ? Lx != L0 : (Lx == 0xFFFFFFFFu || special(Lx)));
+      const uint32_t n = stop ? (uint32_t)__builtin_ctzll(stop) : 64u;
+      uint32_t qs = q + n < q_end ? q + n : q_end;
+      // pin the segment's scalars in SGPRs: rematerialized from the scan's
+      // VGPR after a specialized loop, they cost a vmcnt(0) drain there
+      asm volatile("" : "+s"(L0), "+s"(qs));
+      switch (sp ? L0 : 0u) {  // wave-uniform
+        case 2: fixed(std::integral_constant<uint32_t, 2>{}, q, qs); break;
+        case 3: fixed(std::integral_constant<uint32_t, 3>{}, q, qs); break;
+        case 8: fixed(std::integral_constant<uint32_t, 8>{}, q, qs); break;
+        case 9: fixed(std::integral_constant<uint32_t, 9>{}, q, qs); break;
+        case 32: fixed(std::integral_constant<uint32_t, 32>{}, q, qs); break;
+        case 33: fixed(std::integral_constant<uint32_t, 33>{}, q, qs); break;
+        default: generic(q, qs); break;
+      }
+      q = qs;
     }
   }
-  };
-  if (a.ctr->odd == 0)
-    fold_loop(std::true_type{});
-  else
-    fold_loop(std::false_type{});
   if (!(ABL & 16) && q_end != round_q0) flush(q_end);
-  if ((ABL & 48) && r[0] == 0x12345678u) a.bres[0] = r[1];
+  if ((ABL & 48) && sink == 0x12345678u) a.bres[0] = sink;
   if ((ABL & 8192) && lane == 0) {  // timing only: end stamp after every store has left
     __builtin_amdgcn_s_waitcnt(0);
     a.out[4 * wave + 1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
@@ -1012,24 +1214,33 @@ struct SmallPk {
   }
 };
 
+// Chunks of 64 small-pool packets are taken dynamically (ctr->small_next):
+// two launches share the pool -- one on a few CUs beside the fold on a side
+// stream, one after the fold on every CU that finds what is left (nothing,
+// on C4, whose one-line packets are 2 % of its bytes).
 __global__ __launch_bounds__(kBlock) void icrc_rsmall_kernel(RsckArgs a) {
   __shared__ uint32_t lds[kLdsWords];
-  const uint32_t tab_v = table_entry(g_tab);
   const uint32_t count = a.ctr->small;
+  if ((uint32_t)__builtin_amdgcn_readfirstlane(*(volatile uint32_t *)&a.ctr->small_next) >= count) return;  // nothing left
+  const uint32_t tab_v = table_entry(g_tab);
   table_store(lds, tab_v);
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63;
-  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const LaneTab lt{(lane & 31) << 2, ((lane & 31) << 2) | 0x10000u};
-  const uint32_t step = gridDim.x * kWaves * 64u;
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.res, 4u * count);
   auto desc_at = [&](uint32_t pos) -> RsDesc { return a.desc[pos < count ? pos : (count ? count - 1u : 0u)]; };
-  uint32_t base = (blockIdx.x * kWaves + wid) * 64u;
+  auto take = [&]() -> uint32_t {  // the wave's next chunk (wave-uniform)
+    uint32_t c = 0;
+    if (lane == 0) c = atomicAdd(&a.ctr->small_next, 64u);
+    return __builtin_amdgcn_readfirstlane(c);
+  };
+  uint32_t base = take();
+  uint32_t next = base < count ? take() : count;
   RsDesc dn = desc_at(base + lane);
-  for (; base < count; base += step) {
+  for (; base < count; base = next, next = next < count ? take() : count) {
     const uint32_t pos = base + lane;
     const RsDesc d = dn;
-    dn = desc_at(pos + step);  // the next round's descriptor, in flight meanwhile
+    dn = desc_at(next + lane);  // the next chunk's descriptor, in flight meanwhile
     uint32_t K = (((d.hi >> 16) - 4u) + 4u + 15u) >> 4;  // this lane's blocks
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) K = max(K, (uint32_t)__shfl_xor((int)K, o));
@@ -1152,7 +1363,8 @@ static void launch_bucket(const RsckArgs &a, int pgrid, hipStream_t st) {
   else launch_bucket_u<kPassUnroll>(a, pgrid, st);
 }
 
-hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, hipStream_t st) {
+hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, hipStream_t st, hipStream_t side, hipEvent_t ev_bucket,
+                       hipEvent_t ev_side, int side_grid) {
   (void)hipGetLastError();  // a stale error of an earlier, unrelated HIP call must not fail this launch
   if (a.count == 0) return hipSuccess;
   if (a.count > kRsMaxCount) return hipErrorInvalidValue;
@@ -1163,9 +1375,22 @@ hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, hipStream_t st) {
   if (pass_cap > 0 && pass_cap < pgrid) pgrid = pass_cap;
   a.nblk = (uint32_t)pgrid;
   launch_bucket(a, pgrid, st);
-  hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, st, a);
-  // the small pool [0, ctr->small): one lane per packet
+  const bool beside = side && ev_bucket && ev_side && side_grid > 0 && side_grid < grid;
+  if (beside) {  // the one-line kernel on side_grid CUs, beside the fold on the rest
+    hipError_t e = hipEventRecord(ev_bucket, st);
+    if (e == hipSuccess) e = hipStreamWaitEvent(side, ev_bucket, 0);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(icrc_rsmall_kernel, dim3(side_grid), dim3(kBlock), 0, side, a);
+    if ((e = hipEventRecord(ev_side, side)) != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(beside ? grid - side_grid : grid), dim3(kBlock), 0, st, a);
+  // the small pool [0, ctr->small): one lane per packet (beside: whatever the
+  // side launch has not taken yet, on every CU)
   hipLaunchKernelGGL(icrc_rsmall_kernel, dim3(grid), dim3(kBlock), 0, st, a);
+  if (beside) {
+    const hipError_t e = hipStreamWaitEvent(st, ev_side, 0);  // the gather reads both launches' results
+    if (e != hipSuccess) return e;
+  }
   // the gather's blocks are the bucket pass's (block b serves pass block b's packets)
   if (pass_big(a, pgrid)) hipLaunchKernelGGL(rsck_gather<kPassUnrollBig>, dim3(pgrid), dim3(kPassBlock), 0, st, a);
   else hipLaunchKernelGGL(rsck_gather<kPassUnroll>, dim3(pgrid), dim3(kPassBlock), 0, st, a);

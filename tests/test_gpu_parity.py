@@ -546,6 +546,49 @@ def test_ragged_strided_chain_word_aligned(ctx):
         np.testing.assert_array_equal(_host_u32(out), want)
 
 
+@pytest.mark.parametrize("grid", [None, 5])
+def test_ragged_fold_specialized_line_counts(ctx, ctx_env, grid):
+    """Round 4: word-aligned runs of one line count L in {2, 3, 8, 9, 32, 33}
+    take the fold specialized on L (static schedule: P = D / gcd(L, D)
+    groups unrolled per period, the last n % P groups after the loop), other
+    classes the generic fold, segment by segment (64 groups of look-ahead).
+    Starts at every multiple of 4 (headers running into line 1: a second head
+    line), sizes drawn so every specialized class occurs with both parities of
+    a period and next to generic classes; a capped fold grid makes every wave
+    cross many segments.  Verify mode on the same batch."""
+    if grid is not None:
+        ctx = ctx_env(RICRC_RSCK_GRID=grid)
+    rng = np.random.default_rng(404)
+    count = 40_000
+    lens = rng.choice(np.array([256, 1024, 4096, 2048, 1500, 64, 300, 8192], np.uint32), size=count,
+                      p=[.25, .25, .25, .05, .05, .05, .05, .05])
+    lens &= ~np.uint32(3)
+    gaps = (rng.integers(0, 33, size=count) * 4).astype(np.uint64)
+    gaps[rng.random(count) < 0.5] = 0  # runs packed back to back too
+    offs = np.zeros(count, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + gaps[:-1])
+    offs += 12
+    buf = rng.integers(0, 256, size=int(offs[-1] + lens[-1]) + 128, dtype=np.uint8)
+    starts = (offs & 127).astype(np.int64)
+    line_counts = (starts + lens.astype(np.int64) - 4 + 127) // 128
+    for L in (2, 3, 8, 9, 32, 33):
+        assert (line_counts == L).sum() > 500, L
+    assert ((starts > 88) & np.isin(line_counts, [2, 3, 8, 9, 32, 33])).sum() > 1000  # second head lines
+    want = oracle_c.icrc_batch(buf, offsets=offs, lengths=lens, threads=16)
+    d, d_off, d_len = _dev(buf), _dev(offs.view(np.int64)), _dev(lens.view(np.int32))
+    out = _out(count)
+    ctx.batch_device(d, count, out, offsets=d_off, lengths=d_len, stream=_stream())
+    np.testing.assert_array_equal(_host_u32(out), want)
+    stamped = buf.copy()
+    for i in range(0, count, 3):
+        o, n = int(offs[i]), int(lens[i])
+        stamped[o + n - 4:o + n] = np.frombuffer(int(want[i]).to_bytes(4, "little"), np.uint8)
+    exp = np.zeros(count, np.uint32)
+    exp[::3] = 1
+    ctx.batch_device(_dev(stamped), count, out, offsets=d_off, lengths=d_len, stream=_stream(), verify=True)
+    np.testing.assert_array_equal(_host_u32(out), exp)
+
+
 def test_ragged_workspace_reuse_across_sizes_and_streams(ctx):
     """The ragged path's context-owned workspaces (one per stream, grown on
     demand, class counters re-zeroed by the last pass of every call): calls of
