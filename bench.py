@@ -110,6 +110,9 @@ def parse(argv=None):
     ap.add_argument("--step-events", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="wall budget of the CPU baseline")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--pass-times", action="store_true",
+                    help="diagnostics (--mix): HIP events between the ragged pipeline's passes (RICRC_PASS_TIMES; "
+                         "a few us per step) -> pass_ms, and the GPU's clocks / power around the timed steps")
     ap.add_argument("--plan-only", action="store_true",
                     help="print the shard plan every rank would run (gloo, no GPU) and exit")
     a = ap.parse_args(argv)
@@ -215,6 +218,20 @@ def rccl_version():
         return ".".join(map(str, v)) if isinstance(v, tuple) else str(v)
     except Exception:
         return None
+
+
+def gpu_state(dev):
+    """Clock / power / temperature readings of GPU `dev` right now (amd-smi,
+    else rocm-smi; JSON as the tool prints it), or an error string."""
+    for cmd in (["amd-smi", "metric", "-g", str(dev), "-c", "-p", "-t", "--json"],
+                ["rocm-smi", "-d", str(dev), "--showclocks", "--showpower", "--showtemp", "--json"]):
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=20)
+            if r.returncode == 0 and r.stdout.strip():
+                return {"tool": cmd[0], "t": round(time.time(), 3), "data": json.loads(r.stdout)}
+        except (OSError, subprocess.SubprocessError, ValueError):
+            continue
+    return "unavailable"
 
 
 def cpu_share():
@@ -493,7 +510,7 @@ class HipBackend:
 
     dist_backend = "nccl"
 
-    def __init__(self, local):
+    def __init__(self, local, pass_times=False):
         import torch
 
         import roce_icrc
@@ -501,6 +518,8 @@ class HipBackend:
         self.torch = torch
         torch.cuda.set_device(local)
         self.dev = torch.device("cuda", local)
+        if pass_times:  # read once, by ricrc_create
+            os.environ["RICRC_PASS_TIMES"] = "1"
         self.ctx = roce_icrc.Context(devices=[local])
         self.stream = torch.cuda.current_stream()
 
@@ -533,6 +552,9 @@ class HipBackend:
     def prime(self, ms):
         if ms > 0:
             self.ctx.prime(int(ms * 1000))
+
+    def pass_times(self):
+        return self.ctx.pass_times()
 
     def host_bytes(self, b, nbytes):
         return b["buf"][:nbytes].cpu().numpy()
@@ -598,6 +620,11 @@ def run(args, world, rank, be, distributed):
     for i in range(args.warmup):
         step(i)
     drain()
+    diag = {}
+    if args.pass_times and hasattr(be, "pass_times"):
+        be.sync()
+        be.pass_times()  # forget the warmup's calls
+        diag["gpu_state_before"] = gpu_state(be.dev.index)
     n_ev = args.steps if args.step_events else 1
     evs = [(be.event(), be.event()) for _ in range(n_ev)]
     be.sync()
@@ -620,6 +647,12 @@ def run(args, world, rank, be, distributed):
     be.sync()
     elapsed = time.perf_counter() - t0
     kern_ms = sum(a.elapsed_time(c) for a, c in evs) / max(args.steps, 1)
+    if args.pass_times and hasattr(be, "pass_times"):
+        diag["gpu_state_after"] = gpu_state(be.dev.index)
+        calls, ms = be.pass_times()
+        diag["pass_ms"] = {k: round(v / max(calls, 1), 4) for k, v in
+                           zip(("bucket", "fold", "one_line", "gather"), ms)} if calls else None
+        diag["pass_calls"] = calls
 
     # ---- N > 1, after the timed region: the step's two parts timed apart
     # (compute-only and with-gather scaling reported
@@ -719,6 +752,7 @@ def run(args, world, rank, be, distributed):
                      "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": alg_bytes},
         "oracle_sampled_all_ranks": True,
     }
+    result.update(diag)
     if distributed:
         result["world_size"] = dist.get_world_size()
         result["collective_backend"] = dist.get_backend()
@@ -745,7 +779,7 @@ def main(argv=None):
 
     import torch.distributed as dist
 
-    be = HipBackend(local)
+    be = HipBackend(local, pass_times=args.pass_times)
     distributed = world > 1 or "MASTER_ADDR" in os.environ
     result, full_h, b = run(args, world, rank, be, distributed)
     count = b["sizes"][rank]

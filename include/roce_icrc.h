@@ -375,6 +375,16 @@ void *ricrc_stream(ricrc_ctx *ctx, int dev);
 const char *ricrc_kernel_path(const ricrc_ctx *ctx, const void *d_base, const uint64_t *d_off, const uint32_t *d_len,
                               uint32_t stride, uint64_t count, uint32_t l3_offset, uint32_t flags);
 
+/* Diagnostics: with RICRC_PASS_TIMES set when the context was created, every
+ * ragged-pipeline call on device dev records timing events between its
+ * passes (costing a few microseconds per call); this waits for the recorded
+ * calls, writes into ms[0..min(n,4)) the summed milliseconds of the bucket
+ * pass, the fold, the one-line kernel (with the wait for its side launch)
+ * and the gather, and returns how many calls were summed (then forgets
+ * them; the last 64 calls are kept).
+ * 0 without RICRC_PASS_TIMES; -EINVAL, -ENODEV, -EIO. */
+int ricrc_pass_times(ricrc_ctx *ctx, int dev, float *ms, int n);
+
 const char *ricrc_strerror(int err);
 
 #ifdef __cplusplus

@@ -53,6 +53,7 @@ struct Knobs {
   uint32_t gcost = 0;      // RICRC_RS_GCOST: the ragged fold's per-group cost, quarter lines (0: kRsGroupCost)
   int pass_grid = 0;       // RICRC_RS_PASS_GRID: cap the ragged bucket / gather pass grid (schedule studies)
   int rs_side = -1;        // RICRC_RS_SIDE: CUs of the one-line kernel beside the fold (-1: n_cu / 16; 0: in order)
+  bool pass_times = false; // RICRC_PASS_TIMES: timing events between the ragged passes (ricrc_pass_times)
   long fail_chunk = -1;    // RICRC_FAIL_CHUNK: the next ricrc_batch_host fails after queueing chunk k (tests; once)
   int host_threads = 16;   // RICRC_HOST_THREADS: CPU copy threads of ricrc_batch_host
 };
@@ -104,6 +105,11 @@ struct Dev {
   // calls on different streams are ordered on the side stream by the events.
   hipStream_t side = nullptr;
   hipEvent_t ev_bucket = nullptr, ev_side = nullptr;
+  // RICRC_PASS_TIMES: kPtSets sets of 5 timing events, one set per ragged
+  // call in turn; ricrc_pass_times sums the sets recorded since its last call.
+  static constexpr int kPtSets = 64;
+  std::vector<hipEvent_t> pt_ev;
+  int pt_next = 0, pt_used = 0;
   std::vector<Ws> ws;
   std::vector<hipEvent_t> spare;  // events of workspaces evicted for bytes, reused by the next new one
 };
@@ -222,6 +228,8 @@ void free_dev(Dev &d) {
   d.ws.clear();
   for (hipEvent_t e : d.spare) (void)hipEventSynchronize(e), (void)hipEventDestroy(e);
   d.spare.clear();
+  for (hipEvent_t e : d.pt_ev) (void)hipEventDestroy(e);
+  d.pt_ev.clear();
   if (d.side) (void)hipStreamSynchronize(d.side), (void)hipStreamDestroy(d.side);
   if (d.ev_bucket) (void)hipEventDestroy(d.ev_bucket);
   if (d.ev_side) (void)hipEventDestroy(d.ev_side);
@@ -376,7 +384,17 @@ int launch_rsck_range(Dev &d, const uint8_t *base, const uint64_t *off, const ui
     HIP_TRY(hipEventCreateWithFlags(&d.ev_bucket, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&d.ev_side, hipEventDisableTiming));
   }
-  const hipError_t e = launch_rsck(k, rgrid, d.knobs.pass_grid, st, d.side, d.ev_bucket, d.ev_side, side_grid);
+  hipEvent_t *pev = nullptr;
+  if (d.knobs.pass_times) {
+    if (d.pt_ev.empty()) {
+      d.pt_ev.resize(5 * Dev::kPtSets);
+      for (hipEvent_t &ev : d.pt_ev) HIP_TRY(hipEventCreate(&ev));
+    }
+    pev = &d.pt_ev[5 * d.pt_next];  // a ring: the last kPtSets calls are kept
+    d.pt_next = (d.pt_next + 1) % Dev::kPtSets;
+    d.pt_used = std::min(d.pt_used + 1, Dev::kPtSets);
+  }
+  const hipError_t e = launch_rsck(k, rgrid, d.knobs.pass_grid, st, d.side, d.ev_bucket, d.ev_side, side_grid, pev);
   if (e != hipSuccess) ws->dirty = true;
   const hipError_t e2 = hipEventRecord(ws->done, st);
   return hip_err(e != hipSuccess ? e : e2);
@@ -680,6 +698,7 @@ Knobs read_knobs() {
   k.gcost = (uint32_t)std::min(1024L, std::max(0L, num("RICRC_RS_GCOST", 0)));  // the packed work counter's range
   k.pass_grid = (int)std::max(0L, num("RICRC_RS_PASS_GRID", 0));
   k.rs_side = (int)std::max(-1L, num("RICRC_RS_SIDE", -1));
+  k.pass_times = getenv("RICRC_PASS_TIMES") != nullptr;
   k.fail_chunk = num("RICRC_FAIL_CHUNK", -1);
   const unsigned hw = std::thread::hardware_concurrency();
   k.host_threads = (int)std::max(1L, std::min(64L, num("RICRC_HOST_THREADS", (long)std::min(16u, std::max(1u, hw)))));
@@ -750,6 +769,26 @@ int ricrc_device_count(const ricrc_ctx *ctx) { return ctx ? (int)ctx->devs.size(
 void *ricrc_stream(ricrc_ctx *ctx, int dev) {
   if (!ctx || dev < 0 || dev >= (int)ctx->devs.size()) return nullptr;
   return ctx->devs[dev].stream;
+}
+
+int ricrc_pass_times(ricrc_ctx *ctx, int dev, float *ms, int n) {
+  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size() || (n > 0 && !ms)) return -EINVAL;
+  Dev &d = ctx->devs[dev];
+  DeviceGuard g(d.id);
+  if (!g.ok()) return -ENODEV;
+  for (int k = 0; k < n; ++k) ms[k] = 0.f;
+  const int used = d.pt_used;
+  for (int c = 0; c < used; ++c) {  // the oldest recorded set first
+    hipEvent_t *e = &d.pt_ev[5 * ((d.pt_next - used + c + Dev::kPtSets) % Dev::kPtSets)];
+    HIP_TRY(hipEventSynchronize(e[4]));
+    for (int k = 0; k < 4 && k < n; ++k) {
+      float t = 0.f;
+      HIP_TRY(hipEventElapsedTime(&t, e[k], e[k + 1]));
+      ms[k] += t;
+    }
+  }
+  d.pt_used = 0;
+  return used;
 }
 
 const char *ricrc_kernel_path(const ricrc_ctx *ctx, const void *d_base, const uint64_t *d_off, const uint32_t *d_len,

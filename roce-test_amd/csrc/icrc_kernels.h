@@ -140,8 +140,12 @@ constexpr uint64_t kRsMaxCount = 1ull << 28;
 // side: a second stream on the same device and two events (the workspace's):
 // the one-line kernel runs there on `side_grid` CUs, beside the fold on the
 // others (side_grid 0: everything in order on st).
+// pass_ev (diagnostics, RICRC_PASS_TIMES): 5 timing events recorded on st
+// before the bucket pass and after the bucket, fold, one-line (joined) and
+// gather passes.
 hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, hipStream_t st, hipStream_t side = nullptr,
-                       hipEvent_t ev_bucket = nullptr, hipEvent_t ev_side = nullptr, int side_grid = 0);
+                       hipEvent_t ev_bucket = nullptr, hipEvent_t ev_side = nullptr, int side_grid = 0,
+                       hipEvent_t *pass_ev = nullptr);
 
 struct SynthArgs {
   uint8_t *buf;

@@ -1364,7 +1364,7 @@ static void launch_bucket(const RsckArgs &a, int pgrid, hipStream_t st) {
 }
 
 hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, hipStream_t st, hipStream_t side, hipEvent_t ev_bucket,
-                       hipEvent_t ev_side, int side_grid) {
+                       hipEvent_t ev_side, int side_grid, hipEvent_t *pass_ev) {
   (void)hipGetLastError();  // a stale error of an earlier, unrelated HIP call must not fail this launch
   if (a.count == 0) return hipSuccess;
   if (a.count > kRsMaxCount) return hipErrorInvalidValue;
@@ -1374,7 +1374,11 @@ hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, hipStream_t st, hipS
   int pgrid = (int)(want < kPassBlocks ? want : kPassBlocks);
   if (pass_cap > 0 && pass_cap < pgrid) pgrid = pass_cap;
   a.nblk = (uint32_t)pgrid;
+  // RICRC_PASS_TIMES: timing events between the passes on st (diagnostics)
+  auto mark = [&](int k) { if (pass_ev) (void)hipEventRecord(pass_ev[k], st); };
+  mark(0);
   launch_bucket(a, pgrid, st);
+  mark(1);
   const bool beside = side && ev_bucket && ev_side && side_grid > 0 && side_grid < grid;
   if (beside) {  // the one-line kernel on side_grid CUs, beside the fold on the rest
     hipError_t e = hipEventRecord(ev_bucket, st);
@@ -1384,6 +1388,7 @@ hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, hipStream_t st, hipS
     if ((e = hipEventRecord(ev_side, side)) != hipSuccess) return e;
   }
   hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(beside ? grid - side_grid : grid), dim3(kBlock), 0, st, a);
+  mark(2);
   // the small pool [0, ctr->small): one lane per packet (beside: whatever the
   // side launch has not taken yet, on every CU)
   hipLaunchKernelGGL(icrc_rsmall_kernel, dim3(grid), dim3(kBlock), 0, st, a);
@@ -1391,9 +1396,11 @@ hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, hipStream_t st, hipS
     const hipError_t e = hipStreamWaitEvent(st, ev_side, 0);  // the gather reads both launches' results
     if (e != hipSuccess) return e;
   }
+  mark(3);
   // the gather's blocks are the bucket pass's (block b serves pass block b's packets)
   if (pass_big(a, pgrid)) hipLaunchKernelGGL(rsck_gather<kPassUnrollBig>, dim3(pgrid), dim3(kPassBlock), 0, st, a);
   else hipLaunchKernelGGL(rsck_gather<kPassUnroll>, dim3(pgrid), dim3(kPassBlock), 0, st, a);
+  mark(4);
   return hipGetLastError();
 }
 

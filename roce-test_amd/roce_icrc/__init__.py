@@ -50,6 +50,7 @@ EXPORTED = CPU_EXPORTED + (
     "ricrc_host_register", "ricrc_host_unregister", "ricrc_synth_device", "ricrc_synth_ragged_device",
     "ricrc_prime", "ricrc_stream", "ricrc_comm_init", "ricrc_batch_device_all", "ricrc_allgather", "ricrc_sync",
     "ricrc_batch_device_st", "ricrc_batch_host_st", "ricrc_classify_device", "ricrc_kernel_path",
+    "ricrc_pass_times",
 )
 
 # Per-packet status of the *_st batch calls (include/roce_icrc.h).
@@ -103,6 +104,7 @@ _SIG = {
     "ricrc_batch_host_st": ([_vp, _vp, _vp, _vp, _u32, _u64, _u32, _vp, _vp, _u32], _i32),
     "ricrc_classify_device": ([_vp, _i32, _vp, _vp, _vp, _u32, _u64, _u32, _vp, _vp], _i32),
     "ricrc_kernel_path": ([_vp, _vp, _vp, _vp, _u32, _u64, _u32, _u32], ctypes.c_char_p),
+    "ricrc_pass_times": ([_vp, _i32, ctypes.POINTER(ctypes.c_float), _i32], _i32),
 }
 
 
@@ -479,6 +481,16 @@ class Context:
                                                  _ptr(buf), _stream_ptr(stream))
         if rc:
             raise ICRCError(rc, "ricrc_synth_ragged_device")
+
+    def pass_times(self, dev: int = 0):
+        """``ricrc_pass_times`` (RICRC_PASS_TIMES set at creation): (calls,
+        summed ms of the ragged pipeline's bucket, fold, one-line and gather
+        passes since the last query)."""
+        ms = (ctypes.c_float * 4)()
+        rc = self._lib.ricrc_pass_times(self._h, dev, ms, 4)
+        if rc < 0:
+            raise ICRCError(rc, "ricrc_pass_times")
+        return rc, [float(v) for v in ms]
 
     def prime(self, usec: int = 20000, dev: int = 0) -> None:
         """``ricrc_prime``: bring the device out of its idle power state."""
