@@ -52,7 +52,6 @@ struct Knobs {
   int rsck_grid = 0;       // RICRC_RSCK_GRID: cap the ragged fold grid (tests)
   uint32_t gcost = 0;      // RICRC_RS_GCOST: the ragged fold's per-group cost, quarter lines (0: kRsGroupCost)
   int pass_grid = 0;       // RICRC_RS_PASS_GRID: cap the ragged bucket / gather pass grid (schedule studies)
-  int rs_side = -1;        // RICRC_RS_SIDE: CUs of the one-line kernel beside the fold (-1: n_cu / 16; 0: in order)
   bool pass_times = false; // RICRC_PASS_TIMES: timing events between the ragged passes (ricrc_pass_times)
   long fail_chunk = -1;    // RICRC_FAIL_CHUNK: the next ricrc_batch_host fails after queueing chunk k (tests; once)
   int host_threads = 16;   // RICRC_HOST_THREADS: CPU copy threads of ricrc_batch_host
@@ -99,12 +98,6 @@ struct Dev {
     bool dirty;  // a call failed part-way: zero the counters before the next one
     hipEvent_t done;
   };
-  // The ragged pipeline's side stream (the one-line kernel beside the fold)
-  // and its two fork / join events.  One per device: a call's side work is
-  // joined back into its stream before the call returns to the queue, and
-  // calls on different streams are ordered on the side stream by the events.
-  hipStream_t side = nullptr;
-  hipEvent_t ev_bucket = nullptr, ev_side = nullptr;
   // RICRC_PASS_TIMES: kPtSets sets of 5 timing events, one set per ragged
   // call in turn; ricrc_pass_times sums the sets recorded since its last call.
   static constexpr int kPtSets = 64;
@@ -230,9 +223,6 @@ void free_dev(Dev &d) {
   d.spare.clear();
   for (hipEvent_t e : d.pt_ev) (void)hipEventDestroy(e);
   d.pt_ev.clear();
-  if (d.side) (void)hipStreamSynchronize(d.side), (void)hipStreamDestroy(d.side);
-  if (d.ev_bucket) (void)hipEventDestroy(d.ev_bucket);
-  if (d.ev_side) (void)hipEventDestroy(d.ev_side);
   (void)hipFree(d.d_tzb);
   (void)hipFree(d.d_x8n);
   if (d.stream) (void)hipStreamDestroy(d.stream);
@@ -374,16 +364,6 @@ int launch_rsck_range(Dev &d, const uint8_t *base, const uint64_t *off, const ui
   rs_bind_workspace(k, ws->p);
   int rgrid = d.n_cu;
   if (d.knobs.rsck_grid > 0) rgrid = std::min(rgrid, d.knobs.rsck_grid);
-  // The one-line kernel (C4's 64-byte packets: 2 % of the bytes, fetched as
-  // whole lines at 3.8 TB/s) runs on 1/16 of the CUs beside the fold instead
-  // of after it; a second launch after the fold on every CU takes whatever
-  // it has not reached (icrc_rsck.hip).
-  const int side_grid = d.knobs.rs_side < 0 ? std::max(1, d.n_cu / 16) : d.knobs.rs_side;
-  if (side_grid > 0 && !d.side) {
-    HIP_TRY(hipStreamCreateWithFlags(&d.side, hipStreamNonBlocking));
-    HIP_TRY(hipEventCreateWithFlags(&d.ev_bucket, hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&d.ev_side, hipEventDisableTiming));
-  }
   hipEvent_t *pev = nullptr;
   if (d.knobs.pass_times) {
     if (d.pt_ev.empty()) {
@@ -394,7 +374,7 @@ int launch_rsck_range(Dev &d, const uint8_t *base, const uint64_t *off, const ui
     d.pt_next = (d.pt_next + 1) % Dev::kPtSets;
     d.pt_used = std::min(d.pt_used + 1, Dev::kPtSets);
   }
-  const hipError_t e = launch_rsck(k, rgrid, d.knobs.pass_grid, st, d.side, d.ev_bucket, d.ev_side, side_grid, pev);
+  const hipError_t e = launch_rsck(k, rgrid, d.knobs.pass_grid, st, pev);
   if (e != hipSuccess) ws->dirty = true;
   const hipError_t e2 = hipEventRecord(ws->done, st);
   return hip_err(e != hipSuccess ? e : e2);
@@ -697,7 +677,6 @@ Knobs read_knobs() {
   k.rsck_grid = (int)std::max(0L, num("RICRC_RSCK_GRID", 0));
   k.gcost = (uint32_t)std::min(1024L, std::max(0L, num("RICRC_RS_GCOST", 0)));  // the packed work counter's range
   k.pass_grid = (int)std::max(0L, num("RICRC_RS_PASS_GRID", 0));
-  k.rs_side = (int)std::max(-1L, num("RICRC_RS_SIDE", -1));
   k.pass_times = getenv("RICRC_PASS_TIMES") != nullptr;
   k.fail_chunk = num("RICRC_FAIL_CHUNK", -1);
   const unsigned hw = std::thread::hardware_concurrency();

@@ -73,8 +73,6 @@ struct RsCounters {
   uint32_t odd;                // a big packet not starting or ending on a 4-byte word
   uint32_t small;              // small-pool packets
   unsigned long long pool;     // big pool: groups | work << kRsGroupBits
-  uint32_t small_next;         // one-line kernel: the next chunk of 64 small-pool packets to take
-  uint32_t pad;
 };
 struct RsBlock {               // pass block b's ranges (runs == 0: no big packets)
   uint32_t g0, groups, runs;   // big pool: groups [g0, g0 + groups), its runs
@@ -137,15 +135,10 @@ hipError_t rs_zero_counters(void *ws, hipStream_t st);
 // count <= kRsMaxCount (the host cuts larger batches: the big pool's group
 // count must fit kRsGroupBits).
 constexpr uint64_t kRsMaxCount = 1ull << 28;
-// side: a second stream on the same device and two events (the workspace's):
-// the one-line kernel runs there on `side_grid` CUs, beside the fold on the
-// others (side_grid 0: everything in order on st).
 // pass_ev (diagnostics, RICRC_PASS_TIMES): 5 timing events recorded on st
-// before the bucket pass and after the bucket, fold, one-line (joined) and
-// gather passes.
-hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, hipStream_t st, hipStream_t side = nullptr,
-                       hipEvent_t ev_bucket = nullptr, hipEvent_t ev_side = nullptr, int side_grid = 0,
-                       hipEvent_t *pass_ev = nullptr);
+// before the bucket pass and after the bucket, fold, one-line and gather
+// passes.
+hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, hipStream_t st, hipEvent_t *pass_ev = nullptr);
 
 struct SynthArgs {
   uint8_t *buf;

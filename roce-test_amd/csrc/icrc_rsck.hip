@@ -360,7 +360,7 @@ __global__ __launch_bounds__(kPassBlock) void rsck_gather(RsckArgs a) {
   __shared__ uint32_t lres[kStage];
   // The counters are dead now (the bucket pass and both folds have read
   // them): zero them for the next call on this workspace.
-  if (blockIdx.x == 0 && threadIdx.x == 0) *a.ctr = RsCounters{0u, 0u, 0ull, 0u, 0u};
+  if (blockIdx.x == 0 && threadIdx.x == 0) *a.ctr = RsCounters{0u, 0u, 0ull};
   uint32_t lo, hi;
   {
     uint64_t l, h_;
@@ -451,7 +451,8 @@ __device__ __forceinline__ void static_for(F &&f) {
 // 512 (with 2) 192 result slots, 1024 / 2048 / 4096 result stores nt / default / sc0 sc1,
 // 8192 per-wave s_memrealtime start / end stamps, groups and first group into a.out
 // (4 words per wave; tools/microbench/bucket_abl.hip), 16384 no line loads, 32768 every
-// edge line through the head-line path (the round-3 session-23 fold).
+// edge line through the head-line path (the round-3 session-23 fold), 131072
+// the fold specialized on the line count (round 4; tools/microbench/fold_var.hip).
 template <int ABL>
 __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   // Result slots per wave (a round of 8 groups leaves in one store; a store
@@ -1048,10 +1049,13 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
     });
   };
   // Specialized line counts (C4's classes); other classes and byte-granular
-  // batches take the generic fold.
+  // batches take the generic fold.  Timing variant only (ABL 131072,
+  // tools/microbench/fold_var.hip): bit-exact, but 921.5 us against the
+  // generic fold's 918.5 on C4 (profiles/r04/s2_mb_fold_var.txt), so the
+  // product runs the generic fold.
   auto special = [](uint32_t L) { return L == 2u || L == 3u || L == 8u || L == 9u || L == 32u || L == 33u; };
 
-  if (ABL != 0 || a.ctr->odd != 0) {
+  if (!(ABL & 131072) || a.ctr->odd != 0) {
     generic(q_begin, q_end);
   } else {
     // Segments of the wave's groups: a run of one specialized L, or a run of
@@ -1214,33 +1218,25 @@ struct SmallPk {
   }
 };
 
-// Chunks of 64 small-pool packets are taken dynamically (ctr->small_next):
-// two launches share the pool -- one on a few CUs beside the fold on a side
-// stream, one after the fold on every CU that finds what is left (nothing,
-// on C4, whose one-line packets are 2 % of its bytes).
 __global__ __launch_bounds__(kBlock) void icrc_rsmall_kernel(RsckArgs a) {
   __shared__ uint32_t lds[kLdsWords];
   const uint32_t count = a.ctr->small;
-  if ((uint32_t)__builtin_amdgcn_readfirstlane(*(volatile uint32_t *)&a.ctr->small_next) >= count) return;  // nothing left
+  if (count == 0) return;  // no one-line packets (wave-uniform): no table build either
   const uint32_t tab_v = table_entry(g_tab);
   table_store(lds, tab_v);
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const LaneTab lt{(lane & 31) << 2, ((lane & 31) << 2) | 0x10000u};
+  const uint32_t step = gridDim.x * kWaves * 64u;
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.res, 4u * count);
   auto desc_at = [&](uint32_t pos) -> RsDesc { return a.desc[pos < count ? pos : (count ? count - 1u : 0u)]; };
-  auto take = [&]() -> uint32_t {  // the wave's next chunk (wave-uniform)
-    uint32_t c = 0;
-    if (lane == 0) c = atomicAdd(&a.ctr->small_next, 64u);
-    return __builtin_amdgcn_readfirstlane(c);
-  };
-  uint32_t base = take();
-  uint32_t next = base < count ? take() : count;
+  uint32_t base = (blockIdx.x * kWaves + wid) * 64u;
   RsDesc dn = desc_at(base + lane);
-  for (; base < count; base = next, next = next < count ? take() : count) {
+  for (; base < count; base += step) {
     const uint32_t pos = base + lane;
     const RsDesc d = dn;
-    dn = desc_at(next + lane);  // the next chunk's descriptor, in flight meanwhile
+    dn = desc_at(pos + step);  // the next round's descriptor, in flight meanwhile
     uint32_t K = (((d.hi >> 16) - 4u) + 4u + 15u) >> 4;  // this lane's blocks
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) K = max(K, (uint32_t)__shfl_xor((int)K, o));
@@ -1363,8 +1359,7 @@ static void launch_bucket(const RsckArgs &a, int pgrid, hipStream_t st) {
   else launch_bucket_u<kPassUnroll>(a, pgrid, st);
 }
 
-hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, hipStream_t st, hipStream_t side, hipEvent_t ev_bucket,
-                       hipEvent_t ev_side, int side_grid, hipEvent_t *pass_ev) {
+hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, hipStream_t st, hipEvent_t *pass_ev) {
   (void)hipGetLastError();  // a stale error of an earlier, unrelated HIP call must not fail this launch
   if (a.count == 0) return hipSuccess;
   if (a.count > kRsMaxCount) return hipErrorInvalidValue;
@@ -1379,23 +1374,13 @@ hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, hipStream_t st, hipS
   mark(0);
   launch_bucket(a, pgrid, st);
   mark(1);
-  const bool beside = side && ev_bucket && ev_side && side_grid > 0 && side_grid < grid;
-  if (beside) {  // the one-line kernel on side_grid CUs, beside the fold on the rest
-    hipError_t e = hipEventRecord(ev_bucket, st);
-    if (e == hipSuccess) e = hipStreamWaitEvent(side, ev_bucket, 0);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(icrc_rsmall_kernel, dim3(side_grid), dim3(kBlock), 0, side, a);
-    if ((e = hipEventRecord(ev_side, side)) != hipSuccess) return e;
-  }
-  hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(beside ? grid - side_grid : grid), dim3(kBlock), 0, st, a);
+  hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, st, a);
   mark(2);
-  // the small pool [0, ctr->small): one lane per packet (beside: whatever the
-  // side launch has not taken yet, on every CU)
+  // the small pool [0, ctr->small): one lane per packet.  (Round 4 ran it on
+  // 1/16 of the CUs on a second stream beside the fold instead: the step
+  // took 1.050 against 0.999 ms -- its scattered half-line reads slowed the
+  // fold by 60 us, profiles/r04/s2_*.)
   hipLaunchKernelGGL(icrc_rsmall_kernel, dim3(grid), dim3(kBlock), 0, st, a);
-  if (beside) {
-    const hipError_t e = hipStreamWaitEvent(st, ev_side, 0);  // the gather reads both launches' results
-    if (e != hipSuccess) return e;
-  }
   mark(3);
   // the gather's blocks are the bucket pass's (block b serves pass block b's packets)
   if (pass_big(a, pgrid)) hipLaunchKernelGGL(rsck_gather<kPassUnrollBig>, dim3(pgrid), dim3(kPassBlock), 0, st, a);

@@ -234,6 +234,27 @@ def test_ragged_bucket_layout_lds_or_overflow(ctx, ctx_env, hi):
         np.testing.assert_array_equal(_host_u32(out), want)
 
 
+def test_ragged_bucket_17_per_thread_one_round_unstaged(ctx, ctx_env):
+    """a pass block of 17 packets per thread (more than 16 x 1024
+    packets on one block: RICRC_RS_PASS_GRID=1, 17400 packets) whose packets
+    fit one round (<= 17 x 1024) but whose layout overflows the LDS stage
+    (17920 entries; ~235 line classes of lengths up to 30000 B pad their last
+    groups by ~800) places its packets from the registers, and the gather
+    takes its unstaged path."""
+    rng = np.random.default_rng(17000)
+    count = 17400
+    lens = rng.integers(44, 30001, size=count).astype(np.uint32)
+    offs = np.zeros(count, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + 5, dtype=np.uint64)
+    buf = rng.integers(0, 256, size=int(offs[-1] + lens[-1]) + 64, dtype=np.uint8)
+    want = oracle_c.icrc_batch(buf, offsets=offs, lengths=lens, threads=16)
+    d_buf, d_offs, d_lens = _dev(buf), _dev(offs), _dev(lens)
+    for c in (ctx_env(RICRC_RS_PASS_GRID=1), ctx):
+        out = _out(count)
+        c.batch_device(d_buf, count, out, offsets=d_offs, lengths=d_lens, stream=_stream())
+        np.testing.assert_array_equal(_host_u32(out), want)
+
+
 def test_ragged_kernel_offsets_only_and_lengths_only(ctx):
     """Descriptor modes: offsets with a fixed length (stride - l3_offset), and
     per-packet lengths at a fixed stride."""

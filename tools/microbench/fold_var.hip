@@ -65,26 +65,24 @@ int main() {
     for (uint64_t i = 0; i < npos; ++i) bad += got[i] != ref[i];
     printf("  %-28s results %s (%llu differ)\n", nm, bad ? "DIFFER" : "match", (unsigned long long)bad);
   };
-  // reference: the generic fold (ABL 65536: any ABL bit takes the generic
-  // path, this one changes nothing else)
-  hipLaunchKernelGGL((icrc_rsck_kernel<65536>), dim3(grid), dim3(kBlock), 0, 0, a);
+  // reference: the generic fold (the product)
+  hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, 0, a);
   CK(hipDeviceSynchronize());
   CK(hipMemcpy(ref.data(), a.res, 4 * npos, hipMemcpyDeviceToHost));
   printf("%.2f GiB in %llu packets\n", bytes / 1073741824.0, (unsigned long long)count);
   CK(hipMemset(a.res, 0, 4 * npos));
-  hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, 0, a);
-  check("specialized fold (product) vs generic");
+  hipLaunchKernelGGL((icrc_rsck_kernel<131072>), dim3(grid), dim3(kBlock), 0, 0, a);
+  check("specialized fold vs generic");
   // (Round-3 variants, measured on this harness and since removed from the
   // kernel: the round-2 fold 952-955 us; one-compare edge test 949-952;
   // + blocks of D quiet steps, D = 8 (spills) 945-949; D = 6 929-933 (kept);
   // a per-step quiet / full branch 1114-1120; D = 6 alone 954.)
-  // Round 4: the fold specialized on the line count (product) against the
-  // generic fold, alternating, same process; and both on 240 CUs (the grid
-  // the product uses beside the one-line kernel).
+  // Round 4: the fold specialized on the line count (ABL 131072) against the
+  // generic fold (product), alternating, same process.  Session r4s2 (then
+  // the specialized fold was the product): 921.5 / 918.5 us, 921.7 / 919.8.
   for (int r = 0; r < 3; ++r) {
-    printf("fold specialized (product) %8.1f us\n", 1e3f * timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10));
-    printf("fold generic (round 3)     %8.1f us\n", 1e3f * timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<65536>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10));
-    printf("fold specialized, %d CUs   %8.1f us\n", grid - grid / 16, 1e3f * timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid - grid / 16), dim3(kBlock), 0, 0, a); }, 10));
+    printf("fold generic (product)     %8.1f us\n", 1e3f * timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10));
+    printf("fold specialized           %8.1f us\n", 1e3f * timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<131072>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10));
   }
   return 0;
 }
