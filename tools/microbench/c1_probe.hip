@@ -146,6 +146,17 @@ int main() {
     printf("  quad R1 F1    %7.2f us\n", timeit([&] { hipLaunchKernelGGL((icrc_quad_kernel<0, 1, 1>), dim3(cu), dim3(kBlock), 0, 0, q); }));
     printf("  quad R4 F2    %7.2f us\n", timeit([&] { hipLaunchKernelGGL((icrc_quad_kernel<0, 4, 2>), dim3(cu), dim3(kBlock), 0, 0, q); }));
   }
+  // Round 4, the one launch-trim A/B: the product launch
+  // against fewer, fatter workgroups (half the grid: 8 steps per wave, half
+  // the table fills and dispatches) and against two 512-thread workgroups
+  // per CU (a CU starts folding after half the table fill), alternating.
+  printf("launch-trim A/B\n");
+  for (int r = 0; r < 5; ++r) {
+    const float t0 = timeit([&] { CK(launch_quad(q, cu, 0)); });
+    const float t1 = timeit([&] { hipLaunchKernelGGL((icrc_quad_kernel<0, 2, 2, 16, true>), dim3(cu / 2), dim3(kBlock), 0, 0, q); });
+    const float t2 = timeit([&] { hipLaunchKernelGGL((icrc_quad_kernel<0, 2, 2, 8, true>), dim3(2 * cu), dim3(512), 0, 0, q); });
+    printf("  product %d x 1024 %6.2f us | %d x 1024 %6.2f us | %d x 512 %6.2f us\n", cu, t0, cu / 2, t1, 2 * cu, t2);
+  }
   for (int m : {1, 2, 3}) {
     std::vector<uint64_t> st(2 * 16 * cu);
     QuadArgs qs = q;
