@@ -15,6 +15,16 @@
 using namespace ricrc;
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s line %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 
+template <typename F> float timeit(F launch, int reps) {
+  hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  for (int w = 0; w < 3; ++w) launch();
+  CK(hipDeviceSynchronize()); CK(hipEventRecord(e0));
+  for (int i = 0; i < reps; ++i) launch();
+  CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+  CK(hipEventDestroy(e0)); CK(hipEventDestroy(e1));
+  return 1e3f * ms / reps;
+}
+
 struct Cfg {
   const char *name;
   std::vector<uint32_t> sizes;  // drawn uniformly per packet
@@ -85,6 +95,28 @@ int main() {
            (unsigned long long)c.count, pos / 1e9, tot, alg / tot / 1e6, alg / tot / 8e6);
     for (int k = 0; k < 4; ++k) printf(" %s %6.1f", pass[k], sum[k]);
     printf(" | fold %.2f TB/s of its packets' bytes\n", fold_bytes ? fold_bytes / sum[1] / 1e6 : 0.0);
+    // The fold alone after one bucket pass (it leaves the counters as they
+    // are; the gather would zero them), by variant: the product, the fold
+    // specialized on the line count, the memory path (no table fold, no
+    // finish), no finish, and the compute alone (no line loads).
+    const uint64_t want = (c.count + kPassBlock - 1) / kPassBlock;
+    a.nblk = (uint32_t)(want < kPassBlocks ? want : kPassBlocks);
+    launch_bucket(a, (int)a.nblk, 0);
+    CK(hipDeviceSynchronize());
+    if (fold_bytes) {
+      for (int r = 0; r < 2; ++r) {
+        const float f0 = timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10);
+        const float f1 = timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<131072>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10);
+        const float f2 = timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<3>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10);
+        const float f3 = timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<2>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10);
+        const float f4 = timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<16384>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10);
+        printf("    fold alone: product %6.1f | specialized %6.1f | memory path %6.1f | no finish %6.1f | "
+               "compute, no loads %6.1f us\n", f0, f1, f2, f3, f4);
+      }
+    }
+    // the next configuration's bucket pass starts from zeroed counters
+    CK(rs_zero_counters(ws, 0));
+    CK(hipDeviceSynchronize());
   }
   return 0;
 }
