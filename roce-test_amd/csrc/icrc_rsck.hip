@@ -1218,6 +1218,14 @@ struct SmallPk {
   }
 };
 
+constexpr int kSmallRounds = 2;  // icrc_rsmall_kernel's rounds per batch (below)
+
+// R rounds of 64 packets per wave are taken together: when every one of
+// them is a wave of half-line packets (C4's 64-byte packets), all R rounds'
+// coalesced loads are issued before the first is folded, so a wave waits on
+// memory once per R rounds instead of once per round (1 M packets fill 4
+// rounds of 256 CUs x 16 waves).  Other waves fold their R rounds one by one.
+template <int R>
 __global__ __launch_bounds__(kBlock) void icrc_rsmall_kernel(RsckArgs a) {
   __shared__ uint32_t lds[kLdsWords];
   const uint32_t count = a.ctr->small;
@@ -1232,23 +1240,34 @@ __global__ __launch_bounds__(kBlock) void icrc_rsmall_kernel(RsckArgs a) {
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.res, 4u * count);
   auto desc_at = [&](uint32_t pos) -> RsDesc { return a.desc[pos < count ? pos : (count ? count - 1u : 0u)]; };
   uint32_t base = (blockIdx.x * kWaves + wid) * 64u;
-  RsDesc dn = desc_at(base + lane);
-  for (; base < count; base += step) {
-    const uint32_t pos = base + lane;
-    const RsDesc d = dn;
-    dn = desc_at(pos + step);  // the next round's descriptor, in flight meanwhile
+  RsDesc dn[R];
+  static_for<R>([&](auto rc) { dn[decltype(rc)::value] = desc_at(base + decltype(rc)::value * step + lane); });
+  // one round's wave-uniform shape
+  struct Round {
+    RsDesc d;
+    uint32_t Kmax;
+    bool wa, uk, halfw;
+    uint64_t hb;  // the lane's half line (halfw)
+  };
+  auto shape = [&](const RsDesc &d) __attribute__((always_inline)) -> Round {
+    Round o;
+    o.d = d;
     uint32_t K = (((d.hi >> 16) - 4u) + 4u + 15u) >> 4;  // this lane's blocks
+    // the wave's largest, rounded up to a multiple of 4: by ballots for
+    // one-line packets (K <= 8), a shuffle reduction beyond
+    if (__builtin_amdgcn_ballot_w64(K > 4u) == 0) {
+      o.Kmax = 4u;
+    } else if (__builtin_amdgcn_ballot_w64(K > 8u) == 0) {
+      o.Kmax = 8u;
+    } else {
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) K = max(K, (uint32_t)__shfl_xor((int)K, o));
-    const uint32_t Kmax = __builtin_amdgcn_readfirstlane((K + 3u) & ~3u);
-    SmallPk P;
-    P.init(d, Kmax);
-    // Kmax = 16 q + r (r a multiple of 4): one chunk of r blocks, then q of
-    // 16 (wave-uniform choices; at most 17 units = 68 VGPRs in flight).
+      for (int w = 32; w >= 1; w >>= 1) K = max(K, (uint32_t)__shfl_xor((int)K, w));
+      o.Kmax = __builtin_amdgcn_readfirstlane((K + 3u) & ~3u);
+    }
     // wave-uniform variants: word-aligned packets; every packet Kmax blocks long
-    const bool wa = __builtin_amdgcn_ballot_w64(((d.lo | (d.hi >> 16)) & 3u) != 0) == 0;
+    o.wa = __builtin_amdgcn_ballot_w64(((d.lo | (d.hi >> 16)) & 3u) != 0) == 0;
     // heads in blocks 0..3: rel_4 = M - 16 Kmax + 64 >= 40 for every lane
-    const bool uk = __builtin_amdgcn_ballot_w64((d.hi >> 16) - 4u + 24u < 16u * Kmax) == 0;
+    o.uk = __builtin_amdgcn_ballot_w64((d.hi >> 16) - 4u + 24u < 16u * o.Kmax) == 0;
     // Half-line packets: every covered byte in one aligned 64-byte half
     // line hb .. hb + 63 whose last 16-byte unit holds the covered end, not
     // at the half line's end (C4's 64-byte packets: 64-byte aligned, 60
@@ -1261,49 +1280,103 @@ __global__ __launch_bounds__(kBlock) void icrc_rsmall_kernel(RsckArgs a) {
     // quad kernel in icrc_kernels.hip).
     const uint64_t pa = ((uint64_t)(d.hi & 0xFFFFu) << 32) | d.lo;
     const uint64_t pe = pa + ((d.hi >> 16) - 4u);
-    const uint64_t hb = (pe - 1u) & ~63ull;
-    const bool half = pa >= hb && ((uint32_t)pe & 63u) > 48u;
-    const bool halfw = Kmax == 4u && __builtin_amdgcn_ballot_w64(!half) == 0;
-    auto half_line_units = [&](u32x4 (&U)[5]) {
-      const uint32_t hlo = (uint32_t)hb, hhi = (uint32_t)(hb >> 32), q = lane & 3u;
+    o.hb = (pe - 1u) & ~63ull;
+    const bool half = pa >= o.hb && ((uint32_t)pe & 63u) > 48u;
+    o.halfw = o.Kmax == 4u && __builtin_amdgcn_ballot_w64(!half) == 0;
+    return o;
+  };
+  auto half_line_load = [&](const Round &o, u32x4 (&H)[4]) __attribute__((always_inline)) {
+    const uint32_t hlo = (uint32_t)o.hb, hhi = (uint32_t)(o.hb >> 32), q = lane & 3u;
+    auto at = [&](uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32 | lo) + 16u * q; };
+    H[0] = gload16(at(dpp_quad_bcast<0>(hlo), dpp_quad_bcast<0>(hhi)));
+    H[1] = gload16(at(dpp_quad_bcast<1>(hlo), dpp_quad_bcast<1>(hhi)));
+    H[2] = gload16(at(dpp_quad_bcast<2>(hlo), dpp_quad_bcast<2>(hhi)));
+    H[3] = gload16(at(dpp_quad_bcast<3>(hlo), dpp_quad_bcast<3>(hhi)));
+  };
+  // fold a half-line round from its loaded units
+  auto half_line_fold = [&](const Round &o, u32x4 (&H)[4], uint32_t pos, auto words,
+                            auto uniform) __attribute__((always_inline)) {
+    constexpr bool WA = decltype(words)::value;
+    constexpr int M1 = decltype(uniform)::value ? 1 : 2;
+    quad_transpose(H, lane & 3u);
+    const u32x4 U[5] = {H[0], H[0], H[1], H[2], H[3]};
+    SmallPk P;
+    P.init(o.d, 4u);
+    P.blocks<4, WA, M1>(lds, lt, U);
+    __builtin_amdgcn_raw_buffer_store_b32(~P.reg, ro, pos < count ? 4u * pos : 0x7FFFFFF0u, 0, 0);
+  };
+  // any round, its loads issued and folded here
+  auto one_round = [&](const Round &o, uint32_t pos) __attribute__((always_inline)) {
+    if (o.halfw) {  // wave-uniform
       u32x4 H[4];
-      auto at = [&](uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32 | lo) + 16u * q; };
-      H[0] = gload16(at(dpp_quad_bcast<0>(hlo), dpp_quad_bcast<0>(hhi)));
-      H[1] = gload16(at(dpp_quad_bcast<1>(hlo), dpp_quad_bcast<1>(hhi)));
-      H[2] = gload16(at(dpp_quad_bcast<2>(hlo), dpp_quad_bcast<2>(hhi)));
-      H[3] = gload16(at(dpp_quad_bcast<3>(hlo), dpp_quad_bcast<3>(hhi)));
-      quad_transpose(H, q);
-      U[0] = H[0];
-      U[1] = H[0];
-      U[2] = H[1];
-      U[3] = H[2];
-      U[4] = H[3];
-    };
-    auto run = [&](auto words, auto uniform) {
+      half_line_load(o, H);
+      if (o.wa && o.uk)
+        half_line_fold(o, H, pos, std::true_type{}, std::true_type{});
+      else if (o.uk)
+        half_line_fold(o, H, pos, std::false_type{}, std::true_type{});
+      else
+        half_line_fold(o, H, pos, std::false_type{}, std::false_type{});
+      return;
+    }
+    SmallPk P;
+    P.init(o.d, o.Kmax);
+    auto run = [&](auto words, auto uniform) __attribute__((always_inline)) {
       constexpr bool WA = decltype(words)::value;
       constexpr int M1 = decltype(uniform)::value ? 1 : 2, M2 = decltype(uniform)::value ? 0 : 2;
-      if (halfw) {  // wave-uniform
-        u32x4 U[5];
-        half_line_units(U);
-        P.blocks<4, WA, M1>(lds, lt, U);
-        return;
-      }
+      // Kmax = 8 q + r (r = 0 or 4): a first chunk of r or 8 blocks, then
+      // chunks of 8 (one-line packets: M <= 124, Kmax <= 8 -- one chunk, at
+      // most 9 units = 36 VGPRs in flight; longer chunks spilled once two
+      // rounds' descriptors are live)
       uint32_t j = 0;
-      switch (Kmax & 15u) {
-        case 4: P.chunk<4, WA, M1>(lds, lt, 0); j = 4; break;
-        case 8: P.chunk<8, WA, M1>(lds, lt, 0); j = 8; break;
-        case 12: P.chunk<12, WA, M1>(lds, lt, 0); j = 12; break;
-        default: P.chunk<16, WA, M1>(lds, lt, 0); j = 16; break;
+      if ((o.Kmax & 7u) == 4u) {  // wave-uniform
+        P.chunk<4, WA, M1>(lds, lt, 0);
+        j = 4;
+      } else {
+        P.chunk<8, WA, M1>(lds, lt, 0);
+        j = 8;
       }
-      for (; j < Kmax; j += 16) P.chunk<16, WA, M2>(lds, lt, j);
+      for (; j < o.Kmax; j += 8) P.chunk<8, WA, M2>(lds, lt, j);
     };
-    if (wa && uk)
+    if (o.wa && o.uk)
       run(std::true_type{}, std::true_type{});
-    else if (uk)
+    else if (o.uk)
       run(std::false_type{}, std::true_type{});
     else
       run(std::false_type{}, std::false_type{});
     __builtin_amdgcn_raw_buffer_store_b32(~P.reg, ro, pos < count ? 4u * pos : 0x7FFFFFF0u, 0, 0);
+  };
+  for (; base < count; base += R * step) {
+    RsDesc d[R];
+    Round o[R];
+    bool all_half = true;
+    static_for<R>([&](auto rc) {
+      constexpr int r = decltype(rc)::value;
+      d[r] = dn[r];
+      dn[r] = desc_at(base + (R + r) * step + lane);  // the next iteration's descriptors, in flight meanwhile
+      if (R > 1) {
+        o[r] = shape(d[r]);
+        all_half = all_half & o[r].halfw & o[r].wa & o[r].uk;
+      }
+    });
+    // wave-uniform: rounds of word-aligned half-line packets (C4's 64-byte
+    // packets; one fold variant, no branch between the rounds' folds, so the
+    // compiler cannot sink a round's loads to its fold)
+    if (R > 1 && all_half) {
+      u32x4 H[R][4];
+      static_for<R>([&](auto rc) { half_line_load(o[decltype(rc)::value], H[decltype(rc)::value]); });
+      __builtin_amdgcn_sched_barrier(0);
+      static_for<R>([&](auto rc) {
+        constexpr int r = decltype(rc)::value;
+        half_line_fold(o[r], H[r], base + r * step + lane, std::true_type{}, std::true_type{});
+      });
+    } else {
+      // (only the descriptors stay live across a round: the shape is
+      // recomputed, so a 16-block chunk's units do not spill the others)
+      static_for<R>([&](auto rc) {
+        constexpr int r = decltype(rc)::value;
+        if (base + r * step < count) one_round(shape(d[r]), base + r * step + lane);  // wave-uniform
+      });
+    }
   }
 }
 
@@ -1380,7 +1453,7 @@ hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, hipStream_t st, hipE
   // 1/16 of the CUs on a second stream beside the fold instead: the step
   // took 1.050 against 0.999 ms -- its scattered half-line reads slowed the
   // fold by 60 us, profiles/r04/s2_*.)
-  hipLaunchKernelGGL(icrc_rsmall_kernel, dim3(grid), dim3(kBlock), 0, st, a);
+  hipLaunchKernelGGL((icrc_rsmall_kernel<kSmallRounds>), dim3(grid), dim3(kBlock), 0, st, a);
   mark(3);
   // the gather's blocks are the bucket pass's (block b serves pass block b's packets)
   if (pass_big(a, pgrid)) hipLaunchKernelGGL(rsck_gather<kPassUnrollBig>, dim3(pgrid), dim3(kPassBlock), 0, st, a);

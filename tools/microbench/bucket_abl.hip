@@ -165,7 +165,7 @@ int main(int argc, char **argv) {
     rep("fold, no edge masks", timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<8>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10));
     rep("fold, no finish", timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<2>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10));
     rep("fold, memory path, no edges, no stores", timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<3 | 8 | 16>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10));
-    rep("one-line (icrc_rsmall_kernel)", timeit([&] { hipLaunchKernelGGL(icrc_rsmall_kernel, dim3(grid), dim3(kBlock), 0, 0, a); }, 20));
+    rep("one-line (icrc_rsmall_kernel)", timeit([&] { hipLaunchKernelGGL((icrc_rsmall_kernel<kSmallRounds>), dim3(grid), dim3(kBlock), 0, 0, a); }, 20));
     {  // the gather zeroes the counters: restore them before each timed launch
       RsCounters *saved; CK(hipMalloc(&saved, sizeof(RsCounters)));
       CK(hipMemcpy(saved, a.ctr, sizeof(RsCounters), hipMemcpyDeviceToDevice));

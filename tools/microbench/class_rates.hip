@@ -114,6 +114,16 @@ int main() {
                "compute, no loads %6.1f us\n", f0, f1, f2, f3, f4);
       }
     }
+    // the one-line kernel alone by rounds batched per wave (R = 1: one
+    // round at a time; the product runs kSmallRounds)
+    if (fold_bytes != pos) {
+      for (int r = 0; r < 3; ++r) {
+        const float s1 = timeit([&] { hipLaunchKernelGGL((icrc_rsmall_kernel<1>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10);
+        const float s2 = timeit([&] { hipLaunchKernelGGL((icrc_rsmall_kernel<2>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10);
+        const float s4 = timeit([&] { hipLaunchKernelGGL((icrc_rsmall_kernel<4>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10);
+        printf("    one-line alone: R = 1 %6.1f | R = 2 %6.1f | R = 4 %6.1f us\n", s1, s2, s4);
+      }
+    }
     // the next configuration's bucket pass starts from zeroed counters
     CK(rs_zero_counters(ws, 0));
     CK(hipDeviceSynchronize());

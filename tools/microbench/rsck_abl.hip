@@ -81,7 +81,7 @@ int main(int argc, char **argv) {
         rep(nm, timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<7>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10), b);
       }
       snprintf(nm, sizeof nm, "%s small kernel", tag);
-      rep(nm, timeit([&] { hipLaunchKernelGGL(icrc_rsmall_kernel, dim3(grid), dim3(kBlock), 0, 0, a); }, 10), b);
+      rep(nm, timeit([&] { hipLaunchKernelGGL((icrc_rsmall_kernel<kSmallRounds>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10), b);
     }
     if (d_off) {  // the bench's order: passes, fold, small, gather per step; fold timed inside
       hipEvent_t f0, f1; CK(hipEventCreate(&f0)); CK(hipEventCreate(&f1));
@@ -95,7 +95,7 @@ int main(int argc, char **argv) {
           CK(hipEventRecord(f0, 0));
           hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, 0, a);
           CK(hipEventRecord(f1, 0));
-          hipLaunchKernelGGL(icrc_rsmall_kernel, dim3(grid), dim3(kBlock), 0, 0, a);
+          hipLaunchKernelGGL((icrc_rsmall_kernel<kSmallRounds>), dim3(grid), dim3(kBlock), 0, 0, a);
           hipLaunchKernelGGL(rsck_gather<kPassUnroll>, dim3(pgrid), dim3(kPassBlock), 0, 0, a);
           CK(hipEventSynchronize(f1));
           float ms; CK(hipEventElapsedTime(&ms, f0, f1));
