@@ -1218,7 +1218,7 @@ struct SmallPk {
   }
 };
 
-constexpr int kSmallRounds = 2;  // icrc_rsmall_kernel's rounds per batch (below)
+constexpr int kSmallRounds = 1;  // icrc_rsmall_kernel's rounds per batch (below; 2 measured slower: profiles/r04/s6_*)
 
 // R rounds of 64 packets per wave are taken together: when every one of
 // them is a wave of half-line packets (C4's 64-byte packets), all R rounds'

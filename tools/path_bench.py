@@ -61,11 +61,54 @@ def time_device(torch, ctx, fn, reps, warm):
     return sum(a.elapsed_time(b) for a, b in evs) / reps
 
 
+def ring_bench(args, np, ctx, oracle_c):
+    # -- Ethernet-framed NIC ring through the status route -----------------
+    # 4 KiB slots: 12 bytes of MACs, EtherType 0x0800, then a RoCEv2 packet of
+    # 64..4096-14 B (a quarter carry 2 bytes of padding + a 4-byte FCS inside
+    # the descriptor length: RICRC_F_FRAMELEN takes the IP length).
+    import icrc_oracle as O
+
+    slot, l3 = 4096, 14
+    ring_n = (1 << 18) if args.quick else (1 << 20)
+    sizes = np.random.default_rng(5).choice(np.array([64, 256, 1024, slot - l3 - 6], np.uint32), size=ring_n)
+    extra = np.where(np.random.default_rng(6).random(ring_n) < 0.25, 6, 0).astype(np.uint32)
+    ring = np.zeros(ring_n * slot, np.uint8)
+    tmpl = {n: oracle_c.synth_batch(SEED, 0, 4096, int(n)) for n in np.unique(sizes)}
+    for n in np.unique(sizes):
+        idx = np.flatnonzero(sizes == n)
+        rows = ring.reshape(ring_n, slot)
+        rows[idx, 12] = 0x08
+        rows[idx, l3:l3 + n] = tmpl[n][np.arange(len(idx)) % 4096]
+    descr = sizes + extra
+    offs = np.arange(ring_n, dtype=np.uint64) * slot
+    ns = 4096
+    w_out, w_st = O.status_batch(ring[: ns * slot], offsets=offs[:ns], lengths=descr[:ns], l3_offset=l3,
+                                 strict=True, framelen=True)
+    for label, kw in (("strict", dict(strict=True)), ("strict+framelen", dict(strict=True, framelen=True))):
+        if "framelen" not in kw:  # the descriptor lengths are the datagrams' here
+            lens_k = sizes
+        else:
+            lens_k = descr
+        got, st = ctx.batch_host_st(ring, offs, lens_k, l3_offset=l3, **kw)  # warm
+        if "framelen" in kw and not (np.array_equal(st[:ns], w_st) and np.array_equal(got[:ns], w_out)):
+            raise SystemExit("host ring status route: mismatch against the oracle")
+        if (st != 0).any():
+            raise SystemExit(f"host ring {label}: {int((st != 0).sum())} packets rejected")
+        t0 = time.perf_counter()
+        for _ in range(3):
+            ctx.batch_host_st(ring, offs, lens_k, l3_offset=l3, **kw)
+        dt = (time.perf_counter() - t0) / 3
+        nb = int(sizes.sum(dtype=np.uint64))
+        emit(path="host", input=f"Ethernet NIC ring, 4 KiB slots, ricrc_batch_host_st {label}", packets=ring_n,
+             bytes=nb, ring_bytes=ring.size, ms=round(dt * 1e3, 2), gib_s=round(nb / dt / 2**30, 2))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--skip-host", action="store_true")
     ap.add_argument("--only-ragged", action="store_true", help="only the C4 ragged device measurement")
+    ap.add_argument("--only-ring", action="store_true", help="only the Ethernet-framed NIC ring (status route)")
     ap.add_argument("--ragged-paths", default="rsck", help="which ragged paths to time (rsck)")
     args = ap.parse_args()
     import numpy as np
@@ -75,6 +118,10 @@ def main():
     import roce_icrc
 
     ctx = roce_icrc.Context(devices=[0])
+    if args.only_ring:
+        ring_bench(args, np, ctx, oracle_c)
+        ctx.close()
+        return
     dev = torch.device("cuda", 0)
     reps, warm = (10, 5) if args.quick else (50, 20)
     total = 1 << 30 if args.quick else 4 << 30
@@ -221,45 +268,7 @@ def main():
     ctx.host_unregister(hb)
     del hb
 
-    # -- Ethernet-framed NIC ring through the status route -----------------
-    # 4 KiB slots: 12 bytes of MACs, EtherType 0x0800, then a RoCEv2 packet of
-    # 64..4096-14 B (a quarter carry 2 bytes of padding + a 4-byte FCS inside
-    # the descriptor length: RICRC_F_FRAMELEN takes the IP length).
-    import icrc_oracle as O
-
-    slot, l3 = 4096, 14
-    ring_n = (1 << 18) if args.quick else (1 << 20)
-    sizes = np.random.default_rng(5).choice(np.array([64, 256, 1024, slot - l3 - 6], np.uint32), size=ring_n)
-    extra = np.where(np.random.default_rng(6).random(ring_n) < 0.25, 6, 0).astype(np.uint32)
-    ring = np.zeros(ring_n * slot, np.uint8)
-    tmpl = {n: oracle_c.synth_batch(SEED, 0, 4096, int(n)) for n in np.unique(sizes)}
-    for n in np.unique(sizes):
-        idx = np.flatnonzero(sizes == n)
-        rows = ring.reshape(ring_n, slot)
-        rows[idx, 12] = 0x08
-        rows[idx, l3:l3 + n] = tmpl[n][np.arange(len(idx)) % 4096]
-    descr = sizes + extra
-    offs = np.arange(ring_n, dtype=np.uint64) * slot
-    ns = 4096
-    w_out, w_st = O.status_batch(ring[: ns * slot], offsets=offs[:ns], lengths=descr[:ns], l3_offset=l3,
-                                 strict=True, framelen=True)
-    for label, kw in (("strict", dict(strict=True)), ("strict+framelen", dict(strict=True, framelen=True))):
-        if "framelen" not in kw:  # the descriptor lengths are the datagrams' here
-            lens_k = sizes
-        else:
-            lens_k = descr
-        got, st = ctx.batch_host_st(ring, offs, lens_k, l3_offset=l3, **kw)  # warm
-        if "framelen" in kw and not (np.array_equal(st[:ns], w_st) and np.array_equal(got[:ns], w_out)):
-            raise SystemExit("host ring status route: mismatch against the oracle")
-        if (st != 0).any():
-            raise SystemExit(f"host ring {label}: {int((st != 0).sum())} packets rejected")
-        t0 = time.perf_counter()
-        for _ in range(3):
-            ctx.batch_host_st(ring, offs, lens_k, l3_offset=l3, **kw)
-        dt = (time.perf_counter() - t0) / 3
-        nb = int(sizes.sum(dtype=np.uint64))
-        emit(path="host", input=f"Ethernet NIC ring, 4 KiB slots, ricrc_batch_host_st {label}", packets=ring_n,
-             bytes=nb, ring_bytes=ring.size, ms=round(dt * 1e3, 2), gib_s=round(nb / dt / 2**30, 2))
+    ring_bench(args, np, ctx, oracle_c)
     ctx.close()
 
 
