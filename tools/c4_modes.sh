@@ -10,17 +10,5 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/${TAG:-c4_modes}; mkdir -p $O
 for r in $(seq 1 ${RUNS:-6}); do
   timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-cpu --mix --pass-times ${ARGS:-} > $O/run_$r.json 2> $O/run_$r.err || exit 3
-  python3 - "$O/run_$r.json" <<'PY'
-import json, sys
-d = json.load(open(sys.argv[1]))
-def clocks(st):
-    if not isinstance(st, dict):
-        return st
-    s = json.dumps(st["data"])
-    import re
-    nums = re.findall(r'"(gfx_?\d*|sclk|mclk|fclk|socclk|uclk|power|average_socket_power|socket_power|temperature_\w+|hotspot|edge)"\s*:\s*\{?\s*"?(?:value"?\s*:\s*)?"?([0-9.]+)', s, re.I)
-    return nums[:12]
-print(f"ms/step {d['ms_per_step']:.4f} kernel {d['roofline']['kernel_ms']:.4f} passes {d.get('pass_ms')} "
-      f"calls {d.get('pass_calls')} | before {clocks(d.get('gpu_state_before'))} | after {clocks(d.get('gpu_state_after'))}")
-PY
+  python3 tools/c4_modes_summary.py "$O/run_$r.json"
 done

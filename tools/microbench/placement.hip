@@ -1,0 +1,85 @@
+// C4's per-process spread, inside one process: the ragged
+// pipeline on FOUR copies of the same C4-shaped batch (4 M packets, 64/256/
+// 1024/4096 B, back to back) in four separate 5.7 GB allocations, each with
+// its own workspace, alternating copy by copy for several rounds -- and every
+// batch with the first copy's workspace.  If a copy's time stays apart from
+// the others' round after round, the physical placement of the batch (or of
+// the workspace) is what differs between bench processes; if all copies read
+// the same, placement is ruled out within a process.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 placement.hip -o placement
+#include "../../roce-test_amd/csrc/icrc_kernels.hip"
+#include "../../roce-test_amd/csrc/icrc_rsck.hip"
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <vector>
+using namespace ricrc;
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s line %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
+
+int main() {
+  hipDeviceProp_t p; CK(hipGetDeviceProperties(&p, 0));
+  const int grid = p.multiProcessorCount;
+  const uint64_t count = 4ull << 20;
+  std::vector<uint64_t> off(count);
+  std::vector<uint32_t> len(count);
+  uint64_t x = 0x1CEC0DEull, pos = 0;
+  const uint32_t sizes[4] = {64, 256, 1024, 4096};
+  for (uint64_t i = 0; i < count; ++i) {
+    x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+    len[i] = sizes[(x >> 33) & 3];
+    off[i] = pos;
+    pos += len[i];
+  }
+  const uint64_t bytes = pos;
+  constexpr int kCopies = 4;
+  uint8_t *buf[kCopies];
+  void *ws[kCopies];
+  uint64_t *d_off; uint32_t *d_len, *out, *tzb;
+  {
+    std::vector<uint64_t> h((bytes + 7) / 8);
+    for (auto &v : h) { x ^= x << 13; x ^= x >> 7; x ^= x << 17; v = x; }
+    for (int c = 0; c < kCopies; ++c) {
+      CK(hipMalloc(&buf[c], bytes + 4096));
+      CK(hipMemcpy(buf[c], h.data(), bytes, hipMemcpyHostToDevice));
+      CK(hipMalloc(&ws[c], rs_workspace_bytes(count)));
+      CK(rs_zero_counters(ws[c], 0));
+    }
+  }
+  CK(hipMalloc(&d_off, 8 * count)); CK(hipMalloc(&d_len, 4 * count)); CK(hipMalloc(&out, 4 * count));
+  CK(hipMemcpy(d_off, off.data(), 8 * count, hipMemcpyHostToDevice));
+  CK(hipMemcpy(d_len, len.data(), 4 * count, hipMemcpyHostToDevice));
+  CK(hipMalloc(&tzb, 4 * 1024)); CK(hipMemset(tzb, 0x35, 4 * 1024));
+  hipEvent_t ev[5];
+  for (auto &evk : ev) CK(hipEventCreate(&evk));
+  auto run = [&](int c, int w, int reps, double (&sum)[4]) {
+    RsckArgs a{};
+    a.base = buf[c]; a.off = d_off; a.len = d_len; a.count = count;
+    a.out = out; a.tzb = tzb; a.group_cost = kRsGroupCost;
+    for (int j = 0; j < 32; ++j) { a.XB[j] = 0x85EBCA6Bu * (j + 3); a.XB2[j] = 0x27D4EB2Fu * (j + 5); a.XB3[j] = 0x165667B1u * (j + 7); }
+    for (int s = 0; s < 8; ++s) a.QS[s] = 0x9E3779B9u * (s + 1);
+    rs_bind_workspace(a, ws[w]);
+    for (int k = 0; k < 4; ++k) sum[k] = 0;
+    for (int r = 0; r < 3 + reps; ++r) {
+      CK(launch_rsck(a, grid, 0, 0, ev));
+      CK(hipEventSynchronize(ev[4]));
+      if (r < 3) continue;
+      for (int k = 0; k < 4; ++k) {
+        float ms; CK(hipEventElapsedTime(&ms, ev[k], ev[k + 1]));
+        sum[k] += 1e3 * ms / reps;
+      }
+    }
+  };
+  printf("%.2f GiB in %llu packets, %d copies (batch at %p %p %p %p)\n", bytes / 1073741824.0,
+         (unsigned long long)count, kCopies, (void *)buf[0], (void *)buf[1], (void *)buf[2], (void *)buf[3]);
+  for (int round = 0; round < 4; ++round) {
+    for (int c = 0; c < kCopies; ++c) {
+      double own[4], first[4];
+      run(c, c, 10, own);
+      run(c, 0, 10, first);
+      printf("round %d copy %d: own workspace: bucket %5.1f fold %6.1f one-line %5.1f gather %5.1f | "
+             "copy 0's workspace: bucket %5.1f fold %6.1f one-line %5.1f gather %5.1f us\n",
+             round, c, own[0], own[1], own[2], own[3], first[0], first[1], first[2], first[3]);
+    }
+  }
+  return 0;
+}
