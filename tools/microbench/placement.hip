@@ -5,7 +5,12 @@
 // batch with the first copy's workspace.  If a copy's time stays apart from
 // the others' round after round, the physical placement of the batch (or of
 // the workspace) is what differs between bench processes; if all copies read
-// the same, placement is ruled out within a process.
+// the same, placement is ruled out within a process.  Then (round 4, the
+// microbench's fold read 911 us where bench.py's process read 925 by rocprof
+// and 965-993 by its pass events): copy 1 regenerated with the product's
+// synthetic RoCE packets (synth_ragged_kernel, bench.py's data) against the
+// random bytes of copy 0, each timed with a host sync after every step (as
+// above) and as 10 steps back to back (as bench.py runs them).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 placement.hip -o placement
 #include "../../roce-test_amd/csrc/icrc_kernels.hip"
 #include "../../roce-test_amd/csrc/icrc_rsck.hip"
@@ -79,6 +84,43 @@ int main() {
       printf("round %d copy %d: own workspace: bucket %5.1f fold %6.1f one-line %5.1f gather %5.1f | "
              "copy 0's workspace: bucket %5.1f fold %6.1f one-line %5.1f gather %5.1f us\n",
              round, c, own[0], own[1], own[2], own[3], first[0], first[1], first[2], first[3]);
+    }
+  }
+  // Data and cadence.
+  {
+    SynthArgs sa{};
+    sa.buf = buf[1]; sa.seed = 0x1CEC0DEull; sa.first = 0; sa.count = count; sa.off = d_off; sa.len = d_len;
+    CK(launch_synth_ragged(sa, 0));
+    CK(hipDeviceSynchronize());
+  }
+  constexpr int kB2B = 10;
+  std::vector<hipEvent_t> bev(5 * kB2B);
+  for (auto &evk : bev) CK(hipEventCreate(&evk));
+  auto b2b = [&](int c, double (&sum)[4]) {
+    RsckArgs a{};
+    a.base = buf[c]; a.off = d_off; a.len = d_len; a.count = count;
+    a.out = out; a.tzb = tzb; a.group_cost = kRsGroupCost;
+    for (int j = 0; j < 32; ++j) { a.XB[j] = 0x85EBCA6Bu * (j + 3); a.XB2[j] = 0x27D4EB2Fu * (j + 5); a.XB3[j] = 0x165667B1u * (j + 7); }
+    for (int s = 0; s < 8; ++s) a.QS[s] = 0x9E3779B9u * (s + 1);
+    rs_bind_workspace(a, ws[c]);
+    for (int r = 0; r < 3; ++r) CK(launch_rsck(a, grid, 0, 0, nullptr));  // warm, back to back
+    for (int i = 0; i < kB2B; ++i) CK(launch_rsck(a, grid, 0, 0, &bev[5 * i]));
+    CK(hipDeviceSynchronize());
+    for (int k = 0; k < 4; ++k) sum[k] = 0;
+    for (int i = 0; i < kB2B; ++i)
+      for (int k = 0; k < 4; ++k) {
+        float ms; CK(hipEventElapsedTime(&ms, bev[5 * i + k], bev[5 * i + k + 1]));
+        sum[k] += 1e3 * ms / kB2B;
+      }
+  };
+  for (int round = 0; round < 3; ++round) {
+    for (int c = 0; c < 2; ++c) {
+      double sy[4], bb[4];
+      run(c, c, 10, sy);
+      b2b(c, bb);
+      printf("round %d %-22s synced: bucket %5.1f fold %6.1f one-line %5.1f gather %5.1f | back to back: bucket %5.1f "
+             "fold %6.1f one-line %5.1f gather %5.1f us\n", round, c ? "synthetic RoCE packets" : "random bytes",
+             sy[0], sy[1], sy[2], sy[3], bb[0], bb[1], bb[2], bb[3]);
     }
   }
   return 0;
