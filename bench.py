@@ -113,6 +113,8 @@ def parse(argv=None):
     ap.add_argument("--pass-times", action="store_true",
                     help="diagnostics (--mix): HIP events between the ragged pipeline's passes (RICRC_PASS_TIMES; "
                          "a few us per step) -> pass_ms, and the GPU's clocks / power around the timed steps")
+    ap.add_argument("--no-gpu-state", action="store_true",
+                    help="with --pass-times: skip the amd-smi readings around the timed steps")
     ap.add_argument("--plan-only", action="store_true",
                     help="print the shard plan every rank would run (gloo, no GPU) and exit")
     a = ap.parse_args(argv)
@@ -624,7 +626,8 @@ def run(args, world, rank, be, distributed):
     if args.pass_times and hasattr(be, "pass_times"):
         be.sync()
         be.pass_times()  # forget the warmup's calls
-        diag["gpu_state_before"] = gpu_state(be.dev.index)
+        if not args.no_gpu_state:
+            diag["gpu_state_before"] = gpu_state(be.dev.index)
     n_ev = args.steps if args.step_events else 1
     evs = [(be.event(), be.event()) for _ in range(n_ev)]
     be.sync()
@@ -648,7 +651,8 @@ def run(args, world, rank, be, distributed):
     elapsed = time.perf_counter() - t0
     kern_ms = sum(a.elapsed_time(c) for a, c in evs) / max(args.steps, 1)
     if args.pass_times and hasattr(be, "pass_times"):
-        diag["gpu_state_after"] = gpu_state(be.dev.index)
+        if not args.no_gpu_state:
+            diag["gpu_state_after"] = gpu_state(be.dev.index)
         calls, ms = be.pass_times()
         diag["pass_ms"] = {k: round(v / max(calls, 1), 4) for k, v in
                            zip(("bucket", "fold", "one_line", "gather"), ms)} if calls else None
