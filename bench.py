@@ -115,6 +115,8 @@ def parse(argv=None):
                          "a few us per step) -> pass_ms, and the GPU's clocks / power around the timed steps")
     ap.add_argument("--no-gpu-state", action="store_true",
                     help="with --pass-times: skip the amd-smi readings around the timed steps")
+    ap.add_argument("--gpu-state-delay", type=float, default=0.0,
+                    help="with --pass-times: seconds to wait after the first amd-smi reading (diagnostics)")
     ap.add_argument("--plan-only", action="store_true",
                     help="print the shard plan every rank would run (gloo, no GPU) and exit")
     a = ap.parse_args(argv)
@@ -628,6 +630,8 @@ def run(args, world, rank, be, distributed):
         be.pass_times()  # forget the warmup's calls
         if not args.no_gpu_state:
             diag["gpu_state_before"] = gpu_state(be.dev.index)
+            if args.gpu_state_delay > 0:
+                time.sleep(args.gpu_state_delay)
     n_ev = args.steps if args.step_events else 1
     evs = [(be.event(), be.event()) for _ in range(n_ev)]
     be.sync()
