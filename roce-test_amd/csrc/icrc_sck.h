@@ -19,6 +19,10 @@ struct SckArgs {
   uint32_t QS[8];    // x^(-32 (4 s + 1)): lane slot s's chain 0 -> packet end
   uint32_t family;   // kFamV4 / kFamV6 / kFamAuto: masks applied by the kernel itself
   uint64_t *stamps;  // diagnostic builds only (tools/microbench); null in the product
+  // Per-wave share of the groups by XCD parity (workgroup b runs on XCD
+  // b % 8): a wave of an even-indexed workgroup takes wt_even parts, of an
+  // odd one wt_odd.  0 / 0: equal contiguous blocks of ceil(G / waves).
+  uint32_t wt_even, wt_odd;
 };
 
 // Returns hipErrorInvalidValue for an n it has no instantiation for.

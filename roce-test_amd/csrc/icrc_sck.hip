@@ -95,9 +95,22 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
   // The wave's groups: the contiguous block [g0, g1).  (A per-XCD dynamic
   // tail schedule balanced the waves' end times but measured slower,
   // tools/microbench/sck_tail.hip, profiles/r02/sck_tail.txt.)
-  const uint64_t per = (G + nwaves - 1) / nwaves;
-  const uint32_t g0 = (uint32_t)(wave * per < G ? wave * per : G);
-  const uint32_t g1 = (uint32_t)(g0 + per < G ? g0 + per : G);
+  uint32_t g0, g1;
+  if (a.wt_even == 0u) {
+    const uint64_t per = (G + nwaves - 1) / nwaves;
+    g0 = (uint32_t)(wave * per < G ? wave * per : G);
+    g1 = (uint32_t)(g0 + per < G ? g0 + per : G);
+  } else {
+    // weighted by XCD parity: W(w) = the parts of the waves before w, the
+    // wave takes groups [G W(w) / Wtot, G W(w + 1) / Wtot)
+    const uint64_t b = blockIdx.x, nb = gridDim.x;
+    const uint64_t we = a.wt_even, wo = a.wt_odd;
+    const uint64_t wb = (b & 1u) ? wo : we;
+    const uint64_t before = kWaves * (we * ((b + 1) >> 1) + wo * (b >> 1)) + wid * wb;
+    const uint64_t wtot = kWaves * (we * ((nb + 1) >> 1) + wo * (nb >> 1));
+    g0 = (uint32_t)((uint64_t)G * before / wtot);
+    g1 = (uint32_t)((uint64_t)G * (before + wb) / wtot);
+  }
   auto after = [&](uint32_t q) -> uint32_t { return q + 1 < g1 ? q + 1 : G; };
   uint32_t qcur = g0 < g1 ? g0 : G;
   uint32_t qnext = qcur < G ? after(qcur) : G;
