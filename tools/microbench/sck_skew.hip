@@ -32,7 +32,8 @@ int main(int argc, char **argv) {
     CK(hipMemcpy(buf, h.data(), bytes, hipMemcpyHostToDevice));
   }
   hipDeviceProp_t p; CK(hipGetDeviceProperties(&p, 0));
-  const int grid = p.multiProcessorCount - p.multiProcessorCount / 16;  // the product's grid for 1 M packets
+  // the product's grid for 1 M packets, or argv[2]
+  const int grid = argc > 2 ? atoi(argv[2]) : p.multiProcessorCount - p.multiProcessorCount / 16;
   const int waves = grid * kWaves;
   CK(hipMalloc(&stamps, 16ull * waves));
   SckArgs a{};
@@ -58,7 +59,10 @@ int main(int argc, char **argv) {
     float ms; CK(hipEventElapsedTime(&ms, e0, e1));
     return 1e3f * ms / 20;
   };
-  const uint32_t W[][2] = {{0, 0}, {1000, 1000}, {1030, 970}, {1050, 950}, {1070, 930}, {1100, 900}, {970, 1030}};
+  // (session r4s13: 0/0 632.5-633.1, 1000/1000 629.0-629.6, 1030/970
+  // 618.6-621.1, 1050/950 625.6-626.3, 1070/930 635, 1100/900 642, 970/1030
+  // 640-641 us on 4 KiB packets)
+  const uint32_t W[][2] = {{0, 0}, {1000, 1000}, {1010, 990}, {1020, 980}, {1030, 970}, {1040, 960}, {1050, 950}};
   const int nv = sizeof(W) / sizeof(W[0]);
   printf("%llu x %llu B, grid %d; us per launch (HIP events, 20 launches), variants alternating\n",
          (unsigned long long)count, (unsigned long long)n, grid);
@@ -72,7 +76,7 @@ int main(int argc, char **argv) {
     printf("\n");
   }
   // per-XCD wave ends for three of them
-  for (int v : {0, 3, 5}) {
+  for (int v : {0, 4}) {
     SckArgs k = a;
     k.wt_even = W[v][0]; k.wt_odd = W[v][1]; k.stamps = stamps;
     for (int r = 0; r < 5; ++r) launch(k, true);
