@@ -16,6 +16,21 @@ static constexpr int kBlock = 64 * kWaves;
 static constexpr int kLdsWords = 32768;  // 128 KiB
 
 // ---------------------------------------------------------------- helpers
+// The share [lo, hi) of `total` units that wave `wid` of workgroup blockIdx.x
+// takes when a wave of an even-indexed workgroup weighs `we` and one of an
+// odd-indexed workgroup `wo` (workgroup b runs on XCD b % 8: the odd XCDs'
+// waves stream HBM 5-10 % slower, tools/microbench/sck_skew.hip).  The
+// shares are contiguous, in wave order, and cover [0, total).
+__device__ __forceinline__ void xcd_share(uint64_t total, uint32_t we, uint32_t wo, uint32_t wid, uint64_t &lo,
+                                          uint64_t &hi) {
+  const uint64_t b = blockIdx.x, nb = gridDim.x;
+  const uint64_t wb = (b & 1u) ? wo : we;
+  const uint64_t before = (uint64_t)kWaves * (we * ((b + 1) >> 1) + wo * (b >> 1)) + wid * wb;
+  const uint64_t wtot = (uint64_t)kWaves * (we * ((nb + 1) >> 1) + wo * (nb >> 1));
+  lo = total * before / wtot;
+  hi = total * (before + wb) / wtot;
+}
+
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }

@@ -100,16 +100,11 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
     const uint64_t per = (G + nwaves - 1) / nwaves;
     g0 = (uint32_t)(wave * per < G ? wave * per : G);
     g1 = (uint32_t)(g0 + per < G ? g0 + per : G);
-  } else {
-    // weighted by XCD parity: W(w) = the parts of the waves before w, the
-    // wave takes groups [G W(w) / Wtot, G W(w + 1) / Wtot)
-    const uint64_t b = blockIdx.x, nb = gridDim.x;
-    const uint64_t we = a.wt_even, wo = a.wt_odd;
-    const uint64_t wb = (b & 1u) ? wo : we;
-    const uint64_t before = kWaves * (we * ((b + 1) >> 1) + wo * (b >> 1)) + wid * wb;
-    const uint64_t wtot = kWaves * (we * ((nb + 1) >> 1) + wo * (nb >> 1));
-    g0 = (uint32_t)((uint64_t)G * before / wtot);
-    g1 = (uint32_t)((uint64_t)G * (before + wb) / wtot);
+  } else {  // weighted by XCD parity
+    uint64_t lo, hi;
+    xcd_share(G, a.wt_even, a.wt_odd, wid, lo, hi);
+    g0 = (uint32_t)lo;
+    g1 = (uint32_t)hi;
   }
   auto after = [&](uint32_t q) -> uint32_t { return q + 1 < g1 ? q + 1 : G; };
   uint32_t qcur = g0 < g1 ? g0 : G;

@@ -80,9 +80,28 @@ int main() {
   // Round 4: the fold specialized on the line count (ABL 131072) against the
   // generic fold (product), alternating, same process.  Session r4s2 (then
   // the specialized fold was the product): 921.5 / 918.5 us, 921.7 / 919.8.
-  for (int r = 0; r < 3; ++r) {
+  for (int r = 0; r < 1; ++r) {
     printf("fold generic (product)     %8.1f us\n", 1e3f * timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10));
     printf("fold specialized           %8.1f us\n", 1e3f * timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<131072>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10));
+  }
+  // Round 4: the product fold with its work split weighted by XCD parity
+  // (a.wt_even / a.wt_odd, xcd_share), alternating.
+  {
+    const uint32_t W[][2] = {{0, 0}, {1000, 1000}, {1020, 980}, {1040, 960}, {1060, 940}, {1080, 920}};
+    for (int r = 0; r < 3; ++r) {
+      printf("xcd weights, round %d:", r);
+      for (const auto &w : W) {
+        RsckArgs k = a;
+        k.wt_even = w[0]; k.wt_odd = w[1];
+        printf(" | %u/%u %6.1f", w[0], w[1], 1e3f * timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, 0, k); }, 10));
+      }
+      printf("\n");
+    }
+    RsckArgs k = a;
+    k.wt_even = 1040; k.wt_odd = 960;
+    CK(hipMemset(a.res, 0, 4 * npos));
+    hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, 0, k);
+    check("fold 1040/960 vs 0/0");
   }
   return 0;
 }

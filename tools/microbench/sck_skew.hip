@@ -20,7 +20,7 @@ using namespace ricrc;
 
 int main(int argc, char **argv) {
   const int L = argc > 1 ? atoi(argv[1]) : 32;  // 32: 4 KiB packets; 8: 1 KiB (super-groups)
-  const uint64_t count = 1ull << 20;
+  const uint64_t count = argc > 3 ? strtoull(argv[3], nullptr, 0) : 1ull << 20;  // C3: 4194304
   const uint64_t n = L == 32 ? 4096 : 1024;
   const uint64_t bytes = count * n;
   uint8_t *buf; uint32_t *out; uint64_t *stamps;
@@ -62,8 +62,13 @@ int main(int argc, char **argv) {
   // (session r4s13: 0/0 632.5-633.1, 1000/1000 629.0-629.6, 1030/970
   // 618.6-621.1, 1050/950 625.6-626.3, 1070/930 635, 1100/900 642, 970/1030
   // 640-641 us on 4 KiB packets)
-  const uint32_t W[][2] = {{0, 0}, {1000, 1000}, {1010, 990}, {1020, 980}, {1030, 970}, {1040, 960}, {1050, 950}};
-  const int nv = sizeof(W) / sizeof(W[0]);
+  // (session r4s14, 240 CUs: 0/0 630-631, 1000/1000 628.5-629, 1010/990
+  // 624-625, 1020/980 620-621, 1030/970 619-621, 1040/960 625-627, 1050/950
+  // 628-629; 256 CUs: 0/0 645-647, 1030/970 636-640, 1050/950 622-625 us)
+  const uint32_t W240[][2] = {{0, 0}, {1000, 1000}, {1015, 985}, {1020, 980}, {1025, 975}, {1030, 970}, {1035, 965}};
+  const uint32_t W256[][2] = {{0, 0}, {1000, 1000}, {1040, 960}, {1050, 950}, {1060, 940}, {1070, 930}, {1080, 920}};
+  const auto &W = grid >= p.multiProcessorCount ? W256 : W240;
+  const int nv = sizeof(W240) / sizeof(W240[0]);
   printf("%llu x %llu B, grid %d; us per launch (HIP events, 20 launches), variants alternating\n",
          (unsigned long long)count, (unsigned long long)n, grid);
   for (int r = 0; r < 3; ++r) {
@@ -76,7 +81,7 @@ int main(int argc, char **argv) {
     printf("\n");
   }
   // per-XCD wave ends for three of them
-  for (int v : {0, 4}) {
+  for (int v : {0, 4}) {  // 0/0 and the fifth variant
     SckArgs k = a;
     k.wt_even = W[v][0]; k.wt_odd = W[v][1]; k.stamps = stamps;
     for (int r = 0; r < 5; ++r) launch(k, true);
