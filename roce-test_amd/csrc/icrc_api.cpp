@@ -55,7 +55,26 @@ struct Knobs {
   bool pass_times = false; // RICRC_PASS_TIMES: timing events between the ragged passes (ricrc_pass_times)
   long fail_chunk = -1;    // RICRC_FAIL_CHUNK: the next ricrc_batch_host fails after queueing chunk k (tests; once)
   int host_threads = 16;   // RICRC_HOST_THREADS: CPU copy threads of ricrc_batch_host
+  int xcd_skew = -1;       // RICRC_XCD_SKEW: per-mille work moved to even XCDs (-1: per kernel, 0: equal shares)
 };
+
+// Work split by XCD parity (xcd_share in icrc_device.h): a wave of an
+// even-indexed workgroup takes (1000 + skew) parts, of an odd one (1000 -
+// skew).  On every MI355X box of rounds 2-4 the odd XCDs' waves ended 5-10 %
+// after the even ones' with equal work (profiles/r02/sck_tail.txt,
+// profiles/r03/s17_bucket_abl.txt); weighting them evens the ends
+// (tools/microbench/sck_skew.hip, fold_var.hip, profiles/r04/s15_*): 1 M x
+// 4 KiB on 240 CUs 630.7-631.1 -> 618.1-619.7 us at 25; 4 M x 4 KiB on 256
+// CUs 2558-2568 -> 2485-2488 us at 50; the C4 fold 919.5-924.1 -> 912.6-912.9
+// us at 40.  The 1 KiB super-group schedule gains nothing (0).
+struct XcdWeights {
+  uint32_t even, odd;
+};
+XcdWeights xcd_weights(const Knobs &kn, int auto_skew) {
+  const int skew = kn.xcd_skew >= 0 ? kn.xcd_skew : auto_skew;
+  if (skew <= 0) return {0u, 0u};  // the kernels' equal-share split
+  return {1000u + (uint32_t)skew, 1000u - (uint32_t)skew};
+}
 bool g_debug = false;  // RICRC_DEBUG: print the HIP/RCCL error behind an -EIO
 
 struct Slot {
@@ -340,6 +359,9 @@ int launch_rsck_range(Dev &d, const uint8_t *base, const uint64_t *off, const ui
   k.l3_offset = l3_offset;
   k.verify = verify ? 1u : 0u;
   k.group_cost = d.knobs.gcost ? d.knobs.gcost : kRsGroupCost;
+  const XcdWeights xw = xcd_weights(d.knobs, 40);
+  k.wt_even = xw.even;
+  k.wt_odd = xw.odd;
   k.out = out;
   k.tzb = d.d_tzb;
   // GF(2) constants of the fold's finish (the same for every call)
@@ -446,6 +468,9 @@ int launch_batch_v4(Dev &d, const uint8_t *base, const uint64_t *off, const uint
       const uint32_t xi = gf_xinv8n(4);
       for (int j = 0; j < 32; ++j) k.XB[j] = gf_mul(xi, 1u << j);
       for (int s = 0; s < 8; ++s) k.QS[s] = gf_xinv8n(16ull * s + 4);
+      const XcdWeights xw = xcd_weights(d.knobs, fixed_len != 4096 ? 0 : sgrid < d.n_cu ? 25 : 50);
+      k.wt_even = xw.even;
+      k.wt_odd = xw.odd;
       return hip_err(launch_sck(k, sgrid, st));
     }
     const uint32_t M = fixed_len - 4;
@@ -679,6 +704,7 @@ Knobs read_knobs() {
   k.pass_grid = (int)std::max(0L, num("RICRC_RS_PASS_GRID", 0));
   k.pass_times = getenv("RICRC_PASS_TIMES") != nullptr;
   k.fail_chunk = num("RICRC_FAIL_CHUNK", -1);
+  k.xcd_skew = (int)std::min(500L, std::max(-1L, num("RICRC_XCD_SKEW", -1)));
   const unsigned hw = std::thread::hardware_concurrency();
   k.host_threads = (int)std::max(1L, std::min(64L, num("RICRC_HOST_THREADS", (long)std::min(16u, std::max(1u, hw)))));
   return k;
