@@ -14,6 +14,8 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <array>
+#include <string.h>
 #include <vector>
 using namespace ricrc;
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s line %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
@@ -67,8 +69,16 @@ int main(int argc, char **argv) {
   // 628-629; 256 CUs: 0/0 645-647, 1030/970 636-640, 1050/950 622-625 us)
   const uint32_t W240[][2] = {{0, 0}, {1000, 1000}, {1015, 985}, {1020, 980}, {1025, 975}, {1030, 970}, {1035, 965}};
   const uint32_t W256[][2] = {{0, 0}, {1000, 1000}, {1040, 960}, {1050, 950}, {1060, 940}, {1070, 930}, {1080, 920}};
-  const auto &W = grid >= p.multiProcessorCount ? W256 : W240;
-  const int nv = sizeof(W240) / sizeof(W240[0]);
+  std::vector<std::array<uint32_t, 2>> W;
+  if (argc > 4) {  // per-mille skews, comma-separated ("0" = the equal ceil split)
+    for (char *t = strtok(argv[4], ","); t; t = strtok(nullptr, ",")) {
+      const uint32_t d = (uint32_t)atoi(t);
+      W.push_back(d ? std::array<uint32_t, 2>{1000 + d, 1000 - d} : std::array<uint32_t, 2>{0, 0});
+    }
+  } else {
+    for (const auto &w : (grid >= p.multiProcessorCount ? W256 : W240)) W.push_back({w[0], w[1]});
+  }
+  const int nv = (int)W.size();
   printf("%llu x %llu B, grid %d; us per launch (HIP events, 20 launches), variants alternating\n",
          (unsigned long long)count, (unsigned long long)n, grid);
   for (int r = 0; r < 3; ++r) {
@@ -81,7 +91,7 @@ int main(int argc, char **argv) {
     printf("\n");
   }
   // per-XCD wave ends for three of them
-  for (int v : {0, 4}) {  // 0/0 and the fifth variant
+  for (int v : {0, std::min(4, nv - 1)}) {  // the first and the fifth variant
     SckArgs k = a;
     k.wt_even = W[v][0]; k.wt_odd = W[v][1]; k.stamps = stamps;
     for (int r = 0; r < 5; ++r) launch(k, true);
