@@ -97,6 +97,26 @@ int main() {
       }
       printf("\n");
     }
+    // grids x weights (FOLD_GRIDS="224,240,256" in the environment)
+    if (const char *gs = getenv("FOLD_GRIDS")) {
+      std::vector<int> grids;
+      for (const char *c = gs; *c;) {
+        grids.push_back(atoi(c));
+        while (*c && *c != ',') ++c;
+        if (*c == ',') ++c;
+      }
+      const uint32_t S[] = {0, 20, 40, 60};
+      for (int r = 0; r < 2; ++r)
+        for (int gr : grids) {
+          printf("grid %d, round %d:", gr, r);
+          for (uint32_t d : S) {
+            RsckArgs k = a;
+            k.wt_even = d ? 1000 + d : 0; k.wt_odd = d ? 1000 - d : 0;
+            printf(" | skew %u %6.1f", d, 1e3f * timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(gr), dim3(kBlock), 0, 0, k); }, 10));
+          }
+          printf("\n");
+        }
+    }
     RsckArgs k = a;
     k.wt_even = 1040; k.wt_odd = 960;
     CK(hipMemset(a.res, 0, 4 * npos));
