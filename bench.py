@@ -102,6 +102,10 @@ def parse(argv=None):
     # (profiles/r02/ramp_probe.jsonl); ricrc_prime keeps the device busy this
     # long right before the warmup (untimed).
     ap.add_argument("--prime-ms", type=float, default=25.0)
+    # ... and the board's power ramps over tens of ms of sustained load: the
+    # workload's own steps (kernels only, untimed) for this long before the
+    # warmup steps (profiles/r04/s23_*).
+    ap.add_argument("--warm-ms", type=float, default=0.0)
     # HIP events bracket the K timed steps as a whole (kernel_ms = their span
     # / K, inter-kernel gaps included: a conservative launch duration); with
     # --step-events every step's kernel(s) get their own pair -- two event
@@ -621,6 +625,16 @@ def run(args, world, rank, be, distributed):
 
     be.sync()
     be.prime(args.prime_ms)
+    if args.warm_ms > 0 and count:
+        t_w = time.perf_counter()
+        i = 0
+        while True:
+            be.compute(b, count, outs[i & 1], args)
+            i += 1
+            if i % 8 == 0:
+                be.sync()
+                if (time.perf_counter() - t_w) * 1e3 >= args.warm_ms:
+                    break
     for i in range(args.warmup):
         step(i)
     drain()
