@@ -105,7 +105,7 @@ def parse(argv=None):
     # ... and the board's power ramps over tens of ms of sustained load: the
     # workload's own steps (kernels only, untimed) for this long before the
     # warmup steps (profiles/r04/s23_*).
-    ap.add_argument("--warm-ms", type=float, default=0.0)
+    ap.add_argument("--warm-ms", type=float, default=100.0)
     # HIP events bracket the K timed steps as a whole (kernel_ms = their span
     # / K, inter-kernel gaps included: a conservative launch duration); with
     # --step-events every step's kernel(s) get their own pair -- two event
