@@ -24,11 +24,12 @@ __global__ __launch_bounds__(1024) void xcc_probe(uint32_t *out) {
   if (threadIdx.x == 0) out[blockIdx.x] = __builtin_amdgcn_s_getreg((3 << 11) | 20) | (lds[1] << 8);
 }
 
-int main() {
+int main(int argc, char **argv) {
+  const bool cold = argc > 1;  // "cold": no host copy first (the kernels are the process's first GPU work)
   const uint64_t count = 1ull << 20, n = 4096, bytes = count * n;
   uint8_t *buf; uint32_t *out, *xo; uint64_t *stamps;
   CK(hipMalloc(&buf, bytes)); CK(hipMalloc(&out, 4 * count)); CK(hipMalloc(&xo, 4 * 512));
-  {
+  if (!cold) {
     std::vector<uint64_t> h(bytes / 8);
     uint64_t x = 0x9E3779B97F4A7C15ull;
     for (auto &v : h) { x ^= x << 13; x ^= x >> 7; x ^= x << 17; v = x; }
@@ -42,10 +43,10 @@ int main() {
   for (int s = 0; s < 8; ++s) a.QS[s] = 0x9E3779B9u * (s + 1);
   std::vector<uint32_t> hx(512);
   std::vector<uint64_t> st(2 * waves);
-  for (int trial = 0; trial < 12; ++trial) {
-    hipStream_t s;
-    CK(hipStreamCreateWithFlags(&s, trial % 2 ? hipStreamNonBlocking : hipStreamDefault));
+  uint32_t *sink; CK(hipMalloc(&sink, 4096));
+  auto trial = [&](const char *what, hipStream_t s, int pre) {
     for (int w = 0; w < 3; ++w) hipLaunchKernelGGL((icrc_sck_kernel<32, 0>), dim3(grid), dim3(kBlock), 0, s, a);
+    if (pre > 0) hipLaunchKernelGGL(xcc_probe, dim3(pre), dim3(1024), 0, s, sink);
     hipLaunchKernelGGL(xcc_probe, dim3(grid), dim3(1024), 0, s, xo);
     hipLaunchKernelGGL((icrc_sck_kernel<32, 64>), dim3(grid), dim3(kBlock), 0, s, a);
     hipLaunchKernelGGL(xcc_probe, dim3(grid), dim3(1024), 0, s, xo + 256);
@@ -63,13 +64,21 @@ int main() {
       byb[b % 8] += e; ++cb[b % 8];
       byx[(b + k0) % 8] += e; ++cx[(b + k0) % 8];
     }
-    printf("trial %2d: k before %d after %d; span %.1f us | mean end by blockIdx%%8:", trial, k0, k1, (t1 - t0) / 100.0);
+    printf("%-34s k before %d after %d; span %.1f us | mean end by blockIdx%%8:", what, k0, k1, (t1 - t0) / 100.0);
     for (int i = 0; i < 8; ++i) printf(" %.0f", byb[i] / cb[i]);
     printf(" | by XCD:");
     for (int i = 0; i < 8; ++i) printf(" %.0f", byx[i] / cx[i]);
-    double ev = 0, od = 0;
-    for (int i = 0; i < 8; i += 2) { ev += byb[i] / cb[i]; od += byb[i + 1] / cb[i + 1]; }
-    printf(" | odd-even blocks %+.0f us\n", (od - ev) / 4);
+    double ev = 0, od = 0, evx = 0, odx = 0;
+    for (int i = 0; i < 8; i += 2) { ev += byb[i] / cb[i]; od += byb[i + 1] / cb[i + 1]; evx += byx[i] / cx[i]; odx += byx[i + 1] / cx[i + 1]; }
+    printf(" | odd-even blocks %+.0f, odd-even XCDs %+.0f us\n", (od - ev) / 4, (odx - evx) / 4);
+  };
+  char nm[64];
+  for (int t = 0; t < 12; ++t) {
+    hipStream_t s;
+    CK(hipStreamCreateWithFlags(&s, t % 2 ? hipStreamNonBlocking : hipStreamDefault));
+    const int pre = t % 4 == 1 ? 1 : t % 4 == 2 ? 7 : t % 4 == 3 ? 3 : 0;
+    snprintf(nm, sizeof nm, "trial %2d (%d-workgroup kernel first)", t, pre);
+    trial(nm, s, pre);
     CK(hipStreamDestroy(s));
   }
   return 0;
