@@ -17,6 +17,10 @@
 using namespace ricrc;
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s line %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 
+__global__ void xcc_one(uint32_t *out) {  // one 64-thread workgroup: the XCD it lands on
+  if (threadIdx.x == 0) out[0] = __builtin_amdgcn_s_getreg((3 << 11) | 20);
+}
+
 __global__ __launch_bounds__(1024) void xcc_probe(uint32_t *out) {
   __shared__ uint32_t lds[32768];  // 128 KiB: one workgroup per CU, like the SCK
   lds[threadIdx.x] = threadIdx.x;
@@ -47,6 +51,7 @@ int main(int argc, char **argv) {
   auto trial = [&](const char *what, hipStream_t s, int pre) {
     for (int w = 0; w < 3; ++w) hipLaunchKernelGGL((icrc_sck_kernel<32, 0>), dim3(grid), dim3(kBlock), 0, s, a);
     if (pre > 0) hipLaunchKernelGGL(xcc_probe, dim3(pre), dim3(1024), 0, s, sink);
+    hipLaunchKernelGGL(xcc_one, dim3(1), dim3(64), 0, s, xo + 511);
     hipLaunchKernelGGL(xcc_probe, dim3(grid), dim3(1024), 0, s, xo);
     hipLaunchKernelGGL((icrc_sck_kernel<32, 64>), dim3(grid), dim3(kBlock), 0, s, a);
     hipLaunchKernelGGL(xcc_probe, dim3(grid), dim3(1024), 0, s, xo + 256);
@@ -64,7 +69,8 @@ int main(int argc, char **argv) {
       byb[b % 8] += e; ++cb[b % 8];
       byx[(b + k0) % 8] += e; ++cx[(b + k0) % 8];
     }
-    printf("%-34s k before %d after %d; span %.1f us | mean end by blockIdx%%8:", what, k0, k1, (t1 - t0) / 100.0);
+    printf("%-34s 1-workgroup detector %u;", what, hx[511] & 15u);
+    printf(" k before %d after %d; span %.1f us | mean end by blockIdx%%8:", k0, k1, (t1 - t0) / 100.0);
     for (int i = 0; i < 8; ++i) printf(" %.0f", byb[i] / cb[i]);
     printf(" | by XCD:");
     for (int i = 0; i < 8; ++i) printf(" %.0f", byx[i] / cx[i]);
