@@ -70,6 +70,10 @@ struct Knobs {
 struct XcdWeights {
   uint32_t even, odd;
 };
+// The start XCD of the next launch on this device: the latest one a kernel
+// recorded (it is stable over many launches; a stale value costs speed only).
+uint32_t xcd_start(const uint32_t *h_xcd) { return h_xcd ? __atomic_load_n(h_xcd, __ATOMIC_RELAXED) & 7u : 0u; }
+
 XcdWeights xcd_weights(const Knobs &kn, int auto_skew) {
   const int skew = kn.xcd_skew >= 0 ? kn.xcd_skew : auto_skew;
   if (skew <= 0) return {0u, 0u};  // the kernels' equal-share split
@@ -97,6 +101,10 @@ struct Dev {
   hipStream_t stream = nullptr;
   uint32_t *d_tzb = nullptr;   // [kTzWords]: basis words 4q of x^(-8 tz) at 2 tz + q (ragged strided-chain path)
   uint32_t *d_x8n = nullptr;   // x^(8 k), k < 65536 (incremental repair)
+  // Pinned word where workgroup 0 of the SCK / ragged fold records its XCD;
+  // the next launch passes it as xcd_k (xcd_share in icrc_device.h).
+  uint32_t *h_xcd = nullptr;
+  uint32_t *d_xcd_rec = nullptr;  // the same word as the device addresses it
   Slot slot[2];
   uint8_t *d_status[2] = {nullptr, nullptr};  // batch_host_st: per-slot status staging (device / pinned)
   uint8_t *h_status[2] = {nullptr, nullptr};
@@ -188,6 +196,9 @@ int init_dev(Dev &d) {
     const int tz = std::min(m >> 1, 127), q = m - 2 * tz;
     tzb[m] = q < 8 ? gf_mul(gf_xinv8n((uint64_t)tz), 1u << (4 * q)) : 0u;
   }
+  HIP_TRY(hipHostMalloc((void **)&d.h_xcd, 64, hipHostMallocCoherent));
+  *d.h_xcd = 0;  // until a kernel has recorded it: workgroup b on XCD b % 8
+  HIP_TRY(hipHostGetDevicePointer((void **)&d.d_xcd_rec, d.h_xcd, 0));
   HIP_TRY(hipMalloc(&d.d_tzb, tzb.size() * sizeof(uint32_t)));
   HIP_TRY(hipMemcpy(d.d_tzb, tzb.data(), tzb.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
   std::vector<uint32_t> x8n(65536);  // x^(8 k): a repair's shift over the bytes after the rewrite
@@ -244,6 +255,7 @@ void free_dev(Dev &d) {
   d.pt_ev.clear();
   (void)hipFree(d.d_tzb);
   (void)hipFree(d.d_x8n);
+  if (d.h_xcd) (void)hipDeviceSynchronize(), (void)hipHostFree(d.h_xcd);  // no kernel may still record into it
   if (d.stream) (void)hipStreamDestroy(d.stream);
 }
 
@@ -362,6 +374,8 @@ int launch_rsck_range(Dev &d, const uint8_t *base, const uint64_t *off, const ui
   const XcdWeights xw = xcd_weights(d.knobs, 40);
   k.wt_even = xw.even;
   k.wt_odd = xw.odd;
+  k.xcd_k = xcd_start(d.h_xcd);
+  k.xcd_rec = d.d_xcd_rec;
   k.out = out;
   k.tzb = d.d_tzb;
   // GF(2) constants of the fold's finish (the same for every call)
@@ -471,6 +485,8 @@ int launch_batch_v4(Dev &d, const uint8_t *base, const uint64_t *off, const uint
       const XcdWeights xw = xcd_weights(d.knobs, fixed_len != 4096 ? 0 : sgrid < d.n_cu ? 25 : 50);
       k.wt_even = xw.even;
       k.wt_odd = xw.odd;
+      k.xcd_k = xcd_start(d.h_xcd);
+      k.xcd_rec = d.d_xcd_rec;
       return hip_err(launch_sck(k, sgrid, st));
     }
     const uint32_t M = fixed_len - 4;

@@ -17,18 +17,32 @@ static constexpr int kLdsWords = 32768;  // 128 KiB
 
 // ---------------------------------------------------------------- helpers
 // The share [lo, hi) of `total` units that wave `wid` of workgroup blockIdx.x
-// takes when a wave of an even-indexed workgroup weighs `we` and one of an
-// odd-indexed workgroup `wo` (workgroup b runs on XCD b % 8: the odd XCDs'
-// waves stream HBM 5-10 % slower, tools/microbench/sck_skew.hip).  The
-// shares are contiguous, in wave order, and cover [0, total).
-__device__ __forceinline__ void xcd_share(uint64_t total, uint32_t we, uint32_t wo, uint32_t wid, uint64_t &lo,
-                                          uint64_t &hi) {
+// takes when a wave of a workgroup on an even-numbered XCD weighs `we` and
+// one on an odd-numbered XCD `wo` (the odd XCDs' waves stream HBM 5-10 %
+// slower, tools/microbench/sck_skew.hip, xcd_slow.hip).  Workgroups are dealt
+// round-robin over the 8 XCDs starting at XCD k, which changes between
+// processes (tools/microbench/xcc_probe.hip): workgroup b is on XCD (b + k) %
+// 8.  k comes from the host (a kernel argument, so every wave uses the same
+// value: the shares are contiguous, in wave order, and cover [0, total) for
+// any k); a wrong k costs speed, never a packet.
+__device__ __forceinline__ void xcd_share(uint64_t total, uint32_t we, uint32_t wo, uint32_t k, uint32_t wid,
+                                          uint64_t &lo, uint64_t &hi) {
   const uint64_t b = blockIdx.x, nb = gridDim.x;
-  const uint64_t wb = (b & 1u) ? wo : we;
-  const uint64_t before = (uint64_t)kWaves * (we * ((b + 1) >> 1) + wo * (b >> 1)) + wid * wb;
-  const uint64_t wtot = (uint64_t)kWaves * (we * ((nb + 1) >> 1) + wo * (nb >> 1));
+  auto evens = [&](uint64_t n) -> uint64_t { return (k & 1u) ? (n >> 1) : ((n + 1) >> 1); };  // even-XCD blocks in [0, n)
+  const uint64_t wb = ((b + k) & 1u) ? wo : we;
+  const uint64_t eb = evens(b), en = evens(nb);
+  const uint64_t before = (uint64_t)kWaves * (we * eb + wo * (b - eb)) + wid * wb;
+  const uint64_t wtot = (uint64_t)kWaves * (we * en + wo * (nb - en));
   lo = total * before / wtot;
   hi = total * (before + wb) / wtot;
+}
+
+// Workgroup 0 records the XCD it runs on (HW_REG_XCC_ID) for the host's next
+// launch (xcd_share's k): a system-scope store to pinned host memory.
+__device__ __forceinline__ void xcd_record(uint32_t *rec) {
+  if (rec != nullptr && blockIdx.x == 0 && threadIdx.x == 0)
+    __hip_atomic_store(rec, (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 20), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {

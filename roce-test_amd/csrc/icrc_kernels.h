@@ -95,6 +95,8 @@ struct RsckArgs {
   uint32_t verify;
   uint32_t group_cost;  // a group's finish in line-steps of the fold's work split (launch_rsck sets it)
   uint32_t wt_even, wt_odd;  // the fold's work split by XCD parity (xcd_share; 0 / 0: equal shares)
+  uint32_t xcd_k;            // workgroup b of the fold runs on XCD (b + xcd_k) % 8 (host's latest record)
+  uint32_t *xcd_rec;         // where the fold's workgroup 0 records its XCD (or null)
   uint32_t *out;
   // device workspace (icrc_api.cpp sizes it: rs_workspace_bytes)
   RsCounters *ctr;      // zeroed on allocation and by the gather pass of every call

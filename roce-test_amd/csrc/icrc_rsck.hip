@@ -585,7 +585,8 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
     return q < gend ? (uint32_t)q : gend;
   };
   uint64_t x0 = wave * share < S ? wave * share : S, x1 = x0 + share;
-  if (a.wt_even != 0u) xcd_share(S, a.wt_even, a.wt_odd, wid, x0, x1);  // weighted by XCD parity
+  if (a.wt_even != 0u) xcd_share(S, a.wt_even, a.wt_odd, a.xcd_k, wid, x0, x1);  // weighted by XCD parity
+  xcd_record(a.xcd_rec);
   const uint32_t q_begin = first_group_at(x0), q_end = first_group_at(x1);
   if ((ABL & 8192) && lane == 0) {  // timing only: per-wave start stamp, groups, first group
     const uint32_t t_start = (uint32_t)__builtin_amdgcn_s_memrealtime();

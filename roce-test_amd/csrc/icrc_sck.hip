@@ -102,7 +102,7 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
     g1 = (uint32_t)(g0 + per < G ? g0 + per : G);
   } else {  // weighted by XCD parity
     uint64_t lo, hi;
-    xcd_share(G, a.wt_even, a.wt_odd, wid, lo, hi);
+    xcd_share(G, a.wt_even, a.wt_odd, a.xcd_k, wid, lo, hi);
     g0 = (uint32_t)lo;
     g1 = (uint32_t)hi;
   }
@@ -121,6 +121,7 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
   // The first D lines are in flight while the workgroup builds its tables
   // (the table load is issued first, so waiting for it leaves them in flight).
   const uint64_t t_start = (ABL & 64) ? __builtin_amdgcn_s_memrealtime() : 0u;
+  xcd_record(a.xcd_rec);
   const uint32_t tab_v = table_entry(g_tab128);
   u32x4 ring[D];
 #pragma unroll
