@@ -36,26 +36,30 @@ int main(int argc, char **argv) {
   for (int j = 0; j < 32; ++j) a.XB[j] = 0x85EBCA6Bu * (j + 3);
   for (int s = 0; s < 8; ++s) a.QS[s] = 0x9E3779B9u * (s + 1);
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  hipStream_t st = 0;
   auto run = [&](int v) {  // 0 equal shares, 1 skew assuming k = 0, 2 skew with the recorded k
     SckArgs k = a;
     if (v) { k.wt_even = 1025; k.wt_odd = 975; }
     k.xcd_k = v == 2 ? __atomic_load_n(h_rec, __ATOMIC_RELAXED) & 7u : 0u;
-    hipLaunchKernelGGL((icrc_sck_kernel<32, 0>), dim3(grid), dim3(kBlock), 0, 0, k);
+    hipLaunchKernelGGL((icrc_sck_kernel<32, 0>), dim3(grid), dim3(kBlock), 0, st, k);
   };
   auto timeit = [&](int v) {
     for (int r = 0; r < 5; ++r) run(v);
-    CK(hipEventRecord(e0));
+    CK(hipEventRecord(e0, st));
     for (int r = 0; r < 20; ++r) run(v);
-    CK(hipEventRecord(e1));
+    CK(hipEventRecord(e1, st));
     CK(hipEventSynchronize(e1));
     float ms; CK(hipEventElapsedTime(&ms, e0, e1));
     return 1e3f * ms / 20;
   };
   printf("%s; 1 M x 4 KiB, 240 CUs\n", cold ? "cold (no host copy first)" : "data copied from the host first");
-  for (int r = 0; r < 4; ++r) {
+  // a fresh stream per round (the start XCD has changed after stream creation, xcd_slow.hip)
+  for (int r = 0; r < 8; ++r) {
+    CK(hipStreamCreateWithFlags(&st, r % 2 ? hipStreamNonBlocking : hipStreamDefault));
     const float t0 = timeit(0), t1 = timeit(1), t2 = timeit(2);
     printf("round %d (recorded start XCD %u): equal %6.1f | skew 25, k = 0 assumed %6.1f | skew 25, k recorded %6.1f us\n",
            r, *h_rec & 7u, t0, t1, t2);
+    CK(hipStreamDestroy(st));
   }
   return 0;
 }
