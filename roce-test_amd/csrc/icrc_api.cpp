@@ -101,8 +101,9 @@ struct Dev {
   hipStream_t stream = nullptr;
   uint32_t *d_tzb = nullptr;   // [kTzWords]: basis words 4q of x^(-8 tz) at 2 tz + q (ragged strided-chain path)
   uint32_t *d_x8n = nullptr;   // x^(8 k), k < 65536 (incremental repair)
-  // Pinned word where workgroup 0 of the SCK / ragged fold records its XCD;
-  // the next launch passes it as xcd_k (xcd_share in icrc_device.h).
+  // Pinned word where workgroup 0 of the SCK records its XCD; the next SCK
+  // launch passes it as xcd_k (xcd_share in icrc_device.h).  (The ragged
+  // fold reads the XCD its own call's bucket pass recorded, RsCounters::xcd.)
   uint32_t *h_xcd = nullptr;
   uint32_t *d_xcd_rec = nullptr;  // the same word as the device addresses it
   Slot slot[2];
@@ -196,9 +197,14 @@ int init_dev(Dev &d) {
     const int tz = std::min(m >> 1, 127), q = m - 2 * tz;
     tzb[m] = q < 8 ? gf_mul(gf_xinv8n((uint64_t)tz), 1u << (4 * q)) : 0u;
   }
-  HIP_TRY(hipHostMalloc((void **)&d.h_xcd, 64, hipHostMallocCoherent));
-  *d.h_xcd = 0;  // until a kernel has recorded it: workgroup b on XCD b % 8
-  HIP_TRY(hipHostGetDevicePointer((void **)&d.d_xcd_rec, d.h_xcd, 0));
+  // (a speed hint only: without it the SCK assumes workgroup b on XCD b % 8)
+  if (hipHostMalloc((void **)&d.h_xcd, 64, hipHostMallocCoherent) == hipSuccess) {
+    *d.h_xcd = 0;  // until a kernel has recorded it: workgroup b on XCD b % 8
+    if (hipHostGetDevicePointer((void **)&d.d_xcd_rec, d.h_xcd, 0) != hipSuccess) d.d_xcd_rec = nullptr;
+  } else {
+    d.h_xcd = nullptr;
+  }
+  (void)hipGetLastError();
   HIP_TRY(hipMalloc(&d.d_tzb, tzb.size() * sizeof(uint32_t)));
   HIP_TRY(hipMemcpy(d.d_tzb, tzb.data(), tzb.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
   std::vector<uint32_t> x8n(65536);  // x^(8 k): a repair's shift over the bytes after the rewrite
@@ -374,8 +380,6 @@ int launch_rsck_range(Dev &d, const uint8_t *base, const uint64_t *off, const ui
   const XcdWeights xw = xcd_weights(d.knobs, 40);
   k.wt_even = xw.even;
   k.wt_odd = xw.odd;
-  k.xcd_k = xcd_start(d.h_xcd);
-  k.xcd_rec = d.d_xcd_rec;
   k.out = out;
   k.tzb = d.d_tzb;
   // GF(2) constants of the fold's finish (the same for every call)

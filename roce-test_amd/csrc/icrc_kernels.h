@@ -73,6 +73,8 @@ struct RsCounters {
   uint32_t odd;                // a big packet not starting or ending on a 4-byte word
   uint32_t small;              // small-pool packets
   unsigned long long pool;     // big pool: groups | work << kRsGroupBits
+  uint32_t xcd;                // the XCD the bucket pass's workgroup 0 ran on (the fold's xcd_share k)
+  uint32_t pad;
 };
 struct RsBlock {               // pass block b's ranges (runs == 0: no big packets)
   uint32_t g0, groups, runs;   // big pool: groups [g0, g0 + groups), its runs
@@ -95,8 +97,6 @@ struct RsckArgs {
   uint32_t verify;
   uint32_t group_cost;  // a group's finish in line-steps of the fold's work split (launch_rsck sets it)
   uint32_t wt_even, wt_odd;  // the fold's work split by XCD parity (xcd_share; 0 / 0: equal shares)
-  uint32_t xcd_k;            // workgroup b of the fold runs on XCD (b + xcd_k) % 8 (host's latest record)
-  uint32_t *xcd_rec;         // where the fold's workgroup 0 records its XCD (or null)
   uint32_t *out;
   // device workspace (icrc_api.cpp sizes it: rs_workspace_bytes)
   RsCounters *ctr;      // zeroed on allocation and by the gather pass of every call

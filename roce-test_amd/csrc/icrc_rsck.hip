@@ -161,6 +161,10 @@ __global__ __launch_bounds__(kPassBlock) void rsck_bucket(RsckArgs a) {
   __shared__ uint32_t blk_g0, blk_small, blk_stot, blk_total;
   __shared__ uint64_t blk_s0;
   __shared__ uint64_t stage[kStage];  // the block's layout: small range | big range (132 / 140 KiB)
+  // The XCD this launch's workgroup 0 runs on: the fold that follows on the
+  // same stream starts dealing its workgroups there too
+  // (tools/microbench/xcd_slow.hip), and splits its work by it (xcd_share).
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.ctr->xcd = __builtin_amdgcn_s_getreg((3 << 11) | 20);
   for (int t = threadIdx.x; t < kRsClasses; t += blockDim.x) {
     h[t] = 0;
     cur[t] = 0;
@@ -360,7 +364,7 @@ __global__ __launch_bounds__(kPassBlock) void rsck_gather(RsckArgs a) {
   __shared__ uint32_t lres[kStage];
   // The counters are dead now (the bucket pass and both folds have read
   // them): zero them for the next call on this workspace.
-  if (blockIdx.x == 0 && threadIdx.x == 0) *a.ctr = RsCounters{0u, 0u, 0ull};
+  if (blockIdx.x == 0 && threadIdx.x == 0) *a.ctr = RsCounters{};
   uint32_t lo, hi;
   {
     uint64_t l, h_;
@@ -585,8 +589,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
     return q < gend ? (uint32_t)q : gend;
   };
   uint64_t x0 = wave * share < S ? wave * share : S, x1 = x0 + share;
-  if (a.wt_even != 0u) xcd_share(S, a.wt_even, a.wt_odd, a.xcd_k, wid, x0, x1);  // weighted by XCD parity
-  xcd_record(a.xcd_rec);
+  if (a.wt_even != 0u) xcd_share(S, a.wt_even, a.wt_odd, a.ctr->xcd, wid, x0, x1);  // weighted by XCD parity
   const uint32_t q_begin = first_group_at(x0), q_end = first_group_at(x1);
   if ((ABL & 8192) && lane == 0) {  // timing only: per-wave start stamp, groups, first group
     const uint32_t t_start = (uint32_t)__builtin_amdgcn_s_memrealtime();
