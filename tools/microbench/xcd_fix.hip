@@ -15,6 +15,13 @@
 using namespace ricrc;
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s line %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 
+__global__ __launch_bounds__(1024) void lds_one(uint32_t *out) {  // one 1024-thread, 128 KiB-LDS workgroup
+  __shared__ uint32_t lds[32768];
+  lds[threadIdx.x] = threadIdx.x;
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] = lds[7];
+}
+
 int main(int argc, char **argv) {
   const bool cold = argc > 1;
   const uint64_t count = 1ull << 20, n = 4096, bytes = count * n;
@@ -56,6 +63,9 @@ int main(int argc, char **argv) {
   // a fresh stream per round (the start XCD has changed after stream creation, xcd_slow.hip)
   for (int r = 0; r < 8; ++r) {
     CK(hipStreamCreateWithFlags(&st, r % 2 ? hipStreamNonBlocking : hipStreamDefault));
+    // (xcd_slow.hip: after such a one-workgroup kernel the launches of a
+    // cold process started dealing at XCD 7)
+    hipLaunchKernelGGL(lds_one, dim3(1), dim3(1024), 0, st, out);
     const float t0 = timeit(0), t1 = timeit(1), t2 = timeit(2);
     printf("round %d (recorded start XCD %u): equal %6.1f | skew 25, k = 0 assumed %6.1f | skew 25, k recorded %6.1f us\n",
            r, *h_rec & 7u, t0, t1, t2);
