@@ -56,6 +56,7 @@ struct Knobs {
   long fail_chunk = -1;    // RICRC_FAIL_CHUNK: the next ricrc_batch_host fails after queueing chunk k (tests; once)
   int host_threads = 16;   // RICRC_HOST_THREADS: CPU copy threads of ricrc_batch_host
   int xcd_skew = -1;       // RICRC_XCD_SKEW: per-mille work moved to even XCDs (-1: per kernel, 0: equal shares)
+  uint32_t xcd_w[8] = {};  // RICRC_XCD_WEIGHTS=w0,...,w7: parts per wave on XCD x (overrides the skew)
 };
 
 // Work split by XCD parity (xcd_share in icrc_device.h): a wave of an
@@ -68,16 +69,22 @@ struct Knobs {
 // CUs 2558-2568 -> 2485-2488 us at 50; the C4 fold 919.5-924.1 -> 912.6-912.9
 // us at 40.  The 1 KiB super-group schedule gains nothing (0).
 struct XcdWeights {
-  uint32_t even, odd;
+  uint32_t w[8];  // parts per wave on XCD x; w[0] == 0: equal shares
 };
 // The start XCD of the next launch on this device: the latest one a kernel
 // recorded (it is stable over many launches; a stale value costs speed only).
 uint32_t xcd_start(const uint32_t *h_xcd) { return h_xcd ? __atomic_load_n(h_xcd, __ATOMIC_RELAXED) & 7u : 0u; }
 
 XcdWeights xcd_weights(const Knobs &kn, int auto_skew) {
+  XcdWeights r{};
+  if (kn.xcd_w[0] != 0u) {  // RICRC_XCD_WEIGHTS
+    for (int x = 0; x < 8; ++x) r.w[x] = kn.xcd_w[x];
+    return r;
+  }
   const int skew = kn.xcd_skew >= 0 ? kn.xcd_skew : auto_skew;
-  if (skew <= 0) return {0u, 0u};  // the kernels' equal-share split
-  return {1000u + (uint32_t)skew, 1000u - (uint32_t)skew};
+  if (skew <= 0) return r;  // the kernels' equal-share split
+  for (int x = 0; x < 8; ++x) r.w[x] = (x & 1) ? 1000u - (uint32_t)skew : 1000u + (uint32_t)skew;
+  return r;
 }
 bool g_debug = false;  // RICRC_DEBUG: print the HIP/RCCL error behind an -EIO
 
@@ -378,8 +385,7 @@ int launch_rsck_range(Dev &d, const uint8_t *base, const uint64_t *off, const ui
   k.verify = verify ? 1u : 0u;
   k.group_cost = d.knobs.gcost ? d.knobs.gcost : kRsGroupCost;
   const XcdWeights xw = xcd_weights(d.knobs, 40);
-  k.wt_even = xw.even;
-  k.wt_odd = xw.odd;
+  for (int x = 0; x < 8; ++x) k.xw[x] = xw.w[x];
   k.out = out;
   k.tzb = d.d_tzb;
   // GF(2) constants of the fold's finish (the same for every call)
@@ -487,8 +493,7 @@ int launch_batch_v4(Dev &d, const uint8_t *base, const uint64_t *off, const uint
       for (int j = 0; j < 32; ++j) k.XB[j] = gf_mul(xi, 1u << j);
       for (int s = 0; s < 8; ++s) k.QS[s] = gf_xinv8n(16ull * s + 4);
       const XcdWeights xw = xcd_weights(d.knobs, fixed_len != 4096 ? 0 : sgrid < d.n_cu ? 25 : 50);
-      k.wt_even = xw.even;
-      k.wt_odd = xw.odd;
+      for (int x = 0; x < 8; ++x) k.xw[x] = xw.w[x];
       k.xcd_k = xcd_start(d.h_xcd);
       k.xcd_rec = d.d_xcd_rec;
       return hip_err(launch_sck(k, sgrid, st));
@@ -725,6 +730,19 @@ Knobs read_knobs() {
   k.pass_times = getenv("RICRC_PASS_TIMES") != nullptr;
   k.fail_chunk = num("RICRC_FAIL_CHUNK", -1);
   k.xcd_skew = (int)std::min(500L, std::max(-1L, num("RICRC_XCD_SKEW", -1)));
+  if (const char *e = getenv("RICRC_XCD_WEIGHTS")) {  // eight weights in 1..10000, else ignored
+    uint32_t w[8];
+    int n = 0;
+    for (const char *c = e; *c && n < 8;) {
+      const long v = atol(c);
+      if (v < 1 || v > 10000) break;
+      w[n++] = (uint32_t)v;
+      while (*c && *c != ',') ++c;
+      if (*c == ',') ++c;
+    }
+    if (n == 8)
+      for (int x = 0; x < 8; ++x) k.xcd_w[x] = w[x];
+  }
   const unsigned hw = std::thread::hardware_concurrency();
   k.host_threads = (int)std::max(1L, std::min(64L, num("RICRC_HOST_THREADS", (long)std::min(16u, std::max(1u, hw)))));
   return k;

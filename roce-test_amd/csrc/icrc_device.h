@@ -17,22 +17,28 @@ static constexpr int kLdsWords = 32768;  // 128 KiB
 
 // ---------------------------------------------------------------- helpers
 // The share [lo, hi) of `total` units that wave `wid` of workgroup blockIdx.x
-// takes when a wave of a workgroup on an even-numbered XCD weighs `we` and
-// one on an odd-numbered XCD `wo` (the odd XCDs' waves stream HBM 5-10 %
-// slower, tools/microbench/sck_skew.hip, xcd_slow.hip).  Workgroups are dealt
-// round-robin over the 8 XCDs starting at XCD k, which changes between
-// processes (tools/microbench/xcc_probe.hip): workgroup b is on XCD (b + k) %
-// 8.  k comes from the host (a kernel argument, so every wave uses the same
-// value: the shares are contiguous, in wave order, and cover [0, total) for
-// any k); a wrong k costs speed, never a packet.
-__device__ __forceinline__ void xcd_share(uint64_t total, uint32_t we, uint32_t wo, uint32_t k, uint32_t wid,
+// takes when a wave on XCD x weighs w[x] (the odd-numbered XCDs' waves, and
+// XCD 0's a little, stream HBM 5-10 % slower: tools/microbench/sck_skew.hip,
+// xcd_slow.hip).  Workgroups are dealt round-robin over the 8 XCDs starting
+// at XCD k, which changes between processes (tools/microbench/xcc_probe.hip):
+// workgroup b is on XCD (b + k) % 8.  w and k come from the host or from an
+// earlier kernel of the same stream, so every wave uses the same values: the
+// shares are contiguous, in wave order, and cover [0, total) for any k; a
+// wrong k costs speed, never a packet.
+__device__ __forceinline__ void xcd_share(uint64_t total, const uint32_t (&w)[8], uint32_t k, uint32_t wid,
                                           uint64_t &lo, uint64_t &hi) {
   const uint64_t b = blockIdx.x, nb = gridDim.x;
-  auto evens = [&](uint64_t n) -> uint64_t { return (k & 1u) ? (n >> 1) : ((n + 1) >> 1); };  // even-XCD blocks in [0, n)
-  const uint64_t wb = ((b + k) & 1u) ? wo : we;
-  const uint64_t eb = evens(b), en = evens(nb);
-  const uint64_t before = (uint64_t)kWaves * (we * eb + wo * (b - eb)) + wid * wb;
-  const uint64_t wtot = (uint64_t)kWaves * (we * en + wo * (nb - en));
+  uint64_t cyc = 0;
+#pragma unroll
+  for (int x = 0; x < 8; ++x) cyc += w[x];
+  auto cum = [&](uint64_t n) -> uint64_t {  // the weight of workgroups [0, n)
+    uint64_t s = (n >> 3) * cyc;
+    for (uint32_t j = 0; j < (uint32_t)(n & 7u); ++j) s += w[(k + j) & 7u];
+    return s;
+  };
+  const uint64_t wb = w[(b + k) & 7u];
+  const uint64_t before = (uint64_t)kWaves * cum(b) + wid * wb;
+  const uint64_t wtot = (uint64_t)kWaves * cum(nb);
   lo = total * before / wtot;
   hi = total * (before + wb) / wtot;
 }

@@ -96,7 +96,7 @@ struct RsckArgs {
   uint32_t l3_offset;
   uint32_t verify;
   uint32_t group_cost;  // a group's finish in line-steps of the fold's work split (launch_rsck sets it)
-  uint32_t wt_even, wt_odd;  // the fold's work split by XCD parity (xcd_share; 0 / 0: equal shares)
+  uint32_t xw[8];            // the fold's work split by XCD (xcd_share; xw[0] == 0: equal shares)
   uint32_t *out;
   // device workspace (icrc_api.cpp sizes it: rs_workspace_bytes)
   RsCounters *ctr;      // zeroed on allocation and by the gather pass of every call

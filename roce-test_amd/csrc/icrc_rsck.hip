@@ -589,7 +589,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
     return q < gend ? (uint32_t)q : gend;
   };
   uint64_t x0 = wave * share < S ? wave * share : S, x1 = x0 + share;
-  if (a.wt_even != 0u) xcd_share(S, a.wt_even, a.wt_odd, a.ctr->xcd, wid, x0, x1);  // weighted by XCD parity
+  if (a.xw[0] != 0u) xcd_share(S, a.xw, a.ctr->xcd, wid, x0, x1);  // weighted by XCD
   const uint32_t q_begin = first_group_at(x0), q_end = first_group_at(x1);
   if ((ABL & 8192) && lane == 0) {  // timing only: per-wave start stamp, groups, first group
     const uint32_t t_start = (uint32_t)__builtin_amdgcn_s_memrealtime();

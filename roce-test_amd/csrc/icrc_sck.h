@@ -19,11 +19,12 @@ struct SckArgs {
   uint32_t QS[8];    // x^(-32 (4 s + 1)): lane slot s's chain 0 -> packet end
   uint32_t family;   // kFamV4 / kFamV6 / kFamAuto: masks applied by the kernel itself
   uint64_t *stamps;  // diagnostic builds only (tools/microbench); null in the product
-  // Per-wave share of the groups by XCD parity (xcd_share): a wave on an
-  // even-numbered XCD takes wt_even parts, on an odd one wt_odd; workgroup b
-  // runs on XCD (b + xcd_k) % 8.  0 / 0: equal contiguous blocks of
-  // ceil(G / waves).  xcd_rec: where workgroup 0 records its XCD (or null).
-  uint32_t wt_even, wt_odd, xcd_k;
+  // Per-wave share of the groups by XCD (xcd_share): a wave on XCD x takes
+  // xw[x] parts; workgroup b runs on XCD (b + xcd_k) % 8.  xw[0] == 0: equal
+  // contiguous blocks of ceil(G / waves).  xcd_rec: where workgroup 0
+  // records its XCD (or null).
+  uint32_t xw[8];
+  uint32_t xcd_k;
   uint32_t *xcd_rec;
 };
 

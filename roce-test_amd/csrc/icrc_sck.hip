@@ -96,13 +96,13 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
   // tail schedule balanced the waves' end times but measured slower,
   // tools/microbench/sck_tail.hip, profiles/r02/sck_tail.txt.)
   uint32_t g0, g1;
-  if (a.wt_even == 0u) {
+  if (a.xw[0] == 0u) {
     const uint64_t per = (G + nwaves - 1) / nwaves;
     g0 = (uint32_t)(wave * per < G ? wave * per : G);
     g1 = (uint32_t)(g0 + per < G ? g0 + per : G);
-  } else {  // weighted by XCD parity
+  } else {  // weighted by XCD
     uint64_t lo, hi;
-    xcd_share(G, a.wt_even, a.wt_odd, a.xcd_k, wid, lo, hi);
+    xcd_share(G, a.xw, a.xcd_k, wid, lo, hi);
     g0 = (uint32_t)lo;
     g1 = (uint32_t)hi;
   }

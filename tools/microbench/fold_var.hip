@@ -85,14 +85,14 @@ int main() {
     printf("fold specialized           %8.1f us\n", 1e3f * timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<131072>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10));
   }
   // Round 4: the product fold with its work split weighted by XCD parity
-  // (a.wt_even / a.wt_odd, xcd_share), alternating.
+  // (a.xw by XCD parity, xcd_share), alternating.
   {
     const uint32_t W[][2] = {{0, 0}, {1000, 1000}, {1020, 980}, {1040, 960}, {1060, 940}, {1080, 920}};
     for (int r = 0; r < 3; ++r) {
       printf("xcd weights, round %d:", r);
       for (const auto &w : W) {
         RsckArgs k = a;
-        k.wt_even = w[0]; k.wt_odd = w[1];
+        for (int x = 0; x < 8; ++x) k.xw[x] = w[x & 1];
         printf(" | %u/%u %6.1f", w[0], w[1], 1e3f * timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, 0, k); }, 10));
       }
       printf("\n");
@@ -111,14 +111,14 @@ int main() {
           printf("grid %d, round %d:", gr, r);
           for (uint32_t d : S) {
             RsckArgs k = a;
-            k.wt_even = d ? 1000 + d : 0; k.wt_odd = d ? 1000 - d : 0;
+            for (int x = 0; x < 8; ++x) k.xw[x] = d ? ((x & 1) ? 1000 - d : 1000 + d) : 0u;
             printf(" | skew %u %6.1f", d, 1e3f * timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(gr), dim3(kBlock), 0, 0, k); }, 10));
           }
           printf("\n");
         }
     }
     RsckArgs k = a;
-    k.wt_even = 1040; k.wt_odd = 960;
+    for (int x = 0; x < 8; ++x) k.xw[x] = (x & 1) ? 960u : 1040u;
     CK(hipMemset(a.res, 0, 4 * npos));
     hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, 0, k);
     check("fold 1040/960 vs 0/0");

@@ -5,7 +5,7 @@
 // 574-578 us, odd by 627-637 us; the ragged fold's "mean end by blockIdx % 8"
 // lines of profiles/r03/s17_bucket_abl.txt).  Here the headline batch (1 M x
 // 4 KiB, random bytes, the product's 240-CU grid) runs with the waves of
-// even workgroups taking wt_even parts of the groups and odd ones wt_odd,
+// even workgroups taking W[0] parts of the groups and odd ones W[1] (xw),
 // alternating over several rounds, and with per-wave stamps per XCD.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 sck_skew.hip -o sck_skew
 #include "../../roce-test_amd/csrc/icrc_kernels.hip"
@@ -85,7 +85,7 @@ int main(int argc, char **argv) {
     printf("round %d:", r);
     for (int v = 0; v < nv; ++v) {
       SckArgs k = a;
-      k.wt_even = W[v][0]; k.wt_odd = W[v][1];
+      for (int x = 0; x < 8; ++x) k.xw[x] = W[v][0] ? W[v][x & 1] : 0u;
       printf(" | %u/%u %6.1f", W[v][0], W[v][1], timeit(k));
     }
     printf("\n");
@@ -93,7 +93,7 @@ int main(int argc, char **argv) {
   // per-XCD wave ends for three of them
   for (int v : {0, std::min(4, nv - 1)}) {  // the first and the fifth variant
     SckArgs k = a;
-    k.wt_even = W[v][0]; k.wt_odd = W[v][1]; k.stamps = stamps;
+    for (int x = 0; x < 8; ++x) k.xw[x] = W[v][0] ? W[v][x & 1] : 0u; k.stamps = stamps;
     for (int r = 0; r < 5; ++r) launch(k, true);
     CK(hipDeviceSynchronize());
     std::vector<uint64_t> st(2 * waves);

@@ -52,7 +52,7 @@ int main() {
   CK(hipMalloc(&tzb, 4 * 1024)); CK(hipMemset(tzb, 0x35, 4 * 1024));
   RsckArgs a{};
   a.base = buf; a.off = d_off; a.len = d_len; a.count = count;
-  a.out = out; a.tzb = tzb; a.group_cost = kRsGroupCost; a.wt_even = 1040; a.wt_odd = 960;
+  a.out = out; a.tzb = tzb; a.group_cost = kRsGroupCost; for (int x = 0; x < 8; ++x) a.xw[x] = (x & 1) ? 960u : 1040u;
   for (int j = 0; j < 32; ++j) { a.XB[j] = 0x85EBCA6Bu * (j + 3); a.XB2[j] = 0x27D4EB2Fu * (j + 5); a.XB3[j] = 0x165667B1u * (j + 7); }
   for (int s = 0; s < 8; ++s) a.QS[s] = 0x9E3779B9u * (s + 1);
   void *ws; CK(hipMalloc(&ws, rs_workspace_bytes(count)));

@@ -46,7 +46,7 @@ int main(int argc, char **argv) {
   hipStream_t st = 0;
   auto run = [&](int v) {  // 0 equal shares, 1 skew assuming k = 0, 2 skew with the recorded k
     SckArgs k = a;
-    if (v) { k.wt_even = 1025; k.wt_odd = 975; }
+    if (v) for (int x = 0; x < 8; ++x) k.xw[x] = (x & 1) ? 975u : 1025u;
     k.xcd_k = v == 2 ? __atomic_load_n(h_rec, __ATOMIC_RELAXED) & 7u : 0u;
     hipLaunchKernelGGL((icrc_sck_kernel<32, 0>), dim3(grid), dim3(kBlock), 0, st, k);
   };
