@@ -496,27 +496,29 @@ def test_strided_chain_kernel(ctx, ctx_env, n, count, grid):
     np.testing.assert_array_equal(_host_u32(out2), want)
 
 
-@pytest.mark.parametrize("skew", [0, 25, 50, 500])
+@pytest.mark.parametrize("skew", [0, 25, 50, 500, "1,10000,3,7,5000,2,9,1"])
 @pytest.mark.parametrize("count,grid", [(70001, None), (8 * 16 * 200 + 3, 3), (1 << 20 | 5, None)])
 def test_xcd_weighted_split(ctx_env, skew, count, grid):
-    """The work split weighted by XCD parity (xcd_share, RICRC_XCD_SKEW; the
-    product's defaults are 25 / 50 for the SCK, 40 for the ragged fold): any
-    weight gives contiguous per-wave ranges covering every group exactly
-    once -- odd grids (the last workgroup even), waves with no groups, more
+    """The work split weighted by XCD (xcd_share; RICRC_XCD_SKEW parity
+    weights -- the product's defaults are 25 / 50 for the SCK, 40 for the
+    ragged fold -- or RICRC_XCD_WEIGHTS, eight per-XCD weights, here lopsided
+    ones), from the start XCD the kernels record: any weights give
+    contiguous per-wave ranges covering every group exactly once -- odd grids (the last workgroup even), waves with no groups, more
     groups than the grid's waves -- on 4 KiB packets and on a ragged mix."""
-    env = {"RICRC_XCD_SKEW": skew}
+    env = {"RICRC_XCD_WEIGHTS": skew} if isinstance(skew, str) else {"RICRC_XCD_SKEW": skew}
     if grid is not None:
         env["RICRC_SCK_GRID"] = grid
         env["RICRC_RSCK_GRID"] = grid
     c = ctx_env(**env)
     n = 4096
     m = min(count, 200000)
-    host = oracle_c.synth_batch(SEED ^ skew, 11, m, n)
+    seed = SEED ^ (skew if isinstance(skew, int) else 77)
+    host = oracle_c.synth_batch(seed, 11, m, n)
     want = oracle_c.icrc_batch(host, stride=n, threads=16)
     out = _out(m)
     c.batch_device(_dev(host), m, out, stride=n, stream=_stream())
     np.testing.assert_array_equal(_host_u32(out), want)
-    rng = np.random.default_rng(count + skew)
+    rng = np.random.default_rng(count + (skew if isinstance(skew, int) else 77))
     lens = rng.choice(np.array([64, 256, 1024, 4096], np.uint32), size=count)
     offs = np.zeros(count, np.uint64)
     offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
