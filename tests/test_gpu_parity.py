@@ -503,8 +503,9 @@ def test_xcd_weighted_split(ctx_env, skew, count, grid):
     weights -- the product's defaults are 25 / 50 for the SCK, 40 for the
     ragged fold -- or RICRC_XCD_WEIGHTS, eight per-XCD weights, here lopsided
     ones), from the start XCD the kernels record: any weights give
-    contiguous per-wave ranges covering every group exactly once -- odd grids (the last workgroup even), waves with no groups, more
-    groups than the grid's waves -- on 4 KiB packets and on a ragged mix."""
+    contiguous per-wave ranges covering every group exactly once -- odd
+    grids (the last workgroup even), waves with no groups, more groups than
+    the grid's waves -- on 4 KiB packets and on a ragged mix."""
     env = {"RICRC_XCD_WEIGHTS": skew} if isinstance(skew, str) else {"RICRC_XCD_SKEW": skew}
     if grid is not None:
         env["RICRC_SCK_GRID"] = grid
