@@ -145,9 +145,11 @@ uint32_t ricrc_combine(uint32_t crc1, uint32_t crc2, uint64_t len2);
 /* ------------------------------------------------------------------ context
  * n_gpus > 0: use devices 0..n_gpus-1; n_gpus < 0: every visible device;
  * n_gpus == 0 -> -EINVAL.  No GPU -> -ENODEV (there is no CPU fallback).
- * The context owns per-device streams, staging buffers and kernel state; it
- * is not thread-safe (lock externally), exactly like the reference's
- * endpoint objects. */
+ * The context owns per-device streams, staging buffers and kernel state
+ * (including one pinned 64-byte word per device where the big kernels record
+ * which XCD their first workgroup ran on, a scheduling hint for the next
+ * launch); it is not thread-safe (lock externally), exactly like the
+ * reference's endpoint objects. */
 int ricrc_create(ricrc_ctx **ctx, int n_gpus);
 /* Same, on an explicit device list (one process per GPU: pass {LOCAL_RANK}). */
 int ricrc_create_devices(ricrc_ctx **ctx, const int *devices, int n);
