@@ -84,6 +84,20 @@ int main() {
     printf("fold generic (product)     %8.1f us\n", 1e3f * timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10));
     printf("fold specialized           %8.1f us\n", 1e3f * timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<131072>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10));
   }
+  // What the result stores cost the fold (ABL 32: result slots kept, no
+  // global stores; with the product's XCD weights), alternating.
+  if (getenv("FOLD_STORES")) {
+    for (int r = 0; r < 3; ++r) {
+      RsckArgs k = a;
+      for (int x = 0; x < 8; ++x) k.xw[x] = (x & 1) ? 960u : 1040u;
+      const float t0 = 1e3f * timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, 0, k); }, 10);
+      const float t1 = 1e3f * timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<32>), dim3(grid), dim3(kBlock), 0, 0, k); }, 10);
+      const float t2 = 1e3f * timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<3>), dim3(grid), dim3(kBlock), 0, 0, k); }, 10);
+      const float t3 = 1e3f * timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<35>), dim3(grid), dim3(kBlock), 0, 0, k); }, 10);
+      printf("stores, round %d: product %6.1f | no global stores %6.1f | memory path %6.1f | memory path, no global stores %6.1f us\n",
+             r, t0, t1, t2, t3);
+    }
+  }
   // Round 4: the product fold with its work split weighted by XCD parity
   // (a.xw by XCD parity, xcd_share), alternating.
   {
