@@ -26,7 +26,7 @@ static constexpr int kLdsWords = 32768;  // 128 KiB
 // shares are contiguous, in wave order, and cover [0, total) for any k; a
 // wrong k costs speed, never a packet.
 __device__ __forceinline__ void xcd_share(uint64_t total, const uint32_t (&w)[8], uint32_t k, uint32_t wid,
-                                          uint64_t &lo, uint64_t &hi, uint32_t wpb = kWaves) {  // wpb: sharing waves per workgroup
+                                          uint64_t &lo, uint64_t &hi) {
   const uint64_t b = blockIdx.x, nb = gridDim.x;
   uint64_t cyc = 0;
 #pragma unroll
@@ -37,8 +37,8 @@ __device__ __forceinline__ void xcd_share(uint64_t total, const uint32_t (&w)[8]
     return s;
   };
   const uint64_t wb = w[(b + k) & 7u];
-  const uint64_t before = (uint64_t)wpb * cum(b) + wid * wb;
-  const uint64_t wtot = (uint64_t)wpb * cum(nb);
+  const uint64_t before = (uint64_t)kWaves * cum(b) + wid * wb;
+  const uint64_t wtot = (uint64_t)kWaves * cum(nb);
   lo = total * before / wtot;
   hi = total * (before + wb) / wtot;
 }

@@ -456,9 +456,7 @@ __device__ __forceinline__ void static_for(F &&f) {
 // 8192 per-wave s_memrealtime start / end stamps, groups and first group into a.out
 // (4 words per wave; tools/microbench/bucket_abl.hip), 16384 no line loads, 32768 every
 // edge line through the head-line path (the round-3 session-23 fold), 131072
-// the fold specialized on the line count (round 4; tools/microbench/fold_var.hip),
-// 262144 15 folding waves per workgroup, 524288 15 folding waves and a
-// store wave (below).
+// the fold specialized on the line count (round 4; tools/microbench/fold_var.hip).
 template <int ABL>
 __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   // Result slots per wave (a round of 8 groups leaves in one store; a store
@@ -535,50 +533,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
     x2tl[threadIdx.x] = t2;
     x3tl[threadIdx.x] = t3;
   }
-  // Store wave (ABL 524288): waves 0..14 fold and leave each round of 64
-  // results in their LDS slots with a note in a mailbox; wave 15 only moves
-  // the rounds to HBM.  A global store holds back, in the in-order vmcnt,
-  // every load a folding wave queues after it until the store is
-  // acknowledged (the stores cost the fold ~30 us, tools/microbench/
-  // fold_var.hip); the store wave takes them out of the folding waves'
-  // queues.  Mailbox of wave w: words 4w..4w+2 of wave 15's area: state (0
-  // free, 1 a round waits in the slots, 2 the wave is done), first group,
-  // valid results.
-  constexpr bool kSW = (ABL & 524288) != 0;
-  uint32_t *mbox = tzl + kTzW + (kWaves - 1) * kWaveWords;
-  // mailbox states: release stores after the data they publish, acquire loads before using it
-  auto mb_get = [&](uint32_t i) -> uint32_t {
-    return __hip_atomic_load(mbox + i, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-  };
-  auto mb_put = [&](uint32_t i, uint32_t v) { __hip_atomic_store(mbox + i, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP); };
-  if (kSW && threadIdx.x < 64) mbox[threadIdx.x] = 0u;
   __syncthreads();
-
-  if (kSW && wid == kWaves - 1) {  // the store wave (wave-uniform): drain rounds until every folding wave is done
-    uint32_t spins = 0;
-    while (true) {
-      const uint32_t st = lane < kWaves - 1 ? mb_get(4 * lane) : 2u;
-      const uint64_t full = __ballot(st == 1u);
-      if (__ballot(st == 2u) == ~0ull) break;  // every folding wave done and drained
-      if (full == 0) {
-        if (++spins > (1u << 26)) break;  // bound (~seconds): a lost wave must not hang the GPU
-        __builtin_amdgcn_s_sleep(1);
-        continue;
-      }
-      uint64_t m = full;
-      while (m) {
-        const uint32_t w = (uint32_t)__builtin_ctzll(m);
-        m &= m - 1;
-        const uint32_t q0 = __builtin_amdgcn_readfirstlane(mbox[4 * w + 1]);
-        const uint32_t valid = __builtin_amdgcn_readfirstlane(mbox[4 * w + 2]);
-        const uint32_t v = tzl[kTzW + w * kWaveWords + lane];  // slot `lane` of wave w's round
-        if (lane == 0) mb_put(4 * w, 0u);                     // (release: after the read above)
-        const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.bres + 8ull * q0, 4u * valid);
-        __builtin_amdgcn_raw_buffer_store_b32(v, ro, 4u * lane, 0, 16);
-      }
-    }
-    return;
-  }
 
   // This wave's groups: those whose first line lies in its share of steps.
   // The big pool: NG groups, S weighted work (the bucket pass's packed
@@ -587,12 +542,8 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   const unsigned long long pool = a.ctr->pool;
   const uint32_t NG = (uint32_t)(pool & ((1ull << kRsGroupBits) - 1u));
   const uint64_t S = pool >> kRsGroupBits;
-  // (ABL 262144, timing only: 15 folding waves per workgroup, wave 15 idle --
-  // the cost of giving one wave another job.)
-  constexpr uint32_t kFoldWaves = (ABL & (262144 | 524288)) ? 15u : (uint32_t)kWaves;
-  if (wid >= kFoldWaves) return;  // (no barrier below)
-  const uint64_t wave = (uint64_t)blockIdx.x * kFoldWaves + wid;
-  const uint64_t nwaves = (uint64_t)gridDim.x * kFoldWaves;
+  const uint64_t wave = (uint64_t)blockIdx.x * kWaves + wid;
+  const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
   const uint64_t share = (S + nwaves - 1) / nwaves;
   // First group whose work starts at or after x (within the run holding x):
   // the pass block whose work range holds x (one ballot per 64 blocks), then
@@ -638,8 +589,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
     return q < gend ? (uint32_t)q : gend;
   };
   uint64_t x0 = wave * share < S ? wave * share : S, x1 = x0 + share;
-  if (a.xw[0] != 0u && (kSW || kFoldWaves == (uint32_t)kWaves))
-    xcd_share(S, a.xw, a.ctr->xcd, wid, x0, x1, kFoldWaves);  // weighted by XCD
+  if (a.xw[0] != 0u) xcd_share(S, a.xw, a.ctr->xcd, wid, x0, x1);  // weighted by XCD
   const uint32_t q_begin = first_group_at(x0), q_end = first_group_at(x1);
   if ((ABL & 8192) && lane == 0) {  // timing only: per-wave start stamp, groups, first group
     const uint32_t t_start = (uint32_t)__builtin_amdgcn_s_memrealtime();
@@ -648,17 +598,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
     a.out[4 * wave + 2] = q_end > q_begin ? q_end - q_begin : 0u;
     a.out[4 * wave + 3] = q_begin;
   }
-  auto mb_done = [&]() {  // the store wave: this wave has no more rounds (after its last one was taken)
-    if (kSW && lane == 0) {
-      uint32_t spins = 0;
-      while (mb_get(4 * wid) != 0u && ++spins < (1u << 26)) __builtin_amdgcn_s_sleep(1);
-      mb_put(4 * wid, 2u);
-    }
-  };
-  if (q_begin >= q_end) {
-    mb_done();
-    return;  // no barrier below
-  }
+  if (q_begin >= q_end) return;  // no barrier below
 
   const LaneTab lt{(lane & 31) << 2, ((lane & 31) << 2) | 0x10000u};
   const uint32_t *qrow = qtl + s * kQtStride;
@@ -693,14 +633,6 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
     const uint32_t valid = 8u * (q_stop - round_q0);
     const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.bres + 8ull * round_q0, 4u * valid);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the slot writes have landed
-    if (kSW) {  // the round to the store wave: note, then state 1
-      if (lane == 0) {
-        mbox[4 * wid + 1] = round_q0;
-        mbox[4 * wid + 2] = valid;
-        mb_put(4 * wid, 1u);  // (release: after the slots and the note)
-      }
-      return;
-    }
     if (ABL & 32) {
       sink ^= slots[lane] ^ slots[kSlots - 64 + lane];  // keep the slot reads
       return;
@@ -748,10 +680,6 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
     if (ABL & 16) {
       sink ^= R;  // keep the value live
       return;
-    }
-    if (kSW && q == round_q0) {  // a new round: the store wave must have taken the last one
-      uint32_t spins = 0;
-      while (__builtin_amdgcn_readfirstlane(mb_get(4 * wid)) != 0u && ++spins < (1u << 26)) __builtin_amdgcn_s_sleep(1);
     }
     slots[((q - round_q0) << 3) | g] = ~R;
     if (q + 1 - round_q0 == kRound) {  // wave-uniform
@@ -1167,7 +1095,6 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
     }
   }
   if (!(ABL & 16) && q_end != round_q0) flush(q_end);
-  mb_done();
   if ((ABL & 48) && sink == 0x12345678u) a.bres[0] = sink;
   if ((ABL & 8192) && lane == 0) {  // timing only: end stamp after every store has left
     __builtin_amdgcn_s_waitcnt(0);

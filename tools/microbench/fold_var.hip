@@ -87,18 +87,6 @@ int main() {
   // What the result stores cost the fold (ABL 32: result slots kept, no
   // global stores; with the product's XCD weights), alternating.
   if (getenv("FOLD_STORES")) {
-    {  // the store-wave fold (ABL 524288) against the product, results first
-      RsckArgs k = a;
-      for (int x = 0; x < 8; ++x) k.xw[x] = (x & 1) ? 960u : 1040u;
-      CK(hipMemset(a.res, 0, 4 * npos));
-      hipLaunchKernelGGL((icrc_rsck_kernel<524288>), dim3(grid), dim3(kBlock), 0, 0, k);
-      check("store-wave fold vs product");
-      for (int r = 0; r < 4; ++r) {
-        const float t0 = 1e3f * timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, 0, k); }, 10);
-        const float t1 = 1e3f * timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<524288>), dim3(grid), dim3(kBlock), 0, 0, k); }, 10);
-        printf("store wave, round %d: product %6.1f | 15 folding waves + a store wave %6.1f us\n", r, t0, t1);
-      }
-    }
     for (int r = 0; r < 2; ++r) {
       RsckArgs k = a;
       for (int x = 0; x < 8; ++x) k.xw[x] = (x & 1) ? 960u : 1040u;
@@ -108,13 +96,7 @@ int main() {
       const float t3 = 1e3f * timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<35>), dim3(grid), dim3(kBlock), 0, 0, k); }, 10);
       printf("stores, round %d: product %6.1f | no global stores %6.1f | memory path %6.1f | memory path, no global stores %6.1f us\n",
              r, t0, t1, t2, t3);
-      RsckArgs e = a;  // equal shares (the 15-wave variant has no XCD weights)
-      const float u0 = 1e3f * timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<65536>), dim3(grid), dim3(kBlock), 0, 0, e); }, 10);
-      const float u1 = 1e3f * timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<32>), dim3(grid), dim3(kBlock), 0, 0, e); }, 10);
-      const float u2 = 1e3f * timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<262144>), dim3(grid), dim3(kBlock), 0, 0, e); }, 10);
-      const float u3 = 1e3f * timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<262144 | 32>), dim3(grid), dim3(kBlock), 0, 0, e); }, 10);
-      printf("   equal shares: 16 waves %6.1f | 16 waves, no global stores %6.1f | 15 waves %6.1f | 15 waves, no global stores %6.1f us\n",
-             u0, u1, u2, u3);
+
     }
   }
   // Round 4: the product fold with its work split weighted by XCD parity
