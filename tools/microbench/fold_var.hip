@@ -87,6 +87,15 @@ int main() {
   // What the result stores cost the fold (ABL 32: result slots kept, no
   // global stores; with the product's XCD weights), alternating.
   if (getenv("FOLD_STORES")) {
+    for (int r = 0; r < 3; ++r) {  // round size: 64 vs 192 result slots per wave (both without the finish)
+      RsckArgs k = a;
+      for (int x = 0; x < 8; ++x) k.xw[x] = (x & 1) ? 960u : 1040u;
+      const float v0 = 1e3f * timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<2>), dim3(grid), dim3(kBlock), 0, 0, k); }, 10);
+      const float v1 = 1e3f * timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<2 | 512>), dim3(grid), dim3(kBlock), 0, 0, k); }, 10);
+      const float v2 = 1e3f * timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<2 | 32>), dim3(grid), dim3(kBlock), 0, 0, k); }, 10);
+      printf("no finish, round %d: 64 slots (8 groups per store) %6.1f | 192 slots (24 groups) %6.1f | no global stores %6.1f us\n",
+             r, v0, v1, v2);
+    }
     for (int r = 0; r < 2; ++r) {
       RsckArgs k = a;
       for (int x = 0; x < 8; ++x) k.xw[x] = (x & 1) ? 960u : 1040u;
