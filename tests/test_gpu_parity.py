@@ -428,6 +428,25 @@ def test_headline_full_size_bit_exact(ctx):
 
 
 @pytest.mark.slow
+def test_c3_grid_path_bit_exact(ctx):
+    """The strided-chain kernel on every CU (batches past 48 groups per wave
+    of 240 CUs, C3's path: 256 CUs, XCD weights 1050 / 950): 1,600,000 x
+    4096 B (6.6 GB, 200,000 groups) generated on the device, every ICRC
+    compared with the C oracle on the very same bytes (copied back)."""
+    import roce_icrc
+
+    count, n = 1_600_000, 4096
+    d = torch.empty(count * n, dtype=torch.uint8, device="cuda")
+    assert roce_icrc.kernel_path(d, count, stride=n, ctx=ctx) == "icrc_sck_kernel"
+    ctx.synth_device(d, SEED ^ 3, 0, count, n, stream=_stream())
+    out = _out(count)
+    ctx.batch_device(d, count, out, stride=n, stream=_stream())
+    got = _host_u32(out)
+    want = oracle_c.icrc_batch(d.cpu().numpy(), stride=n, threads=16)
+    np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.slow
 def test_c4_full_size_bit_exact(ctx):
     """BASELINE C4 at full size: 4,194,304 packets of 64/256/1024/4096 B
     (PCG64 on the bench seed, packed back to back, 5.7 GB) generated on the
