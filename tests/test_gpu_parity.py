@@ -428,6 +428,28 @@ def test_headline_full_size_bit_exact(ctx):
 
 
 @pytest.mark.slow
+def test_c2_full_size_bit_exact(ctx):
+    """BASELINE C2: 1,048,576 x 1024 B (the SCK's 4 KiB super-groups of four
+    packets) generated on the device, every ICRC compared with the C oracle
+    on the very same bytes, then every trailer stamped and verified."""
+    import roce_icrc
+
+    count, n = 1 << 20, 1024
+    d = torch.empty(count * n, dtype=torch.uint8, device="cuda")
+    assert roce_icrc.kernel_path(d, count, stride=n, ctx=ctx) == "icrc_sck_kernel"
+    ctx.synth_device(d, SEED ^ 2, 0, count, n, stream=_stream())
+    out = _out(count)
+    ctx.batch_device(d, count, out, stride=n, stream=_stream())
+    got = _host_u32(out)
+    host = d.cpu().numpy()
+    np.testing.assert_array_equal(got, oracle_c.icrc_batch(host, stride=n, threads=16))
+    host.reshape(count, n)[:, n - 4:] = got.view(np.uint8).reshape(count, 4)
+    d.copy_(torch.from_numpy(host))
+    ctx.batch_device(d, count, out, stride=n, stream=_stream(), verify=True)
+    assert int(_host_u32(out).sum()) == count
+
+
+@pytest.mark.slow
 def test_c3_grid_path_bit_exact(ctx):
     """The strided-chain kernel on every CU (batches past 48 groups per wave
     of 240 CUs, C3's path: 256 CUs, XCD weights 1050 / 950): 1,600,000 x
