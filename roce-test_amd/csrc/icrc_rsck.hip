@@ -456,7 +456,9 @@ __device__ __forceinline__ void static_for(F &&f) {
 // 8192 per-wave s_memrealtime start / end stamps, groups and first group into a.out
 // (4 words per wave; tools/microbench/bucket_abl.hip), 16384 no line loads, 32768 every
 // edge line through the head-line path (the round-3 session-23 fold), 131072
-// the fold specialized on the line count (round 4; tools/microbench/fold_var.hip).
+// the fold specialized on the line count (round 4; tools/microbench/fold_var.hip),
+// 262144 each result stored straight to out[i], with a.pos_of holding the big
+// pool's packet indexes (the "no gather" layout; tools/microbench/no_gather.hip).
 template <int ABL>
 __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   // Result slots per wave (a round of 8 groups leaves in one store; a store
@@ -629,8 +631,20 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   };
   uint32_t round_q0 = q_begin;  // first group of the current round of result slots
   uint32_t sink = 0;             // timing ablations: values kept live
+  // (ABL 262144: the round's packet indexes, one per lane, loaded a round ahead)
+  uint32_t idx_r = 0;
+  if (ABL & 262144) idx_r = a.pos_of[8ull * q_begin + lane < npos ? 8ull * q_begin + lane : npos - 1];
   auto flush = [&](uint32_t q_stop) {  // groups [round_q0, q_stop) of the round
     const uint32_t valid = 8u * (q_stop - round_q0);
+    if (ABL & 262144) {
+      static_assert(!(ABL & 262144) || kSlots == 64, "one result per lane");
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+      const uint32_t v = slots[lane];
+      if (lane < valid) a.out[idx_r] = v;
+      const uint64_t nx = 8ull * q_stop + lane;
+      idx_r = a.pos_of[nx < npos ? nx : npos - 1];
+      return;
+    }
     const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.bres + 8ull * round_q0, 4u * valid);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the slot writes have landed
     if (ABL & 32) {
