@@ -147,15 +147,9 @@ __device__ __forceinline__ T wave_scan(T v) {
 // Blocks whose packets take several rounds re-read them for step 4 (ranks
 // from a second LDS cursor: any order of ranks is a valid layout) and store
 // from the registers.
-// A staged block does not wait for its reservation (step 3) before it builds
-// its layout: the LDS layout is block-local, and only the final stores, the
-// block record and the runs need the pool positions, so the reservation's two
-// device-scope atomics (256 blocks on one counter each) stay in flight while
-// the layout is built.
 // ABL (timing-only ablations, tools/microbench/bucket_abl.hip): 1 stop after
 // the ranking round, 2 no LDS atomics (rank 0), 4 stop after the reservation,
-// 8 no pos_of stores, 16 no descriptor stores, 32 no LDS staging, 64 wait for
-// the reservation before the layout (the round-3 order).
+// 8 no pos_of stores, 16 no descriptor stores, 32 no LDS staging.
 // LDS layout entries of a block: a round's packets + room for group padding
 __host__ __device__ constexpr uint32_t stage_entries(int U) { return (uint32_t)U * kPassBlock + 512u; }
 template <bool OFF, bool LEN, int ABL = 0, int U = kPassUnroll>
@@ -252,40 +246,26 @@ __global__ __launch_bounds__(kPassBlock) void rsck_bucket(RsckArgs a) {
     jf += wf[w];
     iw += ww[w];
   }
-  // Block totals: thread `last` reserves the ranges.  publish() waits for the
-  // reservation and writes its results into LDS and the block record.
-  const uint32_t last = blockDim.x - 1;
-  constexpr bool late = !(ABL & 64);
-  unsigned long long res_pool = 0ull;
-  uint32_t res_small = 0u;
-  auto publish = [&] {
-    blk_g0 = (uint32_t)(res_pool & ((1ull << kRsGroupBits) - 1u));
-    blk_s0 = res_pool >> kRsGroupBits;
-    blk_small = res_small;
-    const bool st = !(ABL & 32) && one && is + 8u * ig <= kStage;
-    a.blk[blockIdx.x] = RsBlock{blk_g0, ig, ig ? jf : 0u, blk_small, is, st ? 1u : 0u, blk_s0, iw};
-  };
-  if (t == last) {
-    res_pool = ig ? atomicAdd(&a.ctr->pool, ((unsigned long long)iw << kRsGroupBits) | ig) : 0ull;
-    res_small = is ? atomicAdd(&a.ctr->small, is) : 0u;
+  if (t == blockDim.x - 1) {  // block totals: reserve the ranges
+    const unsigned long long old =
+        ig ? atomicAdd(&a.ctr->pool, ((unsigned long long)iw << kRsGroupBits) | ig) : 0ull;
+    blk_g0 = (uint32_t)(old & ((1ull << kRsGroupBits) - 1u));
+    blk_s0 = old >> kRsGroupBits;
+    blk_small = is ? atomicAdd(&a.ctr->small, is) : 0u;
     blk_stot = is;
     blk_total = is + 8u * ig;
-    if (!late) publish();
+    const bool st = !(ABL & 32) && one && is + 8u * ig <= kStage;
+    a.blk[blockIdx.x] = RsBlock{blk_g0, ig, ig ? jf : 0u, blk_small, is, st ? 1u : 0u, blk_s0, iw};
   }
   __syncthreads();
   const uint32_t Stot = blk_stot, total = blk_total;
   const bool staged = !(ABL & 32) && one && total <= kStage;  // block-uniform
-  const bool early = !late || !staged;                         // block-uniform: pool positions needed now
-  if (late && !staged) {
-    if (t == last) publish();
-    __syncthreads();
-  }
   // at[c]: the class's first position -- in the LDS layout when staged, else in its pool
   if (t < (uint32_t)kRsClasses)
     at[t] = staged ? (big ? Stot + 8u * (ig - G) : is - Sm) : big ? 8u * (blk_g0 + ig - G) : blk_small + is - Sm;
-  if (early && f) a.runs[(uint64_t)blockIdx.x * kRsRuns + (jf - 1u)] = RsRun{blk_g0 + ig - G, G, L, 0u, blk_s0 + iw - W};
+  if (f) a.runs[(uint64_t)blockIdx.x * kRsRuns + (jf - 1u)] = RsRun{blk_g0 + ig - G, G, L, 0u, blk_s0 + iw - W};
   __syncthreads();
-  if (ABL & 4) {  // (late, staged: the reservation issued, not awaited)
+  if (ABL & 4) {
     uint32_t x = 0;
 #pragma unroll
     for (int k = 0; k < U; ++k) x ^= cr[k] ^ dlo[k] ^ dhi[k];
@@ -315,6 +295,7 @@ __global__ __launch_bounds__(kPassBlock) void rsck_bucket(RsckArgs a) {
     }
   };
   if (staged) {  // block-uniform: the round's descriptors are still in registers
+    const uint32_t big0 = 8u * blk_g0, small0 = blk_small;
 #pragma unroll
     for (int k = 0; k < U; ++k) {
       const uint32_t i = lo + (uint32_t)k * blockDim.x + threadIdx.x;
@@ -328,11 +309,8 @@ __global__ __launch_bounds__(kPassBlock) void rsck_bucket(RsckArgs a) {
       if (bc && rk + 1u == h[c])  // the class's last packet pads its run's last group with copies of itself
         for (uint32_t q = lp + 1u; (q - Stot) & 7u; ++q) stage[q] = d;
     }
-    if (late && t == last) publish();  // the reservation has been in flight since the scan
     __syncthreads();
-    if (late && f) a.runs[(uint64_t)blockIdx.x * kRsRuns + (jf - 1u)] = RsRun{blk_g0 + ig - G, G, L, 0u, blk_s0 + iw - W};
     if (ABL & 16) return;
-    const uint32_t big0 = 8u * blk_g0, small0 = blk_small;
     uint64_t *sm = reinterpret_cast<uint64_t *>(a.desc) + small0;
     uint64_t *bg = reinterpret_cast<uint64_t *>(a.bdesc) + big0 - Stot;
     // streaming stores: the folds that follow read these once, and dirty
