@@ -458,9 +458,7 @@ __device__ __forceinline__ void static_for(F &&f) {
 // edge line through the head-line path (the round-3 session-23 fold), 131072
 // the fold specialized on the line count (round 4; tools/microbench/fold_var.hip),
 // 262144 each result stored straight to out[i], with a.pos_of holding the big
-// pool's packet indexes (the "no gather" layout; tools/microbench/no_gather.hip),
-// 524288 line loads with the default cache policy, 1048576 the same for the
-// packets' first and last lines only (tools/microbench/fold_policy.hip).
+// pool's packet indexes (the "no gather" layout; tools/microbench/no_gather.hip).
 template <int ABL>
 __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   // Result slots per wave (a round of 8 groups leaves in one store; a store
@@ -774,8 +772,6 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
     // (ABL 16384, timing only: no line loads, a value derived from the address)
     auto line_load = [&](uint64_t addr) -> u32x4 {
       if (ABL & 16384) return u32x4{(uint32_t)addr, (uint32_t)(addr >> 7), lane, (uint32_t)addr * 3u};
-      if (ABL & 524288) return gload16(addr);
-      if ((ABL & 1048576) && (ld_k == 0 || ld_k + 1 == ld_L)) return gload16(addr);  // wave-uniform
       return gload16_nt(addr);
     };
     auto ld_issue = [&]() -> u32x4 { return line_load(ld.line0 + 128ull * ld_k); };
