@@ -437,7 +437,6 @@ __device__ __forceinline__ uint32_t edge_word(uint32_t w, int rel, int M) {
 
 }  // namespace
 
-constexpr uint32_t cgcd(uint32_t a, uint32_t b) { return b == 0u ? a : cgcd(b, a % b); }
 // f(integral_constant<0>), ..., f(integral_constant<N - 1>), unrolled.
 template <class F, uint32_t... I>
 __device__ __forceinline__ void static_for_impl(F &&f, std::integer_sequence<uint32_t, I...>) {
@@ -448,24 +447,18 @@ __device__ __forceinline__ void static_for(F &&f) {
   static_for_impl(f, std::make_integer_sequence<uint32_t, N>{});
 }
 
-// ABL (timing-only ablations, tools/microbench/rsck_abl.hip): 1 no table
-// fold, 2 no finish, 4 descriptors by arithmetic (uniform batch in natural
-// order: packet 8 q + g at base + (8 q + g) stride, no descriptor ring),
-// 8 no edge masks, 16 no result slots / stores, 32 no global stores (slots kept),
-// 512 (with 2) 192 result slots, 1024 / 2048 / 4096 result stores nt / default / sc0 sc1,
-// 8192 per-wave s_memrealtime start / end stamps, groups and first group into a.out
-// (4 words per wave; tools/microbench/bucket_abl.hip), 16384 no line loads, 32768 every
-// edge line through the head-line path (the round-3 session-23 fold), 131072
-// the fold specialized on the line count (round 4; tools/microbench/fold_var.hip),
-// 262144 each result stored straight to out[i], with a.pos_of holding the big
-// pool's packet indexes (the "no gather" layout; tools/microbench/no_gather.hip).
+// ABL (timing-only ablations, tools/microbench/shard.hip, bucket_abl.hip,
+// fold_var.hip): 1 no table fold, 2 no finish, 8 no edge masks, 16 no result
+// slots / stores, 32 no global stores (slots kept), 16384 no line loads,
+// 524288 per-wave s_memrealtime stamps (entry, tables built, work split
+// found, end) and the wave's groups into a.out, 8 words per wave.
 template <int ABL>
 __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   // Result slots per wave (a round of 8 groups leaves in one store; a store
   // holds back every load queued behind it in vmcnt until its write is
   // acknowledged: the stores cost ~4 % of the fold on a 4 GiB mix, the same
   // for rounds of 8 or 16 groups and 4- or 8-byte stores, rsck_abl.hip).
-  constexpr uint32_t kSlots = (ABL & 512) ? 192 : 64, kRound = kSlots / 8;
+  constexpr uint32_t kSlots = 64, kRound = kSlots / 8;
   constexpr uint32_t kBlk = 128;                          // words per descriptor block (8 groups x 8 x 8 B)
   constexpr uint32_t kWaveWords = kSlots + 2 * kBlk + 64;  // slots | 2-block ring | 8-group info FIFO
   // lines in flight per wave: 6 (with the quiet blocks below, 8 lines in
@@ -476,14 +469,11 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   // Finish tables first, so every lookup's constant part fits a ds_read's
   // 16-bit offset: x^-32 nibble table (128 words) | x^(-128 s) nibble tables
   // (8 x 132 words: rows padded by 4 words so the 8 lane slots spread over
-  // the banks) | 128 KiB slice-by-4 tables | 1 KiB tz bases | 1.5 KiB per
-  // wave = 157.7 KiB.
-  // (ABL 512, timing only, with 2: 192 result slots per wave in the room of
-  // the finish tables.)
-  // (+ x^-64 and x^-96 nibble tables, 2 x 128 words, after the head masks)
-  constexpr uint32_t kQtStride = 132, kSmallWords = (ABL & 512) ? 0 : 128 + 8 * kQtStride + 32 + 256;  // 1472: a multiple of 32 words
-  constexpr uint32_t kTzW = (ABL & 512) ? 0 : kTzWords;
-  __shared__ uint32_t lds[kSmallWords + kLdsWords + kTzW + kWaves * kWaveWords];
+  // the banks) | head masks (32 words) | x^-64, x^-96 nibble tables (2 x 128
+  // words) | 128 KiB slice-by-4 tables | 1 KiB tz bases | 1.5 KiB per wave =
+  // 157.7 KiB.
+  constexpr uint32_t kQtStride = 132, kSmallWords = 128 + 8 * kQtStride + 32 + 256;  // 1472: a multiple of 32 words
+  __shared__ uint32_t lds[kSmallWords + kLdsWords + kTzWords + kWaves * kWaveWords];
   uint32_t *xtl = lds;
   uint32_t *qtl = lds + 128;
   uint32_t *etl = lds + 128 + 8 * kQtStride;  // whole-word head masks: (or, xor) of word k = rel / 4
@@ -494,12 +484,73 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t s = lane & 7, g = lane >> 3;
+  const uint32_t t_entry = (ABL & 524288) ? (uint32_t)__builtin_amdgcn_s_memrealtime() : 0u;
 
+  // Everything a wave needs from memory before it can stream is requested at
+  // once, ahead of the table build: its table entries, the counters and
+  // every pass block's work range.  The work split then costs one more round
+  // trip (the runs of the two pass blocks holding the wave's share ends),
+  // issued before the table build too, and the wave's first descriptors and
+  // lines are in flight before the workgroup barrier.  (The round-4 fold
+  // chased blocks and runs through up to a dozen dependent loads after the
+  // barrier: at C4's 8-GPU shard its waves found their share 11 us after
+  // entry at the median, 27 us at worst, tools/microbench/shard.hip,
+  // profiles/r05/s1_mb_shard_baseline.txt.)
   const uint32_t tab_v = table_entry(g_tab128);
   const uint32_t tz_v = a.tzb[threadIdx.x < kTzWords ? threadIdx.x : 0];
+  const RsCounters C = *a.ctr;
+  constexpr int kBq = kPassBlocks / 64;  // pass blocks per lane
+  uint64_t bs0[kBq], bwk[kBq];
+  uint32_t brn[kBq];
+#pragma unroll
+  for (int k = 0; k < kBq; ++k) {  // unconditional loads, index clamped: issued back to back
+    const uint32_t bb = 64u * (uint32_t)k + lane;
+    const RsBlock *B = a.blk + (bb < a.nblk ? bb : 0u);
+    bs0[k] = B->s0;
+    bwk[k] = B->work;
+    brn[k] = B->runs;
+  }
+  // The big pool: NG groups, S weighted work (the bucket pass's packed
+  // counter); block b's groups [g0, g0 + groups) hold work [s0, s0 + work),
+  // its runs split that range by class.
+  const uint32_t NG = (uint32_t)(C.pool & ((1ull << kRsGroupBits) - 1u));
+  const uint64_t S = C.pool >> kRsGroupBits;
+  if (NG == 0) return;  // no packet of >= 2 lines: every wave leaves here (no barrier above)
+#pragma unroll
+  for (int k = 0; k < kBq; ++k) brn[k] = 64u * (uint32_t)k + lane < a.nblk ? brn[k] : 0u;
+  // This wave's groups: those whose first line lies in its share of the work.
+  const uint64_t wave = (uint64_t)blockIdx.x * kWaves + wid;
+  const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
+  const uint64_t share = (S + nwaves - 1) / nwaves;
+  uint64_t x0 = wave * share < S ? wave * share : S, x1 = x0 + share;
+  if (a.xw[0] != 0u) xcd_share(S, a.xw, C.xcd, wid, x0, x1);  // weighted by XCD
+  // the pass block whose work range holds x (ballots over the loaded ranges)
+  auto block_of = [&](uint64_t x) -> uint32_t {
+    uint32_t b = 0;
+#pragma unroll
+    for (int k = 0; k < kBq; ++k) {
+      const uint64_t m = __ballot(brn[k] != 0u && bs0[k] <= x && x - bs0[k] < bwk[k]);
+      if (m) b = 64u * (uint32_t)k + (uint32_t)__builtin_ctzll(m);
+    }
+    return __builtin_amdgcn_readfirstlane(b);
+  };
+  auto runs_of = [&](uint32_t b) -> uint32_t {  // (scalar selects: a VGPR select became a scratch array)
+    uint32_t v = 0;
+#pragma unroll
+    for (int k = 0; k < kBq; ++k) {
+      const uint32_t c = __builtin_amdgcn_readlane(brn[k], b & 63u);
+      v = (b >> 6) == (uint32_t)k ? c : v;
+    }
+    return v;
+  };
+  const uint32_t b0 = block_of(x0), b1 = block_of(x1);
+  const uint32_t n0 = runs_of(b0), n1 = runs_of(b1);
+  const RsRun *R0 = a.runs + (uint64_t)b0 * kRsRuns, *R1 = a.runs + (uint64_t)b1 * kRsRuns;
+  RsRun Q0 = R0[lane < n0 ? lane : 0u], Q1 = R1[lane < n1 ? lane : 0u];  // both in flight during the table build
+
   table_store(tab, tab_v);
-  if (!(ABL & 512) && threadIdx.x < kTzWords) tzl[threadIdx.x] = tz_v;
-  if (!(ABL & 512)) {  // entry (s, w, v) = (nibble v at bits 4w..4w+3) * x^(-128 s), where bit
+  if (threadIdx.x < kTzWords) tzl[threadIdx.x] = tz_v;
+  {  // entry (s, w, v) = (nibble v at bits 4w..4w+3) * x^(-128 s), where bit
      // j of a value stands for QS[s] x^(31 - j)
     const uint32_t bs = threadIdx.x >> 7, w = (threadIdx.x >> 4) & 7u, v = threadIdx.x & 15u;
     uint32_t p = a.QS[0];
@@ -514,13 +565,13 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
     }
     qtl[bs * kQtStride + 16u * w + v] = e;
   }
-  if (!(ABL & 512) && threadIdx.x < 16) {  // word k of the header (rel = 4k): IPv4 invariant fields -> 0xFF, the seed at 0
+  if (threadIdx.x < 16) {  // word k of the header (rel = 4k): IPv4 invariant fields -> 0xFF, the seed at 0
     const uint32_t k = threadIdx.x;
     const uint32_t orm = k == 0 ? kMaskW0 : k == 2 ? kMaskW2 : k == 6 ? kMaskW6 : k == 8 ? kMaskW8 : 0u;
     etl[2 * k] = orm;
     etl[2 * k + 1] = k == 0 ? kSeed : 0u;
   }
-  if (!(ABL & 512) && threadIdx.x < 128) {  // entry 16 w + v: (nibble v at bits 4w..4w+3) * x^-32
+  if (threadIdx.x < 128) {  // entry 16 w + v: (nibble v at bits 4w..4w+3) * x^-32
     const uint32_t w = threadIdx.x >> 4, v = threadIdx.x & 15u;
     uint32_t t = 0;
 #pragma unroll
@@ -535,76 +586,36 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
     x2tl[threadIdx.x] = t2;
     x3tl[threadIdx.x] = t3;
   }
-  __syncthreads();
 
-  // This wave's groups: those whose first line lies in its share of steps.
-  // The big pool: NG groups, S weighted work (the bucket pass's packed
-  // counter); block b's groups [g0, g0 + groups) hold work [s0, s0 + work),
-  // its runs split that range by class.
-  const unsigned long long pool = a.ctr->pool;
-  const uint32_t NG = (uint32_t)(pool & ((1ull << kRsGroupBits) - 1u));
-  const uint64_t S = pool >> kRsGroupBits;
-  const uint64_t wave = (uint64_t)blockIdx.x * kWaves + wid;
-  const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
-  const uint64_t share = (S + nwaves - 1) / nwaves;
-  // First group whose work starts at or after x (within the run holding x):
-  // the pass block whose work range holds x (one ballot per 64 blocks), then
-  // its run (one ballot per 64 runs).
-  auto first_group_at = [&](uint64_t x) -> uint32_t {
-    if (x >= S) return NG;
-    uint32_t b = 0;
-    for (uint32_t b0 = 0; b0 < a.nblk; b0 += 64) {
-      const uint32_t bb = b0 + lane;
-      bool in = false;
-      if (bb < a.nblk) {
-        const RsBlock B = a.blk[bb];
-        in = B.runs != 0u && B.s0 <= x && x - B.s0 < B.work;
-      }
-      const uint64_t m = __ballot(in);
+  // First group whose work starts at or after x: the run of the pass block
+  // (b, its nr runs at R; Q = this lane's run of the first 64) holding x.
+  auto group_at = [&](uint64_t x, uint32_t nr, const RsRun *R, RsRun Q) -> uint32_t {
+    if (x >= S) return NG;  // wave-uniform
+    for (uint32_t r0 = 0; r0 < nr; r0 += 64) {  // (more than 64 classes in one pass block: rare)
+      if (r0 != 0) Q = R[r0 + lane < nr ? r0 + lane : r0];
+      const uint64_t m = __ballot(r0 + lane < nr && Q.s0 <= x &&
+                                  x - Q.s0 < (uint64_t)Q.groups * (4u * Q.L + a.group_cost));
       if (m) {  // wave-uniform
-        b = b0 + (uint32_t)__builtin_ctzll(m);
-        break;
+        const uint32_t r = (uint32_t)__builtin_ctzll(m);
+        const uint32_t g0 = __builtin_amdgcn_readlane(Q.g0, r), gs = __builtin_amdgcn_readlane(Q.groups, r);
+        const uint32_t L = __builtin_amdgcn_readlane(Q.L, r);
+        const uint64_t s0 = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(Q.s0 >> 32), r) << 32) |
+                            __builtin_amdgcn_readlane((uint32_t)Q.s0, r);
+        const uint64_t w = 4u * L + a.group_cost;  // quarter line-steps
+        const uint64_t q = g0 + (x - s0 + w - 1) / w;
+        const uint32_t gend = g0 + gs < NG ? g0 + gs : NG;  // (never past the pool)
+        return q < gend ? (uint32_t)q : gend;
       }
     }
-    b = __builtin_amdgcn_readfirstlane(b);
-    const uint32_t nr = a.blk[b].runs;
-    const RsRun *R = a.runs + (uint64_t)b * kRsRuns;
-    uint32_t r = 0;
-    for (uint32_t r0 = 0; r0 < nr; r0 += 64) {
-      const uint32_t rr = r0 + lane;
-      bool in = false;
-      if (rr < nr) {
-        const RsRun Q = R[rr];
-        in = Q.s0 <= x && x - Q.s0 < (uint64_t)Q.groups * (4u * Q.L + a.group_cost);
-      }
-      const uint64_t m = __ballot(in);
-      if (m) {  // wave-uniform
-        r = r0 + (uint32_t)__builtin_ctzll(m);
-        break;
-      }
-    }
-    r = __builtin_amdgcn_readfirstlane(r);
-    const RsRun Q = R[r];
-    const uint64_t w = 4u * Q.L + a.group_cost;  // quarter line-steps
-    const uint64_t q = Q.g0 + (x - Q.s0 + w - 1) / w;
-    const uint32_t gend = Q.g0 + Q.groups < NG ? Q.g0 + Q.groups : NG;  // (never past the pool)
-    return q < gend ? (uint32_t)q : gend;
+    return NG;  // (not reached: x < S lies in a run)
   };
-  uint64_t x0 = wave * share < S ? wave * share : S, x1 = x0 + share;
-  if (a.xw[0] != 0u) xcd_share(S, a.xw, a.ctr->xcd, wid, x0, x1);  // weighted by XCD
-  const uint32_t q_begin = first_group_at(x0), q_end = first_group_at(x1);
-  if ((ABL & 8192) && lane == 0) {  // timing only: per-wave start stamp, groups, first group
-    const uint32_t t_start = (uint32_t)__builtin_amdgcn_s_memrealtime();
-    a.out[4 * wave] = t_start;
-    a.out[4 * wave + 1] = t_start;
-    a.out[4 * wave + 2] = q_end > q_begin ? q_end - q_begin : 0u;
-    a.out[4 * wave + 3] = q_begin;
-  }
-  if (q_begin >= q_end) return;  // no barrier below
+  const uint32_t q_begin = group_at(x0, n0, R0, Q0), q_end = group_at(x1, n1, R1, Q1);
+  const uint32_t t_split = (ABL & 524288) ? (uint32_t)__builtin_amdgcn_s_memrealtime() : 0u;
+  const bool work = q_begin < q_end;  // wave-uniform
 
   const LaneTab lt{(lane & 31) << 2, ((lane & 31) << 2) | 0x10000u};
   const uint32_t *qrow = qtl + s * kQtStride;
-  uint32_t *slots = tzl + kTzW + wid * kWaveWords;
+  uint32_t *slots = tzl + kTzWords + wid * kWaveWords;
   uint32_t *dring = slots + kSlots;
   uint32_t *fifo = dring + 2 * kBlk;
   const uint64_t npos = 8ull * NG;
@@ -629,32 +640,88 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   auto put_block = [&](uint32_t b, const u32x2 &v) {
     *reinterpret_cast<u32x2 *>(dring + (b & 1u) * kBlk + 2u * lane) = v;
   };
+  const uint32_t qb = q_begin, qe = q_end;
+  struct LInfo {
+    uint64_t line0;  // lane's slot in the packet's first line
+  };
+  // Load cursor enters group q: line base, L, and (a, M) into the FIFO.
+  auto ld_enter = [&](uint32_t q, LInfo &li) -> uint32_t {
+    const u32x2 d = *reinterpret_cast<const u32x2 *>(dring + ((q >> 3) & 1u) * kBlk + 2u * (8u * (q & 7u) + g));
+    const uint64_t addr = ((uint64_t)(d[1] & 0xFFFFu) << 32) | d[0];
+    const uint32_t gM = (d[1] >> 16) - 4u;
+    const uint32_t ga = (uint32_t)addr & 127u;
+    li.line0 = (addr & ~127ull) + 16u * s;
+    fifo[((q & 7u) << 3) | g] = (gM << 7) | ga;
+    return __builtin_amdgcn_readfirstlane((ga + gM + 127u) >> 7);  // equal within a group
+  };
+  // (ABL 16384, timing only: no line loads, a value derived from the address)
+  auto line_load = [&](uint64_t addr) -> u32x4 {
+    if (ABL & 16384) return u32x4{(uint32_t)addr, (uint32_t)(addr >> 7), lane, (uint32_t)addr * 3u};
+    return gload16_nt(addr);
+  };
+  LInfo ld;
+  u32x2 NB = {0u, 0u};
+  uint32_t ld_q = qb, ld_k = 0, ld_L = 1;
+  auto ld_issue = [&]() -> u32x4 { return line_load(ld.line0 + 128ull * ld_k); };
+  auto ld_advance = [&]() {
+    if (++ld_k == ld_L) {  // wave-uniform
+      ld_k = 0;
+      if (ld_q + 1 < qe) {
+        ++ld_q;
+        if ((ld_q & 7u) == 0) {
+          put_block((ld_q >> 3) + 1, NB);
+          NB = load_block((ld_q >> 3) + 2);
+        }
+        ld_L = ld_enter(ld_q, ld);
+      } else {
+        ld_L = 1;  // done: re-read line 0 of the last group (ld_k wraps to 0 every step)
+      }
+    }
+  };
+  // The wave's first descriptor blocks and D lines, requested before the
+  // barrier: they arrive while the other waves finish the tables.
+  u32x4 ring[D];
+  if (work) {  // wave-uniform
+    const uint32_t b = qb >> 3;
+    put_block(b, load_block(b));
+    put_block(b + 1, load_block(b + 1));
+    NB = load_block(b + 2);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    ld_L = ld_enter(ld_q, ld);
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      __builtin_amdgcn_sched_barrier(0);
+      ring[u] = ld_issue();
+      ld_advance();
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  __syncthreads();  // the tables are built
+  const uint32_t t_tab = (ABL & 524288) ? (uint32_t)__builtin_amdgcn_s_memrealtime() : 0u;
+  const uint64_t wave8 = 8ull * wave;
+  if ((ABL & 524288) && lane == 0) {
+    a.out[wave8] = t_entry;
+    a.out[wave8 + 1] = t_tab;
+    a.out[wave8 + 2] = t_split;
+    a.out[wave8 + 3] = t_split;
+    a.out[wave8 + 4] = work ? q_end - q_begin : 0u;
+    a.out[wave8 + 5] = q_begin;
+  }
+  if (!work) return;
+
   uint32_t round_q0 = q_begin;  // first group of the current round of result slots
   uint32_t sink = 0;             // timing ablations: values kept live
-  // (ABL 262144: the round's packet indexes, one per lane, loaded a round ahead)
-  uint32_t idx_r = 0;
-  if (ABL & 262144) idx_r = a.pos_of[8ull * q_begin + lane < npos ? 8ull * q_begin + lane : npos - 1];
+  uint32_t done_work = 0;        // (ABL 524288: the work of the wave's groups)
   auto flush = [&](uint32_t q_stop) {  // groups [round_q0, q_stop) of the round
     const uint32_t valid = 8u * (q_stop - round_q0);
-    if (ABL & 262144) {
-      static_assert(!(ABL & 262144) || kSlots == 64, "one result per lane");
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-      const uint32_t v = slots[lane];
-      if (lane < valid) a.out[idx_r] = v;
-      const uint64_t nx = 8ull * q_stop + lane;
-      idx_r = a.pos_of[nx < npos ? nx : npos - 1];
-      return;
-    }
     const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.bres + 8ull * round_q0, 4u * valid);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the slot writes have landed
     if (ABL & 32) {
-      sink ^= slots[lane] ^ slots[kSlots - 64 + lane];  // keep the slot reads
+      sink ^= slots[lane];  // keep the slot reads
       return;
     }
-#pragma unroll
-    for (uint32_t h = 0; h < kSlots / 64; ++h)  // slots past `valid` fall outside the range check
-      __builtin_amdgcn_raw_buffer_store_b32(slots[64 * h + lane], ro, 4u * (64 * h + lane), 0,
-                                            (ABL & 1024) ? 2 : (ABL & 2048) ? 0 : (ABL & 4096) ? 17 : 16);
+    // slots past `valid` fall outside the range check
+    __builtin_amdgcn_raw_buffer_store_b32(slots[lane], ro, 4u * lane, 0, 16);
   };
   // A group's finish: its chain registers rr (after its last line), L lines,
   // first-byte offsets ga and covered lengths gM of its 8 packets (per lane
@@ -691,6 +758,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
       }
       R = group_xor(p, 3);
     }
+    if (ABL & 524288) done_work += 4u * Lg + a.group_cost;
     if (ABL & 16) {
       sink ^= R;  // keep the value live
       return;
@@ -702,207 +770,142 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
     }
   };
 
+  // The fold over groups [qb, qe): any mix of line counts, byte- or
+  // word-granular edges (two cursors, quiet blocks).
+  uint32_t fd_q = qb, fd_k = 0, fd_L, fd_a, fd_M;
+  auto fd_enter = [&](uint32_t q) {
+    const uint32_t v = fifo[((q & 7u) << 3) | g];
+    fd_a = v & 127u;
+    fd_M = v >> 7;
+    fd_L = __builtin_amdgcn_readfirstlane((fd_a + fd_M + 127u) >> 7);
+  };
+  fd_enter(fd_q);
+  // head lines of the group: 2 when some packet's header runs into line 1 (a
+  // plain uint32 so the edge test below is SALU arithmetic and one branch:
+  // short-circuit || on a ballot-derived bool compiled to five branches per
+  // step, and C4's fold ran 1.5 % slower)
+  uint32_t fd_hl = __ballot(fd_a > 88u) != 0 ? 2u : 1u;
+  // edge line <=> fd_k < fd_hl or fd_k == fd_L - 1 <=> (fd_k - fd_hl) >= fd_span, unsigned
+  uint32_t fd_span = fd_L - 1u > fd_hl ? fd_L - 1u - fd_hl : 0u;  // 0: every line is an edge line
 
-  // The generic fold over groups [qb, qe): any mix of line counts, byte- or
-  // word-granular edges (round 3's fold: two cursors, quiet blocks).
-  auto generic = [&](uint32_t qb, uint32_t qe) {
-    u32x2 NB = {0u, 0u};
-    if (!(ABL & 4)) {
-      const uint32_t b = qb >> 3;
-      put_block(b, load_block(b));
-      put_block(b + 1, load_block(b + 1));
-      NB = load_block(b + 2);
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+  uint32_t r[4] = {0u, 0u, 0u, 0u};
+  // Two copies of the fold loop: one with whole-word edges when the bucket
+  // pass found every strided-chain packet word-aligned in start and length
+  // (a per-group choice inside the loop made the compiler rotate the load
+  // ring through copies and drain vmcnt(0) at the loop head).
+  // The fold keeps xr = r ^ (the current line's word), the lookup input: the
+  // XOR with the next line's word rides in the step's last 3-input XOR (as in
+  // the SCK), 4 VALU per line fewer.  An edge line corrects xr by
+  // w ^ masked(w) on its own step; a group's last line leaves the next
+  // group's first word alone in xr (its chains start from zero).
+  uint32_t xr[4] = {ring[0][0], ring[0][1], ring[0][2], ring[0][3]};
+  // Quiet steps.  Per-step cursor control cost the fold 16 SALU and 4.5
+  // branches per wave step against 1.7 and 0.1 in the SCK (rocprofv3 --pmc,
+  // profiles/r03/pmc_insts.txt).  A run of steps in which neither cursor
+  // changes group and the fold cursor's line is no edge line (not a head
+  // line, not the group's last) needs none of it: a step is then the 16
+  // lookups, the XORs and a load.  Every full step computes the length of
+  // the run that follows it (quiet); a block of D steps that starts with a
+  // run of >= D ahead is D quiet steps with no per-step test at all, and
+  // shorter runs go through full steps (a per-step quiet / full branch
+  // measured 17 % slower: 1115 against 953 us, tools/microbench/fold_var.hip).
+  uint32_t quiet = 0;
+  auto quiet_step = [&](int u, uint32_t ahead) {  // ahead: lines the load cursor is past ld_k within the block
+    const u32x4 wn = ring[(u + 1) % D];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t t0 = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0400u));
+      const uint32_t t1 = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0500u) + 128);
+      const uint32_t t2 = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo1, 0x0C020600u));
+      const uint32_t t3 = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo1, 0x0C020700u) + 128);
+      xr[i] = xor3(t0, t1, xor3(t2, t3, wn[i]));
     }
-
-    struct LInfo {
-      uint64_t line0;  // lane's slot in the packet's first line
-    };
-    // Load cursor enters group q: line base, L, and (a, M) into the FIFO.
-    auto ld_enter = [&](uint32_t q, LInfo &li) -> uint32_t {
-      uint64_t addr;
-      uint32_t gM;
-      if (ABL & 4) {
-        addr = (uint64_t)(uintptr_t)a.base + (8ull * q + g) * a.stride;
-        gM = a.fixed_len - 4u;
-      } else {
-        const u32x2 d = *reinterpret_cast<const u32x2 *>(dring + ((q >> 3) & 1u) * kBlk + 2u * (8u * (q & 7u) + g));
-        addr = ((uint64_t)(d[1] & 0xFFFFu) << 32) | d[0];
-        gM = (d[1] >> 16) - 4u;
-      }
-      const uint32_t ga = (uint32_t)addr & 127u;
-      li.line0 = (addr & ~127ull) + 16u * s;
-      fifo[((q & 7u) << 3) | g] = (gM << 7) | ga;
-      return __builtin_amdgcn_readfirstlane((ga + gM + 127u) >> 7);  // equal within a group
-    };
-
-    LInfo ld;
-    uint32_t ld_q = qb, ld_k = 0, ld_L = ld_enter(ld_q, ld);
-    uint32_t fd_q = qb, fd_k = 0, fd_L = ld_L, fd_a, fd_M;
-    auto fd_enter = [&](uint32_t q) {
-      const uint32_t v = fifo[((q & 7u) << 3) | g];
-      fd_a = v & 127u;
-      fd_M = v >> 7;
-      fd_L = __builtin_amdgcn_readfirstlane((fd_a + fd_M + 127u) >> 7);
-    };
-    fd_enter(fd_q);
-    // head lines of the group: 2 when some packet's header runs into line 1 (a
-    // plain uint32 so the edge test below is SALU arithmetic and one branch:
-    // short-circuit || on a ballot-derived bool compiled to five branches per
-    // step, and C4's fold ran 1.5 % slower)
-    uint32_t fd_hl = __ballot(fd_a > 88u) != 0 ? 2u : 1u;
-    // edge line <=> fd_k < fd_hl or fd_k == fd_L - 1 <=> (fd_k - fd_hl) >= fd_span, unsigned
-    uint32_t fd_span = fd_L - 1u > fd_hl ? fd_L - 1u - fd_hl : 0u;  // 0: every line is an edge line
-
-    auto ld_advance = [&]() {
-      if (++ld_k == ld_L) {  // wave-uniform
-        ld_k = 0;
-        if (ld_q + 1 < qe) {
-          ++ld_q;
-          if (!(ABL & 4) && (ld_q & 7u) == 0) {
-            put_block((ld_q >> 3) + 1, NB);
-            NB = load_block((ld_q >> 3) + 2);
-          }
-          ld_L = ld_enter(ld_q, ld);
-        } else {
-          ld_L = 1;  // done: re-read line 0 of the last group (ld_k wraps to 0 every step)
-        }
-      }
-    };
-    // (ABL 16384, timing only: no line loads, a value derived from the address)
-    auto line_load = [&](uint64_t addr) -> u32x4 {
-      if (ABL & 16384) return u32x4{(uint32_t)addr, (uint32_t)(addr >> 7), lane, (uint32_t)addr * 3u};
-      return gload16_nt(addr);
-    };
-    auto ld_issue = [&]() -> u32x4 { return line_load(ld.line0 + 128ull * ld_k); };
-
-    u32x4 ring[D];
-  #pragma unroll
-    for (int u = 0; u < D; ++u) {
-      __builtin_amdgcn_sched_barrier(0);
-      ring[u] = ld_issue();
-      ld_advance();
-    }
-    __builtin_amdgcn_sched_barrier(0);
-
-    uint32_t r[4] = {0u, 0u, 0u, 0u};
-    // Two copies of the fold loop: one with whole-word edges when the bucket
-    // pass found every strided-chain packet word-aligned in start and length
-    // (a per-group choice inside the loop made the compiler rotate the load
-    // ring through copies and drain vmcnt(0) at the loop head).
-    // The fold keeps xr = r ^ (the current line's word), the lookup input: the
-    // XOR with the next line's word rides in the step's last 3-input XOR (as in
-    // the SCK), 4 VALU per line fewer.  An edge line corrects xr by
-    // w ^ masked(w) on its own step; a group's last line leaves the next
-    // group's first word alone in xr (its chains start from zero).
-    uint32_t xr[4] = {ring[0][0], ring[0][1], ring[0][2], ring[0][3]};
-    // Quiet steps.  Per-step cursor control cost the fold 16 SALU and 4.5
-    // branches per wave step against 1.7 and 0.1 in the SCK (rocprofv3 --pmc,
-    // profiles/r03/pmc_insts.txt).  A run of steps in which neither cursor
-    // changes group and the fold cursor's line is no edge line (not a head
-    // line, not the group's last) needs none of it: a step is then the 16
-    // lookups, the XORs and a load.  Every full step computes the length of
-    // the run that follows it (quiet); a block of D steps that starts with a
-    // run of >= D ahead is D quiet steps with no per-step test at all, and
-    // shorter runs go through full steps (a per-step quiet / full branch
-    // measured 17 % slower: 1115 against 953 us, tools/microbench/fold_var.hip).
-    uint32_t quiet = 0;
-    auto quiet_step = [&](int u, uint32_t ahead) {  // ahead: lines the load cursor is past ld_k within the block
-      const u32x4 wn = ring[(u + 1) % D];
-  #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const uint32_t t0 = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0400u));
-        const uint32_t t1 = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0500u) + 128);
-        const uint32_t t2 = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo1, 0x0C020600u));
-        const uint32_t t3 = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo1, 0x0C020700u) + 128);
-        xr[i] = xor3(t0, t1, xor3(t2, t3, wn[i]));
-      }
-      ring[u] = line_load(ld.line0 + 128ull * (ld_k + ahead));
-    };
-    auto fold_loop = [&](auto words) {
+    ring[u] = line_load(ld.line0 + 128ull * (ld_k + ahead));
+  };
+  auto fold_loop = [&](auto words) {
     // One full step: edge masks, group finish and both cursors' group changes.
     auto full_step = [&](int u, bool &done) {
-        const u32x4 wn = ring[(u + 1) % D];  // the next line, raw
-        if (!(ABL & 8) && fd_k - fd_hl >= fd_span) {  // wave-uniform: an edge line
-          const u32x4 wc = ring[u];
-          const int rel0 = (int)(128u * fd_k + 16u * s) - (int)fd_a;
-          if constexpr (decltype(words)::value) {
-            if ((ABL & 32768) || fd_k < fd_hl) {  // wave-uniform: a head line
-  #pragma unroll
-              for (int i = 0; i < 4; ++i) {
-                // whole words: keep 0 <= rel < M by sign arithmetic (compare +
-                // select pairs needed hazard NOPs), head masks from a 16-entry
-                // table (rel >= 40 and rel < 0 index the zero entry 15)
-                const int rel = rel0 + 4 * i;
-                const uint32_t keep = (uint32_t)(((rel - (int)fd_M) & ~rel) >> 31);
-                const uint32_t k = __builtin_elementwise_min((uint32_t)rel >> 2, 15u);
-                typedef uint32_t u32x2e __attribute__((ext_vector_type(2)));
-                const u32x2e e = *reinterpret_cast<const u32x2e *>(etl + 2 * k);
-                xr[i] = xor3(xr[i], wc[i], ((wc[i] & keep) | e[0]) ^ e[1]);
-              }
-            } else {
-              // the group's last line past its head lines: rel >= 40 (no head
-              // masks), only the bytes at rel >= M dropped -- 3 VALU a word
-              // instead of 10 and a table read
-              const int lim = (int)fd_M - 1 - rel0;
-  #pragma unroll
-              for (int i = 0; i < 4; ++i) xr[i] ^= wc[i] & (uint32_t)((lim - 4 * i) >> 31);
+      const u32x4 wn = ring[(u + 1) % D];  // the next line, raw
+      if (!(ABL & 8) && fd_k - fd_hl >= fd_span) {  // wave-uniform: an edge line
+        const u32x4 wc = ring[u];
+        const int rel0 = (int)(128u * fd_k + 16u * s) - (int)fd_a;
+        if constexpr (decltype(words)::value) {
+          if (fd_k < fd_hl) {  // wave-uniform: a head line
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              // whole words: keep 0 <= rel < M by sign arithmetic (compare +
+              // select pairs needed hazard NOPs), head masks from a 16-entry
+              // table (rel >= 40 and rel < 0 index the zero entry 15)
+              const int rel = rel0 + 4 * i;
+              const uint32_t keep = (uint32_t)(((rel - (int)fd_M) & ~rel) >> 31);
+              const uint32_t k = __builtin_elementwise_min((uint32_t)rel >> 2, 15u);
+              typedef uint32_t u32x2e __attribute__((ext_vector_type(2)));
+              const u32x2e e = *reinterpret_cast<const u32x2e *>(etl + 2 * k);
+              xr[i] = xor3(xr[i], wc[i], ((wc[i] & keep) | e[0]) ^ e[1]);
             }
           } else {
-  #pragma unroll
-            for (int i = 0; i < 4; ++i) xr[i] = xor3(xr[i], wc[i], edge_word(wc[i], rel0 + 4 * i, (int)fd_M));
-          }
-        }
-        uint32_t t[4][4];
-  #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          if (ABL & 1) {
-            t[i][0] = __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0400u);
-            t[i][1] = xr[i] >> 7;
-            t[i][2] = 0u;
-            t[i][3] = 0u;
-          } else {
-            t[i][0] = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0400u));
-            t[i][1] = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0500u) + 128);
-            t[i][2] = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo1, 0x0C020600u));
-            t[i][3] = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo1, 0x0C020700u) + 128);
-          }
-        }
-        if (++fd_k == fd_L) {  // wave-uniform: group fd_q folded
-  #pragma unroll
-          for (int i = 0; i < 4; ++i) r[i] = xor3(t[i][0], t[i][1], t[i][2] ^ t[i][3]);
-          finish_group(r, fd_L, fd_a, fd_M, fd_q);
-  #pragma unroll
-          for (int i = 0; i < 4; ++i) xr[i] = wn[i];
-          fd_k = 0;
-          if (fd_q + 1 < qe) {
-            ++fd_q;
-            fd_enter(fd_q);
-            fd_hl = __ballot(fd_a > 88u) != 0 ? 2u : 1u;
-            fd_span = fd_L - 1u > fd_hl ? fd_L - 1u - fd_hl : 0u;
-          } else {
-            done = true;
-            fd_L = 0xFFFFFFFFu;
+            // the group's last line past its head lines: rel >= 40 (no head
+            // masks), only the bytes at rel >= M dropped -- 3 VALU a word
+            // instead of 10 and a table read
+            const int lim = (int)fd_M - 1 - rel0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) xr[i] ^= wc[i] & (uint32_t)((lim - 4 * i) >> 31);
           }
         } else {
-  #pragma unroll
-          for (int i = 0; i < 4; ++i) xr[i] = xor3(t[i][0], t[i][1], xor3(t[i][2], t[i][3], wn[i]));
+#pragma unroll
+          for (int i = 0; i < 4; ++i) xr[i] = xor3(xr[i], wc[i], edge_word(wc[i], rel0 + 4 * i, (int)fd_M));
         }
-        // Refill after folding: the FIFO entry the fold just read may be
-        // rewritten by this step's load-cursor advance.
-        ring[u] = ld_issue();
-        ld_advance();
-        // The quiet run that follows: fold lines fd_k .. fd_L - 2 past the head
-        // lines, loads up to the line before the load cursor's group change
-        // (ld_L = 1 once every group is loaded: no run).
-        const uint32_t nf = (fd_k >= fd_hl && fd_k + 1 < fd_L) ? fd_L - 1u - fd_k : 0u;
-        const uint32_t nl = ld_L - 1u - ld_k;
-        quiet = nf < nl ? nf : nl;
+      }
+      uint32_t t[4][4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (ABL & 1) {
+          t[i][0] = __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0400u);
+          t[i][1] = xr[i] >> 7;
+          t[i][2] = 0u;
+          t[i][3] = 0u;
+        } else {
+          t[i][0] = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0400u));
+          t[i][1] = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0500u) + 128);
+          t[i][2] = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo1, 0x0C020600u));
+          t[i][3] = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo1, 0x0C020700u) + 128);
+        }
+      }
+      if (++fd_k == fd_L) {  // wave-uniform: group fd_q folded
+#pragma unroll
+        for (int i = 0; i < 4; ++i) r[i] = xor3(t[i][0], t[i][1], t[i][2] ^ t[i][3]);
+        finish_group(r, fd_L, fd_a, fd_M, fd_q);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) xr[i] = wn[i];
+        fd_k = 0;
+        if (fd_q + 1 < qe) {
+          ++fd_q;
+          fd_enter(fd_q);
+          fd_hl = __ballot(fd_a > 88u) != 0 ? 2u : 1u;
+          fd_span = fd_L - 1u > fd_hl ? fd_L - 1u - fd_hl : 0u;
+        } else {
+          done = true;
+          fd_L = 0xFFFFFFFFu;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) xr[i] = xor3(t[i][0], t[i][1], xor3(t[i][2], t[i][3], wn[i]));
+      }
+      // Refill after folding: the FIFO entry the fold just read may be
+      // rewritten by this step's load-cursor advance.
+      ring[u] = ld_issue();
+      ld_advance();
+      // The quiet run that follows: fold lines fd_k .. fd_L - 2 past the head
+      // lines, loads up to the line before the load cursor's group change
+      // (ld_L = 1 once every group is loaded: no run).
+      const uint32_t nf = (fd_k >= fd_hl && fd_k + 1 < fd_L) ? fd_L - 1u - fd_k : 0u;
+      const uint32_t nl = ld_L - 1u - ld_k;
+      quiet = nf < nl ? nf : nl;
     };
     bool done = false;
     while (!done) {
       if (!(ABL & 8) && quiet >= (uint32_t)D) {  // wave-uniform: D quiet steps, no per-step control
-  #pragma unroll
+#pragma unroll
         for (int u = 0; u < D; ++u) {
           __builtin_amdgcn_sched_barrier(0);
           quiet_step(u, (uint32_t)u);
@@ -912,210 +915,26 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
         ld_k += D;
         continue;
       }
-  #pragma unroll
+#pragma unroll
       for (int u = 0; u < D; ++u) {  // full steps (correct in any state; each one measures the next run)
         __builtin_amdgcn_sched_barrier(0);
         full_step(u, done);
       }
     }
-    };
-    if (a.ctr->odd == 0)
-      fold_loop(std::true_type{});
-    else
-      fold_loop(std::false_type{});
   };
-
-  // The fold specialized on the line count (round 4).  A run of groups of
-  // one class L (C4: L = 2, 3 for 256 B, 8, 9 for 1 KiB, 32, 33 for 4 KiB
-  // packets at 128- / 64-byte alignment) with every packet word-aligned runs
-  // like the SCK: the schedule is static -- step k of a group folds its line
-  // k, its head line (k = 0, and 1 when a header runs into line 1) and last
-  // line (k = L - 1) take the edge masks, the finish follows step L - 1, and
-  // the load of step k + D is line (k + D) % L of group (k + D) / L ahead --
-  // so a step has no cursor arithmetic, no quiet-run bookkeeping and no
-  // per-step branch (round 3's generic fold: 16.4 SALU and 4.5 branches per
-  // wave step against the SCK's 1.7 and 0.1, profiles/r03/pmc_insts.txt).
-  // The ring index of step k must be a constant: P = D / gcd(L, D) groups
-  // are unrolled together (L = 33, D = 6: two groups, 66 steps).  Group
-  // descriptors: groups q .. q + J (J = the farthest group a load reaches)
-  // are kept per lane (first-line slot address, a, M); group q + J + 1's
-  // descriptor is loaded P groups (one unrolled period) before the group
-  // change that needs it, into the register that change consumes -- every
-  // period issues the same loads, so the compiler counts vmcnt exactly across
-  // the loop (a descriptor block refilled every 8 groups, as the generic fold
-  // does, cost a vmcnt(0) drain of the line ring each time); groups past the
-  // repeat the run's last group (their loads are never folded).
-  auto fixed = [&](auto Lc, uint32_t qb, uint32_t qs) {
-    constexpr uint32_t L = decltype(Lc)::value;
-    constexpr uint32_t D = (L % 8u == 0u) ? 8u : 6u;        // lines in flight
-    constexpr uint32_t P = D / cgcd(L, D);                    // groups per unrolled period
-    static_assert((P * L) % D == 0u, "the ring index must repeat every period");
-    constexpr uint32_t J = (L - 1u + D) / L;                  // the farthest group a load reaches
-    uint64_t l0[J + 1];
-    uint32_t ga[J + 1], gm[J + 1];
-    auto set_info = [&](const u32x2 &d, uint32_t j) {
-      const uint64_t addr = ((uint64_t)(d[1] & 0xFFFFu) << 32) | d[0];
-      l0[j] = (addr & ~127ull) + 16u * s;
-      ga[j] = (uint32_t)addr & 127u;
-      gm[j] = (d[1] >> 16) - 4u;
-    };
-    auto gdesc = [&](uint32_t x) -> u32x2 {  // group x's descriptor of this lane's packet
-      return *reinterpret_cast<const u32x2 __attribute__((address_space(1))) *>(
-          (uintptr_t)reinterpret_cast<const uint32_t *>(a.bdesc + 8ull * x + g));
-    };
-#pragma unroll
-    for (uint32_t j = 0; j <= J; ++j) {
-      if (j == 0u || qb + j < qs) {  // wave-uniform
-        set_info(gdesc(qb + j), j);
-      } else {
-        l0[j] = l0[j - 1u];
-        ga[j] = ga[j - 1u];
-        gm[j] = gm[j - 1u];
-      }
-    }
-    // nd[p]: the descriptor the group change after unrolled group p needs
-    // (group x = q + J + 1 when entering q + 1), clamped into the run
-    auto clamp_q = [&](uint32_t x) { return x < qs ? x : qs - 1u; };
-    u32x2 nd[P];
-#pragma unroll
-    for (uint32_t p = 0; p < P; ++p) nd[p] = gdesc(clamp_q(qb + J + 1u + p));
-    u32x4 ring[D];
-#pragma unroll
-    for (uint32_t k = 0; k < D; ++k) {
-      __builtin_amdgcn_sched_barrier(0);
-      ring[k] = gload16_nt(l0[k / L] + 128ull * (k % L));
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    uint32_t xr[4] = {ring[0][0], ring[0][1], ring[0][2], ring[0][3]};
-    uint32_t hl2 = __ballot(ga[0] > 88u) != 0 ? 1u : 0u;  // some header runs into line 1
-    uint32_t q = qb;
-    // One group at position p of the period (the ring slots of its steps).
-    auto group_at = [&](auto pc) {
-      constexpr uint32_t p = decltype(pc)::value;
-#pragma unroll
-      for (uint32_t k = 0; k < L; ++k) {
-        const uint32_t u = (p * L + k) % D;
-        __builtin_amdgcn_sched_barrier(0);
-        const u32x4 wc = ring[u];
-        const u32x4 wn = ring[(u + 1u) % D];
-        if (k == 0u || (k == 1u && hl2)) {  // a head line: keep [0, M), invariant masks, seed
-          const int rel0 = (int)(128u * k + 16u * s) - (int)ga[0];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int rel = rel0 + 4 * i;
-            const uint32_t keep = (uint32_t)(((rel - (int)gm[0]) & ~rel) >> 31);
-            const uint32_t kk = __builtin_elementwise_min((uint32_t)rel >> 2, 15u);
-            typedef uint32_t u32x2e __attribute__((ext_vector_type(2)));
-            const u32x2e e = *reinterpret_cast<const u32x2e *>(etl + 2 * kk);
-            xr[i] = xor3(xr[i], wc[i], ((wc[i] & keep) | e[0]) ^ e[1]);
-          }
-        } else if (k == L - 1u) {  // the last line: the bytes at rel >= M dropped
-          const int lim = (int)gm[0] - 1 - ((int)(128u * k + 16u * s) - (int)ga[0]);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) xr[i] ^= wc[i] & (uint32_t)((lim - 4 * i) >> 31);
-        }
-        uint32_t t[4][4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          t[i][0] = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0400u));
-          t[i][1] = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0500u) + 128);
-          t[i][2] = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo1, 0x0C020600u));
-          t[i][3] = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo1, 0x0C020700u) + 128);
-        }
-        if (k == L - 1u) {
-          uint32_t rr[4];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) rr[i] = xor3(t[i][0], t[i][1], t[i][2] ^ t[i][3]);
-          finish_group(rr, L, ga[0], gm[0], q);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) xr[i] = wn[i];  // the next group's line 0: its chains start from zero
-        } else {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) xr[i] = xor3(t[i][0], t[i][1], xor3(t[i][2], t[i][3], wn[i]));
-        }
-        // refill: the line of step k + D (after the fold read this slot)
-        ring[u] = gload16_nt(l0[(k + D) / L] + 128ull * ((k + D) % L));
-      }
-      // group q is folded; the next one's info moves to the front
-      ++q;
-#pragma unroll
-      for (uint32_t j = 0; j < J; ++j) {
-        l0[j] = l0[j + 1u];
-        ga[j] = ga[j + 1u];
-        gm[j] = gm[j + 1u];
-      }
-      if (q + J < qs) {  // wave-uniform: group q + J exists
-        set_info(nd[p], J);
-      } else {
-        l0[J] = l0[J - 1u];
-        ga[J] = ga[J - 1u];
-        gm[J] = gm[J - 1u];
-      }
-      nd[p] = gdesc(clamp_q(q + J + P));  // the same change one period later
-      hl2 = __ballot(ga[0] > 88u) != 0 ? 1u : 0u;
-    };
-    // Whole periods in a loop with one exit; the last n % P groups after it
-    // (an exit after any group of an unrolled period made the compiler carry
-    // the group counter through a VGPR phi -- a readfirstlane and a vmcnt(0)
-    // drain of the line ring at every period).
-    uint32_t n = qs - qb;
-    while (n >= P) {  // wave-uniform
-      static_for<P>(group_at);
-      n -= P;
-    }
-    static_for<P - 1>([&](auto pc) {
-      if (decltype(pc)::value < n) group_at(pc);  // wave-uniform
-    });
-  };
-  // Specialized line counts (C4's classes); other classes and byte-granular
-  // batches take the generic fold.  Timing variant only (ABL 131072,
-  // tools/microbench/fold_var.hip): bit-exact, but 921.5 us against the
-  // generic fold's 918.5 on C4 (profiles/r04/s2_mb_fold_var.txt), so the
-  // product runs the generic fold.
-  auto special = [](uint32_t L) { return L == 2u || L == 3u || L == 8u || L == 9u || L == 32u || L == 33u; };
-
-  if (!(ABL & 131072) || a.ctr->odd != 0) {
-    generic(q_begin, q_end);
-  } else {
-    // Segments of the wave's groups: a run of one specialized L, or a run of
-    // other classes (up to 64 groups of look-ahead per segment).
-    uint32_t q = q_begin;
-    while (q < q_end) {  // wave-uniform
-      const uint32_t x = q + lane;
-      uint32_t Lx = 0xFFFFFFFFu;
-      if (x < q_end) {
-        const u32x2 d = *reinterpret_cast<const u32x2 __attribute__((address_space(1))) *>(
-            (uintptr_t)reinterpret_cast<const uint32_t *>(a.bdesc + 8ull * x));
-        Lx = ((d[0] & 127u) + (d[1] >> 16) - 4u + 127u) >> 7;
-      }
-      uint32_t L0 = __builtin_amdgcn_readfirstlane(Lx);
-      const bool sp = special(L0);
-      const uint64_t stop = __ballot(sp ? Lx != L0 : (Lx == 0xFFFFFFFFu || special(Lx)));
-      const uint32_t n = stop ? (uint32_t)__builtin_ctzll(stop) : 64u;
-      uint32_t qs = q + n < q_end ? q + n : q_end;
-      // pin the segment's scalars in SGPRs: rematerialized from the scan's
-      // VGPR after a specialized loop, they cost a vmcnt(0) drain there
-      asm volatile("" : "+s"(L0), "+s"(qs));
-      switch (sp ? L0 : 0u) {  // wave-uniform
-        case 2: fixed(std::integral_constant<uint32_t, 2>{}, q, qs); break;
-        case 3: fixed(std::integral_constant<uint32_t, 3>{}, q, qs); break;
-        case 8: fixed(std::integral_constant<uint32_t, 8>{}, q, qs); break;
-        case 9: fixed(std::integral_constant<uint32_t, 9>{}, q, qs); break;
-        case 32: fixed(std::integral_constant<uint32_t, 32>{}, q, qs); break;
-        case 33: fixed(std::integral_constant<uint32_t, 33>{}, q, qs); break;
-        default: generic(q, qs); break;
-      }
-      q = qs;
-    }
-  }
+  if (C.odd == 0)
+    fold_loop(std::true_type{});
+  else
+    fold_loop(std::false_type{});
   if (!(ABL & 16) && q_end != round_q0) flush(q_end);
   if ((ABL & 48) && sink == 0x12345678u) a.bres[0] = sink;
-  if ((ABL & 8192) && lane == 0) {  // timing only: end stamp after every store has left
+  if ((ABL & 524288) && lane == 0) {  // timing only: end stamp after every store has left
     __builtin_amdgcn_s_waitcnt(0);
-    a.out[4 * wave + 1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    a.out[wave8 + 3] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    a.out[wave8 + 6] = done_work;
+    a.out[wave8 + 7] = (uint32_t)(x1 - x0);
   }
 }
-
 
 // =======================================================================
 // Small packets of the ragged path (<= kRsSmallL lines: the 64 / 256-byte
@@ -1442,13 +1261,43 @@ static void launch_bucket_u(const RsckArgs &a, int pgrid, hipStream_t st) {
   else if (a.len) hipLaunchKernelGGL((rsck_bucket<false, true, 0, U>), dim3(pgrid), dim3(kPassBlock), 0, st, a);
   else hipLaunchKernelGGL((rsck_bucket<false, false, 0, U>), dim3(pgrid), dim3(kPassBlock), 0, st, a);
 }
-// Packets per thread of the bucket and gather passes for a batch on pgrid blocks.
-static bool pass_big(const RsckArgs &a, int pgrid) {
-  return a.count > (uint64_t)pgrid * kPassBlock * kPassUnroll;
+// The bucket and gather passes' shape for a batch: packets per thread U (the
+// smallest of 4, 8, 16, 17 whose round covers the batch on 256 blocks) and
+// pass blocks (as many as one round of U per thread needs).  A latency-bound
+// pass: at C4's 8-GPU shard (524 K packets) the round-4 shape, U = 16 on 256
+// blocks (2 live packets per thread, 14 clamped loads), took 16.3 us; U = 4
+// on 128 blocks 10.2, U = 2 on 256 blocks 12.4, U = 8 on 64 blocks 11.4
+// (tools/microbench/shard.hip, profiles/r05/s1_mb_shard_baseline.txt).
+struct PassShape {
+  int grid, U;
+};
+static PassShape pass_shape(uint64_t count, int pass_cap) {
+  int U = kPassUnrollBig;
+  for (int u : {4, 8, kPassUnroll})
+    if (count <= (uint64_t)kPassBlocks * kPassBlock * u) {
+      U = u;
+      break;
+    }
+  const uint64_t want = (count + (uint64_t)U * kPassBlock - 1) / ((uint64_t)U * kPassBlock);
+  int grid = (int)(want < (uint64_t)kPassBlocks ? (want ? want : 1) : kPassBlocks);
+  if (pass_cap > 0 && pass_cap < grid) grid = pass_cap;  // RICRC_RS_PASS_GRID (blocks then take several rounds)
+  return PassShape{grid, U};
 }
-static void launch_bucket(const RsckArgs &a, int pgrid, hipStream_t st) {
-  if (pass_big(a, pgrid)) launch_bucket_u<kPassUnrollBig>(a, pgrid, st);
-  else launch_bucket_u<kPassUnroll>(a, pgrid, st);
+static void launch_bucket(const RsckArgs &a, const PassShape &ps, hipStream_t st) {
+  switch (ps.U) {
+    case 4: launch_bucket_u<4>(a, ps.grid, st); break;
+    case 8: launch_bucket_u<8>(a, ps.grid, st); break;
+    case kPassUnroll: launch_bucket_u<kPassUnroll>(a, ps.grid, st); break;
+    default: launch_bucket_u<kPassUnrollBig>(a, ps.grid, st); break;
+  }
+}
+static void launch_gather(const RsckArgs &a, const PassShape &ps, hipStream_t st) {
+  switch (ps.U) {  // the gather's blocks are the bucket pass's (block b serves pass block b's packets)
+    case 4: hipLaunchKernelGGL(rsck_gather<4>, dim3(ps.grid), dim3(kPassBlock), 0, st, a); break;
+    case 8: hipLaunchKernelGGL(rsck_gather<8>, dim3(ps.grid), dim3(kPassBlock), 0, st, a); break;
+    case kPassUnroll: hipLaunchKernelGGL(rsck_gather<kPassUnroll>, dim3(ps.grid), dim3(kPassBlock), 0, st, a); break;
+    default: hipLaunchKernelGGL(rsck_gather<kPassUnrollBig>, dim3(ps.grid), dim3(kPassBlock), 0, st, a); break;
+  }
 }
 
 hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, hipStream_t st, hipEvent_t *pass_ev) {
@@ -1457,14 +1306,12 @@ hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, hipStream_t st, hipE
   if (a.count > kRsMaxCount) return hipErrorInvalidValue;
   // a.ctr is zero here: zeroed when the workspace was allocated, and again
   // by rsck_gather at the end of every call.
-  const uint64_t want = (a.count + kPassBlock - 1) / kPassBlock;
-  int pgrid = (int)(want < kPassBlocks ? want : kPassBlocks);
-  if (pass_cap > 0 && pass_cap < pgrid) pgrid = pass_cap;
-  a.nblk = (uint32_t)pgrid;
+  const PassShape ps = pass_shape(a.count, pass_cap);
+  a.nblk = (uint32_t)ps.grid;
   // RICRC_PASS_TIMES: timing events between the passes on st (diagnostics)
   auto mark = [&](int k) { if (pass_ev) (void)hipEventRecord(pass_ev[k], st); };
   mark(0);
-  launch_bucket(a, pgrid, st);
+  launch_bucket(a, ps, st);
   mark(1);
   hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, st, a);
   mark(2);
@@ -1474,9 +1321,7 @@ hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, hipStream_t st, hipE
   // fold by 60 us, profiles/r04/s2_*.)
   hipLaunchKernelGGL((icrc_rsmall_kernel<kSmallRounds>), dim3(grid), dim3(kBlock), 0, st, a);
   mark(3);
-  // the gather's blocks are the bucket pass's (block b serves pass block b's packets)
-  if (pass_big(a, pgrid)) hipLaunchKernelGGL(rsck_gather<kPassUnrollBig>, dim3(pgrid), dim3(kPassBlock), 0, st, a);
-  else hipLaunchKernelGGL(rsck_gather<kPassUnroll>, dim3(pgrid), dim3(kPassBlock), 0, st, a);
+  launch_gather(a, ps, st);
   mark(4);
   return hipGetLastError();
 }
