@@ -213,8 +213,13 @@ def kernel_path(args, base=0x100000, count=1):
 
 
 def kernel_label(args, base=0x100000, count=1):
-    """Human-readable label of kernel_path: 'role (kernel) -> role (kernel)'."""
-    return " -> ".join(f"{KERNEL_ROLES.get(k, k)} ({k})" for k in kernel_path(args, base, count).split("+"))
+    """Human-readable label of kernel_path: 'role (kernel) -> role (kernel)'.
+    Batches of up to 1 M packets fold their one-line packets in the gather
+    pass (no icrc_rsmall_kernel launch)."""
+    ks = kernel_path(args, base, count).split("+")
+    role = lambda k: ("gather, folding the one-line packets" if k == "rsck_gather" and "rsck_bucket" in ks  # noqa: E731
+                      and "icrc_rsmall_kernel" not in ks else KERNEL_ROLES.get(k, k))
+    return " -> ".join(f"{role(k)} ({k})" for k in ks)
 
 
 def rccl_version():

@@ -461,13 +461,13 @@ Path choose_path(const Knobs &kn, const uint8_t *base, const uint64_t *off, cons
   return cpl ? Path::kStream : Path::kRagged;
 }
 
-const char *path_kernels(Path p) {
+const char *path_kernels(Path p, bool fused) {
   switch (p) {
     case Path::kSck: return "icrc_sck_kernel";
     case Path::kQuad: return "icrc_quad_kernel";
     case Path::kTsk: return "icrc_tsk_kernel";
     case Path::kStream: return "icrc_stream_kernel";
-    default: return "rsck_bucket+icrc_rsck_kernel+icrc_rsmall_kernel+rsck_gather";
+    default: return fused ? "rsck_bucket+icrc_rsck_kernel+rsck_gather" : "rsck_bucket+icrc_rsck_kernel+icrc_rsmall_kernel+rsck_gather";
   }
 }
 
@@ -840,12 +840,16 @@ const char *ricrc_kernel_path(const ricrc_ctx *ctx, const void *d_base, const ui
   if ((!d_off && stride == 0) || (!d_len && stride <= l3_offset)) return nullptr;
   const Knobs kn = ctx ? ctx->knobs : Knobs{};
   const Path p = choose_path(kn, (const uint8_t *)d_base, d_off, d_len, stride, l3_offset);
-  if (flags == RICRC_F_IPV4 || p == Path::kSck) return path_kernels(p);  // the SCK applies every family natively
+  // the ragged pipeline's first range (launch_batch_v4 cuts at kRsChunk) decides the one-line pass
+  const bool fused = rs_fused(std::min<uint64_t>(count, kRsChunk), kn.pass_grid);
+  if (flags == RICRC_F_IPV4 || p == Path::kSck) return path_kernels(p, fused);  // the SCK applies every family natively
   switch (p) {  // IPv6 / AUTO: the IPv4-mask kernels, then the linear header fix-up
     case Path::kQuad: return "icrc_quad_kernel+family_fix_kernel";
     case Path::kTsk: return "icrc_tsk_kernel+family_fix_kernel";
     case Path::kStream: return "icrc_stream_kernel+family_fix_kernel";
-    default: return "rsck_bucket+icrc_rsck_kernel+icrc_rsmall_kernel+rsck_gather+family_fix_kernel";
+    default:
+      return fused ? "rsck_bucket+icrc_rsck_kernel+rsck_gather+family_fix_kernel"
+                   : "rsck_bucket+icrc_rsck_kernel+icrc_rsmall_kernel+rsck_gather+family_fix_kernel";
   }
 }
 

@@ -142,6 +142,9 @@ constexpr uint64_t kRsMaxCount = 1ull << 28;
 // before the bucket pass and after the bucket, fold, one-line and gather
 // passes.
 hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, hipStream_t st, hipEvent_t *pass_ev = nullptr);
+// Whether a batch of `count` packets takes the fused pipeline (bucket, fold,
+// gather folding the one-line packets: no icrc_rsmall_kernel launch).
+bool rs_fused(uint64_t count, int pass_cap);
 
 struct SynthArgs {
   uint8_t *buf;

@@ -151,7 +151,11 @@ __device__ __forceinline__ T wave_scan(T v) {
 // the ranking round, 2 no LDS atomics (rank 0), 4 stop after the reservation,
 // 8 no pos_of stores, 16 no descriptor stores, 32 no LDS staging.
 // LDS layout entries of a block: a round's packets + room for group padding
-__host__ __device__ constexpr uint32_t stage_entries(int U) { return (uint32_t)U * kPassBlock + 512u; }
+// (U <= 4: room for the worst case, 7 padding entries for each of kRsRuns
+// classes, so every block of such a batch is staged: PassShape::fused.)
+__host__ __device__ constexpr uint32_t stage_entries(int U) {
+  return (uint32_t)U * kPassBlock + (U <= 4 ? 7u * (uint32_t)kRsRuns : 512u);
+}
 template <bool OFF, bool LEN, int ABL = 0, int U = kPassUnroll>
 __global__ __launch_bounds__(kPassBlock) void rsck_bucket(RsckArgs a) {
   constexpr uint32_t kStage = stage_entries(U);
@@ -351,73 +355,6 @@ __device__ __forceinline__ uint32_t gather_one(const RsckArgs &a, uint64_t i, ui
     v = gload4_unaligned((uintptr_t)(addr + n - 4u)) == v ? 1u : 0u;
   }
   return v;
-}
-
-// Gather: block b serves pass block b's packets.  A staged block's results
-// sit in two contiguous ranges (its small range, its big range): they are
-// read coalesced into LDS in the block's layout order and pos_of indexes
-// that copy, instead of one 4-byte read per packet scattered over the class
-// runs of the pools.
-template <int PU>  // the bucket pass's packets per thread
-__global__ __launch_bounds__(kPassBlock) void rsck_gather(RsckArgs a) {
-  constexpr uint32_t kStage = stage_entries(PU);
-  __shared__ uint32_t lres[kStage];
-  // The counters are dead now (the bucket pass and both folds have read
-  // them): zero them for the next call on this workspace.
-  if (blockIdx.x == 0 && threadIdx.x == 0) *a.ctr = RsCounters{};
-  uint32_t lo, hi;
-  {
-    uint64_t l, h_;
-    pass_range(a.count, l, h_);
-    lo = (uint32_t)l;
-    hi = (uint32_t)h_;
-  }
-  const RsBlock B = a.blk[blockIdx.x];
-  constexpr int U = 4;  // packets per thread in flight at once
-  if (B.staged) {  // block-uniform (a staged block's packets fit one round: hi - lo <= PU x blockDim)
-    // every load of the block issued before the barrier: the positions, then
-    // the results into LDS
-    uint32_t p[PU];
-#pragma unroll
-    for (int k = 0; k < PU; ++k) {
-      const uint32_t i = lo + (uint32_t)k * blockDim.x + threadIdx.x;
-      p[k] = i < hi ? __builtin_nontemporal_load(a.pos_of + i) : 0xFFFFFFFFu;
-    }
-    const uint32_t total = B.small + 8u * B.groups;
-    const uint32_t *rs = a.res + B.small0, *rb = a.bres + 8ull * B.g0 - B.small;
-    constexpr int R = (kStage + kPassBlock - 1) / kPassBlock;
-    uint32_t v[R];
-#pragma unroll
-    for (int k = 0; k < R; ++k) {
-      const uint32_t j = (uint32_t)k * blockDim.x + threadIdx.x;
-      v[k] = j < total ? __builtin_nontemporal_load((j < B.small ? rs : rb) + j) : 0u;
-    }
-#pragma unroll
-    for (int k = 0; k < R; ++k) {
-      const uint32_t j = (uint32_t)k * blockDim.x + threadIdx.x;
-      if (j < total) lres[j] = v[k];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < PU; ++k) {
-      const uint32_t i = lo + (uint32_t)k * blockDim.x + threadIdx.x;
-      if (i < hi) __builtin_nontemporal_store(gather_one(a, i, p[k], p[k] != 0xFFFFFFFFu ? lres[p[k]] : 0u), a.out + i);
-    }
-    return;
-  }
-  for (uint32_t i0 = lo + threadIdx.x; i0 < hi; i0 += U * blockDim.x) {
-    uint32_t p[U], v[U];
-#pragma unroll
-    for (int k = 0; k < U; ++k) p[k] = i0 + k * blockDim.x < hi ? a.pos_of[i0 + k * blockDim.x] : 0xFFFFFFFFu;
-#pragma unroll
-    for (int k = 0; k < U; ++k) v[k] = p[k] != 0xFFFFFFFFu ? a.res[p[k]] : 0u;
-#pragma unroll
-    for (int k = 0; k < U; ++k) {
-      const uint32_t i = i0 + k * blockDim.x;
-      if (i >= hi) break;
-      a.out[i] = gather_one(a, i, p[k], v[k]);
-    }
-  }
 }
 
 // Bytes [0, M) of the packet kept, invariant masks, seed: word i of a slot whose
@@ -1056,164 +993,214 @@ struct SmallPk {
   }
 };
 
-constexpr int kSmallRounds = 1;  // icrc_rsmall_kernel's rounds per batch (below; 2 measured slower: profiles/r04/s6_*)
+// The ICRC of every lane's one-line packet d: wave-collective (every lane of
+// the wave calls it together; a lane without a packet passes a copy of a
+// valid descriptor and ignores the result), since the wave's shape -- its
+// largest block count, whether every packet is word-aligned, half-line --
+// is decided by ballots.  lds: the slice-by-4 tables (fill_tables).
+__device__ __forceinline__ uint32_t small_icrc(const uint32_t *lds, const LaneTab &lt, const RsDesc &d,
+                                               uint32_t lane) {
+  uint32_t K = (((d.hi >> 16) - 4u) + 4u + 15u) >> 4;  // this lane's blocks
+  // the wave's largest, rounded up to a multiple of 4: by ballots for
+  // one-line packets (K <= 8), a shuffle reduction beyond
+  uint32_t Kmax;
+  if (__builtin_amdgcn_ballot_w64(K > 4u) == 0) {
+    Kmax = 4u;
+  } else if (__builtin_amdgcn_ballot_w64(K > 8u) == 0) {
+    Kmax = 8u;
+  } else {
+#pragma unroll
+    for (int w = 32; w >= 1; w >>= 1) K = max(K, (uint32_t)__shfl_xor((int)K, w));
+    Kmax = __builtin_amdgcn_readfirstlane((K + 3u) & ~3u);
+  }
+  // wave-uniform variants: word-aligned packets; every packet's head in blocks 0..3
+  const bool wa = __builtin_amdgcn_ballot_w64(((d.lo | (d.hi >> 16)) & 3u) != 0) == 0;
+  // heads in blocks 0..3: rel_4 = M - 16 Kmax + 64 >= 40 for every lane
+  const bool uk = __builtin_amdgcn_ballot_w64((d.hi >> 16) - 4u + 24u < 16u * Kmax) == 0;
+  // Half-line packets: every covered byte in one aligned 64-byte half
+  // line hb .. hb + 63 whose last 16-byte unit holds the covered end, not
+  // at the half line's end (C4's 64-byte packets: 64-byte aligned, 60
+  // covered bytes).  For a wave of them the 5 units of the 4 blocks are
+  // the half line's units 0, 0, 1, 2, 3, and they are read coalesced: in
+  // load c the 4 lanes of quad p read units 0..3 of lane 4 p + c's half
+  // line (64 contiguous bytes), and a 4 x 4 quad transpose hands every lane
+  // its own -- instead of every lane reading its packet's units alone, 64
+  // lines apart (the access pattern that costs C1's direct kernel, see the
+  // quad kernel in icrc_kernels.hip).
+  const uint64_t pa = ((uint64_t)(d.hi & 0xFFFFu) << 32) | d.lo;
+  const uint64_t pe = pa + ((d.hi >> 16) - 4u);
+  const uint64_t hb = (pe - 1u) & ~63ull;
+  const bool half = pa >= hb && ((uint32_t)pe & 63u) > 48u;
+  SmallPk P;
+  if (Kmax == 4u && __builtin_amdgcn_ballot_w64(!half) == 0) {  // wave-uniform: a wave of half-line packets
+    const uint32_t hlo = (uint32_t)hb, hhi = (uint32_t)(hb >> 32), q = lane & 3u;
+    auto at = [&](uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32 | lo) + 16u * q; };
+    u32x4 H[4];
+    H[0] = gload16(at(dpp_quad_bcast<0>(hlo), dpp_quad_bcast<0>(hhi)));
+    H[1] = gload16(at(dpp_quad_bcast<1>(hlo), dpp_quad_bcast<1>(hhi)));
+    H[2] = gload16(at(dpp_quad_bcast<2>(hlo), dpp_quad_bcast<2>(hhi)));
+    H[3] = gload16(at(dpp_quad_bcast<3>(hlo), dpp_quad_bcast<3>(hhi)));
+    quad_transpose(H, lane & 3u);
+    const u32x4 U[5] = {H[0], H[0], H[1], H[2], H[3]};
+    P.init(d, 4u);
+    if (wa && uk)
+      P.blocks<4, true, 1>(lds, lt, U);
+    else if (uk)
+      P.blocks<4, false, 1>(lds, lt, U);
+    else
+      P.blocks<4, false, 2>(lds, lt, U);
+    return ~P.reg;
+  }
+  P.init(d, Kmax);
+  auto run = [&](auto words, auto uniform) __attribute__((always_inline)) {
+    constexpr bool WA = decltype(words)::value;
+    constexpr int M1 = decltype(uniform)::value ? 1 : 2, M2 = decltype(uniform)::value ? 0 : 2;
+    // Kmax = 8 q + r (r = 0 or 4): a first chunk of r or 8 blocks, then
+    // chunks of 8 (one-line packets: M <= 124, Kmax <= 8 -- one chunk, at
+    // most 9 units = 36 VGPRs in flight)
+    uint32_t j = 0;
+    if ((Kmax & 7u) == 4u) {  // wave-uniform
+      P.chunk<4, WA, M1>(lds, lt, 0);
+      j = 4;
+    } else {
+      P.chunk<8, WA, M1>(lds, lt, 0);
+      j = 8;
+    }
+    for (; j < Kmax; j += 8) P.chunk<8, WA, M2>(lds, lt, j);
+  };
+  if (wa && uk)
+    run(std::true_type{}, std::true_type{});
+  else if (uk)
+    run(std::false_type{}, std::true_type{});
+  else
+    run(std::false_type{}, std::false_type{});
+  return ~P.reg;
+}
 
-// R rounds of 64 packets per wave are taken together: when every one of
-// them is a wave of half-line packets (C4's 64-byte packets), all R rounds'
-// coalesced loads are issued before the first is folded, so a wave waits on
-// memory once per R rounds instead of once per round (1 M packets fill 4
-// rounds of 256 CUs x 16 waves).  Other waves fold their R rounds one by one.
-template <int R>
+// The small pool [0, ctr->small), one round of 64 packets per wave at a time
+// (two rounds batched per wave, their coalesced loads all issued before the
+// first fold, measured slower: 29.4 against 26.7 us on C4's mix,
+// profiles/r04/s6_mb_class_rates.txt).  Batches whose gather pass folds its
+// blocks' one-line packets itself (PassShape::fused) do not launch it.
 __global__ __launch_bounds__(kBlock) void icrc_rsmall_kernel(RsckArgs a) {
   __shared__ uint32_t lds[kLdsWords];
   const uint32_t count = a.ctr->small;
   if (count == 0) return;  // no one-line packets (wave-uniform): no table build either
-  const uint32_t tab_v = table_entry(g_tab);
-  table_store(lds, tab_v);
+  fill_tables(lds);
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const LaneTab lt{(lane & 31) << 2, ((lane & 31) << 2) | 0x10000u};
   const uint32_t step = gridDim.x * kWaves * 64u;
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.res, 4u * count);
-  auto desc_at = [&](uint32_t pos) -> RsDesc { return a.desc[pos < count ? pos : (count ? count - 1u : 0u)]; };
+  auto desc_at = [&](uint32_t pos) -> RsDesc { return a.desc[pos < count ? pos : count - 1u]; };
   uint32_t base = (blockIdx.x * kWaves + wid) * 64u;
-  RsDesc dn[R];
-  static_for<R>([&](auto rc) { dn[decltype(rc)::value] = desc_at(base + decltype(rc)::value * step + lane); });
-  // one round's wave-uniform shape
-  struct Round {
-    RsDesc d;
-    uint32_t Kmax;
-    bool wa, uk, halfw;
-    uint64_t hb;  // the lane's half line (halfw)
+  RsDesc dn = desc_at(base + lane);
+  for (; base < count; base += step) {
+    const RsDesc d = dn;
+    dn = desc_at(base + step + lane);  // the next round's descriptors, in flight meanwhile
+    const uint32_t v = small_icrc(lds, lt, d, lane);
+    const uint32_t pos = base + lane;
+    __builtin_amdgcn_raw_buffer_store_b32(v, ro, pos < count ? 4u * pos : 0x7FFFFFF0u, 0, 0);
+  }
+}
+
+// Gather: block b serves pass block b's packets.  A staged block's results
+// sit in two contiguous ranges (its small range, its big range): they are
+// read coalesced into LDS in the block's layout order and pos_of indexes
+// that copy, instead of one 4-byte read per packet scattered over the class
+// runs of the pools.  SMALL (PassShape::fused): the block's one-line packets
+// (its small range, descriptors at desc[small0, small0 + small)) are folded
+// here, one lane per packet, instead of by icrc_rsmall_kernel: at C4's
+// 8-GPU shard that kernel took 11.4 us (its launch, its table build, one
+// round of loads) for 131 K packets, profiles/r05/s1_prof_c4s.txt.
+template <int PU, bool SMALL>  // the bucket pass's packets per thread
+__global__ __launch_bounds__(kPassBlock) void rsck_gather(RsckArgs a) {
+  constexpr uint32_t kStage = stage_entries(PU);
+  __shared__ uint32_t lres[kStage];
+  __shared__ uint32_t tab[SMALL ? kLdsWords : 1];
+  const uint32_t tab_v = SMALL ? table_entry(g_tab) : 0u;
+  // The counters are dead now (the bucket pass and both folds have read
+  // them): zero them for the next call on this workspace.
+  if (blockIdx.x == 0 && threadIdx.x == 0) *a.ctr = RsCounters{};
+  uint32_t lo, hi;
+  {
+    uint64_t l, h_;
+    pass_range(a.count, l, h_);
+    lo = (uint32_t)l;
+    hi = (uint32_t)h_;
+  }
+  const RsBlock B = a.blk[blockIdx.x];
+  const uint32_t lane = threadIdx.x & 63;
+  // SMALL: the first of this thread's one-line descriptors (every lane of a
+  // wave with a valid one: the fold is wave-collective), requested with the
+  // other loads; C4's shard blocks hold ~1 K one-line packets, one per thread
+  auto small_desc = [&](uint32_t j) { return a.desc[B.small0 + (j < B.small ? j : B.small - 1u)]; };
+  RsDesc sd0{0u, 0u};
+  if (SMALL && B.small) sd0 = small_desc(threadIdx.x);
+  auto small_fold = [&](auto store) {  // fold the block's small range, store(j, icrc)
+    if (!SMALL || !B.small) return;
+    table_store(tab, tab_v);
+    __syncthreads();
+    const LaneTab lt{(lane & 31) << 2, ((lane & 31) << 2) | 0x10000u};
+#pragma unroll 1
+    for (uint32_t j0 = 0; j0 < B.small; j0 += blockDim.x) {
+      const uint32_t j = j0 + threadIdx.x;
+      if (j0 + (threadIdx.x & ~63u) < B.small) {  // wave-uniform
+        const uint32_t v = small_icrc(tab, lt, j0 ? small_desc(j) : sd0, lane);
+        if (j < B.small) store(j, v);
+      }
+    }
   };
-  auto shape = [&](const RsDesc &d) __attribute__((always_inline)) -> Round {
-    Round o;
-    o.d = d;
-    uint32_t K = (((d.hi >> 16) - 4u) + 4u + 15u) >> 4;  // this lane's blocks
-    // the wave's largest, rounded up to a multiple of 4: by ballots for
-    // one-line packets (K <= 8), a shuffle reduction beyond
-    if (__builtin_amdgcn_ballot_w64(K > 4u) == 0) {
-      o.Kmax = 4u;
-    } else if (__builtin_amdgcn_ballot_w64(K > 8u) == 0) {
-      o.Kmax = 8u;
-    } else {
+  constexpr int U = 4;  // packets per thread in flight at once
+  if (B.staged) {  // block-uniform (a staged block's packets fit one round: hi - lo <= PU x blockDim)
+    // every load of the block issued before the barrier: the positions, then
+    // the results into LDS
+    uint32_t p[PU];
 #pragma unroll
-      for (int w = 32; w >= 1; w >>= 1) K = max(K, (uint32_t)__shfl_xor((int)K, w));
-      o.Kmax = __builtin_amdgcn_readfirstlane((K + 3u) & ~3u);
+    for (int k = 0; k < PU; ++k) {
+      const uint32_t i = lo + (uint32_t)k * blockDim.x + threadIdx.x;
+      p[k] = i < hi ? __builtin_nontemporal_load(a.pos_of + i) : 0xFFFFFFFFu;
     }
-    // wave-uniform variants: word-aligned packets; every packet Kmax blocks long
-    o.wa = __builtin_amdgcn_ballot_w64(((d.lo | (d.hi >> 16)) & 3u) != 0) == 0;
-    // heads in blocks 0..3: rel_4 = M - 16 Kmax + 64 >= 40 for every lane
-    o.uk = __builtin_amdgcn_ballot_w64((d.hi >> 16) - 4u + 24u < 16u * o.Kmax) == 0;
-    // Half-line packets: every covered byte in one aligned 64-byte half
-    // line hb .. hb + 63 whose last 16-byte unit holds the covered end, not
-    // at the half line's end (C4's 64-byte packets: 64-byte aligned, 60
-    // covered bytes).  For a wave of them the 5 units of the 4 blocks are
-    // the half line's units 0, 0, 1, 2, 3, and they are read coalesced: in
-    // load c the 4 lanes of quad p read units 0..3 of lane 4 p + c's half
-    // line (64 contiguous bytes), and a 4 x 4 quad transpose hands every lane
-    // its own -- instead of every lane reading its packet's units alone, 64
-    // lines apart (the access pattern that costs C1's direct kernel, see the
-    // quad kernel in icrc_kernels.hip).
-    const uint64_t pa = ((uint64_t)(d.hi & 0xFFFFu) << 32) | d.lo;
-    const uint64_t pe = pa + ((d.hi >> 16) - 4u);
-    o.hb = (pe - 1u) & ~63ull;
-    const bool half = pa >= o.hb && ((uint32_t)pe & 63u) > 48u;
-    o.halfw = o.Kmax == 4u && __builtin_amdgcn_ballot_w64(!half) == 0;
-    return o;
-  };
-  auto half_line_load = [&](const Round &o, u32x4 (&H)[4]) __attribute__((always_inline)) {
-    const uint32_t hlo = (uint32_t)o.hb, hhi = (uint32_t)(o.hb >> 32), q = lane & 3u;
-    auto at = [&](uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32 | lo) + 16u * q; };
-    H[0] = gload16(at(dpp_quad_bcast<0>(hlo), dpp_quad_bcast<0>(hhi)));
-    H[1] = gload16(at(dpp_quad_bcast<1>(hlo), dpp_quad_bcast<1>(hhi)));
-    H[2] = gload16(at(dpp_quad_bcast<2>(hlo), dpp_quad_bcast<2>(hhi)));
-    H[3] = gload16(at(dpp_quad_bcast<3>(hlo), dpp_quad_bcast<3>(hhi)));
-  };
-  // fold a half-line round from its loaded units
-  auto half_line_fold = [&](const Round &o, u32x4 (&H)[4], uint32_t pos, auto words,
-                            auto uniform) __attribute__((always_inline)) {
-    constexpr bool WA = decltype(words)::value;
-    constexpr int M1 = decltype(uniform)::value ? 1 : 2;
-    quad_transpose(H, lane & 3u);
-    const u32x4 U[5] = {H[0], H[0], H[1], H[2], H[3]};
-    SmallPk P;
-    P.init(o.d, 4u);
-    P.blocks<4, WA, M1>(lds, lt, U);
-    __builtin_amdgcn_raw_buffer_store_b32(~P.reg, ro, pos < count ? 4u * pos : 0x7FFFFFF0u, 0, 0);
-  };
-  // any round, its loads issued and folded here
-  auto one_round = [&](const Round &o, uint32_t pos) __attribute__((always_inline)) {
-    if (o.halfw) {  // wave-uniform
-      u32x4 H[4];
-      half_line_load(o, H);
-      if (o.wa && o.uk)
-        half_line_fold(o, H, pos, std::true_type{}, std::true_type{});
-      else if (o.uk)
-        half_line_fold(o, H, pos, std::false_type{}, std::true_type{});
-      else
-        half_line_fold(o, H, pos, std::false_type{}, std::false_type{});
-      return;
+    const uint32_t total = B.small + 8u * B.groups;
+    const uint32_t *rs = a.res + B.small0, *rb = a.bres + 8ull * B.g0 - B.small;
+    const uint32_t from = SMALL ? B.small : 0u;  // SMALL: the small range is folded below
+    constexpr int R = (kStage + kPassBlock - 1) / kPassBlock;
+    uint32_t v[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      const uint32_t j = (uint32_t)k * blockDim.x + threadIdx.x;
+      v[k] = j >= from && j < total ? __builtin_nontemporal_load((j < B.small ? rs : rb) + j) : 0u;
     }
-    SmallPk P;
-    P.init(o.d, o.Kmax);
-    auto run = [&](auto words, auto uniform) __attribute__((always_inline)) {
-      constexpr bool WA = decltype(words)::value;
-      constexpr int M1 = decltype(uniform)::value ? 1 : 2, M2 = decltype(uniform)::value ? 0 : 2;
-      // Kmax = 8 q + r (r = 0 or 4): a first chunk of r or 8 blocks, then
-      // chunks of 8 (one-line packets: M <= 124, Kmax <= 8 -- one chunk, at
-      // most 9 units = 36 VGPRs in flight; longer chunks spilled once two
-      // rounds' descriptors are live)
-      uint32_t j = 0;
-      if ((o.Kmax & 7u) == 4u) {  // wave-uniform
-        P.chunk<4, WA, M1>(lds, lt, 0);
-        j = 4;
-      } else {
-        P.chunk<8, WA, M1>(lds, lt, 0);
-        j = 8;
-      }
-      for (; j < o.Kmax; j += 8) P.chunk<8, WA, M2>(lds, lt, j);
-    };
-    if (o.wa && o.uk)
-      run(std::true_type{}, std::true_type{});
-    else if (o.uk)
-      run(std::false_type{}, std::true_type{});
-    else
-      run(std::false_type{}, std::false_type{});
-    __builtin_amdgcn_raw_buffer_store_b32(~P.reg, ro, pos < count ? 4u * pos : 0x7FFFFFF0u, 0, 0);
-  };
-  for (; base < count; base += R * step) {
-    RsDesc d[R];
-    Round o[R];
-    bool all_half = true;
-    static_for<R>([&](auto rc) {
-      constexpr int r = decltype(rc)::value;
-      d[r] = dn[r];
-      dn[r] = desc_at(base + (R + r) * step + lane);  // the next iteration's descriptors, in flight meanwhile
-      if (R > 1) {
-        o[r] = shape(d[r]);
-        all_half = all_half & o[r].halfw & o[r].wa & o[r].uk;
-      }
-    });
-    // wave-uniform: rounds of word-aligned half-line packets (C4's 64-byte
-    // packets; one fold variant, no branch between the rounds' folds, so the
-    // compiler cannot sink a round's loads to its fold)
-    if (R > 1 && all_half) {
-      u32x4 H[R][4];
-      static_for<R>([&](auto rc) { half_line_load(o[decltype(rc)::value], H[decltype(rc)::value]); });
-      __builtin_amdgcn_sched_barrier(0);
-      static_for<R>([&](auto rc) {
-        constexpr int r = decltype(rc)::value;
-        half_line_fold(o[r], H[r], base + r * step + lane, std::true_type{}, std::true_type{});
-      });
-    } else {
-      // (only the descriptors stay live across a round: the shape is
-      // recomputed, so a 16-block chunk's units do not spill the others)
-      static_for<R>([&](auto rc) {
-        constexpr int r = decltype(rc)::value;
-        if (base + r * step < count) one_round(shape(d[r]), base + r * step + lane);  // wave-uniform
-      });
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      const uint32_t j = (uint32_t)k * blockDim.x + threadIdx.x;
+      if (j >= from && j < total) lres[j] = v[k];
+    }
+    small_fold([&](uint32_t j, uint32_t x) { lres[j] = x; });
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PU; ++k) {
+      const uint32_t i = lo + (uint32_t)k * blockDim.x + threadIdx.x;
+      if (i < hi) __builtin_nontemporal_store(gather_one(a, i, p[k], p[k] != 0xFFFFFFFFu ? lres[p[k]] : 0u), a.out + i);
+    }
+    return;
+  }
+  // not staged: the small results go to the pool first (a workgroup-scope
+  // barrier orders those stores before the reads below)
+  small_fold([&](uint32_t j, uint32_t x) { a.res[B.small0 + j] = x; });
+  if (SMALL && B.small) __syncthreads();
+  for (uint32_t i0 = lo + threadIdx.x; i0 < hi; i0 += U * blockDim.x) {
+    uint32_t p[U], v[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) p[k] = i0 + k * blockDim.x < hi ? a.pos_of[i0 + k * blockDim.x] : 0xFFFFFFFFu;
+#pragma unroll
+    for (int k = 0; k < U; ++k) v[k] = p[k] != 0xFFFFFFFFu ? a.res[p[k]] : 0u;
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const uint32_t i = i0 + k * blockDim.x;
+      if (i >= hi) break;
+      a.out[i] = gather_one(a, i, p[k], v[k]);
     }
   }
 }
@@ -1270,6 +1257,7 @@ static void launch_bucket_u(const RsckArgs &a, int pgrid, hipStream_t st) {
 // (tools/microbench/shard.hip, profiles/r05/s1_mb_shard_baseline.txt).
 struct PassShape {
   int grid, U;
+  bool fused;  // the gather folds the one-line packets (U = 4, one staged round per block): no icrc_rsmall_kernel
 };
 static PassShape pass_shape(uint64_t count, int pass_cap) {
   int U = kPassUnrollBig;
@@ -1281,8 +1269,9 @@ static PassShape pass_shape(uint64_t count, int pass_cap) {
   const uint64_t want = (count + (uint64_t)U * kPassBlock - 1) / ((uint64_t)U * kPassBlock);
   int grid = (int)(want < (uint64_t)kPassBlocks ? (want ? want : 1) : kPassBlocks);
   if (pass_cap > 0 && pass_cap < grid) grid = pass_cap;  // RICRC_RS_PASS_GRID (blocks then take several rounds)
-  return PassShape{grid, U};
+  return PassShape{grid, U, U == 4 && (uint64_t)grid * 4u * kPassBlock >= count};
 }
+bool rs_fused(uint64_t count, int pass_cap) { return count > 0 && pass_shape(count, pass_cap).fused; }
 static void launch_bucket(const RsckArgs &a, const PassShape &ps, hipStream_t st) {
   switch (ps.U) {
     case 4: launch_bucket_u<4>(a, ps.grid, st); break;
@@ -1293,10 +1282,13 @@ static void launch_bucket(const RsckArgs &a, const PassShape &ps, hipStream_t st
 }
 static void launch_gather(const RsckArgs &a, const PassShape &ps, hipStream_t st) {
   switch (ps.U) {  // the gather's blocks are the bucket pass's (block b serves pass block b's packets)
-    case 4: hipLaunchKernelGGL(rsck_gather<4>, dim3(ps.grid), dim3(kPassBlock), 0, st, a); break;
-    case 8: hipLaunchKernelGGL(rsck_gather<8>, dim3(ps.grid), dim3(kPassBlock), 0, st, a); break;
-    case kPassUnroll: hipLaunchKernelGGL(rsck_gather<kPassUnroll>, dim3(ps.grid), dim3(kPassBlock), 0, st, a); break;
-    default: hipLaunchKernelGGL(rsck_gather<kPassUnrollBig>, dim3(ps.grid), dim3(kPassBlock), 0, st, a); break;
+    case 4:
+      if (ps.fused) hipLaunchKernelGGL((rsck_gather<4, true>), dim3(ps.grid), dim3(kPassBlock), 0, st, a);
+      else hipLaunchKernelGGL((rsck_gather<4, false>), dim3(ps.grid), dim3(kPassBlock), 0, st, a);
+      break;
+    case 8: hipLaunchKernelGGL((rsck_gather<8, false>), dim3(ps.grid), dim3(kPassBlock), 0, st, a); break;
+    case kPassUnroll: hipLaunchKernelGGL((rsck_gather<kPassUnroll, false>), dim3(ps.grid), dim3(kPassBlock), 0, st, a); break;
+    default: hipLaunchKernelGGL((rsck_gather<kPassUnrollBig, false>), dim3(ps.grid), dim3(kPassBlock), 0, st, a); break;
   }
 }
 
@@ -1315,11 +1307,12 @@ hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, hipStream_t st, hipE
   mark(1);
   hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, st, a);
   mark(2);
-  // the small pool [0, ctr->small): one lane per packet.  (Round 4 ran it on
-  // 1/16 of the CUs on a second stream beside the fold instead: the step
+  // the small pool [0, ctr->small): one lane per packet, unless the gather
+  // folds each block's one-line packets itself (ps.fused).  (Round 4 ran it
+  // on 1/16 of the CUs on a second stream beside the fold instead: the step
   // took 1.050 against 0.999 ms -- its scattered half-line reads slowed the
   // fold by 60 us, profiles/r04/s2_*.)
-  hipLaunchKernelGGL((icrc_rsmall_kernel<kSmallRounds>), dim3(grid), dim3(kBlock), 0, st, a);
+  if (!ps.fused) hipLaunchKernelGGL(icrc_rsmall_kernel, dim3(grid), dim3(kBlock), 0, st, a);
   mark(3);
   launch_gather(a, ps, st);
   mark(4);

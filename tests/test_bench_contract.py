@@ -135,10 +135,16 @@ def test_kernel_labels_follow_the_dispatch():
     assert "(icrc_sck_kernel)" in lab() and "(icrc_sck_kernel)" in lab("--size", "1024")
     assert lab("--size", "64") == "quad ICRC kernel (64-byte packets, lane-quad transposes) (icrc_quad_kernel)"
     assert "(icrc_tsk_kernel)" in lab("--size", "256")
-    mix = lab("--mix")  # the ragged pipeline's passes, in launch order
+    mixa = bench.parse(["--mix"])
+    mix = bench.kernel_label(mixa, count=mixa.count)  # C4's 4 M packets: the ragged pipeline's passes, in launch order
     assert mix.split(" -> ") == ["bucket pass (rsck_bucket)",
                                  "strided-chain fold of packets of >= 2 lines (icrc_rsck_kernel)",
                                  "one-line packets (icrc_rsmall_kernel)", "gather (rsck_gather)"]
+    # C4's 8-GPU shard (about 524 K packets): the gather folds the one-line packets
+    shard = bench.kernel_label(bench.parse(["--mix", "--count", "524288"]), count=524288)
+    assert shard.split(" -> ") == ["bucket pass (rsck_bucket)",
+                                   "strided-chain fold of packets of >= 2 lines (icrc_rsck_kernel)",
+                                   "gather, folding the one-line packets (rsck_gather)"]
     assert "family_fix_kernel" in lab("--size", "64", "--family", "v6")
     assert "family_fix_kernel" not in lab("--family", "v6")  # the SCK applies IPv6 masks natively
     assert "count/plan" not in mix and "scatter" not in mix
