@@ -61,14 +61,18 @@ QUAD_SOURCES = ("icrc_kernels.hip", "icrc_kernels.h", "icrc_device.h", "icrc_mat
 RAGGED_KERNELS = ("rsck_bucket", "icrc_rsck_kernel", "icrc_rsmall_kernel", "rsck_gather")
 
 
-def traffic_record(mix, size, count=None):
+def traffic_record(mix, size, count=None, l3_offset=0, stride=None):
     """(profiles/ file, kernel sources, kernel names) of the PMC traffic
     record for a workload of `count` packets on this rank (tools/pmc_traffic.py
     writes it), or None.  The BASELINE counts (1 M fixed-size packets, 4 M
     mixed) keep their round-3 names; other counts (C3's 16 GiB batch, the
-    8-GPU shard stand-ins) carry the count in the name."""
+    8-GPU shard stand-ins) carry the count in the name; framed rings their
+    slot and L3 offset."""
     std = (4 << 20) if mix else (1 << 20)
     tag = "" if count in (None, std) else f"_{count}"
+    if l3_offset:
+        return (f"pmc_traffic_ring{l3_offset}_{stride or size}{tag}.json", RAGGED_SOURCES,
+                RAGGED_KERNELS + ("icrc_rsck_uni_kernel",))
     if mix:
         return f"pmc_traffic_mix{tag}.json", RAGGED_SOURCES, RAGGED_KERNELS
     if size == 4096:
@@ -123,9 +127,28 @@ def parse(argv=None):
                     help="with --pass-times: seconds to wait after the first amd-smi reading (diagnostics)")
     ap.add_argument("--plan-only", action="store_true",
                     help="print the shard plan every rank would run (gloo, no GPU) and exit")
+    # Ethernet-framed NIC rings (common/huge_malloc.h:12-22):
+    # slots of --stride bytes (default --size), the L3 packet at --l3-offset
+    # in each, stride - l3_offset bytes long.
+    ap.add_argument("--l3-offset", type=int, default=0, help="L3 start inside each slot (14: Ethernet framing)")
+    ap.add_argument("--stride", type=int, default=None, help="slot bytes of a framed ring (default --size)")
+    # The other BASELINE configs, measured by the same command after the
+    # headline: N = 1 adds c1 (1 M x 64 B), c2 (1 M x
+    # 1 KiB) and c4 (the 4 M mix); N > 1 adds c3_strong (4 M x 4 KiB in all)
+    # and c4_strong (the 4 M mix in all, byte-balanced).
+    ap.add_argument("--no-side", action="store_true", help="the main workload only")
+    ap.add_argument("--side-count", type=int, default=None,
+                    help="packets of every side config (tests; default: the BASELINE counts)")
     a = ap.parse_args(argv)
     if a.count is None:
         a.count = (4 << 20) if a.mix else (1 << 20)
+    if a.stride is None:
+        a.stride = a.size
+    if a.mix and (a.l3_offset or a.stride != a.size):
+        ap.error("--l3-offset / --stride describe fixed-slot rings, not --mix")
+    if not 0 <= a.l3_offset < a.stride:
+        ap.error("--l3-offset must lie inside the slot")
+    a.pkt = a.stride - a.l3_offset  # L3 bytes per packet
     return a
 
 
@@ -170,7 +193,7 @@ def load_traffic(args, count):
     """HBM bytes per launch measured by separate rocprofv3 --pmc passes
     (profiles/pmc_traffic*.json, from tools/pmc_traffic.py) on this very
     workload and kernel source, or None."""
-    rec = traffic_record(args.mix, args.size, count)
+    rec = traffic_record(args.mix, args.size, count, args.l3_offset, args.stride)
     if args.family != "v4" or rec is None:
         return None
     name, srcs, _ = rec
@@ -180,6 +203,7 @@ def load_traffic(args, count):
             d = json.load(f)
         same = d.get("count") == count and d.get("kernel_src") == kernel_source_hash(srcs)
         same = same and (d.get("size") == "mix" if args.mix else d.get("size") == args.size)
+        same = same and d.get("l3_offset", 0) == args.l3_offset and d.get("stride", args.size) == args.stride
         if same:
             return d.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
@@ -209,7 +233,7 @@ def kernel_path(args, base=0x100000, count=1):
 
     if args.mix:
         return roce_icrc.kernel_path(base, count, offsets=8, lengths=8, family=args.family)
-    return roce_icrc.kernel_path(base, count, stride=args.size, family=args.family)
+    return roce_icrc.kernel_path(base, count, stride=args.stride, l3_offset=args.l3_offset, family=args.family)
 
 
 def kernel_label(args, base=0x100000, count=1):
@@ -291,8 +315,8 @@ def oracle_check(gathered, sizes, cuts, args, lens_global=None, per_rank=256):
         idx = np.unique(np.concatenate([np.arange(min(per_rank, n)),
                                         np.linspace(0, n - 1, num=min(per_rank, n)).astype(np.int64)]))
         if lens_global is None:
-            pk = np.concatenate([oracle_c.synth_batch(args.seed, lo + int(k), 1, args.size) for k in idx])
-            want = oracle_c.icrc_batch(pk.reshape(-1), stride=args.size, family=args.family)
+            pk = np.concatenate([oracle_c.synth_batch(args.seed, lo + int(k), 1, args.pkt) for k in idx])
+            want = oracle_c.icrc_batch(pk.reshape(-1), stride=args.pkt, family=args.family)
         else:
             lens = lens_global[lo + idx]
             bufs = [oracle_c.synth_ragged(args.seed, lo + int(k), lens[j:j + 1])[0] for j, k in enumerate(idx)]
@@ -449,6 +473,16 @@ def build_batch(torch, np, ctx, dev, stream, args, world, rank):
         ctx.synth_ragged_device(buf, args.seed, lo, len(lens), d_offs, d_lens, stream=stream)
         b.update(buf=buf, d_offs=d_offs, d_lens=d_lens, h_offs=offs, h_lens=lens, lens_global=lens_g,
                  rank_bytes=nbytes)
+    elif args.l3_offset:  # a framed ring: the L3 packet at l3_offset in each stride-byte slot
+        n = hi - lo
+        buf = torch.zeros(max(n * args.stride, 1), dtype=torch.uint8, device=dev)
+        if n:
+            offs = torch.arange(n, dtype=torch.int64, device=dev) * args.stride + args.l3_offset
+            lens = torch.full((n,), args.pkt, dtype=torch.int32, device=dev)
+            ctx.synth_ragged_device(buf, args.seed, lo, n, offs, lens, stream=stream)
+            stream.synchronize()
+            del offs, lens
+        b.update(buf=buf, d_offs=None, d_lens=None, lens_global=None, rank_bytes=n * args.pkt)
     else:
         buf = torch.empty(max((hi - lo) * args.size, 1), dtype=torch.uint8, device=dev)
         ctx.synth_device(buf, args.seed, lo, hi - lo, args.size, stream=stream)
@@ -471,7 +505,7 @@ def plan_only(args, world, rank):
     T, cuts, lens_g = shard_plan(args, world)
     sizes = cuts_to_sizes(cuts)
     lo, hi = cuts[rank], cuts[rank + 1]
-    mine = int(lens_g[lo:hi].sum(dtype=np.uint64)) if lens_g is not None else (hi - lo) * args.size
+    mine = int(lens_g[lo:hi].sum(dtype=np.uint64)) if lens_g is not None else (hi - lo) * args.pkt
     if world > 1:
         dist.init_process_group("gloo")
         got = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
@@ -507,6 +541,10 @@ def metric_for(args, T, count):
         scope = f"{_count_label(T)} in all" if args.global_count is not None else f"{_count_label(args.count)} per GPU"
         return (f"device-resident ICRC GiB/s on mixed-MTU (64/256/1024/4096 B) RoCE packets ({scope}); "
                 "bit-exact vs reference")
+    if args.l3_offset:
+        scope = f"{_count_label(T)} in all" if args.global_count is not None else f"{_count_label(args.count)} per GPU"
+        return (f"device-resident ICRC GiB/s on {args.pkt}B RoCE packets in {args.stride}B Ethernet-framed ring slots "
+                f"(L3 at offset {args.l3_offset}; {scope}); bit-exact vs reference")
     if args.global_count is None and args.size == 4096 and args.count == 1 << 20:
         return METRIC
     if args.global_count is not None:
@@ -551,7 +589,8 @@ class HipBackend:
             self.ctx.batch_device(b["buf"], count, out, offsets=b["d_offs"], lengths=b["d_lens"], stream=self.stream,
                                   family=args.family)
         else:
-            self.ctx.batch_device(b["buf"], count, out, stride=args.size, stream=self.stream, family=args.family)
+            self.ctx.batch_device(b["buf"], count, out, stride=args.stride, l3_offset=args.l3_offset,
+                                  stream=self.stream, family=args.family)
 
     def sync(self):
         self.torch.cuda.synchronize()
@@ -568,6 +607,17 @@ class HipBackend:
 
     def pass_times(self):
         return self.ctx.pass_times()
+
+    def launch_info(self, b, count, args):
+        """The dispatch's launch of this batch (ricrc_launch_info): grid, the
+        per-XCD work-split weights and the recorded start XCD."""
+        if args.mix:
+            return self.ctx.launch_info(b["buf"], count, offsets=b["d_offs"], lengths=b["d_lens"])
+        return self.ctx.launch_info(b["buf"], count, stride=args.stride, l3_offset=args.l3_offset)
+
+    def release(self):
+        self.torch.cuda.synchronize()
+        self.torch.cuda.empty_cache()
 
     def host_bytes(self, b, nbytes):
         return b["buf"][:nbytes].cpu().numpy()
@@ -589,7 +639,7 @@ def run(args, world, rank, be, distributed):
 
     from roce_icrc.dist import IcrcGather
 
-    if distributed:
+    if distributed and not dist.is_initialized():
         be.init_dist()
     b = be.build(args, world, rank)
     count, sizes = b["sizes"][rank], b["sizes"]
@@ -753,6 +803,9 @@ def run(args, world, rank, be, distributed):
                     "lengths uniform over 64/256/1024/4096 B, packed, uint64 offsets + uint32 lengths, "
                     f"shards cut at equal bytes; rank 0: {sizes[0]} packets, {rank_bytes if rank == 0 else '?'} B; "
                     f"device-resident, ragged path: {label}")
+    elif args.l3_offset:
+        workload = (f"{b['T']} x {args.pkt} B RoCEv2 packets in all ({count} on rank 0), each at offset "
+                    f"{args.l3_offset} of a {args.stride} B Ethernet-framed ring slot, device-resident, " + label)
     else:
         workload = (f"{b['T']} x {args.size} B RoCEv2 packets in all ({count} on rank 0), device-resident, "
                     + label)
@@ -772,13 +825,26 @@ def run(args, world, rank, be, distributed):
         "dtype": "u8",
         "data": "synthetic (device-generated RoCEv2 SEND_ONLY packets, seeded; reference P4 header template)",
         "config": {"workload": workload, "packets_total": b["T"], "packets_rank0": sizes[0], "family": args.family,
-                   "packet_bytes": "mix 64/256/1024/4096" if args.mix else args.size,
+                   "packet_bytes": "mix 64/256/1024/4096" if args.mix else args.pkt,
                    "parallelism": f"dp{world}" + (" (all-gather u32 results)" if do_gather else "")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": alg_bytes},
         "oracle_sampled_all_ranks": True,
+        # how the number was taken: untimed, before the warmup
+        # steps, ricrc_prime's streaming reads and the workload's own steps
+        # (the board's power ramps over tens of ms of sustained load)
+        "method": {"prime_ms": args.prime_ms, "warm_ms": args.warm_ms, "warmup_steps": args.warmup,
+                   "timing": "one HIP event pair around the K steps on the kernels' stream; value from wall "
+                             "time between barrier + synchronize"},
     }
+    if args.l3_offset:
+        result["config"].update(l3_offset=args.l3_offset, slot_bytes=args.stride)
+    if hasattr(be, "launch_info") and count:
+        try:
+            result["launch"] = be.launch_info(b, count, args)
+        except Exception as e:  # diagnostics only
+            result["launch"] = f"unavailable: {e}"
     result.update(diag)
     if distributed:
         result["world_size"] = dist.get_world_size()
@@ -786,6 +852,48 @@ def run(args, world, rank, be, distributed):
         result["rccl_version"] = rccl_version()
         result.update(split)
     return result, full_h, b
+
+
+# BASELINE.json's other configs: measured after the main
+# workload in the same process, each with its own warm phase and K steps.
+SIDE_N1 = (("c1", ["--size", "64"]), ("c2", ["--size", "1024"]), ("c4", ["--mix"]))
+SIDE_NX = (("c3_strong", ["--global-count", str(4 << 20)]), ("c4_strong", ["--mix", "--global-count", str(4 << 20)]))
+SIDE_KEYS = ("metric", "value", "unit", "ms_per_step", "scaling", "compute_only_ms_per_step", "gather_ms",
+             "oracle_sampled_all_ranks", "launch")
+
+
+def side_args(args, extra):
+    """The parsed arguments of a side config: the main run's K, W, seed,
+    family, gather mode and warm phase (no second primer: the device is busy
+    already), the config's own shape (--side-count overrides its count)."""
+    argv = extra + ["--gpus", str(args.gpus), "--steps", str(args.steps), "--warmup", str(args.warmup),
+                    "--seed", str(args.seed), "--family", args.family, "--prime-ms", "0",
+                    "--warm-ms", str(args.warm_ms), "--no-side", "--no-cpu"]
+    argv += ["--no-gather"] if args.no_gather else []
+    argv += [] if args.overlap_gather else ["--in-stream-gather"]
+    sa = parse(argv)
+    if args.side_count is not None:
+        if sa.global_count is not None:
+            sa.global_count = args.side_count
+        else:
+            sa.count = args.side_count
+    return sa
+
+
+def run_side(args, world, rank, be, distributed):
+    """{name: compact result} for the side configs of this world size."""
+    out = {}
+    for name, extra in (SIDE_N1 if world == 1 else SIDE_NX):
+        sa = side_args(args, extra)
+        r, _, sb = run(sa, world, rank, be, distributed)
+        d = {k: r[k] for k in SIDE_KEYS if k in r}
+        d["config"] = {k: r["config"][k] for k in ("workload", "packets_total", "packets_rank0")}
+        d["roofline"] = {k: r["roofline"][k] for k in ("achieved", "frac", "traffic", "kernel_ms", "alg_bytes_per_launch")}
+        out[name] = d
+        del sb
+        if hasattr(be, "release"):
+            be.release()
+    return out
 
 
 def main(argv=None):
@@ -804,6 +912,7 @@ def main(argv=None):
     if args.plan_only:
         return plan_only(args, world, rank)
 
+    import numpy as np
     import torch.distributed as dist
 
     be = HipBackend(local, pass_times=args.pass_times)
@@ -821,10 +930,17 @@ def main(argv=None):
             result["cpu_baseline"] = cpu_baseline(sample, got, args.size, args.cpu_seconds,
                                                   offsets=h_offs[:ns].copy(), lengths=h_lens[:ns].copy(),
                                                   family=args.family)
-        else:
-            sample = be.host_bytes(b, ns * args.size).reshape(ns, args.size)
-            result["cpu_baseline"] = cpu_baseline(sample, got, args.size, args.cpu_seconds, family=args.family)
+        else:  # (a framed ring: its slots' L3 packets, contiguous on the host)
+            sample = be.host_bytes(b, ns * args.stride).reshape(ns, args.stride)[:, args.l3_offset:]
+            result["cpu_baseline"] = cpu_baseline(np.ascontiguousarray(sample), got, args.pkt, args.cpu_seconds,
+                                                  family=args.family)
         result["c0"] = c0_latency()
+
+    if not args.no_side:  # the other BASELINE configs, by the same command
+        del full_h, b
+        if hasattr(be, "release"):
+            be.release()
+        result.update(run_side(args, world, rank, be, distributed))
 
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -176,7 +176,19 @@ int ricrc_device_count(const ricrc_ctx *ctx);
  * bad descriptors apart use ricrc_batch_device_st (a status per packet).
  * 16-byte aligned packet starts with a fixed length take the streaming
  * kernels; anything else (offsets, lengths, any alignment or mix of sizes)
- * the ragged pipeline, several packets per wave. */
+ * the ragged pipeline, several packets per wave.
+ *
+ * Buffer extent.  The caller owns the buffers (the reference's huge_malloc
+ * MRs, common/huge_malloc.h:12-22) and every descriptor must lie inside the
+ * caller's allocation: packet i's bytes [off[i] + l3_offset, + len[i]).  The
+ * device calls take no extent and read the packets in place: a descriptor
+ * past the end of the allocation makes the kernels read out of bounds (a GPU
+ * memory fault, as a DMA engine given a bad descriptor would), it is NOT
+ * reported as -EINVAL.  Callers whose descriptors are not trusted use
+ * ricrc_batch_device_bounded / ricrc_batch_host_bounded below.
+ * ricrc_batch_host checks the descriptors against the buffer when it knows
+ * the buffer's size -- base inside a ricrc_host_alloc / ricrc_host_register
+ * range -- and returns -EINVAL (reading nothing) for one past its end. */
 int ricrc_batch_host(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *off, const uint32_t *len,
                      uint32_t stride, uint64_t count, uint32_t l3_offset, uint32_t *out);
 int ricrc_batch_device(ricrc_ctx *ctx, int dev, const void *d_base, const uint64_t *d_off,
@@ -247,6 +259,24 @@ int ricrc_batch_host_st(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *off
 int ricrc_classify_device(ricrc_ctx *ctx, int dev, const void *d_base, const uint64_t *d_off,
                           const uint32_t *d_len, uint32_t stride, uint64_t count, uint32_t l3_offset,
                           uint8_t *d_class, void *stream);
+
+/* Extent-checked batches, for descriptors that are not trusted: base_bytes
+ * is the size of the caller's buffer at base (> 0, else -EINVAL).
+ * ricrc_batch_device_bounded: as ricrc_batch_device_st; a packet whose bytes
+ *   do not all lie in [d_base, d_base + base_bytes) is never read and gets
+ *   RICRC_ST_BADLEN and out[i] = 0.  A fixed-stride batch (no d_off, no
+ *   d_len) that does not fit is -EINVAL.  Per-packet descriptors cost one
+ *   pre-pass over them (12 bytes per packet, the RICRC_F_FRAMELEN pass).
+ * ricrc_batch_host_bounded: as ricrc_batch_host_st with status != NULL (a
+ *   packet outside the buffer: RICRC_ST_BADLEN, never read); with status ==
+ *   NULL (flags: a family, optionally | RICRC_F_FRAMELEN) any packet outside
+ *   the buffer, or of a bad length, is -EINVAL and nothing is computed. */
+int ricrc_batch_device_bounded(ricrc_ctx *ctx, int dev, const void *d_base, uint64_t base_bytes,
+                               const uint64_t *d_off, const uint32_t *d_len, uint32_t stride, uint64_t count,
+                               uint32_t l3_offset, uint32_t *d_out, uint8_t *d_status, void *stream, uint32_t flags);
+int ricrc_batch_host_bounded(ricrc_ctx *ctx, const uint8_t *base, uint64_t base_bytes, const uint64_t *off,
+                             const uint32_t *len, uint32_t stride, uint64_t count, uint32_t l3_offset, uint32_t *out,
+                             uint8_t *status, uint32_t flags);
 
 /* Batch incremental repair on the device, after a header rewrite of packets
  * that were already stamped -- the switch egress's PSN/MSN/opcode patches
@@ -376,6 +406,27 @@ void *ricrc_stream(ricrc_ctx *ctx, int dev);
  * Bench and test labels come from here, so they name what actually ran. */
 const char *ricrc_kernel_path(const ricrc_ctx *ctx, const void *d_base, const uint64_t *d_off, const uint32_t *d_len,
                               uint32_t stride, uint64_t count, uint32_t l3_offset, uint32_t flags);
+
+/* How a batch of that shape would be launched on context device dev, as the
+ * dispatch decides it (no GPU work): the main kernel's workgroups, the
+ * per-XCD weights of its work split (all 0: equal shares; the SCK's 4 KiB
+ * path and the ragged fold weight the odd-numbered XCDs, which stream HBM a
+ * few per cent slower), the XCD the device's last strided-chain launch
+ * started on (the next launch's k in the split), and for the ragged
+ * pipeline its bucket / gather pass blocks, packets per thread and whether
+ * the gather folds the one-line packets.  bench.py reports it next to its
+ * numbers.  0, or -EINVAL as ricrc_kernel_path's NULL. */
+typedef struct {
+  uint32_t grid;           /* workgroups of the main kernel (0: not reported for this path) */
+  uint32_t xcd_weights[8]; /* the main kernel's work split by XCD; all 0 = equal shares */
+  uint32_t start_xcd;      /* recorded by the last strided-chain kernel on this device */
+  uint32_t pass_grid;      /* ragged: bucket / gather blocks (0 otherwise) */
+  uint32_t pass_unroll;    /* ragged: packets per thread of those passes */
+  uint32_t fused;          /* ragged: 1 if the gather folds the one-line packets */
+} ricrc_launch_info_t;
+int ricrc_launch_info(const ricrc_ctx *ctx, int dev, const void *d_base, const uint64_t *d_off,
+                      const uint32_t *d_len, uint32_t stride, uint64_t count, uint32_t l3_offset,
+                      ricrc_launch_info_t *info);
 
 /* Diagnostics: with RICRC_PASS_TIMES set when the context was created, every
  * ragged-pipeline call on device dev records timing events between its

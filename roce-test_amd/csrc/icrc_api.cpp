@@ -411,7 +411,7 @@ int launch_rsck_range(Dev &d, const uint8_t *base, const uint64_t *off, const ui
   int rgrid = d.n_cu;
   if (d.knobs.rsck_grid > 0) rgrid = std::min(rgrid, d.knobs.rsck_grid);
   hipEvent_t *pev = nullptr;
-  if (d.knobs.pass_times) {
+  if (d.knobs.pass_times && count > 0 && count <= kRsMaxCount) {  // (launch_rsck records all five events then)
     if (d.pt_ev.empty()) {
       d.pt_ev.resize(5 * Dev::kPtSets);
       for (hipEvent_t &ev : d.pt_ev) HIP_TRY(hipEventCreate(&ev));
@@ -730,12 +730,16 @@ Knobs read_knobs() {
   k.pass_times = getenv("RICRC_PASS_TIMES") != nullptr;
   k.fail_chunk = num("RICRC_FAIL_CHUNK", -1);
   k.xcd_skew = (int)std::min(500L, std::max(-1L, num("RICRC_XCD_SKEW", -1)));
-  if (const char *e = getenv("RICRC_XCD_WEIGHTS")) {  // eight weights in 1..10000, else ignored
+  // Eight weights in 1..8000, else ignored.  The bound keeps xcd_share's
+  // 64-bit products exact: total work S < 2^28 packets x 2064 quarter-steps
+  // = 2^39.01, times the weight sum of 256 workgroups x 16 waves (at most
+  // 512 x 64000 < 2^24.97) stays below 2^64.
+  if (const char *e = getenv("RICRC_XCD_WEIGHTS")) {
     uint32_t w[8];
     int n = 0;
     for (const char *c = e; *c && n < 8;) {
       const long v = atol(c);
-      if (v < 1 || v > 10000) break;
+      if (v < 1 || v > 8000) break;
       w[n++] = (uint32_t)v;
       while (*c && *c != ',') ++c;
       if (*c == ',') ++c;
@@ -821,6 +825,7 @@ int ricrc_pass_times(ricrc_ctx *ctx, int dev, float *ms, int n) {
   if (!g.ok()) return -ENODEV;
   for (int k = 0; k < n; ++k) ms[k] = 0.f;
   const int used = d.pt_used;
+  d.pt_used = 0;  // forgotten whatever happens below: a failed query does not fail every later one
   for (int c = 0; c < used; ++c) {  // the oldest recorded set first
     hipEvent_t *e = &d.pt_ev[5 * ((d.pt_next - used + c + Dev::kPtSets) % Dev::kPtSets)];
     HIP_TRY(hipEventSynchronize(e[4]));
@@ -830,7 +835,6 @@ int ricrc_pass_times(ricrc_ctx *ctx, int dev, float *ms, int n) {
       ms[k] += t;
     }
   }
-  d.pt_used = 0;
   return used;
 }
 
@@ -851,6 +855,35 @@ const char *ricrc_kernel_path(const ricrc_ctx *ctx, const void *d_base, const ui
       return fused ? "rsck_bucket+icrc_rsck_kernel+rsck_gather+family_fix_kernel"
                    : "rsck_bucket+icrc_rsck_kernel+icrc_rsmall_kernel+rsck_gather+family_fix_kernel";
   }
+}
+
+int ricrc_launch_info(const ricrc_ctx *ctx, int dev, const void *d_base, const uint64_t *d_off,
+                      const uint32_t *d_len, uint32_t stride, uint64_t count, uint32_t l3_offset,
+                      ricrc_launch_info_t *info) {
+  if (!ctx || !info || dev < 0 || dev >= (int)ctx->devs.size() || !d_base || count == 0) return -EINVAL;
+  if ((!d_off && stride == 0) || (!d_len && stride <= l3_offset)) return -EINVAL;
+  const Dev &d = ctx->devs[dev];
+  *info = ricrc_launch_info_t{};
+  info->start_xcd = xcd_start(d.h_xcd);
+  const uint8_t *base = (const uint8_t *)d_base;
+  const Path p = choose_path(ctx->knobs, base, d_off, d_len, stride, l3_offset);
+  XcdWeights xw{};
+  if (p == Path::kSck) {
+    const uint32_t fixed_len = stride - l3_offset;
+    info->grid = (uint32_t)sck_grid(d, base, d_off, d_len, stride, count, l3_offset);
+    xw = xcd_weights(ctx->knobs, fixed_len != 4096 ? 0 : (int)info->grid < d.n_cu ? 25 : 50);
+  } else if (p == Path::kRagged) {
+    info->grid = (uint32_t)(d.knobs.rsck_grid > 0 ? std::min(d.n_cu, d.knobs.rsck_grid) : d.n_cu);
+    xw = xcd_weights(d.knobs, 40);
+    int pg = 0, pu = 0;
+    bool fused = false;
+    rs_pass_info(std::min<uint64_t>(count, kRsChunk), d.knobs.pass_grid, &pg, &pu, &fused);
+    info->pass_grid = (uint32_t)pg;
+    info->pass_unroll = (uint32_t)pu;
+    info->fused = fused ? 1u : 0u;
+  }
+  for (int x = 0; x < 8; ++x) info->xcd_weights[x] = xw.w[x];
+  return 0;
 }
 
 static int batch_device_impl(ricrc_ctx *ctx, int dev, const void *d_base, const uint64_t *d_off,
@@ -893,9 +926,11 @@ int ricrc_verify_device_ex(ricrc_ctx *ctx, int dev, const void *d_base, const ui
   return batch_device_impl(ctx, dev, d_base, d_off, d_len, stride, count, l3_offset, d_out, stream, true, flags);
 }
 
-int ricrc_batch_device_st(ricrc_ctx *ctx, int dev, const void *d_base, const uint64_t *d_off,
-                          const uint32_t *d_len, uint32_t stride, uint64_t count, uint32_t l3_offset,
-                          uint32_t *d_out, uint8_t *d_status, void *stream, uint32_t flags) {
+// The *_st device calls; extent > 0 (ricrc_batch_device_bounded): packets
+// must lie in [d_base, d_base + extent).
+static int batch_device_st_impl(ricrc_ctx *ctx, int dev, const void *d_base, uint64_t extent, const uint64_t *d_off,
+                                const uint32_t *d_len, uint32_t stride, uint64_t count, uint32_t l3_offset,
+                                uint32_t *d_out, uint8_t *d_status, void *stream, uint32_t flags) {
   StFlags f;
   if (!ctx || dev < 0 || dev >= (int)ctx->devs.size() || !decode_st_flags(flags, f)) return -EINVAL;
   if (count == 0) return 0;
@@ -903,14 +938,26 @@ int ricrc_batch_device_st(ricrc_ctx *ctx, int dev, const void *d_base, const uin
   if (!d_off && stride == 0) return -EINVAL;
   if (!d_len && (stride <= l3_offset || stride - l3_offset < kMinLen || stride - l3_offset > kMaxLen))
     return -EINVAL;  // one length for the whole batch: a call error, not a per-packet status
+  // a fixed-stride batch either lies in the extent or is a call error
+  if (extent && !d_off && !d_len && ((count - 1) > (extent / stride) || (count - 1) * stride + stride > extent))
+    return -EINVAL;
   Dev &d = ctx->devs[dev];
   DeviceGuard g(d.id);
   if (!g.ok()) return -ENODEV;
   hipStream_t st = (hipStream_t)stream;
   const uint8_t *base = (const uint8_t *)d_base;
-  uint32_t *eff = nullptr;  // RICRC_F_FRAMELEN: the packets' L3 lengths from their IP headers
-  if (f.framelen) {
-    HIP_TRY(hipMallocAsync((void **)&eff, count * sizeof(uint32_t), st));
+  // RICRC_F_FRAMELEN (the packets' L3 lengths from their IP headers) and / or
+  // an extent over per-packet descriptors: one pre-pass writes the lengths
+  // every later pass runs on (0 for a packet outside the extent), into the
+  // tail of the stream's ragged workspace -- the batch takes the ragged
+  // pipeline on them, whose workspace that is (no allocation per call).
+  const bool pre = f.framelen || (extent && (d_off || d_len));
+  Dev::Ws *ws = nullptr;
+  if (pre) {
+    const uint64_t at = (rs_workspace_bytes(std::min<uint64_t>(count, kRsChunk)) + 255) & ~255ull;
+    const int wrc = ragged_ws(d, st, at + count * sizeof(uint32_t), &ws);
+    if (wrc) return wrc;
+    uint32_t *eff = reinterpret_cast<uint32_t *>(static_cast<char *>(ws->p) + at);
     FrameLenArgs fa{};
     fa.base = base;
     fa.off = d_off;
@@ -920,22 +967,38 @@ int ricrc_batch_device_st(ricrc_ctx *ctx, int dev, const void *d_base, const uin
     fa.fixed_len = d_len ? 0u : stride - l3_offset;
     fa.l3_offset = l3_offset;
     fa.eff = eff;
-    int rc = hip_err(launch_framelen(fa, d.n_cu, st));
-    if (rc) {
-      (void)hipFreeAsync(eff, st);
-      return rc;
-    }
-    d_len = eff;  // every later pass runs on the packets' own lengths
+    fa.extent = extent;
+    fa.framelen = f.framelen ? 1u : 0u;
+    const int rc = hip_err(launch_framelen(fa, d.n_cu, st));
+    if (rc) return rc;
+    d_len = eff;  // every later pass runs on these lengths
   }
   int rc = launch_batch(d, base, d_off, d_len, stride, count, l3_offset, d_out, st, f.verify, f.fam);
   if (!rc)
     rc = launch_status_pass(d, base, d_off, d_len, stride, count, l3_offset, f.accept, f.strict && l3_offset >= 14,
                             d_out, d_status, nullptr, st);
-  if (eff) {
-    const int rc2 = hip_err(hipFreeAsync(eff, st));  // stream-ordered: after the passes that read it
+  // the workspace's last use is the status pass (it reads the lengths): a
+  // later reuse from another stream waits for it
+  if (ws) {
+    const int rc2 = hip_err(hipEventRecord(ws->done, st));
     if (!rc) rc = rc2;
   }
   return rc;
+}
+
+int ricrc_batch_device_st(ricrc_ctx *ctx, int dev, const void *d_base, const uint64_t *d_off,
+                          const uint32_t *d_len, uint32_t stride, uint64_t count, uint32_t l3_offset,
+                          uint32_t *d_out, uint8_t *d_status, void *stream, uint32_t flags) {
+  return batch_device_st_impl(ctx, dev, d_base, 0, d_off, d_len, stride, count, l3_offset, d_out, d_status, stream,
+                              flags);
+}
+
+int ricrc_batch_device_bounded(ricrc_ctx *ctx, int dev, const void *d_base, uint64_t base_bytes,
+                               const uint64_t *d_off, const uint32_t *d_len, uint32_t stride, uint64_t count,
+                               uint32_t l3_offset, uint32_t *d_out, uint8_t *d_status, void *stream, uint32_t flags) {
+  if (base_bytes == 0) return -EINVAL;
+  return batch_device_st_impl(ctx, dev, d_base, base_bytes, d_off, d_len, stride, count, l3_offset, d_out, d_status,
+                              stream, flags);
 }
 
 int ricrc_classify_device(ricrc_ctx *ctx, int dev, const void *d_base, const uint64_t *d_off,
@@ -1207,16 +1270,29 @@ void par_for(uint64_t n, int threads, uint64_t grain, F fn) {
 // With a status array (ricrc_batch_host_st) a descriptor length outside
 // [RICRC_MIN_LEN, RICRC_MAX_LEN] is not an error: the packet is staged as 0
 // bytes, the device reports RICRC_ST_BADLEN for it and out[i] = 0.
+// extent: the bytes from base the caller's buffer holds (0: unknown).  The
+// plain calls know it when base lies in a context range (ricrc_host_alloc /
+// ricrc_host_register); ricrc_batch_host_bounded takes it from the caller.
+// A packet outside it is -EINVAL (with a status array: RICRC_ST_BADLEN), and
+// none of its bytes is read.
 static int batch_host_impl(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *off, const uint32_t *len,
                            uint32_t stride, uint64_t count, uint32_t l3_offset, uint32_t *out, uint8_t *status,
-                           const StFlags &f) {
+                           const StFlags &f, uint64_t extent = 0) {
   if (!ctx || ctx->devs.empty()) return -EINVAL;
   if (count == 0) return 0;
   if (!base || !out) return -EINVAL;
   if (!off && stride == 0) return -EINVAL;
   if (!len && stride <= l3_offset) return -EINVAL;
+  if (extent == 0)
+    for (const HostRange &r : ctx->pinned)
+      if ((uintptr_t)base >= r.lo && (uintptr_t)base < r.hi) extent = r.hi - (uintptr_t)base;
   auto len_ok = [](uint64_t n) { return n >= kMinLen && n <= kMaxLen; };
   auto frame = [&](uint64_t i) -> uint64_t { return off ? off[i] : i * (uint64_t)stride; };
+  // packet i's descriptor bytes [frame + l3_offset, + n) inside the extent
+  auto in_ext = [&](uint64_t i, uint64_t n) {
+    const uint64_t fo = frame(i);
+    return extent == 0 || (fo <= extent && (uint64_t)l3_offset + n <= extent - fo);
+  };
   const int T = ctx->knobs.host_threads;
   // RICRC_F_FRAMELEN: every packet's L3 length from its IP header
   // (frame_l3_len), read once, in parallel (the headers of a NIC ring sit in
@@ -1228,7 +1304,7 @@ static int batch_host_impl(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *
     par_for(count, T, 4096, [&](uint64_t a, uint64_t b) {
       for (uint64_t i = a; i < b; ++i) {
         uint32_t n = len ? len[i] : stride - l3_offset;
-        if (frame_len_applies(n)) {
+        if (frame_len_applies(n) && in_ext(i, n)) {  // (its header only when the frame is in the buffer)
           const uint8_t *l3 = base + frame(i) + l3_offset;
           n = frame_l3_len(n, l3[0], (uint32_t)l3[2] << 8 | l3[3], (uint32_t)l3[4] << 8 | l3[5]);
         }
@@ -1237,15 +1313,16 @@ static int batch_host_impl(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *
     });
   }
   // Bytes staged for packet i (0 for a bad length under a status array).
+  auto desc_len = [&](uint64_t i) -> uint64_t { return len ? len[i] : (uint64_t)stride - l3_offset; };
   auto pkt_len = [&](uint64_t i) -> uint64_t {
-    const uint64_t n = f.framelen ? flen[i] : len ? len[i] : (uint64_t)stride - l3_offset;
-    return (status && !len_ok(n)) ? 0 : n;
+    const uint64_t n = f.framelen ? flen[i] : desc_len(i);
+    return (status && (!len_ok(n) || !in_ext(i, desc_len(i)))) ? 0 : n;
   };
   if (!len && !len_ok((uint64_t)stride - l3_offset)) return -EINVAL;  // the batch's one length
   uint64_t total = 0;
   for (uint64_t i = 0; i < count; ++i) {
     const uint64_t n = pkt_len(i);
-    if (!status && !len_ok(n)) return -EINVAL;
+    if (!status && (!len_ok(n) || !in_ext(i, desc_len(i)))) return -EINVAL;
     total += n;
   }
   const int ndev = (int)ctx->devs.size();
@@ -1434,6 +1511,15 @@ int ricrc_batch_host_st(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *off
   StFlags f;
   if (!decode_st_flags(flags, f) || (count && !status)) return -EINVAL;
   return batch_host_impl(ctx, base, off, len, stride, count, l3_offset, out, status, f);
+}
+
+int ricrc_batch_host_bounded(ricrc_ctx *ctx, const uint8_t *base, uint64_t base_bytes, const uint64_t *off,
+                             const uint32_t *len, uint32_t stride, uint64_t count, uint32_t l3_offset, uint32_t *out,
+                             uint8_t *status, uint32_t flags) {
+  StFlags f;
+  if (!decode_st_flags(flags, f) || base_bytes == 0) return -EINVAL;
+  if (!status && (flags & (RICRC_F_STRICT | RICRC_F_VERIFY))) return -EINVAL;  // those report per packet
+  return batch_host_impl(ctx, base, off, len, stride, count, l3_offset, out, status, f, base_bytes);
 }
 
 }  // extern "C"

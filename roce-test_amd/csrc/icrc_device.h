@@ -24,7 +24,9 @@ static constexpr int kLdsWords = 32768;  // 128 KiB
 // workgroup b is on XCD (b + k) % 8.  w and k come from the host or from an
 // earlier kernel of the same stream, so every wave uses the same values: the
 // shares are contiguous, in wave order, and cover [0, total) for any k; a
-// wrong k costs speed, never a packet.
+// wrong k costs speed, never a packet.  The products total * before stay
+// below 2^64: total < 2^39.01 (the ragged pool's bound) and the host caps
+// the weights (RICRC_XCD_WEIGHTS <= 8000 each, icrc_api.cpp).
 __device__ __forceinline__ void xcd_share(uint64_t total, const uint32_t (&w)[8], uint32_t k, uint32_t wid,
                                           uint64_t &lo, uint64_t &hi) {
   const uint64_t b = blockIdx.x, nb = gridDim.x;

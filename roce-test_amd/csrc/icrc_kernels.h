@@ -145,6 +145,8 @@ hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, hipStream_t st, hipE
 // Whether a batch of `count` packets takes the fused pipeline (bucket, fold,
 // gather folding the one-line packets: no icrc_rsmall_kernel launch).
 bool rs_fused(uint64_t count, int pass_cap);
+// The bucket / gather passes' blocks and packets per thread for such a batch (ricrc_launch_info).
+void rs_pass_info(uint64_t count, int pass_cap, int *grid, int *unroll, bool *fused);
 
 struct SynthArgs {
   uint8_t *buf;
@@ -222,6 +224,9 @@ hipError_t launch_status(const StatusArgs &a, int n_cu, hipStream_t st);
 // RICRC_F_FRAMELEN (icrc_status.hip): eff[i] = the L3 length of packet i
 // from its IP header when its descriptor length is the frame's extent past
 // L3 (frame_l3_len, icrc_math.h); the batch then runs on eff as lengths.
+// With an extent (ricrc_batch_device_bounded), a packet whose bytes do not
+// all lie in [base, base + extent) gets eff[i] = 0 -- a bad length, so no
+// later pass reads it -- and its header is not read here either.
 struct FrameLenArgs {
   const uint8_t *base;
   const uint64_t *off;  // may be null (then i * stride)
@@ -229,6 +234,8 @@ struct FrameLenArgs {
   uint64_t stride, count;
   uint32_t fixed_len, l3_offset;
   uint32_t *eff;
+  uint64_t extent;      // 0: no bound
+  uint32_t framelen;    // 1: the IP-header rule (RICRC_F_FRAMELEN); 0: the descriptor length
 };
 hipError_t launch_framelen(const FrameLenArgs &a, int n_cu, hipStream_t st);
 hipError_t launch_synth_ragged(const SynthArgs &a, hipStream_t st);

@@ -1272,6 +1272,12 @@ static PassShape pass_shape(uint64_t count, int pass_cap) {
   return PassShape{grid, U, U == 4 && (uint64_t)grid * 4u * kPassBlock >= count};
 }
 bool rs_fused(uint64_t count, int pass_cap) { return count > 0 && pass_shape(count, pass_cap).fused; }
+void rs_pass_info(uint64_t count, int pass_cap, int *grid, int *unroll, bool *fused) {
+  const PassShape ps = pass_shape(count, pass_cap);
+  *grid = ps.grid;
+  *unroll = ps.U;
+  *fused = ps.fused;
+}
 static void launch_bucket(const RsckArgs &a, const PassShape &ps, hipStream_t st) {
   switch (ps.U) {
     case 4: launch_bucket_u<4>(a, ps.grid, st); break;

@@ -88,8 +88,9 @@ __global__ __launch_bounds__(kStBlock) void icrc_status_kernel(StatusArgs a) {
   }
 }
 
-// RICRC_F_FRAMELEN: one thread per packet, four packets per thread with the
-// descriptor loads, then the 6 header bytes, issued before any is used.
+// RICRC_F_FRAMELEN and / or an extent: one thread per packet, four packets
+// per thread with the descriptor loads, then the 6 header bytes, issued
+// before any is used.
 __global__ __launch_bounds__(kStBlock) void icrc_framelen_kernel(FrameLenArgs a) {
   const uint64_t T = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < a.count; i0 += kStUnroll * T) {
@@ -99,13 +100,16 @@ __global__ __launch_bounds__(kStBlock) void icrc_framelen_kernel(FrameLenArgs a)
     for (int k = 0; k < kStUnroll; ++k) {
       uint64_t i = i0 + k * T;
       i = i < a.count ? i : a.count - 1;
-      addr[k] = (uint64_t)(uintptr_t)a.base + (a.off ? a.off[i] : i * a.stride) + a.l3_offset;
+      const uint64_t fo = a.off ? a.off[i] : i * a.stride;
+      addr[k] = (uint64_t)(uintptr_t)a.base + fo + a.l3_offset;
       n[k] = a.len ? a.len[i] : a.fixed_len;
+      // outside the caller's allocation: length 0 (nothing reads it)
+      if (a.extent && (fo > a.extent || (uint64_t)a.l3_offset + n[k] > a.extent - fo)) n[k] = 0u;
     }
 #pragma unroll
     for (int k = 0; k < kStUnroll; ++k) {
       b0[k] = h2[k] = h4[k] = 0u;
-      if (frame_len_applies(n[k])) {  // the frame holds at least the IPv4 / BTH headers: bytes 0..5 are in it
+      if (a.framelen && frame_len_applies(n[k])) {  // the frame holds at least the IPv4 / BTH headers: bytes 0..5 are in it
         const gbyte l3 = reinterpret_cast<gbyte>((uintptr_t)addr[k]);
         b0[k] = l3[0];
         h2[k] = be16(l3 + 2);
@@ -115,7 +119,7 @@ __global__ __launch_bounds__(kStBlock) void icrc_framelen_kernel(FrameLenArgs a)
 #pragma unroll
     for (int k = 0; k < kStUnroll; ++k) {
       const uint64_t i = i0 + k * T;
-      if (i < a.count) a.eff[i] = frame_l3_len(n[k], b0[k], h2[k], h4[k]);
+      if (i < a.count) a.eff[i] = a.framelen ? frame_l3_len(n[k], b0[k], h2[k], h4[k]) : n[k];
     }
   }
 }

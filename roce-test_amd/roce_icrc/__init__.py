@@ -50,7 +50,7 @@ EXPORTED = CPU_EXPORTED + (
     "ricrc_host_register", "ricrc_host_unregister", "ricrc_synth_device", "ricrc_synth_ragged_device",
     "ricrc_prime", "ricrc_stream", "ricrc_comm_init", "ricrc_batch_device_all", "ricrc_allgather", "ricrc_sync",
     "ricrc_batch_device_st", "ricrc_batch_host_st", "ricrc_classify_device", "ricrc_kernel_path",
-    "ricrc_pass_times",
+    "ricrc_pass_times", "ricrc_launch_info", "ricrc_batch_device_bounded", "ricrc_batch_host_bounded",
 )
 
 # Per-packet status of the *_st batch calls (include/roce_icrc.h).
@@ -105,7 +105,16 @@ _SIG = {
     "ricrc_classify_device": ([_vp, _i32, _vp, _vp, _vp, _u32, _u64, _u32, _vp, _vp], _i32),
     "ricrc_kernel_path": ([_vp, _vp, _vp, _vp, _u32, _u64, _u32, _u32], ctypes.c_char_p),
     "ricrc_pass_times": ([_vp, _i32, ctypes.POINTER(ctypes.c_float), _i32], _i32),
+    "ricrc_launch_info": ([_vp, _i32, _vp, _vp, _vp, _u32, _u64, _u32, _vp], _i32),
+    "ricrc_batch_device_bounded": ([_vp, _i32, _vp, _u64, _vp, _vp, _u32, _u64, _u32, _vp, _vp, _vp, _u32], _i32),
+    "ricrc_batch_host_bounded": ([_vp, _vp, _u64, _vp, _vp, _u32, _u64, _u32, _vp, _vp, _u32], _i32),
 }
+
+
+class LaunchInfo(ctypes.Structure):
+    """``ricrc_launch_info_t`` (include/roce_icrc.h)."""
+    _fields_ = [("grid", _u32), ("xcd_weights", _u32 * 8), ("start_xcd", _u32), ("pass_grid", _u32),
+                ("pass_unroll", _u32), ("fused", _u32)]
 
 
 class ICRCError(RuntimeError):
@@ -419,6 +428,27 @@ class Context:
             raise ICRCError(rc, "ricrc_batch_host_st")
         return out, st
 
+    def batch_host_bounded(self, buf, base_bytes: int, offsets=None, lengths=None, stride: int = 0,
+                           l3_offset: int = 0, count: int | None = None, family: str = "v4", status: bool = False,
+                           strict: bool = False, verify: bool = False, framelen: bool = False):
+        """``ricrc_batch_host_bounded``: descriptors checked against the first
+        ``base_bytes`` of ``buf`` -- ``out`` (``status=False``: a packet outside
+        raises ICRCError -EINVAL) or ``(out, status)`` (outside: ST_BADLEN)."""
+        buf = np.ascontiguousarray(buf).reshape(-1).view(np.uint8)
+        off = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint64)
+        ln = None if lengths is None else np.ascontiguousarray(lengths, dtype=np.uint32)
+        if count is None:
+            count = len(off) if off is not None else (len(ln) if ln is not None else buf.size // stride)
+        out = np.empty(count, dtype=np.uint32)
+        st = np.empty(count, dtype=np.uint8) if status else None
+        flags = _fam(family) | (F_STRICT if strict else 0) | (F_VERIFY if verify else 0) | (F_FRAMELEN if framelen else 0)
+        rc = self._lib.ricrc_batch_host_bounded(self._h, buf.ctypes.data, base_bytes, _ptr(off), _ptr(ln), stride,
+                                                count, l3_offset, out.ctypes.data,
+                                                st.ctypes.data if st is not None else None, flags)
+        if rc:
+            raise ICRCError(rc, "ricrc_batch_host_bounded")
+        return (out, st) if status else out
+
     # -- device resident --------------------------------------------------
     def batch_device(self, base, count: int, out, stride: int = 0, offsets=None, lengths=None,
                      l3_offset: int = 0, dev: int = 0, stream=None, verify: bool = False,
@@ -441,6 +471,18 @@ class Context:
                                              l3_offset, _ptr(out), _ptr(status), _stream_ptr(stream), flags)
         if rc:
             raise ICRCError(rc, "ricrc_batch_device_st")
+
+    def batch_device_bounded(self, base, base_bytes: int, count: int, out, status, stride: int = 0, offsets=None,
+                             lengths=None, l3_offset: int = 0, dev: int = 0, stream=None, family: str = "v4",
+                             strict: bool = False, verify: bool = False, framelen: bool = False) -> None:
+        """``ricrc_batch_device_bounded``: as :meth:`batch_device_st`, packets
+        outside ``[base, base + base_bytes)`` never read (ST_BADLEN, out 0)."""
+        flags = _fam(family) | (F_STRICT if strict else 0) | (F_VERIFY if verify else 0) | (F_FRAMELEN if framelen else 0)
+        rc = self._lib.ricrc_batch_device_bounded(self._h, dev, _ptr(base), base_bytes, _ptr(offsets), _ptr(lengths),
+                                                  stride, count, l3_offset, _ptr(out), _ptr(status),
+                                                  _stream_ptr(stream), flags)
+        if rc:
+            raise ICRCError(rc, "ricrc_batch_device_bounded")
 
     def classify_device(self, base, count: int, cls, stride: int = 0, offsets=None, lengths=None,
                         l3_offset: int = 0, dev: int = 0, stream=None) -> None:
@@ -491,6 +533,21 @@ class Context:
         if rc < 0:
             raise ICRCError(rc, "ricrc_pass_times")
         return rc, [float(v) for v in ms]
+
+    def launch_info(self, base, count: int, stride: int = 0, offsets=None, lengths=None, l3_offset: int = 0,
+                    dev: int = 0) -> dict:
+        """``ricrc_launch_info``: how the dispatch would launch this batch on
+        ``dev`` -- the main kernel's grid, its per-XCD work-split weights, the
+        recorded start XCD, and the ragged passes' shape."""
+        info = LaunchInfo()
+        rc = self._lib.ricrc_launch_info(self._h, dev, _ptr(base), _ptr(offsets), _ptr(lengths), stride, count,
+                                         l3_offset, ctypes.byref(info))
+        if rc:
+            raise ICRCError(rc, "ricrc_launch_info")
+        d = {"grid": info.grid, "xcd_weights": list(info.xcd_weights), "start_xcd": info.start_xcd}
+        if info.pass_grid:
+            d.update(pass_grid=info.pass_grid, pass_unroll=info.pass_unroll, one_line_in_gather=bool(info.fused))
+        return d
 
     def prime(self, usec: int = 20000, dev: int = 0) -> None:
         """``ricrc_prime``: bring the device out of its idle power state."""

@@ -220,3 +220,49 @@ def test_gpus_2_relaunch_end_to_end_plan_only():
     assert d["scaling"] == "weak" and abs(d["shard_bytes"][0] - d["shard_bytes"][1]) <= 2 * 4096
     d = run("--global-count", "4194304")
     assert d["scaling"] == "strong" and d["shard_packets"] == [2097152, 2097152]
+
+
+def test_side_configs_are_the_baseline_configs():
+    """The driver's one command also measures BASELINE's other configs
+    (VERDICT r4 item 2): N = 1 adds c1 / c2 / c4, N > 1 c3_strong / c4_strong,
+    each with the main run's K, W and seed."""
+    a = bench.parse(["--steps", "7", "--warmup", "2", "--seed", "11"])
+    got = {n: bench.side_args(a, x) for n, x in bench.SIDE_N1}
+    assert set(got) == {"c1", "c2", "c4"}
+    assert (got["c1"].size, got["c1"].count, got["c1"].mix) == (64, 1 << 20, False)
+    assert (got["c2"].size, got["c2"].count, got["c2"].mix) == (1024, 1 << 20, False)
+    assert got["c4"].mix and got["c4"].count == 4 << 20 and got["c4"].global_count is None
+    for sa in got.values():
+        assert (sa.steps, sa.warmup, sa.seed, sa.prime_ms, sa.no_side) == (7, 2, 11, 0.0, True)
+    got = {n: bench.side_args(bench.parse(["--gpus", "8"]), x) for n, x in bench.SIDE_NX}
+    assert set(got) == {"c3_strong", "c4_strong"}
+    assert (got["c3_strong"].global_count, got["c3_strong"].size, got["c3_strong"].mix) == (4 << 20, 4096, False)
+    assert got["c4_strong"].mix and got["c4_strong"].global_count == 4 << 20
+    assert bench.side_args(bench.parse(["--side-count", "99"]), ["--mix"]).count == 99
+
+
+def test_side_configs_run_at_n1_on_cpu_stand_in():
+    """bench.run_side at N = 1 with the CPU stand-in backend (the oracle as
+    the compute, test only): every side key carries its value, step time,
+    kernel time, roofline fraction and the sampled oracle check."""
+    from test_bench_dist import CpuOracleBackend
+
+    a = bench.parse(["--steps", "2", "--warmup", "1", "--prime-ms", "0", "--warm-ms", "0", "--side-count", "1500"])
+    res = bench.run_side(a, 1, 0, CpuOracleBackend(), False)
+    assert set(res) == {"c1", "c2", "c4"}
+    for name, d in res.items():
+        assert d["value"] > 0 and d["ms_per_step"] > 0 and d["oracle_sampled_all_ranks"], name
+        assert d["roofline"]["frac"] > 0 and d["roofline"]["kernel_ms"] > 0 and "traffic" in d["roofline"], name
+        assert d["config"]["packets_total"] == 1500, name
+    assert "mixed-MTU" in res["c4"]["metric"] and "64B" in res["c1"]["metric"] and "1024B" in res["c2"]["metric"]
+
+
+def test_framed_ring_flags():
+    """--l3-offset / --stride: an Ethernet-framed fixed-slot ring (SURVEY
+    8(f)-4); the packet is the slot minus the L3 offset."""
+    a = bench.parse(["--l3-offset", "14", "--stride", "4096"])
+    assert (a.l3_offset, a.stride, a.pkt) == (14, 4096, 4082)
+    assert "framed" in bench.metric_for(a, a.count, a.count)
+    assert bench.traffic_record(False, a.size, a.count, 14, 4096)[0] == "pmc_traffic_ring14_4096.json"
+    with pytest.raises(SystemExit):
+        bench.parse(["--mix", "--l3-offset", "14"])

@@ -111,11 +111,31 @@ def _rank(rank, world, port, argv, q):
             dist.destroy_process_group()
 
 
-def run2(argv, world=2):
+def _rank_side(rank, world, port, argv, q):
+    """_rank, then bench.run_side: the N > 1 side configs (c3_strong, c4_strong)."""
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import bench
+
+    try:
+        args = bench.parse(argv)
+        be = CpuOracleBackend()
+        res, full_h, b = bench.run(args, world, rank, be, True)
+        res.update(bench.run_side(args, world, rank, be, True))
+        q.put((rank, json.dumps(res), full_h.copy(), b["sizes"]))
+    except BaseException as e:
+        q.put((rank, f"ERROR {type(e).__name__}: {e}", None, None))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def run2(argv, world=2, target=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank, args=(r, world, port, argv, q)) for r in range(world)]
+    procs = [ctx.Process(target=target or _rank, args=(r, world, port, argv, q)) for r in range(world)]
     for p in procs:
         p.start()
     got = {}
@@ -181,3 +201,19 @@ def test_bench_run_world2_no_gather():
     assert got[0][0]["compute_only_ms_per_step"] > 0 and "gather_ms" not in got[0][0]
     np.testing.assert_array_equal(got[0][1], want[:1500])
     np.testing.assert_array_equal(got[1][1], want[1500:])
+
+
+def test_bench_side_configs_world2_gloo():
+    """The driver's N > 1 command also runs BASELINE configs 3 and 4 as
+    strong scaling: c3_strong (4 M x 4 KiB in all) and
+    c4_strong (the 4 M mix in all, byte-balanced), each with its own
+    compute-only and gather times -- here scaled down by --side-count."""
+    got = run2(BASE + ["--size", "1024", "--count", "1000", "--side-count", "3001"], target=_rank_side)
+    res = got[0][0]
+    for k in ("c3_strong", "c4_strong"):
+        d = res[k]
+        assert d["scaling"] == "strong" and d["config"]["packets_total"] == 3001, k
+        assert d["compute_only_ms_per_step"] > 0 and d["gather_ms"] > 0 and d["oracle_sampled_all_ranks"], k
+        assert d["roofline"]["frac"] > 0 and d["value"] > 0, k
+        assert got[1][0][k]["value"] == d["value"], k  # one number on every rank
+    assert "mixed-MTU" in res["c4_strong"]["metric"] and "fixed total" in res["c3_strong"]["metric"]

@@ -1,0 +1,114 @@
+"""GPU: the buffer-extent contract of the batch calls.
+
+The caller owns every buffer (the reference's huge_malloc MRs,
+common/huge_malloc.h:12-22) and the plain device calls read packets in place
+with no extent: include/roce_icrc.h states that a descriptor past the
+caller's allocation is the caller's fault.  The extent-checked calls take the
+buffer's size: ricrc_batch_host_bounded returns -EINVAL (status NULL) or
+RICRC_ST_BADLEN per packet, ricrc_batch_device_bounded reports
+RICRC_ST_BADLEN with out = 0 and never reads the packet; ricrc_batch_host
+itself checks descriptors against a ricrc_host_alloc'd buffer's size.  In
+these tests every "outside" descriptor still points into memory the process
+owns (the device buffer is allocated larger than the extent declared), so a
+read past the extent would be a wrong answer, not a fault."""
+import errno
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import icrc_oracle as O  # noqa: E402
+import oracle_c  # noqa: E402
+import roce_icrc  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _ragged(count, seed, slack=0):
+    rng = np.random.default_rng(seed)
+    lens = rng.choice(np.array([64, 256, 1024, 1500, 4096], np.uint32), size=count)
+    gaps = rng.integers(0, 8, size=count).astype(np.uint64) * 4
+    offs = np.zeros(count, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + gaps[:-1])
+    buf = rng.integers(0, 256, size=int(offs[-1] + lens[-1]) + slack, dtype=np.uint8)
+    return buf, offs, lens
+
+
+def test_batch_host_bounded_rejects_descriptor_past_end(ctx):
+    buf, offs, lens = _ragged(5000, 1)
+    extent = int(offs[-1] + lens[-1])
+    want = oracle_c.icrc_batch(buf, offsets=offs, lengths=lens, threads=16)
+    np.testing.assert_array_equal(ctx.batch_host_bounded(buf, extent, offsets=offs, lengths=lens), want)
+    # one byte short: the last packet ends past the buffer
+    with pytest.raises(roce_icrc.ICRCError) as e:
+        ctx.batch_host_bounded(buf, extent - 1, offsets=offs, lengths=lens)
+    assert e.value.rc == -errno.EINVAL
+    # with a status array: that packet is RICRC_ST_BADLEN, the others exact
+    out, st = ctx.batch_host_bounded(buf, extent - 1, offsets=offs, lengths=lens, status=True)
+    assert st[-1] == roce_icrc.ST_BADLEN and out[-1] == 0
+    assert (st[:-1] == roce_icrc.ST_OK).all()
+    np.testing.assert_array_equal(out[:-1], want[:-1])
+    # an offset far past the end (an overflowing sum included)
+    bad = offs.copy()
+    bad[17] = np.uint64(2**64 - 8)
+    bad[18] = np.uint64(extent + 4096)
+    out, st = ctx.batch_host_bounded(buf, extent, offsets=bad, lengths=lens, status=True)
+    assert st[17] == st[18] == roce_icrc.ST_BADLEN and out[17] == out[18] == 0
+    ok = np.ones(len(lens), bool)
+    ok[[17, 18]] = False
+    np.testing.assert_array_equal(out[ok], want[ok])
+
+
+def test_batch_host_checks_descriptors_in_a_host_alloc_buffer(ctx):
+    """ricrc_batch_host knows the size of a buffer the context allocated
+    (ricrc_host_alloc): a descriptor past its end is -EINVAL there."""
+    buf, offs, lens = _ragged(3000, 2)
+    n = int(offs[-1] + lens[-1])
+    pinned = ctx.host_alloc(n)
+    try:
+        pinned[:] = buf[:n]
+        want = oracle_c.icrc_batch(buf, offsets=offs, lengths=lens, threads=16)
+        np.testing.assert_array_equal(ctx.batch_host(pinned, offsets=offs, lengths=lens), want)
+        past = lens.copy()
+        past[-1] += 4  # the last packet now ends 4 bytes past the allocation
+        with pytest.raises(roce_icrc.ICRCError) as e:
+            ctx.batch_host(pinned, offsets=offs, lengths=past)
+        assert e.value.rc == -errno.EINVAL
+    finally:
+        ctx.host_free(pinned)
+
+
+@pytest.mark.parametrize("framelen", [False, True])
+def test_batch_device_bounded_flags_out_of_range_packets(ctx, framelen):
+    count = 20000
+    buf, offs, lens = _ragged(count, 3, slack=1 << 16)  # the device buffer extends past the declared extent
+    rng = np.random.default_rng(4)
+    extent = int(offs[count // 2])  # the second half lies past it ...
+    inside = offs + lens <= extent
+    bad = rng.choice(count // 2, size=50, replace=False)  # ... and so do 50 descriptors of the first half
+    offs = offs.copy()
+    offs[bad] = np.uint64(extent) - (lens[bad].astype(np.uint64) // 2)  # straddling the end
+    inside[bad] = False
+    if framelen:  # RICRC_F_FRAMELEN: random bytes sometimes read as an IPv4 / IPv6 header with a shorter length
+        eff = np.array([O.frame_l3_len(buf[int(o):int(o) + int(n)].tobytes()) if ok else n
+                        for o, n, ok in zip(offs, lens, inside)], np.uint32)
+        want = oracle_c.icrc_batch(buf, offsets=offs, lengths=np.where(inside, eff, lens), threads=16)
+    else:
+        want = oracle_c.icrc_batch(buf, offsets=offs, lengths=lens, threads=16)
+    d = torch.from_numpy(buf).cuda()
+    d_off = torch.from_numpy(offs.view(np.int64)).cuda()
+    d_len = torch.from_numpy(lens.view(np.int32)).cuda()
+    out = torch.full((count,), -1, dtype=torch.int32, device="cuda")
+    st = torch.full((count,), 255, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream()
+    ctx.batch_device_bounded(d, extent, count, out, st, offsets=d_off, lengths=d_len, stream=s, framelen=framelen)
+    torch.cuda.synchronize()
+    got, status = out.cpu().numpy().view(np.uint32), st.cpu().numpy()
+    assert (status[~inside] == roce_icrc.ST_BADLEN).all() and (got[~inside] == 0).all()
+    assert (status[inside] == roce_icrc.ST_OK).all()
+    np.testing.assert_array_equal(got[inside], want[inside])
+    # a fixed-stride batch that does not fit is a call error
+    with pytest.raises(roce_icrc.ICRCError) as e:
+        ctx.batch_device_bounded(d, 4096 * 3 - 1, 3, out, st, stride=4096, stream=s)
+    assert e.value.rc == -errno.EINVAL

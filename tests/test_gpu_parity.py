@@ -643,15 +643,15 @@ def test_ragged_strided_chain_word_aligned(ctx):
 
 
 @pytest.mark.parametrize("grid", [None, 5])
-def test_ragged_fold_specialized_line_counts(ctx, ctx_env, grid):
-    """Round 4: word-aligned runs of one line count L in {2, 3, 8, 9, 32, 33}
-    take the fold specialized on L (static schedule: P = D / gcd(L, D)
-    groups unrolled per period, the last n % P groups after the loop), other
-    classes the generic fold, segment by segment (64 groups of look-ahead).
-    Starts at every multiple of 4 (headers running into line 1: a second head
-    line), sizes drawn so every specialized class occurs with both parities of
-    a period and next to generic classes; a capped fold grid makes every wave
-    cross many segments.  Verify mode on the same batch."""
+def test_ragged_fold_line_count_runs(ctx, ctx_env, grid):
+    """Word-aligned runs of C4's line counts L in {2, 3, 8, 9, 32, 33} next to
+    other classes, through the ragged fold (icrc_rsck_kernel: the one fold;
+    round 4's timing-only fold specialized on L is gone, round 5).  Starts at
+    every multiple of 4 (headers running into line 1: a second head line);
+    the default grid splits each workgroup's work exactly, so groups of every
+    class are cut between waves (head and tail parts, every line offset), and
+    a capped grid makes each wave take many groups of mixed classes.  Verify
+    mode on the same batch."""
     if grid is not None:
         ctx = ctx_env(RICRC_RSCK_GRID=grid)
     rng = np.random.default_rng(404)

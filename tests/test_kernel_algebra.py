@@ -207,6 +207,7 @@ def test_ragged_line_grid_decomposition():
         assert reg ^ 0xFFFFFFFF == o.icrc(pkt), (n, a)
 
 
+
 def _le_words(b: bytes):
     return [int.from_bytes(b[i:i + 4], "little") for i in range(0, len(b), 4)]
 
