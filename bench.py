@@ -70,9 +70,11 @@ def traffic_record(mix, size, count=None, l3_offset=0, stride=None):
     slot and L3 offset."""
     std = (4 << 20) if mix else (1 << 20)
     tag = "" if count in (None, std) else f"_{count}"
-    if l3_offset:
-        return (f"pmc_traffic_ring{l3_offset}_{stride or size}{tag}.json", RAGGED_SOURCES,
-                RAGGED_KERNELS + ("icrc_rsck_uni_kernel",))
+    if l3_offset:  # 1, 2 and 4 KiB slots with the L3 start in line 0: the SCK's framed variant
+        name = f"pmc_traffic_ring{l3_offset}_{stride or size}{tag}.json"
+        if (stride or size) in (1024, 2048, 4096) and l3_offset <= 92:
+            return name, SCK_SOURCES, ("icrc_sck_kernel",)
+        return name, RAGGED_SOURCES, RAGGED_KERNELS
     if mix:
         return f"pmc_traffic_mix{tag}.json", RAGGED_SOURCES, RAGGED_KERNELS
     if size == 4096:

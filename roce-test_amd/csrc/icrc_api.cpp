@@ -46,6 +46,7 @@ constexpr uint64_t kRsChunk = kRsMaxCount;  // the ragged pipeline's group count
 // schedule studies; the launch path never calls getenv).
 struct Knobs {
   bool no_sck = false;     // RICRC_NO_SCK: fixed 1/2/4 KiB batches take the transposed kernel
+  bool no_framed = false;  // RICRC_NO_FRAMED: framed 1/2/4 KiB rings take the ragged pipeline
   bool no_tsk = false;     // RICRC_NO_TSK: ... and 128-512 B batches the direct streaming kernel
   bool no_quad = false;    // RICRC_NO_QUAD: 64 B batches take the direct streaming kernel
   int sck_grid = 0;        // RICRC_SCK_GRID: cap the strided-chain grid (tests: many groups per wave)
@@ -348,9 +349,19 @@ int ragged_ws(Dev &d, hipStream_t st, uint64_t bytes, Dev::Ws **out) {
 // The strided-chain kernel's grid for a batch, or 0 if the batch does not
 // take it (it needs back-to-back 1, 2 or 4 KiB packets, 16-byte aligned); it
 // applies any address family natively.
+// A framed NIC ring the strided-chain kernel folds slot by slot (FR,
+// icrc_sck.hip): 1, 2 or 4 KiB slots, 16-byte aligned, the L3 packet at
+// 0 < l3_offset <= kSckMaxL3 running to the slot's end.
+bool sck_framed(const Knobs &kn, const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
+                uint32_t l3_offset) {
+  return !off && !len && l3_offset > 0 && l3_offset <= kSckMaxL3 && (uintptr_t)base % 16 == 0 && !kn.no_sck &&
+         !kn.no_framed && (stride == 1024 || stride == 2048 || stride == 4096);
+}
+
 int sck_grid(const Dev &d, const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
              uint64_t count, uint32_t l3_offset) {
-  if (off || len || l3_offset != 0 || ((uintptr_t)base % 16) != 0 || d.knobs.no_sck || count == 0) return 0;
+  if (l3_offset != 0 && !sck_framed(d.knobs, base, off, len, stride, l3_offset)) return 0;
+  if (off || len || ((uintptr_t)base % 16) != 0 || d.knobs.no_sck || count == 0) return 0;
   if (stride != 1024 && stride != 2048 && stride != 4096) return 0;
   const uint64_t groups = (count + 7) / 8;
   // One workgroup per CU.  Batches of up to 48 groups per wave (6 GiB of
@@ -429,7 +440,7 @@ int launch_rsck_range(Dev &d, const uint8_t *base, const uint64_t *off, const ui
 // The kernel path of a batch: ONE decision, used by launch_batch_v4 and by
 // ricrc_kernel_path (which bench.py and the tests query, so the labels of a
 // run cannot drift from what ran).
-enum class Path { kSck, kQuad, kTsk, kStream, kRagged };
+enum class Path { kSck, kSckFramed, kQuad, kTsk, kStream, kRagged };
 
 // Chunks of a fixed-length batch per lane of the direct streaming kernel
 // (1, 2 or 4), or 0 if its packets are too long for it.
@@ -445,6 +456,8 @@ Path choose_path(const Knobs &kn, const uint8_t *base, const uint64_t *off, cons
   const uint8_t *first = base + l3_offset;
   const uint32_t fixed_len = stride > l3_offset ? (uint32_t)std::min<uint64_t>(stride - l3_offset, 0xFFFFFFFFu) : 0u;
   const bool aligned = ((uintptr_t)first % 16 == 0) && (stride % 16 == 0);
+  // An Ethernet-framed ring of 1, 2 or 4 KiB slots: the strided-chain kernel over the slots.
+  if (sck_framed(kn, base, off, len, stride, l3_offset) && fixed_len >= kMinLen) return Path::kSckFramed;
   if (off || len || !aligned || fixed_len < kMinLen || fixed_len > kMaxLen || fixed_len % 4 != 0) return Path::kRagged;
   // Back-to-back 1, 2 or 4 KiB packets: the strided-chain kernel (no LDS transpose).
   if (l3_offset == 0 && (uintptr_t)base % 16 == 0 && !kn.no_sck && (stride == 1024 || stride == 2048 || stride == 4096))
@@ -463,7 +476,8 @@ Path choose_path(const Knobs &kn, const uint8_t *base, const uint64_t *off, cons
 
 const char *path_kernels(Path p, bool fused) {
   switch (p) {
-    case Path::kSck: return "icrc_sck_kernel";
+    case Path::kSck:
+    case Path::kSckFramed: return "icrc_sck_kernel";
     case Path::kQuad: return "icrc_quad_kernel";
     case Path::kTsk: return "icrc_tsk_kernel";
     case Path::kStream: return "icrc_stream_kernel";
@@ -480,19 +494,20 @@ int launch_batch_v4(Dev &d, const uint8_t *base, const uint64_t *off, const uint
   const Path path = choose_path(d.knobs, base, off, len, stride, l3_offset);
   if (path != Path::kRagged) {
     // Back-to-back 1, 2 or 4 KiB packets: the strided-chain kernel (no LDS transpose).
-    if (path == Path::kSck) {
+    if (path == Path::kSck || path == Path::kSckFramed) {
       const int sgrid = sck_grid(d, base, off, len, stride, count, l3_offset);
       SckArgs k{};
       k.family = family;
       k.base = base;
       k.count = count;
       k.out = out;
-      k.n = fixed_len;
+      k.n = (uint32_t)stride;
+      k.l3_offset = l3_offset;
       k.verify = verify ? 1u : 0u;
       const uint32_t xi = gf_xinv8n(4);
       for (int j = 0; j < 32; ++j) k.XB[j] = gf_mul(xi, 1u << j);
       for (int s = 0; s < 8; ++s) k.QS[s] = gf_xinv8n(16ull * s + 4);
-      const XcdWeights xw = xcd_weights(d.knobs, fixed_len != 4096 ? 0 : sgrid < d.n_cu ? 25 : 50);
+      const XcdWeights xw = xcd_weights(d.knobs, stride != 4096 ? 0 : sgrid < d.n_cu ? 25 : 50);
       for (int x = 0; x < 8; ++x) k.xw[x] = xw.w[x];
       k.xcd_k = xcd_start(d.h_xcd);
       k.xcd_rec = d.d_xcd_rec;
@@ -721,6 +736,7 @@ Knobs read_knobs() {
     return e ? atol(e) : dflt;
   };
   k.no_sck = getenv("RICRC_NO_SCK") != nullptr;
+  k.no_framed = getenv("RICRC_NO_FRAMED") != nullptr;
   k.no_tsk = getenv("RICRC_NO_TSK") != nullptr;
   k.no_quad = getenv("RICRC_NO_QUAD") != nullptr;
   k.sck_grid = (int)std::max(0L, num("RICRC_SCK_GRID", 0));
@@ -848,6 +864,7 @@ const char *ricrc_kernel_path(const ricrc_ctx *ctx, const void *d_base, const ui
   const bool fused = rs_fused(std::min<uint64_t>(count, kRsChunk), kn.pass_grid);
   if (flags == RICRC_F_IPV4 || p == Path::kSck) return path_kernels(p, fused);  // the SCK applies every family natively
   switch (p) {  // IPv6 / AUTO: the IPv4-mask kernels, then the linear header fix-up
+    case Path::kSckFramed: return "icrc_sck_kernel+family_fix_kernel";
     case Path::kQuad: return "icrc_quad_kernel+family_fix_kernel";
     case Path::kTsk: return "icrc_tsk_kernel+family_fix_kernel";
     case Path::kStream: return "icrc_stream_kernel+family_fix_kernel";
@@ -868,10 +885,9 @@ int ricrc_launch_info(const ricrc_ctx *ctx, int dev, const void *d_base, const u
   const uint8_t *base = (const uint8_t *)d_base;
   const Path p = choose_path(ctx->knobs, base, d_off, d_len, stride, l3_offset);
   XcdWeights xw{};
-  if (p == Path::kSck) {
-    const uint32_t fixed_len = stride - l3_offset;
+  if (p == Path::kSck || p == Path::kSckFramed) {
     info->grid = (uint32_t)sck_grid(d, base, d_off, d_len, stride, count, l3_offset);
-    xw = xcd_weights(ctx->knobs, fixed_len != 4096 ? 0 : (int)info->grid < d.n_cu ? 25 : 50);
+    xw = xcd_weights(ctx->knobs, stride != 4096 ? 0 : (int)info->grid < d.n_cu ? 25 : 50);
   } else if (p == Path::kRagged) {
     info->grid = (uint32_t)(d.knobs.rsck_grid > 0 ? std::min(d.n_cu, d.knobs.rsck_grid) : d.n_cu);
     xw = xcd_weights(d.knobs, 40);

@@ -13,7 +13,8 @@ struct SckArgs {
   const uint8_t *base;
   uint64_t count;
   uint32_t *out;
-  uint32_t n;        // == stride
+  uint32_t n;        // == stride (the slot, for a framed ring)
+  uint32_t l3_offset;  // 0, or a framed ring's L3 offset in each slot (<= kSckMaxL3)
   uint32_t verify;
   uint32_t XB[32];   // basis of x^-32 (Horner step between a lane's chains)
   uint32_t QS[8];    // x^(-32 (4 s + 1)): lane slot s's chain 0 -> packet end
@@ -27,6 +28,10 @@ struct SckArgs {
   uint32_t xcd_k;
   uint32_t *xcd_rec;
 };
+
+// A framed ring's L3 offset: line 0 of the slot must hold the L3 bytes the
+// IPv4 masks and the seed touch (L3 bytes 0..32), so o + 33 <= 128.
+constexpr uint32_t kSckMaxL3 = 92;
 
 // Returns hipErrorInvalidValue for an n it has no instantiation for.
 hipError_t launch_sck(const SckArgs &a, int grid, hipStream_t st);

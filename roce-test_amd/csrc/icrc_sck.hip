@@ -66,9 +66,18 @@ namespace ricrc {
 // 0.628 ms per 4 GiB against 0.678 ms).  Sub-group m of a group (packets
 // 8 S Q + S g + m) is finished S times per group; its results land in the
 // slots in packet order, so the flush is unchanged.
-template <int L, int ABL, int FAM = kFamV4, int PL = L, int D = 8>
+// FR: a framed NIC ring -- 128 L-byte slots, the L3 packet at a.l3_offset in
+// each, running to the slot's end.  The kernel folds the whole slot: with a
+// zero register, the o = l3_offset leading bytes (zeroed) leave it at zero,
+// so the register at the L3 start is seeded by XORing kSeed into L3 bytes
+// 0..3 exactly as for o = 0.  Line 0's transform is per byte of the slot
+// (zero before o, the IPv4 masks and the seed from o on) and is precomputed
+// per lane (fr_and / fr_or / fr_xor); the trailer is still the slot's last
+// word.  IPv4 masks only (other families: the linear fix-up after it).
+template <int L, int ABL, int FAM = kFamV4, int PL = L, int D = 8, int FR = 0>
 __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
   static_assert(L % PL == 0 && PL >= 8, "super-groups: whole packets");
+  static_assert(!FR || FAM == kFamV4, "framed rings: IPv4 masks");
   constexpr uint32_t S = L / PL;  // packets per super-packet
   // finish tables | 128 KiB of slice-by-4 tables | result slots per wave
   constexpr uint32_t kSlots = 256;
@@ -167,6 +176,21 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
   const uint32_t m6w3 = s == 2 ? kMaskV6W11 : 0u;
   const uint32_t keep3 = s == 7 ? 0u : 0xFFFFFFFFu;                  // the trailer word
   const uint32_t *qrow = qtl + s * kQtStride;
+  // FR: line 0's per-byte transform, bytes 16 s + 4 i .. + 3 of the slot
+  uint32_t fr_and[4] = {}, fr_or[4] = {}, fr_xor[4] = {};
+  if constexpr (FR) {
+    const int o = (int)a.l3_offset;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int rel = (int)(16u * s) + 4 * i + k - o;  // the byte's L3 offset
+        if (rel < 0) continue;
+        fr_and[i] |= 0xFFu << (8 * k);
+        fr_or[i] |= mask_byte(kFamV4, (uint32_t)rel) << (8 * k);
+        if (rel < 4) fr_xor[i] |= ((kSeed >> (8 * rel)) & 0xFFu) << (8 * k);
+      }
+  }
 
   struct Fin {
     uint32_t r[4];    // chain registers
@@ -242,7 +266,10 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
   static_assert(PL >= 8, "finish needs 8 fold steps");
   // A packet's first line: the family's invariant masks and the seed.
   auto first_line = [&](u32x4 w, uint32_t (&x)[4]) {
-    if constexpr (FAM == kFamV4) {
+    if constexpr (FR) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) w[i] = ((w[i] & fr_and[i]) | fr_or[i]) ^ fr_xor[i];
+    } else if constexpr (FAM == kFamV4) {
       w[0] = or_xor(w[0], mw0, xw0);
       w[2] |= mw2;
     } else if constexpr (FAM == kFamV6) {
@@ -357,8 +384,22 @@ hipError_t launch_sck_fam(const SckArgs &a, int grid, hipStream_t st) {
   return hipGetLastError();
 }
 
+// Framed rings (a.l3_offset > 0): 1, 2 and 4 KiB slots, IPv4 masks.
+hipError_t launch_sck_framed(const SckArgs &a, int grid, hipStream_t st) {
+  const dim3 g(grid), b(kBlock);
+  if (a.n == 4096) hipLaunchKernelGGL((icrc_sck_kernel<32, 0, kFamV4, 32, 8, 1>), g, b, 0, st, a);
+  else if (a.n == 2048) hipLaunchKernelGGL((icrc_sck_kernel<16, 0, kFamV4, 16, 8, 1>), g, b, 0, st, a);
+  else if (a.n == 1024) hipLaunchKernelGGL((icrc_sck_kernel<32, 0, kFamV4, 8, 8, 1>), g, b, 0, st, a);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
 hipError_t launch_sck(const SckArgs &a, int grid, hipStream_t st) {
   (void)hipGetLastError();  // a stale error of an earlier, unrelated HIP call must not fail this launch
+  if (a.l3_offset != 0) {
+    if (a.family != kFamV4 || a.l3_offset > kSckMaxL3) return hipErrorInvalidValue;
+    return launch_sck_framed(a, grid, st);
+  }
   if (a.family == kFamV6) return launch_sck_fam<kFamV6>(a, grid, st);
   if (a.family == kFamAuto) return launch_sck_fam<kFamAuto>(a, grid, st);
   if (a.family != kFamV4) return hipErrorInvalidValue;

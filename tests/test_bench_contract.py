@@ -145,6 +145,9 @@ def test_kernel_labels_follow_the_dispatch():
     assert shard.split(" -> ") == ["bucket pass (rsck_bucket)",
                                    "strided-chain fold of packets of >= 2 lines (icrc_rsck_kernel)",
                                    "gather, folding the one-line packets (rsck_gather)"]
+    # a framed 4 KiB NIC ring (L3 at 14): the SCK's framed variant over the slots
+    assert "(icrc_sck_kernel)" in lab("--l3-offset", "14", "--stride", "4096")
+    assert "(rsck_bucket)" in lab("--l3-offset", "14", "--stride", "1536")
     assert "family_fix_kernel" in lab("--size", "64", "--family", "v6")
     assert "family_fix_kernel" not in lab("--family", "v6")  # the SCK applies IPv6 masks natively
     assert "count/plan" not in mix and "scatter" not in mix

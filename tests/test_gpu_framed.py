@@ -1,0 +1,143 @@
+"""GPU parity: framed NIC rings through the strided-chain kernel (SURVEY 8(a)
+row a4).
+
+A NIC receive ring of 1, 2 or 4 KiB slots with the L3 packet at l3_offset
+(14: Ethernet, 18: one VLAN tag, 22: two) running to the slot's end takes
+icrc_sck_kernel's framed instantiation (FR, icrc_sck.hip): the kernel folds
+the whole slot from a zero register with the bytes before the L3 start
+zeroed, which leaves the register at zero up to the L3 start, and seeds and
+masks L3 bytes 0..32 in line 0.  Every ICRC is compared bit-exactly with the
+C oracle on the same bytes and with the ragged pipeline the same rings took
+before (RICRC_NO_FRAMED)."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import oracle_c  # noqa: E402
+import roce_icrc  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0xF2A3ED
+
+
+def _dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to("cuda")
+
+
+def _out(count):
+    return torch.full((count,), -1, dtype=torch.int32, device="cuda")
+
+
+def _host_u32(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy().view(np.uint32)
+
+
+@pytest.mark.parametrize("stride", [1024, 2048, 4096])
+@pytest.mark.parametrize("l3", [1, 2, 14, 18, 22, 64, 92])
+def test_framed_ring_matches_oracle(ctx, stride, l3):
+    rng = np.random.default_rng(stride * 131 + l3)
+    count = 3001 if stride < 4096 else 1501
+    frames = rng.integers(0, 256, size=count * stride, dtype=np.uint8)
+    d = _dev(frames)
+    assert roce_icrc.kernel_path(d, count, stride=stride, l3_offset=l3, ctx=ctx) == "icrc_sck_kernel"
+    out = _out(count)
+    ctx.batch_device(d, count, out, stride=stride, l3_offset=l3)
+    want = oracle_c.icrc_batch(frames, stride=stride, count=count, l3_offset=l3, threads=8)
+    np.testing.assert_array_equal(_host_u32(out), want)
+
+
+@pytest.mark.parametrize("count", [1, 7, 8, 9, 63, 64, 65, 8 * 16 * 3 + 5, 70001])
+def test_framed_ring_tails(ctx, count):
+    """Partial groups (8 slots; 32 for 1 KiB super-groups), partial rounds
+    of result slots, a few groups per wave."""
+    for stride in (1024, 4096):
+        rng = np.random.default_rng(count + stride)
+        frames = rng.integers(0, 256, size=count * stride, dtype=np.uint8)
+        out = _out(count)
+        ctx.batch_device(_dev(frames), count, out, stride=stride, l3_offset=14)
+        np.testing.assert_array_equal(_host_u32(out), oracle_c.icrc_batch(frames, stride=stride, count=count,
+                                                                           l3_offset=14, threads=8))
+
+
+def test_framed_ring_same_as_ragged_pipeline(ctx, ctx_env):
+    """RICRC_NO_FRAMED sends the ring to the ragged pipeline (the round-4
+    path): the same ICRCs."""
+    count, stride = 20000, 2048
+    frames = np.random.default_rng(5).integers(0, 256, size=count * stride, dtype=np.uint8)
+    d = _dev(frames)
+    rag = ctx_env(RICRC_NO_FRAMED=1)
+    assert roce_icrc.kernel_path(d, count, stride=stride, l3_offset=18, ctx=rag).startswith("rsck_bucket")
+    a, b = _out(count), _out(count)
+    ctx.batch_device(d, count, a, stride=stride, l3_offset=18)
+    rag.batch_device(d, count, b, stride=stride, l3_offset=18)
+    np.testing.assert_array_equal(_host_u32(a), _host_u32(b))
+
+
+def test_framed_ring_not_taken(ctx):
+    """Rings the framed kernel does not fold: another slot size, an L3 offset
+    past line 0's masks, a misaligned base, per-packet lengths."""
+    d = torch.zeros(4096 * 8 + 16, dtype=torch.uint8, device="cuda")
+    path = lambda **kw: roce_icrc.kernel_path(kw.pop("base", d), 8, ctx=ctx, **kw)  # noqa: E731
+    assert path(stride=4096, l3_offset=14) == "icrc_sck_kernel"
+    assert path(stride=1536, l3_offset=14).startswith("rsck_bucket")
+    assert path(stride=4096, l3_offset=93).startswith("rsck_bucket")
+    assert path(base=d[2:], stride=4096, l3_offset=14).startswith("rsck_bucket")
+    lens = torch.full((8,), 1000, dtype=torch.int32, device="cuda")
+    assert path(stride=4096, l3_offset=14, lengths=lens).startswith("rsck_bucket")
+
+
+def test_framed_ring_verify_mode(ctx):
+    """Stamp every slot's trailer with the oracle, corrupt some, verify."""
+    count, stride, l3 = 5000, 4096, 14
+    rng = np.random.default_rng(77)
+    frames = rng.integers(0, 256, size=(count, stride), dtype=np.uint8)
+    icrcs = oracle_c.icrc_batch(frames, stride=stride, count=count, l3_offset=l3, threads=8)
+    frames[:, stride - 4:] = icrcs.view(np.uint8).reshape(count, 4)
+    bad = rng.choice(count, size=97, replace=False)
+    frames[bad, l3 + 40] ^= 0x5A
+    out = _out(count)
+    ctx.batch_device(_dev(frames), count, out, stride=stride, l3_offset=l3, verify=True)
+    ok = np.ones(count, np.uint32)
+    ok[bad] = 0
+    np.testing.assert_array_equal(_host_u32(out), ok)
+
+
+@pytest.mark.parametrize("family", ["v6", "auto"])
+def test_framed_ring_other_families(ctx, family):
+    """IPv6 / AUTO: the framed kernel's IPv4 masks, then the linear fix-up."""
+    count, stride, l3 = 4000, 1024, 14
+    rng = np.random.default_rng(91)
+    frames = rng.integers(0, 256, size=(count, stride), dtype=np.uint8)
+    frames[: count // 2, l3] = 0x60 | (frames[: count // 2, l3] & 15)  # version 6 for half of them
+    frames[count // 2:, l3] = 0x45
+    out = _out(count)
+    d = _dev(frames)
+    assert roce_icrc.kernel_path(d, count, stride=stride, l3_offset=l3, ctx=ctx, family=family) == \
+        "icrc_sck_kernel+family_fix_kernel"
+    ctx.batch_device(d, count, out, stride=stride, l3_offset=l3, family=family)
+    want = oracle_c.icrc_batch(frames, stride=stride, count=count, l3_offset=l3, threads=8, family=family)
+    np.testing.assert_array_equal(_host_u32(out), want)
+
+
+@pytest.mark.slow
+def test_framed_ring_full_size_bit_exact(ctx):
+    """1,048,576 slots of 4 KiB, L3 at 14 (4082-byte packets, bench.py
+    --l3-offset 14 --stride 4096), slots generated on the device, every ICRC
+    compared with the C oracle on the very same bytes; then every trailer
+    stamped and verified."""
+    count, stride, l3 = 1 << 20, 4096, 14
+    d = torch.empty(count * stride, dtype=torch.uint8, device="cuda")
+    ctx.synth_device(d, SEED, 0, count, stride)
+    out = _out(count)
+    ctx.batch_device(d, count, out, stride=stride, l3_offset=l3)
+    got = _host_u32(out)
+    host = d.cpu().numpy()
+    np.testing.assert_array_equal(got, oracle_c.icrc_batch(host, stride=stride, count=count, l3_offset=l3,
+                                                           threads=16))
+    host.reshape(count, stride)[:, stride - 4:] = got.view(np.uint8).reshape(count, 4)
+    d.copy_(torch.from_numpy(host))
+    ctx.batch_device(d, count, out, stride=stride, l3_offset=l3, verify=True)
+    assert int(_host_u32(out).sum()) == count

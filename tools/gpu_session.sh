@@ -14,6 +14,7 @@
 #   c3        4 M x 4096 B (16 GiB)  c4  4 M mixed 64/256/1024/4096 B
 #   c3s       512 K x 4096 B (C3's shard at N = 8)
 #   c4s       512 K mixed (C4's shard at N = 8: 4 M mixed over 8 GPUs)
+#   ring      1 M x 4096 B Ethernet-framed NIC ring slots, the L3 packet at 14
 # Every GPU step runs under its own timeout; the session stops at the first
 # step that crashes, aborts or times out (rc >= 2); a plain test failure
 # (rc 1) lets the rest run.
@@ -38,6 +39,7 @@ cfg_args() {
     c4) echo "--mix" ;;
     c3s) echo "--count 524288" ;;
     c4s) echo "--mix --count 524288" ;;
+    ring) echo "--l3-offset 14 --stride 4096" ;;
     *) echo "BAD" ;;
   esac
 }
@@ -50,6 +52,7 @@ pmc_args() {
     c4) echo "--mix" ;;
     c3s) echo "--count 524288" ;;
     c4s) echo "--mix --count 524288" ;;
+    ring) echo "--l3-offset 14 --stride 4096" ;;
     *) echo "BAD" ;;
   esac
 }
@@ -82,7 +85,7 @@ print('$cfg', d['value'], d['ms_per_step'], r['kernel_ms'], r['frac'], r.get('tr
     prof)
       a=$(cfg_args "$cfg")
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$cfg" -o run -- \
-        python3 bench.py --steps "$K" --warmup "$W" --no-cpu $a > "$OUT/prof_$cfg.log" 2>&1
+        python3 bench.py --steps "$K" --warmup "$W" --no-cpu --no-side $a > "$OUT/prof_$cfg.log" 2>&1
       ok $? "rocprof $cfg"
       python3 tools/prof_summary.py --last "$K" "$OUT/prof_$cfg/run_kernel_trace.csv" > "$OUT/prof_$cfg.txt"
       grep -v "copyBuffer\|synth\|prime\|fill" "$OUT/prof_$cfg.txt" | grep -A1 "icrc\|rsck\|gather\|bucket\|rs_" \

@@ -17,6 +17,9 @@ WRITE_SIZE is taken as reported.  Both are in KiB.
              doubled FETCH_SIZE against that byte count is reported as a check
              of the x2 correction on scattered traffic
              ("bucket_pass_fetch_over_descriptors").
+  --l3-offset O --stride S
+             a framed NIC ring: 1 M slots of S bytes, the L3 packet at O in
+             each (S - O bytes) -> profiles/pmc_traffic_ringO_S.json
   --count N  packets on the (one) GPU instead of the BASELINE count (1 M, or
              4 M with --mix): C3's 16 GiB batch (--count 4194304) and the
              8-GPU shard stand-ins; the record's name carries N
@@ -39,7 +42,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def run_pass(counter, outdir, bench_args, match):
     cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", outdir, "-o", "run", "--",
-           sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "5", "--warmup", "1", "--no-cpu"] + bench_args
+           sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "5", "--warmup", "1", "--no-cpu", "--no-side"] + bench_args
     subprocess.run(cmd, check=True, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"), timeout=600,
                    stdout=subprocess.DEVNULL)
     per = {}
@@ -60,6 +63,8 @@ def main():
     ap.add_argument("--mix", action="store_true")
     ap.add_argument("--size", type=int, default=4096)
     ap.add_argument("--count", type=int, default=None)
+    ap.add_argument("--l3-offset", type=int, default=0)
+    ap.add_argument("--stride", type=int, default=None)
     ap.add_argument("--out", default=None)
     ap.add_argument("--scratch", default=os.path.join(ROOT, "gpurun_out", "pmc_traffic"))
     a = ap.parse_args()
@@ -68,13 +73,15 @@ def main():
 
     std = (4 << 20) if a.mix else (1 << 20)
     count = a.count or std
-    rec = bench.traffic_record(a.mix, a.size, count)
+    rec = bench.traffic_record(a.mix, a.size, count, a.l3_offset, a.stride)
     if rec is None:
         raise SystemExit(f"no traffic record is kept for --size {a.size}")
     name, srcs, match = rec
     a.out = os.path.abspath(a.out or os.path.join(ROOT, "gpurun_out", name))
-    a.scratch = os.path.abspath(a.scratch + ("_mix" if a.mix else f"_{a.size}") + f"_{count}")
+    a.scratch = os.path.abspath(a.scratch + ("_mix" if a.mix else f"_{a.size}") + f"_{count}_{a.l3_offset}")
     bench_args = (["--mix"] if a.mix else ["--size", str(a.size)]) + ["--count", str(count)]
+    if a.l3_offset:
+        bench_args += ["--l3-offset", str(a.l3_offset), "--stride", str(a.stride or a.size)]
     fetch = run_pass("FETCH_SIZE", os.path.join(a.scratch, "fetch"), bench_args, match)
     write = run_pass("WRITE_SIZE", os.path.join(a.scratch, "write"), bench_args, match)
     if a.mix:
@@ -83,6 +90,10 @@ def main():
         lens = np.random.default_rng(bench.SEED).choice(np.array(bench.MIX_SIZES, np.uint32), size=count)
         alg = int(lens.sum(dtype=np.uint64)) + 16 * count
         src, size = bench.kernel_source_hash(srcs), "mix"
+    elif a.l3_offset:
+        size = a.size
+        alg = count * ((a.stride or a.size) - a.l3_offset) + 4 * count
+        src = bench.kernel_source_hash(srcs)
     else:
         size = a.size
         alg = count * size + 4 * count
@@ -91,6 +102,7 @@ def main():
                    "dispatches": [fetch.get(k, (0, 0))[1], write.get(k, (0, 0))[1]]} for k in match}
     hbm = sum(2.0 * v["FETCH_SIZE_KiB"] * 1024 + v["WRITE_SIZE_KiB"] * 1024 for v in kernels.values())
     res = {"size": size, "count": count, "kernel_src": src, "kernels": kernels,
+           **({"l3_offset": a.l3_offset, "stride": a.stride or a.size} if a.l3_offset else {}),
            "correction": "FETCH_SIZE x2 (gfx950 wide-streaming read undercount, MI355X_MICROARCH.md §HBM)",
            "hbm_bytes_per_launch": hbm, "algorithmic_bytes_per_launch": alg,
            "traffic_over_algorithmic": hbm / alg}
