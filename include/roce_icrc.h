@@ -423,6 +423,7 @@ typedef struct {
   uint32_t pass_grid;      /* ragged: bucket / gather blocks (0 otherwise) */
   uint32_t pass_unroll;    /* ragged: packets per thread of those passes */
   uint32_t fused;          /* ragged: 1 if the gather folds the one-line packets */
+  uint32_t gather_grid;    /* ragged: gather blocks (2 x pass_grid when one-line sides run beside them) */
 } ricrc_launch_info_t;
 int ricrc_launch_info(const ricrc_ctx *ctx, int dev, const void *d_base, const uint64_t *d_off,
                       const uint32_t *d_len, uint32_t stride, uint64_t count, uint32_t l3_offset,

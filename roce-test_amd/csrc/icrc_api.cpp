@@ -47,6 +47,7 @@ constexpr uint64_t kRsChunk = kRsMaxCount;  // the ragged pipeline's group count
 struct Knobs {
   bool no_sck = false;     // RICRC_NO_SCK: fixed 1/2/4 KiB batches take the transposed kernel
   bool no_framed = false;  // RICRC_NO_FRAMED: framed 1/2/4 KiB rings take the ragged pipeline
+  bool no_gather_split = false;  // RICRC_NO_GATHER_SPLIT: the fused gather folds its one-line packets itself
   bool no_tsk = false;     // RICRC_NO_TSK: ... and 128-512 B batches the direct streaming kernel
   bool no_quad = false;    // RICRC_NO_QUAD: 64 B batches take the direct streaming kernel
   int sck_grid = 0;        // RICRC_SCK_GRID: cap the strided-chain grid (tests: many groups per wave)
@@ -397,6 +398,7 @@ int launch_rsck_range(Dev &d, const uint8_t *base, const uint64_t *off, const ui
   k.group_cost = d.knobs.gcost ? d.knobs.gcost : kRsGroupCost;
   const XcdWeights xw = xcd_weights(d.knobs, 40);
   for (int x = 0; x < 8; ++x) k.xw[x] = xw.w[x];
+  k.no_split = d.knobs.no_gather_split ? 1u : 0u;
   k.out = out;
   k.tzb = d.d_tzb;
   // GF(2) constants of the fold's finish (the same for every call)
@@ -737,6 +739,7 @@ Knobs read_knobs() {
   };
   k.no_sck = getenv("RICRC_NO_SCK") != nullptr;
   k.no_framed = getenv("RICRC_NO_FRAMED") != nullptr;
+  k.no_gather_split = getenv("RICRC_NO_GATHER_SPLIT") != nullptr;
   k.no_tsk = getenv("RICRC_NO_TSK") != nullptr;
   k.no_quad = getenv("RICRC_NO_QUAD") != nullptr;
   k.sck_grid = (int)std::max(0L, num("RICRC_SCK_GRID", 0));
@@ -891,12 +894,14 @@ int ricrc_launch_info(const ricrc_ctx *ctx, int dev, const void *d_base, const u
   } else if (p == Path::kRagged) {
     info->grid = (uint32_t)(d.knobs.rsck_grid > 0 ? std::min(d.n_cu, d.knobs.rsck_grid) : d.n_cu);
     xw = xcd_weights(d.knobs, 40);
-    int pg = 0, pu = 0;
+    int pg = 0, pu = 0, gg = 0;
     bool fused = false;
-    rs_pass_info(std::min<uint64_t>(count, kRsChunk), d.knobs.pass_grid, &pg, &pu, &fused);
+    rs_pass_info(std::min<uint64_t>(count, kRsChunk), d.knobs.pass_grid, d.knobs.no_gather_split, &pg, &pu, &fused,
+                 &gg);
     info->pass_grid = (uint32_t)pg;
     info->pass_unroll = (uint32_t)pu;
     info->fused = fused ? 1u : 0u;
+    info->gather_grid = (uint32_t)gg;
   }
   for (int x = 0; x < 8; ++x) info->xcd_weights[x] = xw.w[x];
   return 0;

@@ -97,6 +97,7 @@ struct RsckArgs {
   uint32_t verify;
   uint32_t group_cost;  // a group's finish in line-steps of the fold's work split (launch_rsck sets it)
   uint32_t xw[8];            // the fold's work split by XCD (xcd_share; xw[0] == 0: equal shares)
+  uint32_t no_split;         // host: keep the fused gather on the pass grid (RICRC_NO_GATHER_SPLIT)
   uint32_t *out;
   // device workspace (icrc_api.cpp sizes it: rs_workspace_bytes)
   RsCounters *ctr;      // zeroed on allocation and by the gather pass of every call
@@ -146,7 +147,7 @@ hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, hipStream_t st, hipE
 // gather folding the one-line packets: no icrc_rsmall_kernel launch).
 bool rs_fused(uint64_t count, int pass_cap);
 // The bucket / gather passes' blocks and packets per thread for such a batch (ricrc_launch_info).
-void rs_pass_info(uint64_t count, int pass_cap, int *grid, int *unroll, bool *fused);
+void rs_pass_info(uint64_t count, int pass_cap, bool no_split, int *grid, int *unroll, bool *fused, int *ggrid);
 
 struct SynthArgs {
   uint8_t *buf;

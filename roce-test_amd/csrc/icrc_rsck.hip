@@ -1113,36 +1113,45 @@ __global__ __launch_bounds__(kBlock) void icrc_rsmall_kernel(RsckArgs a) {
 // (its small range, descriptors at desc[small0, small0 + small)) are folded
 // here, one lane per packet, instead of by icrc_rsmall_kernel: at C4's
 // 8-GPU shard that kernel took 11.4 us (its launch, its table build, one
-// round of loads) for 131 K packets, profiles/r05/s1_prof_c4s.txt.
-template <int PU, bool SMALL>  // the bucket pass's packets per thread
+// round of loads) for 131 K packets, profiles/r05/s1_prof_c4s.txt.  With a
+// grid of 2 x nblk (PassShape::split: the pass ran on at most half the CUs)
+// the one-line packets of pass block b are folded by block nblk + b, the
+// "small side", on the CUs the pass left idle: it inverts the block's
+// positions in LDS and writes those packets' out[i] itself, while block b
+// gathers the others -- no result crosses between the two, so neither waits.
+__device__ __forceinline__ void pass_range_of(uint64_t count, uint32_t nblk, uint32_t b, uint32_t &lo,
+                                              uint32_t &hi) {
+  const uint64_t per = ((count + nblk - 1) / nblk + kPassBlock - 1) / kPassBlock * kPassBlock;
+  const uint64_t l = (uint64_t)b * per < count ? (uint64_t)b * per : count;
+  lo = (uint32_t)l;
+  hi = (uint32_t)(l + per < count ? l + per : count);
+}
+
+template <int PU, bool SMALL, bool SPLIT = false>  // the bucket pass's packets per thread
 __global__ __launch_bounds__(kPassBlock) void rsck_gather(RsckArgs a) {
+  static_assert(SMALL || !SPLIT, "small sides fold one-line packets");
   constexpr uint32_t kStage = stage_entries(PU);
   __shared__ uint32_t lres[kStage];
   __shared__ uint32_t tab[SMALL ? kLdsWords : 1];
+  constexpr bool split = SPLIT;  // a grid of 2 x nblk
+  const bool small_side = split && blockIdx.x >= a.nblk;
+  const uint32_t pb = small_side ? blockIdx.x - a.nblk : blockIdx.x;
   const uint32_t tab_v = SMALL ? table_entry(g_tab) : 0u;
   // The counters are dead now (the bucket pass and both folds have read
   // them): zero them for the next call on this workspace.
   if (blockIdx.x == 0 && threadIdx.x == 0) *a.ctr = RsCounters{};
   uint32_t lo, hi;
-  {
-    uint64_t l, h_;
-    pass_range(a.count, l, h_);
-    lo = (uint32_t)l;
-    hi = (uint32_t)h_;
-  }
-  const RsBlock B = a.blk[blockIdx.x];
+  pass_range_of(a.count, a.nblk, pb, lo, hi);
+  const RsBlock B = a.blk[pb];
   const uint32_t lane = threadIdx.x & 63;
+  const LaneTab lt{(lane & 31) << 2, ((lane & 31) << 2) | 0x10000u};
   // SMALL: the first of this thread's one-line descriptors (every lane of a
   // wave with a valid one: the fold is wave-collective), requested with the
   // other loads; C4's shard blocks hold ~1 K one-line packets, one per thread
   auto small_desc = [&](uint32_t j) { return a.desc[B.small0 + (j < B.small ? j : B.small - 1u)]; };
-  RsDesc sd0{0u, 0u};
-  if (SMALL && B.small) sd0 = small_desc(threadIdx.x);
-  auto small_fold = [&](auto store) {  // fold the block's small range, store(j, icrc)
-    if (!SMALL || !B.small) return;
+  auto small_fold = [&](const RsDesc &sd0, auto store) {  // fold the block's small range, store(j, icrc)
     table_store(tab, tab_v);
     __syncthreads();
-    const LaneTab lt{(lane & 31) << 2, ((lane & 31) << 2) | 0x10000u};
 #pragma unroll 1
     for (uint32_t j0 = 0; j0 < B.small; j0 += blockDim.x) {
       const uint32_t j = j0 + threadIdx.x;
@@ -1153,6 +1162,27 @@ __global__ __launch_bounds__(kPassBlock) void rsck_gather(RsckArgs a) {
     }
   };
   constexpr int U = 4;  // packets per thread in flight at once
+  if (small_side) {  // block-uniform
+    if (!B.staged || B.small == 0) return;  // (an unstaged block's gather side folds them)
+    uint32_t p[PU];
+#pragma unroll
+    for (int k = 0; k < PU; ++k) {
+      const uint32_t i = lo + (uint32_t)k * blockDim.x + threadIdx.x;
+      p[k] = i < hi ? __builtin_nontemporal_load(a.pos_of + i) : 0xFFFFFFFFu;
+    }
+    const RsDesc sd0 = small_desc(threadIdx.x);
+    uint32_t *idx = lres;  // small position j -> packet index i
+#pragma unroll
+    for (int k = 0; k < PU; ++k)
+      if (p[k] < B.small) idx[p[k]] = lo + (uint32_t)k * blockDim.x + threadIdx.x;
+    small_fold(sd0, [&](uint32_t j, uint32_t x) {
+      const uint32_t i = idx[j];
+      __builtin_nontemporal_store(gather_one(a, i, j, x), a.out + i);
+    });
+    return;
+  }
+  RsDesc sd0{0u, 0u};
+  if (SMALL && !split && B.small) sd0 = small_desc(threadIdx.x);
   if (B.staged) {  // block-uniform (a staged block's packets fit one round: hi - lo <= PU x blockDim)
     // every load of the block issued before the barrier: the positions, then
     // the results into LDS
@@ -1164,7 +1194,7 @@ __global__ __launch_bounds__(kPassBlock) void rsck_gather(RsckArgs a) {
     }
     const uint32_t total = B.small + 8u * B.groups;
     const uint32_t *rs = a.res + B.small0, *rb = a.bres + 8ull * B.g0 - B.small;
-    const uint32_t from = SMALL ? B.small : 0u;  // SMALL: the small range is folded below
+    const uint32_t from = SMALL ? B.small : 0u;  // SMALL: the small range is folded here or by the small side
     constexpr int R = (kStage + kPassBlock - 1) / kPassBlock;
     uint32_t v[R];
 #pragma unroll
@@ -1177,19 +1207,22 @@ __global__ __launch_bounds__(kPassBlock) void rsck_gather(RsckArgs a) {
       const uint32_t j = (uint32_t)k * blockDim.x + threadIdx.x;
       if (j >= from && j < total) lres[j] = v[k];
     }
-    small_fold([&](uint32_t j, uint32_t x) { lres[j] = x; });
+    if (SMALL && !split && B.small) small_fold(sd0, [&](uint32_t j, uint32_t x) { lres[j] = x; });
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < PU; ++k) {
       const uint32_t i = lo + (uint32_t)k * blockDim.x + threadIdx.x;
-      if (i < hi) __builtin_nontemporal_store(gather_one(a, i, p[k], p[k] != 0xFFFFFFFFu ? lres[p[k]] : 0u), a.out + i);
+      if (i < hi && !(split && p[k] < B.small))  // split: the small side wrote those
+        __builtin_nontemporal_store(gather_one(a, i, p[k], p[k] != 0xFFFFFFFFu ? lres[p[k]] : 0u), a.out + i);
     }
     return;
   }
   // not staged: the small results go to the pool first (a workgroup-scope
   // barrier orders those stores before the reads below)
-  small_fold([&](uint32_t j, uint32_t x) { a.res[B.small0 + j] = x; });
-  if (SMALL && B.small) __syncthreads();
+  if (SMALL && B.small) {
+    small_fold(small_desc(threadIdx.x), [&](uint32_t j, uint32_t x) { a.res[B.small0 + j] = x; });
+    __syncthreads();
+  }
   for (uint32_t i0 = lo + threadIdx.x; i0 < hi; i0 += U * blockDim.x) {
     uint32_t p[U], v[U];
 #pragma unroll
@@ -1258,8 +1291,9 @@ static void launch_bucket_u(const RsckArgs &a, int pgrid, hipStream_t st) {
 struct PassShape {
   int grid, U;
   bool fused;  // the gather folds the one-line packets (U = 4, one staged round per block): no icrc_rsmall_kernel
+  bool split;  // fused on at most half the pass blocks: the gather runs on 2 x grid, small sides beside it
 };
-static PassShape pass_shape(uint64_t count, int pass_cap) {
+static PassShape pass_shape(uint64_t count, int pass_cap, bool no_split = false) {
   int U = kPassUnrollBig;
   for (int u : {4, 8, kPassUnroll})
     if (count <= (uint64_t)kPassBlocks * kPassBlock * u) {
@@ -1269,14 +1303,16 @@ static PassShape pass_shape(uint64_t count, int pass_cap) {
   const uint64_t want = (count + (uint64_t)U * kPassBlock - 1) / ((uint64_t)U * kPassBlock);
   int grid = (int)(want < (uint64_t)kPassBlocks ? (want ? want : 1) : kPassBlocks);
   if (pass_cap > 0 && pass_cap < grid) grid = pass_cap;  // RICRC_RS_PASS_GRID (blocks then take several rounds)
-  return PassShape{grid, U, U == 4 && (uint64_t)grid * 4u * kPassBlock >= count};
+  const bool fused = U == 4 && (uint64_t)grid * 4u * kPassBlock >= count;
+  return PassShape{grid, U, fused, fused && !no_split && 2 * grid <= kPassBlocks};
 }
 bool rs_fused(uint64_t count, int pass_cap) { return count > 0 && pass_shape(count, pass_cap).fused; }
-void rs_pass_info(uint64_t count, int pass_cap, int *grid, int *unroll, bool *fused) {
-  const PassShape ps = pass_shape(count, pass_cap);
+void rs_pass_info(uint64_t count, int pass_cap, bool no_split, int *grid, int *unroll, bool *fused, int *ggrid) {
+  const PassShape ps = pass_shape(count, pass_cap, no_split);
   *grid = ps.grid;
   *unroll = ps.U;
   *fused = ps.fused;
+  *ggrid = ps.split ? 2 * ps.grid : ps.grid;
 }
 static void launch_bucket(const RsckArgs &a, const PassShape &ps, hipStream_t st) {
   switch (ps.U) {
@@ -1289,7 +1325,8 @@ static void launch_bucket(const RsckArgs &a, const PassShape &ps, hipStream_t st
 static void launch_gather(const RsckArgs &a, const PassShape &ps, hipStream_t st) {
   switch (ps.U) {  // the gather's blocks are the bucket pass's (block b serves pass block b's packets)
     case 4:
-      if (ps.fused) hipLaunchKernelGGL((rsck_gather<4, true>), dim3(ps.grid), dim3(kPassBlock), 0, st, a);
+      if (ps.split) hipLaunchKernelGGL((rsck_gather<4, true, true>), dim3(2 * ps.grid), dim3(kPassBlock), 0, st, a);
+      else if (ps.fused) hipLaunchKernelGGL((rsck_gather<4, true>), dim3(ps.grid), dim3(kPassBlock), 0, st, a);
       else hipLaunchKernelGGL((rsck_gather<4, false>), dim3(ps.grid), dim3(kPassBlock), 0, st, a);
       break;
     case 8: hipLaunchKernelGGL((rsck_gather<8, false>), dim3(ps.grid), dim3(kPassBlock), 0, st, a); break;
@@ -1304,7 +1341,7 @@ hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, hipStream_t st, hipE
   if (a.count > kRsMaxCount) return hipErrorInvalidValue;
   // a.ctr is zero here: zeroed when the workspace was allocated, and again
   // by rsck_gather at the end of every call.
-  const PassShape ps = pass_shape(a.count, pass_cap);
+  const PassShape ps = pass_shape(a.count, pass_cap, a.no_split != 0);
   a.nblk = (uint32_t)ps.grid;
   // RICRC_PASS_TIMES: timing events between the passes on st (diagnostics)
   auto mark = [&](int k) { if (pass_ev) (void)hipEventRecord(pass_ev[k], st); };

@@ -255,6 +255,53 @@ def test_ragged_bucket_17_per_thread_one_round_unstaged(ctx, ctx_env):
         np.testing.assert_array_equal(_host_u32(out), want)
 
 
+@pytest.mark.parametrize("count", [3000, 30_000, 200_000, 524_288])
+def test_gather_small_sides(ctx, ctx_env, count):
+    """Batches whose bucket pass runs on at most half the CUs (<= 524,288
+    packets: 4 per thread on <= 128 blocks) launch the gather on twice the
+    blocks: block nblk + b folds pass block b's one-line packets and writes
+    their out[i] itself, block b gathers the rest.  Every class (one-line,
+    2-3 lines, long), short packets finished in the gather (n < 44), invalid
+    lengths, verify mode -- the same words as with RICRC_NO_GATHER_SPLIT
+    (the pass grid's own blocks fold the one-line packets) and the oracle."""
+    import roce_icrc
+
+    rng = np.random.default_rng(count)
+    lens = rng.choice(np.array([20, 44, 60, 64, 100, 124, 256, 1024, 1500, 4096], np.uint32), size=count)
+    offs = np.zeros(count, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + rng.integers(0, 5, size=count - 1).astype(np.uint64))
+    buf = rng.integers(0, 256, size=int(offs[-1] + lens[-1]) + 64, dtype=np.uint8)
+    bad = rng.choice(count, size=min(40, count // 50), replace=False)
+    lens_dev = lens.copy()
+    lens_dev[bad] = 70000
+    want = oracle_c.icrc_batch(buf, offsets=offs, lengths=lens, threads=16)
+    want[bad] = 0
+    d_buf, d_offs, d_lens = _dev(buf), _dev(offs), _dev(lens_dev)
+    whole = ctx_env(RICRC_NO_GATHER_SPLIT=1)
+    li, lw = ctx.launch_info(d_buf, count, offsets=d_offs, lengths=d_lens), \
+        whole.launch_info(d_buf, count, offsets=d_offs, lengths=d_lens)
+    assert li["one_line_in_gather"] and li["gather_grid"] == 2 * li["pass_grid"] <= 256
+    assert lw["gather_grid"] == lw["pass_grid"] == li["pass_grid"]
+    assert roce_icrc.kernel_path(d_buf, count, offsets=d_offs, lengths=d_lens, ctx=ctx) == \
+        "rsck_bucket+icrc_rsck_kernel+rsck_gather"
+    for c in (ctx, whole):
+        out = _out(count)
+        c.batch_device(d_buf, count, out, offsets=d_offs, lengths=d_lens, stream=_stream())
+        np.testing.assert_array_equal(_host_u32(out), want)
+    stamped = buf.copy()
+    want_v = np.zeros(count, np.uint32)
+    for i in range(0, count, 7):
+        if lens_dev[i] != 70000 and lens[i] >= 4:
+            o = int(offs[i]) + int(lens[i]) - 4
+            stamped[o:o + 4] = np.frombuffer(int(want[i]).to_bytes(4, "little"), np.uint8)
+            want_v[i] = 1
+    for c in (ctx, whole):
+        out = _out(count)
+        c.batch_device(_dev(stamped), count, out, offsets=d_offs, lengths=d_lens, stream=_stream(), verify=True)
+        got = _host_u32(out)
+        np.testing.assert_array_equal(got[::7], want_v[::7])
+
+
 def test_ragged_kernel_offsets_only_and_lengths_only(ctx):
     """Descriptor modes: offsets with a fixed length (stride - l3_offset), and
     per-packet lengths at a fixed stride."""
@@ -493,6 +540,45 @@ def test_c4_full_size_bit_exact(ctx):
     tail = (offs + lens.astype(np.uint64) - 4).astype(np.int64)
     idx = (tail[:, None] + np.arange(4, dtype=np.int64)[None, :]).reshape(-1)
     host[idx] = got.view(np.uint8)
+    d.copy_(torch.from_numpy(host))
+    ctx.batch_device(d, count, out, offsets=d_offs, lengths=d_lens, stream=_stream(), verify=True)
+    assert int(_host_u32(out).astype(np.uint64).sum()) == count
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("shard", ["c4s", "c4_strong_rank7"])
+def test_c4_shard_full_size_bit_exact(ctx, shard):
+    """C4's 8-GPU shard at full size, as bench.py builds it: the stand-in
+    (--mix --count 524288: the first 524,288 packets of the bench seed's mix)
+    and rank 7 of C4 strong-scaled over 8 GPUs (4 M packets cut at equal
+    bytes).  Both take the shard's pipeline -- the bucket pass at 4 packets
+    per thread on <= 128 blocks, the gather folding the one-line packets --
+    and every ICRC is compared with the C oracle on the very same bytes, then
+    every trailer stamped and verified."""
+    import bench
+    import roce_icrc
+    from roce_icrc.dist import byte_balanced_cuts
+
+    T = 524288 if shard == "c4s" else 4 << 20
+    lens_g = np.random.default_rng(bench.SEED).choice(np.array(bench.MIX_SIZES, np.uint32), size=T)
+    lo, hi = (0, T) if shard == "c4s" else byte_balanced_cuts(lens_g, 8)[7:9]
+    lens = np.ascontiguousarray(lens_g[lo:hi])
+    count = len(lens)
+    assert 500_000 < count < 540_000
+    offs = np.zeros(count, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    d = torch.empty(int(offs[-1] + lens[-1]), dtype=torch.uint8, device="cuda")
+    d_offs, d_lens = _dev(offs), _dev(lens)
+    assert roce_icrc.kernel_path(d, count, offsets=d_offs, lengths=d_lens, ctx=ctx) == \
+        "rsck_bucket+icrc_rsck_kernel+rsck_gather"
+    ctx.synth_ragged_device(d, bench.SEED, lo, count, d_offs, d_lens, stream=_stream())
+    out = _out(count)
+    ctx.batch_device(d, count, out, offsets=d_offs, lengths=d_lens, stream=_stream())
+    got = _host_u32(out)
+    host = d.cpu().numpy()
+    np.testing.assert_array_equal(got, oracle_c.icrc_batch(host, offsets=offs, lengths=lens, threads=16))
+    tail = (offs + lens.astype(np.uint64) - 4).astype(np.int64)
+    host[(tail[:, None] + np.arange(4, dtype=np.int64)[None, :]).reshape(-1)] = got.view(np.uint8)
     d.copy_(torch.from_numpy(host))
     ctx.batch_device(d, count, out, offsets=d_offs, lengths=d_lens, stream=_stream(), verify=True)
     assert int(_host_u32(out).astype(np.uint64).sum()) == count

@@ -12,7 +12,7 @@ PREV=${PREV:-tools/ab/prev}
 [ -d $PREV ] || { echo "no $PREV snapshot"; exit 3; }
 R=${RUNS:-3}
 for r in $(seq 1 $R); do
-  (cd $PREV && timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-cpu ${ARGS:---mix}) > $O/prev_$r.json 2>$O/prev_$r.err || exit 3
-  timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-cpu ${ARGS:---mix} > $O/new_$r.json 2>$O/new_$r.err || exit 3
+  (cd $PREV && timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-cpu --no-side ${ARGS:---mix}) > $O/prev_$r.json 2>$O/prev_$r.err || exit 3
+  timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-cpu --no-side ${ARGS:---mix} > $O/new_$r.json 2>$O/new_$r.err || exit 3
 done
 for r in $(seq 1 $R); do for v in prev new; do python3 -c "import json; d=json.load(open('$O/${v}_$r.json')); print('$v $r', d['value'], d['ms_per_step'], d['roofline']['kernel_ms'])"; done; done

@@ -7,7 +7,7 @@ O=gpurun_out/${TAG:-ab_env}; mkdir -p $O
 for r in 1 2 3; do
   for m in ${MODES:-base}; do
     if [ "$m" = base ]; then e=""; else e="$m"; fi
-    env $e timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-cpu ${ARGS:---mix} > $O/${m//=/_}_$r.json 2>$O/${m//=/_}_$r.err || exit 3
+    env $e timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-cpu --no-side ${ARGS:---mix} > $O/${m//=/_}_$r.json 2>$O/${m//=/_}_$r.err || exit 3
     python3 -c "import json; d=json.load(open('$O/${m//=/_}_$r.json')); print('$m $r', d['value'], d['ms_per_step'], d['roofline']['kernel_ms'])"
   done
 done

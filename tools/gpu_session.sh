@@ -100,7 +100,8 @@ round(d['traffic_over_algorithmic'], 5))" | tee -a "$OUT/session.txt" ;;
     microbench)
       (cd tools/microbench && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 "$cfg.hip" -o "$cfg" \
         > "../../$OUT/mb_${cfg}_build.log" 2>&1)
-      ok $? "build $cfg"
+      rc=$?; [ $rc -ne 0 ] && rc=2  # a failed build must not run a stale binary
+      ok $rc "build $cfg"
       timeout -k 10 300 "tools/microbench/$cfg" ${MB_ARGS:-} > "$OUT/mb_$cfg.txt" 2>&1
       ok $? "microbench $cfg"
       tail -40 "$OUT/mb_$cfg.txt" ;;

@@ -83,7 +83,6 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&d_off, 8 * count)); CK(hipMalloc(&d_len, 4 * count));
   CK(hipMalloc(&out, 4 * (count > 65536 ? count : 65536)));
   CK(hipMalloc(&tzb, 4 * 1024)); CK(hipMemset(tzb, 0x35, 4 * 1024));
-  uint32_t *x8n; CK(hipMalloc(&x8n, 4 * 65536)); CK(hipMemset(x8n, 0x5A, 4 * 65536));
   CK(hipMalloc(&sink, 8 * 8192 * 4));
   CK(hipMemcpy(d_off, off.data(), 8 * count, hipMemcpyHostToDevice));
   CK(hipMemcpy(d_len, len.data(), 4 * count, hipMemcpyHostToDevice));
@@ -91,7 +90,7 @@ int main(int argc, char **argv) {
   CK(rs_zero_counters(ws, 0));
   RsckArgs a{};
   a.base = buf; a.off = d_off; a.len = d_len; a.count = count;
-  a.out = out; a.tzb = tzb; a.x8n = x8n; a.group_cost = kRsGroupCost;
+  a.out = out; a.tzb = tzb; a.group_cost = kRsGroupCost;
   for (int j = 0; j < 32; ++j) { a.XB[j] = 0x85EBCA6Bu * (j + 3); a.XB2[j] = 0x27D4EB2Fu * (j + 5); a.XB3[j] = 0x165667B1u * (j + 7); }
   for (int s = 0; s < 8; ++s) a.QS[s] = 0x9E3779B9u * (s + 1);
   for (int k = 0; k < 8; ++k) a.xw[k] = 1000u + ((k & 1) ? -40 : 40);
@@ -164,9 +163,6 @@ int main(int argc, char **argv) {
       // the work each wave got (its groups' L + group cost, quarter line-steps) against its share
       std::vector<double> ratio(nw);
       for (int w = 0; w < nw; ++w) ratio[w] = st[8 * w + 7] ? (double)st[8 * w + 6] / st[8 * w + 7] : 0.0;
-      int nex = 0;
-      for (int w = 0; w < nw; ++w) nex += (st[8 * w + 5] >> 31) & 1;
-      printf("  waves in exact-split workgroups: %d of %d\n", nex, nw);
       printf("  work / share: p1 %.3f p10 %.3f p50 %.3f p90 %.3f p99 %.3f max %.3f\n", pct(ratio, 0.01), pct(ratio, 0.1),
              pct(ratio, 0.5), pct(ratio, 0.9), pct(ratio, 0.99), pct(ratio, 1));
       // end time by work ratio decile: does the extra work explain the late waves?
@@ -192,6 +188,23 @@ int main(int argc, char **argv) {
       for (int w = 0; w < nw; ++w) se[w] = (int32_t)(ss[2 * w + 1] - s0) / 100.0;
       printf("  plain stream timeline: end p1 %.1f p10 %.1f p50 %.1f p90 %.1f p99 %.1f max %.1f\n", pct(se, 0.01),
              pct(se, 0.1), pct(se, 0.5), pct(se, 0.9), pct(se, 0.99), pct(se, 1));
+    }
+  }
+  // the gather alone (after the bucket pass and the fold above): split into
+  // gather + small sides (product), fused on the pass grid, and the plain
+  // gather with the one-line kernel before it
+  {
+    CK(rs_zero_counters(ws, 0));
+    launch_bucket(a, ps, 0);
+    hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, 0, a);
+    CK(hipDeviceSynchronize());
+    const int g = ps.grid;
+    for (int r = 0; r < 3; ++r) {
+      const float gs = timeit([&] { hipLaunchKernelGGL((rsck_gather<4, true, true>), dim3(2 * g), dim3(kPassBlock), 0, 0, a); }, 20);
+      const float gf = timeit([&] { hipLaunchKernelGGL((rsck_gather<4, true>), dim3(g), dim3(kPassBlock), 0, 0, a); }, 20);
+      const float gp = timeit([&] { hipLaunchKernelGGL((rsck_gather<4, false>), dim3(g), dim3(kPassBlock), 0, 0, a); }, 20);
+      printf("gather alone: small sides beside it (%d blocks) %.1f us | one-line folded in the gather (%d) %.1f | plain gather %.1f\n",
+             2 * g, gs, g, gf, gp);
     }
   }
   // the bucket pass by packets per thread (one round when U x 1024 x blocks >= count)
