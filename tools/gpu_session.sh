@@ -76,9 +76,11 @@ for step in ${STEPS:-smoke tests bench:headline}; do
       tail -3 "$OUT/gpu_tests.log" ;;
     bench)
       a=$(cfg_args "$cfg")
+      t0=$SECONDS
       timeout -k 10 300 python bench.py --steps "$K" --warmup "$W" $a ${BENCH_ARGS:-} > "$OUT/bench_$cfg.json" \
         2> "$OUT/bench_$cfg.err"
       ok $? "bench $cfg"
+      echo "bench $cfg: $((SECONDS - t0)) s wall (the process, side configs included)" | tee -a "$OUT/session.txt"
       python3 -c "import json; d=json.load(open('$OUT/bench_$cfg.json')); r=d['roofline']; \
 print('$cfg', d['value'], d['ms_per_step'], r['kernel_ms'], r['frac'], r.get('traffic'), d.get('pass_ms'))" \
         | tee -a "$OUT/session.txt" ;;
