@@ -387,8 +387,9 @@ __device__ __forceinline__ void static_for(F &&f) {
 // ABL (timing-only ablations, tools/microbench/shard.hip, bucket_abl.hip,
 // fold_var.hip): 1 no table fold, 2 no finish, 8 no edge masks, 16 no result
 // slots / stores, 32 no global stores (slots kept), 16384 no line loads,
-// 524288 per-wave s_memrealtime stamps (entry, tables built, work split
-// found, end) and the wave's groups into a.out, 8 words per wave.
+// 524288 per-wave s_memrealtime stamps into a.out, 8 words per wave: entry,
+// tables built, work split found, end, first line arrived, counters arrived,
+// the work of the wave's groups, its share.
 template <int ABL>
 __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   // Result slots per wave (a round of 8 groups leaves in one store; a store
@@ -453,6 +454,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   const uint32_t NG = (uint32_t)(C.pool & ((1ull << kRsGroupBits) - 1u));
   const uint64_t S = C.pool >> kRsGroupBits;
   if (NG == 0) return;  // no packet of >= 2 lines: every wave leaves here (no barrier above)
+  const uint32_t t_ctr = (ABL & 524288) ? (uint32_t)__builtin_amdgcn_s_memrealtime() : 0u;
 #pragma unroll
   for (int k = 0; k < kBq; ++k) brn[k] = 64u * (uint32_t)k + lane < a.nblk ? brn[k] : 0u;
   // This wave's groups: those whose first line lies in its share of the work.
@@ -642,7 +644,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
     a.out[wave8 + 2] = t_split;
     a.out[wave8 + 3] = t_split;
     a.out[wave8 + 4] = work ? q_end - q_begin : 0u;
-    a.out[wave8 + 5] = q_begin;
+    a.out[wave8 + 5] = t_ctr;
   }
   if (!work) return;
 
@@ -736,6 +738,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   // w ^ masked(w) on its own step; a group's last line leaves the next
   // group's first word alone in xr (its chains start from zero).
   uint32_t xr[4] = {ring[0][0], ring[0][1], ring[0][2], ring[0][3]};
+  if ((ABL & 524288) && lane == 0) a.out[wave8 + 4] = (uint32_t)__builtin_amdgcn_s_memrealtime() + (xr[0] == 0x9E3779B9u);
   // Quiet steps.  Per-step cursor control cost the fold 16 SALU and 4.5
   // branches per wave step against 1.7 and 0.1 in the SCK (rocprofv3 --pmc,
   // profiles/r03/pmc_insts.txt).  A run of steps in which neither cursor

@@ -148,18 +148,22 @@ int main(int argc, char **argv) {
       CK(hipMemcpy(st.data(), out, 4 * st.size(), hipMemcpyDeviceToHost));
       uint32_t t0 = st[0];
       for (int w = 0; w < nw; ++w) t0 = (int32_t)(st[8 * w] - t0) < 0 ? st[8 * w] : t0;
-      std::vector<double> en(nw), tb(nw), sp(nw), ent(nw), work;
+      std::vector<double> en(nw), tb(nw), sp(nw), ent(nw), c1(nw), l1(nw), work;
       for (int w = 0; w < nw; ++w) {
         ent[w] = (int32_t)(st[8 * w] - t0) / 100.0;
         tb[w] = (int32_t)(st[8 * w + 1] - t0) / 100.0;
         sp[w] = (int32_t)(st[8 * w + 2] - t0) / 100.0;
         en[w] = (int32_t)(st[8 * w + 3] - t0) / 100.0;
+        l1[w] = (int32_t)(st[8 * w + 4] - t0) / 100.0;
+        c1[w] = (int32_t)(st[8 * w + 5] - t0) / 100.0;
       }
       auto pct = [](std::vector<double> v, double q) { std::sort(v.begin(), v.end()); return v[(size_t)(q * (v.size() - 1))]; };
       printf("  timeline (us from the first entry): entry p50 %.1f max %.1f | tables p50 %.1f max %.1f | split p50 %.1f max %.1f | "
              "end p1 %.1f p10 %.1f p50 %.1f p90 %.1f p99 %.1f max %.1f\n",
              pct(ent, 0.5), pct(ent, 1), pct(tb, 0.5), pct(tb, 1), pct(sp, 0.5), pct(sp, 1), pct(en, 0.01), pct(en, 0.1),
              pct(en, 0.5), pct(en, 0.9), pct(en, 0.99), pct(en, 1));
+      printf("  counters arrived p50 %.1f max %.1f | first line arrived p10 %.1f p50 %.1f max %.1f\n", pct(c1, 0.5),
+             pct(c1, 1), pct(l1, 0.1), pct(l1, 0.5), pct(l1, 1));
       // the work each wave got (its groups' L + group cost, quarter line-steps) against its share
       std::vector<double> ratio(nw);
       for (int w = 0; w < nw; ++w) ratio[w] = st[8 * w + 7] ? (double)st[8 * w + 6] / st[8 * w + 7] : 0.0;
