@@ -77,8 +77,9 @@ def test_framed_ring_same_as_ragged_pipeline(ctx, ctx_env):
 
 
 def test_framed_ring_not_taken(ctx):
-    """Rings the framed kernel does not fold: another slot size, an L3 offset
-    past line 0's masks, a misaligned base, per-packet lengths."""
+    """Rings the framed kernels do not fold: another slot size, an L3 offset
+    past line 0's masks, a misaligned base; per-slot lengths on 2 / 4 KiB
+    slots take the length variant."""
     d = torch.zeros(4096 * 8 + 16, dtype=torch.uint8, device="cuda")
     path = lambda **kw: roce_icrc.kernel_path(kw.pop("base", d), 8, ctx=ctx, **kw)  # noqa: E731
     assert path(stride=4096, l3_offset=14) == "icrc_sck_kernel"
@@ -86,7 +87,11 @@ def test_framed_ring_not_taken(ctx):
     assert path(stride=4096, l3_offset=93).startswith("rsck_bucket")
     assert path(base=d[2:], stride=4096, l3_offset=14).startswith("rsck_bucket")
     lens = torch.full((8,), 1000, dtype=torch.int32, device="cuda")
-    assert path(stride=4096, l3_offset=14, lengths=lens).startswith("rsck_bucket")
+    assert path(stride=4096, l3_offset=14, lengths=lens) == "icrc_sck_kernel+icrc_slot_short_kernel"
+    assert path(stride=1024, l3_offset=14, lengths=lens).startswith("rsck_bucket")
+    assert path(stride=4096, l3_offset=93, lengths=lens).startswith("rsck_bucket")
+    offs = torch.zeros(8, dtype=torch.int64, device="cuda")
+    assert path(stride=4096, l3_offset=14, lengths=lens, offsets=offs).startswith("rsck_bucket")
 
 
 def test_framed_ring_verify_mode(ctx):
@@ -141,3 +146,139 @@ def test_framed_ring_full_size_bit_exact(ctx):
     d.copy_(torch.from_numpy(host))
     ctx.batch_device(d, count, out, stride=stride, l3_offset=l3, verify=True)
     assert int(_host_u32(out).sum()) == count
+
+
+# ---- rings with a length per slot (a NIC's completion byte counts) ----------
+
+def _slot_lens(rng, count, stride, l3, odd=True):
+    """Mostly packets inside their slot; with `odd`, a sprinkling of every
+    case the strided-chain kernel leaves to icrc_slot_short_kernel or to 0:
+    4 <= n < 44, n < 4, n > 65535, packets running past their slot."""
+    lens = rng.integers(44, stride - l3 + 1, size=count).astype(np.uint32)
+    lens[rng.random(count) < 0.2] = stride - l3  # full slots
+    if odd:
+        k = max(count // 40, 1)
+        idx = rng.choice(count, size=4 * k, replace=False)
+        lens[idx[:k]] = rng.integers(4, 44, size=k)
+        lens[idx[k:2 * k]] = rng.integers(0, 4, size=k)
+        lens[idx[2 * k:3 * k]] = 70000
+        lens[idx[3 * k:]] = rng.integers(stride - l3 + 1, stride - l3 + 300, size=k)
+    return lens
+
+
+def _want_slots(frames, lens, stride, count, l3, family="v4"):
+    want = oracle_c.icrc_batch(frames, lengths=np.where(lens > 65535, 0, lens).astype(np.uint32), stride=stride,
+                               count=count, l3_offset=l3, threads=8, family=family)  # (n < 4: 0)
+    return want
+
+
+@pytest.mark.parametrize("stride", [2048, 4096])
+@pytest.mark.parametrize("l3", [0, 14, 18, 92])
+def test_slot_lengths_match_oracle_and_ragged_route(ctx, ctx_env, stride, l3):
+    """2 and 4 KiB slots with per-slot lengths take the strided-chain kernel
+    (each lane stops at its packet's end, x^(-8 tz) removes the zero tail);
+    the packets it leaves (short, past their slot) are computed after it --
+    the same words as the oracle and as the ragged route (RICRC_NO_FRAMED)."""
+    rng = np.random.default_rng(stride + 7 * l3)
+    count = 3001
+    frames = rng.integers(0, 256, size=count * stride + 4096, dtype=np.uint8)  # slack: packets past the last slot
+    lens = _slot_lens(rng, count, stride, l3)
+    d, d_len = _dev(frames), _dev(lens)
+    assert roce_icrc.kernel_path(d, count, stride=stride, lengths=d_len, l3_offset=l3, ctx=ctx) == \
+        "icrc_sck_kernel+icrc_slot_short_kernel"
+    want = _want_slots(frames, lens, stride, count, l3)
+    out = _out(count)
+    ctx.batch_device(d, count, out, stride=stride, lengths=d_len, l3_offset=l3)
+    np.testing.assert_array_equal(_host_u32(out), want)
+    rag = ctx_env(RICRC_NO_FRAMED=1)
+    assert roce_icrc.kernel_path(d, count, stride=stride, lengths=d_len, l3_offset=l3, ctx=rag).startswith("rsck_bucket")
+    out2 = _out(count)
+    rag.batch_device(d, count, out2, stride=stride, lengths=d_len, l3_offset=l3)
+    np.testing.assert_array_equal(_host_u32(out2), want)
+
+
+@pytest.mark.parametrize("count", [1, 7, 9, 65, 8 * 16 * 3 + 5, 70001])
+def test_slot_lengths_tails(ctx, count):
+    for stride in (2048, 4096):
+        rng = np.random.default_rng(count * 3 + stride)
+        frames = rng.integers(0, 256, size=count * stride + 4096, dtype=np.uint8)
+        lens = _slot_lens(rng, count, stride, 14, odd=count > 8)
+        out = _out(count)
+        ctx.batch_device(_dev(frames), count, out, stride=stride, lengths=_dev(lens), l3_offset=14)
+        np.testing.assert_array_equal(_host_u32(out), _want_slots(frames, lens, stride, count, 14))
+
+
+def test_slot_lengths_verify_mode(ctx):
+    count, stride, l3 = 6000, 2048, 14
+    rng = np.random.default_rng(123)
+    frames = rng.integers(0, 256, size=(count, stride), dtype=np.uint8)
+    lens = rng.integers(20, stride - l3 + 1, size=count).astype(np.uint32)  # short ones included
+    icrcs = oracle_c.icrc_batch(frames, lengths=lens, stride=stride, count=count, l3_offset=l3, threads=8)
+    for i in range(count):
+        e = l3 + int(lens[i])
+        frames[i, e - 4:e] = np.frombuffer(int(icrcs[i]).to_bytes(4, "little"), np.uint8)
+    bad = rng.choice(count, size=101, replace=False)
+    frames[bad, l3 + 9] ^= 0x21  # the IP protocol byte: not masked
+    out = _out(count)
+    ctx.batch_device(_dev(frames), count, out, stride=stride, lengths=_dev(lens), l3_offset=l3, verify=True)
+    ok = np.ones(count, np.uint32)
+    ok[bad] = 0
+    np.testing.assert_array_equal(_host_u32(out), ok)
+
+
+@pytest.mark.parametrize("family", ["v6", "auto"])
+def test_slot_lengths_other_families(ctx, family):
+    count, stride, l3 = 3000, 4096, 14
+    rng = np.random.default_rng(5150)
+    frames = rng.integers(0, 256, size=(count, stride), dtype=np.uint8)
+    frames[: count // 2, l3] = 0x60 | (frames[: count // 2, l3] & 15)
+    frames[count // 2:, l3] = 0x45
+    lens = _slot_lens(rng, count, stride, l3, odd=False)
+    out = _out(count)
+    d, d_len = _dev(frames), _dev(lens)
+    assert roce_icrc.kernel_path(d, count, stride=stride, lengths=d_len, l3_offset=l3, ctx=ctx, family=family) == \
+        "icrc_sck_kernel+icrc_slot_short_kernel+family_fix_kernel"
+    ctx.batch_device(d, count, out, stride=stride, lengths=d_len, l3_offset=l3, family=family)
+    np.testing.assert_array_equal(_host_u32(out), _want_slots(frames, lens, stride, count, l3, family))
+
+
+def test_slot_lengths_status_and_framelen(ctx):
+    """The status call over such a ring (strict, frame lengths from the IP
+    header) runs its pre-pass and then the same strided-chain kernel."""
+    import icrc_oracle as O
+
+    count, stride, l3 = 2000, 2048, 14
+    rng = np.random.default_rng(77)
+    frames = rng.integers(0, 256, size=(count, stride), dtype=np.uint8)
+    lens = rng.integers(60, stride - l3 + 1, size=count).astype(np.uint32)
+    for i in range(count):  # IPv4 headers whose total_len is the packet, padded frames beyond it
+        n = int(lens[i]) - (4 if i % 3 == 0 else 0)
+        frames[i, 12:14] = (0x08, 0x00)
+        frames[i, l3] = 0x45
+        frames[i, l3 + 2:l3 + 4] = (n >> 8, n & 255)
+        frames[i, l3 + 9] = 17
+        frames[i, l3 + 22:l3 + 24] = (0x12, 0xB7)  # UDP dport 4791
+    out = torch.full((count,), -1, dtype=torch.int32, device="cuda")
+    st = torch.full((count,), 255, dtype=torch.uint8, device="cuda")
+    ctx.batch_device_st(_dev(frames), count, out, st, stride=stride, lengths=_dev(lens), l3_offset=l3,
+                        strict=True, framelen=True)
+    torch.cuda.synchronize()
+    w_out, w_st = O.status_batch(frames.reshape(-1), stride=stride, lengths=lens, count=count, l3_offset=l3,
+                                 strict=True, framelen=True)
+    np.testing.assert_array_equal(st.cpu().numpy(), np.asarray(w_st, np.uint8))
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), np.asarray(w_out, np.uint32))
+
+
+@pytest.mark.slow
+def test_slot_lengths_full_size_bit_exact(ctx):
+    """1,048,576 slots of 2 KiB holding 1500-byte packets behind a 14-byte
+    Ethernet header (MTU-sized traffic in a NIC's 2 KiB receive buffers),
+    every ICRC against the C oracle on the same device-generated bytes."""
+    count, stride, l3 = 1 << 20, 2048, 14
+    d = torch.empty(count * stride, dtype=torch.uint8, device="cuda")
+    ctx.synth_device(d, SEED ^ 5, 0, count, stride)
+    lens = np.full(count, 1500, np.uint32)
+    out = _out(count)
+    ctx.batch_device(d, count, out, stride=stride, lengths=_dev(lens), l3_offset=l3)
+    np.testing.assert_array_equal(_host_u32(out), oracle_c.icrc_batch(d.cpu().numpy(), lengths=lens, stride=stride,
+                                                                      count=count, l3_offset=l3, threads=16))
