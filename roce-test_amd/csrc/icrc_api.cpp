@@ -358,21 +358,11 @@ bool sck_framed(const Knobs &kn, const uint8_t *base, const uint64_t *off, const
   return !off && !len && l3_offset > 0 && l3_offset <= kSckMaxL3 && (uintptr_t)base % 16 == 0 && !kn.no_sck &&
          !kn.no_framed && (stride == 1024 || stride == 2048 || stride == 4096);
 }
-// A ring of 2 or 4 KiB slots with a length per slot (a NIC's completion byte
-// counts), the L3 packet at l3_offset <= kSckMaxL3 (0 included): the
-// strided-chain kernel over the slots, each lane stopping at its packet's end
-// (FR = 2, icrc_sck.hip).
-bool sck_slots(const Knobs &kn, const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
-               uint32_t l3_offset) {
-  return !off && len && l3_offset <= kSckMaxL3 && (uintptr_t)base % 16 == 0 && !kn.no_sck && !kn.no_framed &&
-         (stride == 2048 || stride == 4096);
-}
 
 int sck_grid(const Dev &d, const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
              uint64_t count, uint32_t l3_offset) {
-  const bool slots = sck_slots(d.knobs, base, off, len, stride, l3_offset);
-  if (l3_offset != 0 && !slots && !sck_framed(d.knobs, base, off, len, stride, l3_offset)) return 0;
-  if (off || (len && !slots) || ((uintptr_t)base % 16) != 0 || d.knobs.no_sck || count == 0) return 0;
+  if (l3_offset != 0 && !sck_framed(d.knobs, base, off, len, stride, l3_offset)) return 0;
+  if (off || len || ((uintptr_t)base % 16) != 0 || d.knobs.no_sck || count == 0) return 0;
   if (stride != 1024 && stride != 2048 && stride != 4096) return 0;
   const uint64_t groups = (count + 7) / 8;
   // One workgroup per CU.  Batches of up to 48 groups per wave (6 GiB of
@@ -452,7 +442,7 @@ int launch_rsck_range(Dev &d, const uint8_t *base, const uint64_t *off, const ui
 // The kernel path of a batch: ONE decision, used by launch_batch_v4 and by
 // ricrc_kernel_path (which bench.py and the tests query, so the labels of a
 // run cannot drift from what ran).
-enum class Path { kSck, kSckFramed, kSckSlots, kQuad, kTsk, kStream, kRagged };
+enum class Path { kSck, kSckFramed, kQuad, kTsk, kStream, kRagged };
 
 // Chunks of a fixed-length batch per lane of the direct streaming kernel
 // (1, 2 or 4), or 0 if its packets are too long for it.
@@ -470,8 +460,6 @@ Path choose_path(const Knobs &kn, const uint8_t *base, const uint64_t *off, cons
   const bool aligned = ((uintptr_t)first % 16 == 0) && (stride % 16 == 0);
   // An Ethernet-framed ring of 1, 2 or 4 KiB slots: the strided-chain kernel over the slots.
   if (sck_framed(kn, base, off, len, stride, l3_offset) && fixed_len >= kMinLen) return Path::kSckFramed;
-  // 2 or 4 KiB slots with per-slot lengths: the same, each packet ending where its length says.
-  if (sck_slots(kn, base, off, len, stride, l3_offset)) return Path::kSckSlots;
   if (off || len || !aligned || fixed_len < kMinLen || fixed_len > kMaxLen || fixed_len % 4 != 0) return Path::kRagged;
   // Back-to-back 1, 2 or 4 KiB packets: the strided-chain kernel (no LDS transpose).
   if (l3_offset == 0 && (uintptr_t)base % 16 == 0 && !kn.no_sck && (stride == 1024 || stride == 2048 || stride == 4096))
@@ -492,7 +480,6 @@ const char *path_kernels(Path p, bool fused) {
   switch (p) {
     case Path::kSck:
     case Path::kSckFramed: return "icrc_sck_kernel";
-    case Path::kSckSlots: return "icrc_sck_kernel+icrc_slot_short_kernel";
     case Path::kQuad: return "icrc_quad_kernel";
     case Path::kTsk: return "icrc_tsk_kernel";
     case Path::kStream: return "icrc_stream_kernel";
@@ -509,7 +496,7 @@ int launch_batch_v4(Dev &d, const uint8_t *base, const uint64_t *off, const uint
   const Path path = choose_path(d.knobs, base, off, len, stride, l3_offset);
   if (path != Path::kRagged) {
     // Back-to-back 1, 2 or 4 KiB packets: the strided-chain kernel (no LDS transpose).
-    if (path == Path::kSck || path == Path::kSckFramed || path == Path::kSckSlots) {
+    if (path == Path::kSck || path == Path::kSckFramed) {
       const int sgrid = sck_grid(d, base, off, len, stride, count, l3_offset);
       SckArgs k{};
       k.family = family;
@@ -518,15 +505,10 @@ int launch_batch_v4(Dev &d, const uint8_t *base, const uint64_t *off, const uint
       k.out = out;
       k.n = (uint32_t)stride;
       k.l3_offset = l3_offset;
-      k.len = path == Path::kSckSlots ? len : nullptr;
-      k.tzb = d.d_tzb;
       k.verify = verify ? 1u : 0u;
       const uint32_t xi = gf_xinv8n(4);
       for (int j = 0; j < 32; ++j) k.XB[j] = gf_mul(xi, 1u << j);
-      // lane slot s's chain 0 -> the end of the packet's last line, less the
-      // 4-byte trailer (a slot-length packet's own end: x^(-8 tz) in the kernel)
-      const uint64_t trailer = path == Path::kSckSlots ? 0 : 4;
-      for (int s = 0; s < 8; ++s) k.QS[s] = gf_xinv8n(16ull * s + trailer);
+      for (int s = 0; s < 8; ++s) k.QS[s] = gf_xinv8n(16ull * s + 4);
       const XcdWeights xw = xcd_weights(d.knobs, stride != 4096 ? 0 : sgrid < d.n_cu ? 25 : 50);
       for (int x = 0; x < 8; ++x) k.xw[x] = xw.w[x];
       k.xcd_k = xcd_start(d.h_xcd);
@@ -886,7 +868,6 @@ const char *ricrc_kernel_path(const ricrc_ctx *ctx, const void *d_base, const ui
   if (flags == RICRC_F_IPV4 || p == Path::kSck) return path_kernels(p, fused);  // the SCK applies every family natively
   switch (p) {  // IPv6 / AUTO: the IPv4-mask kernels, then the linear header fix-up
     case Path::kSckFramed: return "icrc_sck_kernel+family_fix_kernel";
-    case Path::kSckSlots: return "icrc_sck_kernel+icrc_slot_short_kernel+family_fix_kernel";
     case Path::kQuad: return "icrc_quad_kernel+family_fix_kernel";
     case Path::kTsk: return "icrc_tsk_kernel+family_fix_kernel";
     case Path::kStream: return "icrc_stream_kernel+family_fix_kernel";
@@ -907,7 +888,7 @@ int ricrc_launch_info(const ricrc_ctx *ctx, int dev, const void *d_base, const u
   const uint8_t *base = (const uint8_t *)d_base;
   const Path p = choose_path(ctx->knobs, base, d_off, d_len, stride, l3_offset);
   XcdWeights xw{};
-  if (p == Path::kSck || p == Path::kSckFramed || p == Path::kSckSlots) {
+  if (p == Path::kSck || p == Path::kSckFramed) {
     info->grid = (uint32_t)sck_grid(d, base, d_off, d_len, stride, count, l3_offset);
     xw = xcd_weights(ctx->knobs, stride != 4096 ? 0 : (int)info->grid < d.n_cu ? 25 : 50);
   } else if (p == Path::kRagged) {

@@ -60,6 +60,7 @@ constexpr int kRsSmallL = RICRC_RS_SMALL_L;
 constexpr int kRsBigBase = 8;                  // small classes 2..8 (P <= 7 for L <= 3)
 constexpr int kRsClasses = kRsBigBase + 514;   // L <= 513 (n <= 65535, any start offset)
 constexpr int kRsRuns = kRsClasses - kRsBigBase;  // big classes a pass block can hold
+constexpr int kTzWords = 264;                  // tz bases: m = 2 tz + q <= 2 * 127 + 7
 // Bucket layout (block-local, one pass): pass block b lays its packets out
 // by class -- the small ones in a range of the small pool, the big ones as
 // "runs" of whole 8-packet groups in a range of the big pool (each run is one

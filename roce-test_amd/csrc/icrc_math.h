@@ -26,7 +26,6 @@ constexpr uint32_t kOne = 0x80000000u;          // x^0
 constexpr uint32_t kSeed = 0xDEBB20E3u;         // register after 8 x 0xFF from ~0 (shuffle_egress.p4:465)
 constexpr uint32_t kMinLen = 20 + 8 + 12 + 4;   // IPv4 + UDP + BTH + ICRC
 constexpr uint32_t kMaxLen = 65535;             // IPv4 total_len is 16 bits (header.p4:45)
-constexpr int kTzWords = 264;  // x^(-8 tz) basis words, m = 2 tz + q <= 2 * 127 + 7 (strided-chain finishes)
 
 // Invariant-field masks as bits of a 64-bit "byte is forced to 0xFF" map over
 // L3 bytes [0,40): tos 1, ttl 8, IPv4 csum 10-11, UDP csum 26-27, BTH byte 4

@@ -74,31 +74,18 @@ namespace ricrc {
 // (zero before o, the IPv4 masks and the seed from o on) and is precomputed
 // per lane (fr_and / fr_or / fr_xor); the trailer is still the slot's last
 // word.  IPv4 masks only (other families: the linear fix-up after it).
-// FR = 2: the slot's packet is a.len[i] bytes from a.l3_offset (a NIC ring's
-// completion lengths; the offset may be 0).  The lanes of a packet load its
-// lines up to its last line kl only (the buffer range check returns zeros for
-// the rest, no memory traffic), zero the bytes past its covered end
-// E = o + n - 4 in line kl, and stop advancing their chains after it, so the
-// finish holds the packet's register followed by tz = 128 (kl + 1) - E zero
-// bytes, which x^(-8 tz) removes (the ragged fold's distributed multiply,
-// tz < 128).  A packet the kernel does not fold (n outside [44, 65535], or
-// not inside its slot) gets 0; icrc_slot_short_kernel then computes those the
-// ragged path computes (4 <= n < 44; a packet running past its slot).
 template <int L, int ABL, int FAM = kFamV4, int PL = L, int D = 8, int FR = 0>
 __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
   static_assert(L % PL == 0 && PL >= 8, "super-groups: whole packets");
   static_assert(!FR || FAM == kFamV4, "framed rings: IPv4 masks");
-  static_assert(FR != 2 || PL == L, "per-slot lengths: one packet per slot");
   constexpr uint32_t S = L / PL;  // packets per super-packet
   // finish tables | 128 KiB of slice-by-4 tables | result slots per wave
   constexpr uint32_t kSlots = 256;
   constexpr uint32_t kRoundMask = kSlots / 8 - 1;  // groups per round of slots - 1
   constexpr uint32_t kQtStride = 132;  // words per lane slot's nibble table (padded across banks)
   constexpr uint32_t kFin = 128 + 8 * kQtStride + 32;  // finish tables: a multiple of 32 words
-  constexpr uint32_t kTzl = FR == 2 ? (uint32_t)kTzWords : 0u;  // x^(-8 tz) basis words (FR = 2)
-  __shared__ uint32_t lds[kFin + kLdsWords + kTzl + kWaves * kSlots];
+  __shared__ uint32_t lds[kFin + kLdsWords + kWaves * kSlots];
   uint32_t *tab = lds + kFin;  // slice-by-4 tables
-  uint32_t *tzl = lds + kFin + kLdsWords;
   const uint32_t *xtl = lds, *qtl = lds + 128;
 
   // D: lines in flight per wave
@@ -132,34 +119,14 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
   uint32_t qcur = g0 < g1 ? g0 : G;
   uint32_t qnext = qcur < G ? after(qcur) : G;
 
-  // Line `line` of absolute group q (q >= G: no group, the range check reads
-  // zeros; FR = 2: nor does a line past the lane's packet's last line kl).
-  auto load = [&](uint32_t q, uint32_t line, uint32_t kl) -> u32x4 {
+  // Line `line` of absolute group q (q >= G: no group, the range check reads zeros).
+  auto load = [&](uint32_t q, uint32_t line) -> u32x4 {
     if (ABL & 8) return u32x4{q * 977u + line, lane, q, 5u};
     const uint64_t b = (uint64_t)q * GB;
     const uint32_t rem = q < G ? (uint32_t)(total - b < GB ? total - b : GB) : 0u;
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(a.base + (q < G ? b : 0), rem);
-    const uint32_t off = (FR == 2 && line > kl) ? 0x80000000u : vo + 128u * line;
-    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 2));
+    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 128u * line, 0, 2));
   };
-  // FR = 2: the covered end E (slot bytes) of lane group g's packet in group
-  // q, 0 for a packet the kernel does not fold, and its last line
-  const uint32_t o3 = a.l3_offset;
-  auto pk_end = [&](uint32_t q) -> uint32_t {
-    if constexpr (FR != 2) return 0u;
-    const uint64_t i = 8ull * q + (lane >> 3);
-    const uint32_t n = (q < G && i < a.count) ? a.len[i] : 0u;
-    return (n >= kMinLen && n <= kMaxLen && o3 + n <= N) ? o3 + n - 4u : 0u;
-  };
-  auto last_line = [](uint32_t E) -> uint32_t { return E ? (E - 1u) >> 7 : 0u; };
-  uint32_t Ec = 0, En = 0, E2 = 0;  // FR = 2: qcur's, qnext's, and the group after's (in flight)
-  auto after2 = [&]() -> uint32_t { return qnext < G ? after(qnext) : G; };
-  if constexpr (FR == 2) {
-    Ec = pk_end(qcur);
-    En = pk_end(qnext);
-    E2 = pk_end(after2());
-  }
-  uint32_t klc = last_line(Ec), kln = last_line(En);
   // The first D lines are in flight while the workgroup builds its tables
   // (the table load is issued first, so waiting for it leaves them in flight).
   const uint64_t t_start = (ABL & 64) ? __builtin_amdgcn_s_memrealtime() : 0u;
@@ -169,12 +136,9 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
 #pragma unroll
   for (int k = 0; k < D; ++k) {  // in order: the loop's vmcnt waits assume it
     __builtin_amdgcn_sched_barrier(0);
-    ring[k] = load(k < L ? qcur : qnext, (uint32_t)(k % L), k < L ? klc : kln);
+    ring[k] = load(k < L ? qcur : qnext, (uint32_t)(k % L));
   }
   __builtin_amdgcn_sched_barrier(0);
-  if constexpr (FR == 2) {
-    if (threadIdx.x < kTzWords) tzl[threadIdx.x] = a.tzb[threadIdx.x];
-  }
   if (!(ABL & 128)) table_store(tab, tab_v);
   if (!(ABL & 128)) {
     if (threadIdx.x < 128) {  // entry 16 w + v: (nibble v at bits 4w..4w+3) * x^-32
@@ -201,7 +165,7 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
   }
   __syncthreads();
 
-  uint32_t *slots = lds + kFin + kLdsWords + kTzl + wid * kSlots;
+  uint32_t *slots = lds + kFin + kLdsWords + wid * kSlots;
   const LaneTab lt{(lane & 31) << 2, ((lane & 31) << 2) | 0x10000u};
   const uint32_t mw0 = s == 0 ? kMaskW0 : (s == 2 ? kMaskW8 : 0u);  // bytes 1 / 32
   const uint32_t xw0 = s == 0 ? kSeed : 0u;
@@ -230,10 +194,9 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
 
   struct Fin {
     uint32_t r[4];    // chain registers
-    uint32_t tr;      // trailer word (lane s = 7; FR = 2: every lane), for verify
+    uint32_t tr;      // trailer word (lane s = 7), for verify
     uint32_t acc[4];  // multiply accumulators
     uint32_t u;       // Horner value
-    uint32_t tz;      // FR = 2: zero bytes after the packet's covered end; ~0u: not folded
   };
   auto take = [](Fin &f) -> uint32_t {
     const uint32_t v = xor3(f.acc[0], f.acc[1], f.acc[2] ^ f.acc[3]);
@@ -285,25 +248,9 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
   };
   auto fin_store = [&](Fin &f, uint32_t jf) {
     const uint32_t crc = (ABL & 2) ? (f.r[0] ^ f.r[1] ^ f.r[2] ^ f.r[3]) : f.u;
-    uint32_t v = group_xor(crc, 3);
-    uint32_t val;
-    if constexpr (FR == 2) {
-      // x^(-8 tz), distributed: lane s takes bits 4s..4s+3 of v (icrc_rsck.hip's finish)
-      const uint32_t tz = f.tz & 127u;
-      uint32_t bw = tzl[2u * tz + s], p = 0;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)v, (int)(4u * s + t), 1);
-        p = and_xor(m, bw, p);
-        bw = and_xor((uint32_t)((int32_t)bw >> 31), kXInv, bw << 1);
-      }
-      v = group_xor(p, 3);
-      const uint32_t chk = f.tr == ~v ? 1u : 0u;
-      val = f.tz == ~0u ? 0u : __builtin_amdgcn_bitop3_b32(vmask, chk, ~v, 0xCA);
-    } else {
-      const uint32_t chk = group_xor(f.tr, 3) == ~v ? 1u : 0u;
-      val = __builtin_amdgcn_bitop3_b32(vmask, chk, ~v, 0xCA);  // vmask ? chk : ~v, bitwise
-    }
+    const uint32_t v = group_xor(crc, 3);
+    const uint32_t chk = group_xor(f.tr, 3) == ~v ? 1u : 0u;
+    const uint32_t val = __builtin_amdgcn_bitop3_b32(vmask, chk, ~v, 0xCA);  // vmask ? chk : ~v, bitwise
     if (ABL & 16) {
       sink ^= val;
       return;
@@ -317,35 +264,11 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
   constexpr int kStoreStep = PL >= 16 ? 8 : PL - 1;
   auto slice_step = [](int sl) constexpr { return PL >= 16 ? sl : sl * (PL - 1) / 8; };
   static_assert(PL >= 8, "finish needs 8 fold steps");
-  // FR = 2: lane's bytes of the current packet's last line kept (below E)
-  uint32_t em[4] = {~0u, ~0u, ~0u, ~0u};
-  auto end_masks = [&]() {
-    const int r0 = (int)Ec - (int)(128u * klc) - (int)(16u * s);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = r0 - 4 * i;
-      em[i] = r >= 4 ? ~0u : r <= 0 ? 0u : (0xFFFFFFFFu >> (32 - 8 * r));
-    }
-  };
-  if constexpr (FR == 2) end_masks();
-  // FR = 2, verify: the trailer of lane group g's packet in the current group
-  uint32_t trc = 0;
-  auto load_trailer = [&]() {
-    if constexpr (FR == 2) {
-      if (vmask && Ec)  // (vmask: wave-uniform)
-        trc = gload4_unaligned((uintptr_t)(a.base + (8ull * qcur + (lane >> 3)) * N + Ec));
-    }
-  };
-  load_trailer();
   // A packet's first line: the family's invariant masks and the seed.
   auto first_line = [&](u32x4 w, uint32_t (&x)[4]) {
     if constexpr (FR) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) w[i] = ((w[i] & fr_and[i]) | fr_or[i]) ^ fr_xor[i];
-      if constexpr (FR == 2) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) w[i] &= klc == 0u ? em[i] : ~0u;
-      }
     } else if constexpr (FAM == kFamV4) {
       w[0] = or_xor(w[0], mw0, xw0);
       w[2] |= mw2;
@@ -368,7 +291,7 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
   uint32_t j = 0;  // the wave's packets of lane group 0 started so far (sub-groups)
   while (qcur < G) {  // qcur: wave-uniform
     const u32x4 w = ring[0];
-    ring[0] = load(D < L ? qcur : qnext, (uint32_t)(D % L), D < L ? klc : kln);
+    ring[0] = load(D < L ? qcur : qnext, (uint32_t)(D % L));
     uint32_t x[4];
     first_line(w, x);
     uint32_t tr = 0;
@@ -382,13 +305,9 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
       u32x4 wn = {0u, 0u, 0u, 0u}, wf = {0u, 0u, 0u, 0u};
       if (k + 1 < L) {
         const u32x4 nx = ring[(k + 1) % D];
-        ring[(k + 1) % D] = load(k + 1 + D < L ? qcur : qnext, (uint32_t)((k + 1 + D) % L), k + 1 + D < L ? klc : kln);
+        ring[(k + 1) % D] = load(k + 1 + D < L ? qcur : qnext, (uint32_t)((k + 1 + D) % L));
         if (last) {
           wf = nx;  // the next packet's first line (PL < L)
-        } else if constexpr (FR == 2) {
-          wn = nx;  // lines past kl arrive as zeros; line kl keeps the bytes below E
-#pragma unroll
-          for (int i = 0; i < 4; ++i) wn[i] &= (uint32_t)(k + 1) == klc ? em[i] : ~0u;
         } else {
           wn = nx;
           if (kp + 1 == PL - 1) {
@@ -421,21 +340,12 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
         fin_store(pf, j - 1);
         if (j > 0 && ((j - 1) & kRoundMask) == kRoundMask) flush(j);  // wave-uniform: a full round of slots
       }
-      if constexpr (FR == 2) {  // chains stop after the packet's last line (kl: per lane)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const uint32_t nxv = xor3(t[i][0], t[i][1], xor3(t[i][2], t[i][3], wn[i]));
-          x[i] = (uint32_t)k <= klc ? nxv : x[i];
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) x[i] = xor3(t[i][0], t[i][1], xor3(t[i][2], t[i][3], wn[i]));
-      }
+      for (int i = 0; i < 4; ++i) x[i] = xor3(t[i][0], t[i][1], xor3(t[i][2], t[i][3], wn[i]));
       if (last) {  // the packet is folded: hand its chains to the finish
 #pragma unroll
         for (int i = 0; i < 4; ++i) pf.r[i] = x[i];
-        pf.tr = FR == 2 ? trc : tr;
-        if constexpr (FR == 2) pf.tz = Ec ? 128u * (klc + 1u) - Ec : ~0u;
+        pf.tr = tr;
         ++j;
         if (k + 1 < L) {
           first_line(wf, x);
@@ -445,15 +355,6 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
     }
     qcur = qnext;  // advance the group sequence (wave-uniform)
     qnext = qcur < G ? after(qcur) : G;
-    if constexpr (FR == 2) {  // the new group's packets; the one after it requested
-      Ec = En;
-      En = E2;
-      E2 = pk_end(after2());
-      klc = last_line(Ec);
-      kln = last_line(En);
-      end_masks();
-      load_trailer();
-    }
   }
   if (j > 0) {
     __builtin_amdgcn_sched_barrier(0);
@@ -466,28 +367,6 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
   if ((ABL & 64) && lane == 0) {  // diagnostic builds (tools/microbench/sck_tail.hip): start / end times
     a.stamps[2 * wave] = t_start;
     a.stamps[2 * wave + 1] = __builtin_amdgcn_s_memrealtime();
-  }
-}
-
-// FR = 2's packets the strided-chain kernel did not fold (it wrote 0 for
-// them) but the ragged path computes: 4 <= n < 44 (shorter than a RoCEv2
-// header) and packets running past their slot -- a Sarwate loop, as the
-// ragged path's gather does for its unbucketed packets (icrc_rsck.hip
-// icrc_small), so both routes give the same words.  Four slots per thread.
-__global__ __launch_bounds__(kBlock) void icrc_slot_short_kernel(SckArgs a) {
-  const uint64_t i0 = (uint64_t)blockIdx.x * 4u * kBlock + threadIdx.x;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const uint64_t i = i0 + (uint64_t)k * kBlock;
-    if (i >= a.count) break;
-    const uint32_t n = a.len[i];
-    if (n < 4u || n > kMaxLen || (n >= kMinLen && a.l3_offset + n <= a.n)) continue;  // 0, or folded
-    const uint8_t *p = a.base + i * a.n + a.l3_offset;
-    uint32_t r = kSeed;
-    for (uint32_t b = 0; b < n - 4u; ++b) r = g_tab.t[0][(r ^ (p[b] | mask_byte(kFamV4, b))) & 0xFFu] ^ (r >> 8);
-    r = ~r;
-    if (a.verify) r = gload4_unaligned((uintptr_t)(p + n - 4u)) == r ? 1u : 0u;
-    a.out[i] = r;
   }
 }
 
@@ -505,18 +384,9 @@ hipError_t launch_sck_fam(const SckArgs &a, int grid, hipStream_t st) {
   return hipGetLastError();
 }
 
-// Framed rings (a.l3_offset > 0): 1, 2 and 4 KiB slots, IPv4 masks; with
-// per-slot lengths (a.len): 2 and 4 KiB slots, then the short packets.
+// Framed rings (a.l3_offset > 0): 1, 2 and 4 KiB slots, IPv4 masks.
 hipError_t launch_sck_framed(const SckArgs &a, int grid, hipStream_t st) {
   const dim3 g(grid), b(kBlock);
-  if (a.len) {
-    if (a.n == 4096) hipLaunchKernelGGL((icrc_sck_kernel<32, 0, kFamV4, 32, 8, 2>), g, b, 0, st, a);
-    else if (a.n == 2048) hipLaunchKernelGGL((icrc_sck_kernel<16, 0, kFamV4, 16, 8, 2>), g, b, 0, st, a);
-    else return hipErrorInvalidValue;
-    const uint64_t blocks = (a.count + 4ull * kBlock - 1) / (4ull * kBlock);
-    hipLaunchKernelGGL(icrc_slot_short_kernel, dim3((uint32_t)blocks), b, 0, st, a);
-    return hipGetLastError();
-  }
   if (a.n == 4096) hipLaunchKernelGGL((icrc_sck_kernel<32, 0, kFamV4, 32, 8, 1>), g, b, 0, st, a);
   else if (a.n == 2048) hipLaunchKernelGGL((icrc_sck_kernel<16, 0, kFamV4, 16, 8, 1>), g, b, 0, st, a);
   else if (a.n == 1024) hipLaunchKernelGGL((icrc_sck_kernel<32, 0, kFamV4, 8, 8, 1>), g, b, 0, st, a);
@@ -526,7 +396,7 @@ hipError_t launch_sck_framed(const SckArgs &a, int grid, hipStream_t st) {
 
 hipError_t launch_sck(const SckArgs &a, int grid, hipStream_t st) {
   (void)hipGetLastError();  // a stale error of an earlier, unrelated HIP call must not fail this launch
-  if (a.l3_offset != 0 || a.len) {
+  if (a.l3_offset != 0) {
     if (a.family != kFamV4 || a.l3_offset > kSckMaxL3) return hipErrorInvalidValue;
     return launch_sck_framed(a, grid, st);
   }

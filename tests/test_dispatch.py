@@ -37,16 +37,12 @@ def test_framed_rings_full_slots():
 
 
 def test_rings_with_slot_lengths():
-    for slot in (2048, 4096):
-        for l3 in (0, 14, 92):
-            assert path(stride=slot, l3_offset=l3, lengths=LEN) == "icrc_sck_kernel+icrc_slot_short_kernel"
-    assert path(stride=4096, l3_offset=14, lengths=LEN, family="v6") == \
-        "icrc_sck_kernel+icrc_slot_short_kernel+family_fix_kernel"
-    # 1 KiB slots (super-groups), other slot sizes, offsets: the ragged pipeline
-    assert path(stride=1024, l3_offset=14, lengths=LEN).startswith("rsck_bucket")
-    assert path(stride=1536, lengths=LEN).startswith("rsck_bucket")
+    """Per-slot lengths: the ragged pipeline buckets them by line count (a
+    strided-chain variant that stops each lane at its packet's end measured
+    no faster overall; profiles/r05/NOTES.md)."""
+    for slot in (1024, 2048, 4096):
+        assert path(stride=slot, l3_offset=14, lengths=LEN).startswith("rsck_bucket")
     assert path(stride=4096, lengths=LEN, offsets=OFF).startswith("rsck_bucket")
-    assert path(stride=4096, l3_offset=93, lengths=LEN).startswith("rsck_bucket")
 
 
 def test_ragged_batches():

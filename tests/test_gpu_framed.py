@@ -77,9 +77,10 @@ def test_framed_ring_same_as_ragged_pipeline(ctx, ctx_env):
 
 
 def test_framed_ring_not_taken(ctx):
-    """Rings the framed kernels do not fold: another slot size, an L3 offset
-    past line 0's masks, a misaligned base; per-slot lengths on 2 / 4 KiB
-    slots take the length variant."""
+    """Rings the framed kernel does not fold: another slot size, an L3 offset
+    past line 0's masks, a misaligned base, per-slot lengths (the ragged
+    pipeline: a strided-chain variant that stopped each lane at its packet's
+    end measured no faster, profiles/r05/NOTES.md)."""
     d = torch.zeros(4096 * 8 + 16, dtype=torch.uint8, device="cuda")
     path = lambda **kw: roce_icrc.kernel_path(kw.pop("base", d), 8, ctx=ctx, **kw)  # noqa: E731
     assert path(stride=4096, l3_offset=14) == "icrc_sck_kernel"
@@ -87,11 +88,7 @@ def test_framed_ring_not_taken(ctx):
     assert path(stride=4096, l3_offset=93).startswith("rsck_bucket")
     assert path(base=d[2:], stride=4096, l3_offset=14).startswith("rsck_bucket")
     lens = torch.full((8,), 1000, dtype=torch.int32, device="cuda")
-    assert path(stride=4096, l3_offset=14, lengths=lens) == "icrc_sck_kernel+icrc_slot_short_kernel"
-    assert path(stride=1024, l3_offset=14, lengths=lens).startswith("rsck_bucket")
-    assert path(stride=4096, l3_offset=93, lengths=lens).startswith("rsck_bucket")
-    offs = torch.zeros(8, dtype=torch.int64, device="cuda")
-    assert path(stride=4096, l3_offset=14, lengths=lens, offsets=offs).startswith("rsck_bucket")
+    assert path(stride=4096, l3_offset=14, lengths=lens).startswith("rsck_bucket")
 
 
 def test_framed_ring_verify_mode(ctx):
@@ -149,11 +146,13 @@ def test_framed_ring_full_size_bit_exact(ctx):
 
 
 # ---- rings with a length per slot (a NIC's completion byte counts) ----------
+# These take the ragged pipeline (bucketed by line count, so groups of equal
+# length fold without waste).
 
 def _slot_lens(rng, count, stride, l3, odd=True):
     """Mostly packets inside their slot; with `odd`, a sprinkling of every
-    case the strided-chain kernel leaves to icrc_slot_short_kernel or to 0:
-    4 <= n < 44, n < 4, n > 65535, packets running past their slot."""
+    odd case: 4 <= n < 44 (computed by the gather), n < 4 and n > 65535 (0),
+    packets running past their slot (their bytes are read where they lie)."""
     lens = rng.integers(44, stride - l3 + 1, size=count).astype(np.uint32)
     lens[rng.random(count) < 0.2] = stride - l3  # full slots
     if odd:
@@ -174,18 +173,15 @@ def _want_slots(frames, lens, stride, count, l3, family="v4"):
 
 @pytest.mark.parametrize("stride", [2048, 4096])
 @pytest.mark.parametrize("l3", [0, 14, 18, 92])
-def test_slot_lengths_match_oracle_and_ragged_route(ctx, ctx_env, stride, l3):
-    """2 and 4 KiB slots with per-slot lengths take the strided-chain kernel
-    (each lane stops at its packet's end, x^(-8 tz) removes the zero tail);
-    the packets it leaves (short, past their slot) are computed after it --
-    the same words as the oracle and as the ragged route (RICRC_NO_FRAMED)."""
+def test_slot_lengths_match_oracle(ctx, ctx_env, stride, l3):
+    """Slots with per-slot lengths, every odd length case, against the oracle;
+    RICRC_NO_FRAMED changes nothing for them."""
     rng = np.random.default_rng(stride + 7 * l3)
     count = 3001
     frames = rng.integers(0, 256, size=count * stride + 4096, dtype=np.uint8)  # slack: packets past the last slot
     lens = _slot_lens(rng, count, stride, l3)
     d, d_len = _dev(frames), _dev(lens)
-    assert roce_icrc.kernel_path(d, count, stride=stride, lengths=d_len, l3_offset=l3, ctx=ctx) == \
-        "icrc_sck_kernel+icrc_slot_short_kernel"
+    assert roce_icrc.kernel_path(d, count, stride=stride, lengths=d_len, l3_offset=l3, ctx=ctx).startswith("rsck_bucket")
     want = _want_slots(frames, lens, stride, count, l3)
     out = _out(count)
     ctx.batch_device(d, count, out, stride=stride, lengths=d_len, l3_offset=l3)
@@ -236,15 +232,15 @@ def test_slot_lengths_other_families(ctx, family):
     lens = _slot_lens(rng, count, stride, l3, odd=False)
     out = _out(count)
     d, d_len = _dev(frames), _dev(lens)
-    assert roce_icrc.kernel_path(d, count, stride=stride, lengths=d_len, l3_offset=l3, ctx=ctx, family=family) == \
-        "icrc_sck_kernel+icrc_slot_short_kernel+family_fix_kernel"
+    assert roce_icrc.kernel_path(d, count, stride=stride, lengths=d_len, l3_offset=l3, ctx=ctx,
+                                 family=family).endswith("+family_fix_kernel")
     ctx.batch_device(d, count, out, stride=stride, lengths=d_len, l3_offset=l3, family=family)
     np.testing.assert_array_equal(_host_u32(out), _want_slots(frames, lens, stride, count, l3, family))
 
 
 def test_slot_lengths_status_and_framelen(ctx):
     """The status call over such a ring (strict, frame lengths from the IP
-    header) runs its pre-pass and then the same strided-chain kernel."""
+    header)."""
     import icrc_oracle as O
 
     count, stride, l3 = 2000, 2048, 14
