@@ -384,9 +384,9 @@ __device__ __forceinline__ void static_for(F &&f) {
   static_for_impl(f, std::make_integer_sequence<uint32_t, N>{});
 }
 
-// ABL (timing-only ablations, tools/microbench/shard.hip, bucket_abl.hip,
-// fold_var.hip): 1 no table fold, 2 no finish, 8 no edge masks, 16 no result
-// slots / stores, 32 no global stores (slots kept), 16384 no line loads,
+// ABL (timing-only ablations, tools/microbench/shard.hip, bucket_abl.hip):
+// 1 no table fold, 2 no finish, 8 no edge masks, 16 no result
+// slots / stores, 16384 no line loads,
 // 524288 per-wave s_memrealtime stamps into a.out, 8 words per wave: entry,
 // tables built, work split found, end, first line arrived, counters arrived,
 // the work of the wave's groups, its share.
@@ -395,14 +395,13 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   // Result slots per wave (a round of 8 groups leaves in one store; a store
   // holds back every load queued behind it in vmcnt until its write is
   // acknowledged: the stores cost ~4 % of the fold on a 4 GiB mix, the same
-  // for rounds of 8 or 16 groups and 4- or 8-byte stores, rsck_abl.hip).
+  // for rounds of 8 or 16 groups and 4- or 8-byte stores, profiles/r02/rsck_abl_*.txt).
   constexpr uint32_t kSlots = 64, kRound = kSlots / 8;
   constexpr uint32_t kBlk = 128;                          // words per descriptor block (8 groups x 8 x 8 B)
   constexpr uint32_t kWaveWords = kSlots + 2 * kBlk + 64;  // slots | 2-block ring | 8-group info FIFO
   // lines in flight per wave: 6 (with the quiet blocks below, 8 lines in
   // flight left no registers for them: 128 VGPRs and spills; fold of a
-  // C4-shaped 5.3 GiB batch 953 -> 930 us, tools/microbench/fold_var.hip,
-  // profiles/r03/fold_var.txt)
+  // C4-shaped 5.3 GiB batch 953 -> 930 us, profiles/r03/fold_var.txt)
   constexpr int D = 6;
   // Finish tables first, so every lookup's constant part fits a ds_read's
   // 16-bit offset: x^-32 nibble table (128 words) | x^(-128 s) nibble tables
@@ -655,10 +654,6 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
     const uint32_t valid = 8u * (q_stop - round_q0);
     const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.bres + 8ull * round_q0, 4u * valid);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the slot writes have landed
-    if (ABL & 32) {
-      sink ^= slots[lane];  // keep the slot reads
-      return;
-    }
     // slots past `valid` fall outside the range check
     __builtin_amdgcn_raw_buffer_store_b32(slots[lane], ro, 4u * lane, 0, 16);
   };
@@ -748,7 +743,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   // the run that follows it (quiet); a block of D steps that starts with a
   // run of >= D ahead is D quiet steps with no per-step test at all, and
   // shorter runs go through full steps (a per-step quiet / full branch
-  // measured 17 % slower: 1115 against 953 us, tools/microbench/fold_var.hip).
+  // measured 17 % slower: 1115 against 953 us, profiles/r03/fold_var.txt).
   uint32_t quiet = 0;
   auto quiet_step = [&](int u, uint32_t ahead) {  // ahead: lines the load cursor is past ld_k within the block
     const u32x4 wn = ring[(u + 1) % D];
@@ -867,7 +862,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   else
     fold_loop(std::false_type{});
   if (!(ABL & 16) && q_end != round_q0) flush(q_end);
-  if ((ABL & 48) && sink == 0x12345678u) a.bres[0] = sink;
+  if ((ABL & 16) && sink == 0x12345678u) a.bres[0] = sink;
   if ((ABL & 524288) && lane == 0) {  // timing only: end stamp after every store has left
     __builtin_amdgcn_s_waitcnt(0);
     a.out[wave8 + 3] = (uint32_t)__builtin_amdgcn_s_memrealtime();

@@ -4,8 +4,7 @@
 //   loads + classify | + LDS ranking atomics | + scan and pool reservation |
 //   full | full without pos_of stores | full without descriptor stores,
 // next to a plain copy of the same descriptor bytes (12 B in, 12 B out per
-// packet) and the other passes of the pipeline, and the fold's per-wave
-// timeline (s_memrealtime stamps) over a group-cost sweep.  Build:
+// packet) and the other passes of the pipeline over a group-cost sweep.  Build:
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 bucket_abl.hip -o bucket_abl
 #include "../../roce-test_amd/csrc/icrc_kernels.hip"
 #include "../../roce-test_amd/csrc/icrc_rsck.hip"
@@ -126,46 +125,16 @@ int main(int argc, char **argv) {
       CK(hipDeviceSynchronize());
       char nm[96]; snprintf(nm, sizeof nm, "fold (icrc_rsck_kernel), group cost %u", gc);
       rep(nm, timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10));
-    {  // per-wave timeline of the fold (stamps at 100 MHz into out: start, end, groups, first group)
-      const int nw = grid * kWaves;
-      std::vector<uint32_t> st(4 * nw);
-      for (int it = 0; it < 3; ++it) hipLaunchKernelGGL((icrc_rsck_kernel<8192>), dim3(grid), dim3(kBlock), 0, 0, a);
-      CK(hipDeviceSynchronize());
-      CK(hipMemcpy(st.data(), out, 4 * st.size(), hipMemcpyDeviceToHost));
-      uint32_t t0 = st[0];
-      for (int w = 0; w < nw; ++w) t0 = (int32_t)(st[4 * w] - t0) < 0 ? st[4 * w] : t0;
-      std::vector<double> st_us(nw), en_us(nw);
-      for (int w = 0; w < nw; ++w) { st_us[w] = (int32_t)(st[4 * w] - t0) / 100.0; en_us[w] = (int32_t)(st[4 * w + 1] - t0) / 100.0; }
-      auto pct = [](std::vector<double> v, double q) { std::sort(v.begin(), v.end()); return v[(size_t)(q * (v.size() - 1))]; };
-      printf("fold timeline (us from the first wave's start): start p50 %.1f max %.1f | end p1 %.1f p10 %.1f p50 %.1f p90 %.1f p99 %.1f max %.1f\n",
-             pct(st_us, 0.5), pct(st_us, 1.0), pct(en_us, 0.01), pct(en_us, 0.1), pct(en_us, 0.5), pct(en_us, 0.9), pct(en_us, 0.99), pct(en_us, 1.0));
-      // the slowest waves: their groups and first group's L
-      std::vector<int> idx(nw); for (int w = 0; w < nw; ++w) idx[w] = w;
-      std::sort(idx.begin(), idx.end(), [&](int x, int y) { return en_us[x] > en_us[y]; });
-      for (int k = 0; k < 4; ++k) { const int w = idx[k]; printf("  slow wave %d (block %d): end %.1f us, %u groups from %u\n", w, w / kWaves, en_us[w], st[4 * w + 2], st[4 * w + 3]); }
-      for (int k = nw - 3; k < nw; ++k) { const int w = idx[k]; printf("  fast wave %d (block %d): end %.1f us, %u groups from %u\n", w, w / kWaves, en_us[w], st[4 * w + 2], st[4 * w + 3]); }
-      // mean end per block-local wave slot and per XCD (blockIdx % 8)
-      double xcd[8] = {0}; int nx[8] = {0};
-      for (int w = 0; w < nw; ++w) { xcd[(w / kWaves) % 8] += en_us[w]; nx[(w / kWaves) % 8]++; }
-      printf("  mean end by blockIdx %% 8:"); for (int x = 0; x < 8; ++x) printf(" %.1f", xcd[x] / nx[x]); printf("\n");
-      double sl[16] = {0};
-      for (int w = 0; w < nw; ++w) sl[w % kWaves] += en_us[w] / grid;
-      printf("  mean end by wave slot in its block:"); for (int x = 0; x < kWaves; ++x) printf(" %.0f", sl[x]); printf("\n");
-    }
     };
     if (r == 0) for (uint32_t gc : {4u, 8u, 16u}) fold_report(gc);
     fold_report(kRsGroupCost);
-    for (int ab = 0; ab < 3; ++ab) {  // same-process A/B of the edge paths, alternating
-      rep("fold A/B: last lines through the head-line path (before)", timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<32768>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10));
-      rep("fold A/B: cheap last-line path (product)", timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10));
-    }
+    // (the fold's per-wave timeline: tools/microbench/shard.hip, ABL 524288)
     rep("fold, no line loads (compute only)", timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<16384>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10));
-    rep("fold, no line loads, head-line path for every edge", timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<16384 | 32768>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10));
     rep("fold, memory path (no table fold, no finish)", timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<3>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10));
     rep("fold, no edge masks", timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<8>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10));
     rep("fold, no finish", timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<2>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10));
     rep("fold, memory path, no edges, no stores", timeit([&] { hipLaunchKernelGGL((icrc_rsck_kernel<3 | 8 | 16>), dim3(grid), dim3(kBlock), 0, 0, a); }, 10));
-    rep("one-line (icrc_rsmall_kernel)", timeit([&] { hipLaunchKernelGGL((icrc_rsmall_kernel<kSmallRounds>), dim3(grid), dim3(kBlock), 0, 0, a); }, 20));
+    rep("one-line (icrc_rsmall_kernel)", timeit([&] { hipLaunchKernelGGL((icrc_rsmall_kernel), dim3(grid), dim3(kBlock), 0, 0, a); }, 20));
     {  // the gather zeroes the counters: restore them before each timed launch
       RsCounters *saved; CK(hipMalloc(&saved, sizeof(RsCounters)));
       CK(hipMemcpy(saved, a.ctr, sizeof(RsCounters), hipMemcpyDeviceToDevice));
@@ -174,7 +143,7 @@ int main(int argc, char **argv) {
       for (int it = 0; it < 23; ++it) {
         CK(hipMemcpyAsync(a.ctr, saved, sizeof(RsCounters), hipMemcpyDeviceToDevice, 0));
         CK(hipEventRecord(e0, 0));
-        hipLaunchKernelGGL(rsck_gather<kPassUnroll>, dim3(pgrid), dim3(kPassBlock), 0, 0, a);
+        hipLaunchKernelGGL((rsck_gather<kPassUnroll, false>), dim3(pgrid), dim3(kPassBlock), 0, 0, a);
         CK(hipEventRecord(e1, 0)); CK(hipEventSynchronize(e1));
         float ms; CK(hipEventElapsedTime(&ms, e0, e1));
         if (it >= 3) tot += ms;
