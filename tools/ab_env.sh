@@ -1,6 +1,6 @@
 #!/bin/bash
 # Same-box A/B of bench configurations that differ only in environment
-# knobs, alternating runs:  MODES="base RICRC_RS_OVERLAP=1" ARGS="--mix" bash tools/ab_env.sh
+# knobs, alternating runs:  MODES="base RICRC_NO_GATHER_SPLIT=1" ARGS="--mix --count 524288" bash tools/ab_env.sh
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/${TAG:-ab_env}; mkdir -p $O
