@@ -79,9 +79,38 @@ __device__ __forceinline__ void table_store_at(uint32_t *lds, uint32_t idx, uint
   for (int k = 0; k < 8; ++k) dst[k] = v4{v, v, v, v};
 }
 __device__ __forceinline__ void table_store(uint32_t *lds, uint32_t v) { table_store_at(lds, threadIdx.x, v); }
+
+// The whole 128 KiB set in address order: store k of thread t writes the 16
+// bytes at 16 (1024 k + t), so a wave's store is one contiguous KiB and no
+// two lanes share a bank; the thread loads the 8 entries it stores (from a
+// 4 KiB table the L2 holds).  table_store -- one entry per thread, its 32
+// copies as 128 contiguous bytes -- put every lane of a wave on the same four
+// banks: the build took ~5 us at the start of the ragged fold
+// (tools/microbench/shard.hip, profiles/r05/NOTES.md).  load early, write
+// late: the loads' latency hides behind a kernel's first global loads.
+struct TableRegs {
+  uint32_t v[8];
+};
+__device__ __forceinline__ TableRegs table_load(const SliceTables<4> &tab) {
+  static_assert(kBlock == 1024 && kLdsWords == 8 * 4 * kBlock, "8 stores of 16 bytes per thread");
+  TableRegs r;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint32_t w = 4u * (1024u * k + threadIdx.x);  // the word the store starts at
+    const uint32_t region = w >> 14, e = (w >> 6) & 255u, half = (w >> 5) & 1u;
+    const uint32_t t = region ? (half ? 0u : 1u) : (half ? 2u : 3u);  // T3 T2 | T1 T0 (table_store_at)
+    r.v[k] = tab.t[t][e];
+  }
+  return r;
+}
+__device__ __forceinline__ void table_write(uint32_t *lds, const TableRegs &r) {
+  typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+  v4 *dst = reinterpret_cast<v4 *>(lds);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) dst[1024u * k + threadIdx.x] = v4{r.v[k], r.v[k], r.v[k], r.v[k]};
+}
 __device__ __forceinline__ void fill_tables(uint32_t *lds, const SliceTables<4> &tab = g_tab) {
-  static_assert(kBlock == 1024, "one table entry per thread");
-  table_store(lds, table_entry(tab));
+  table_write(lds, table_load(tab));
 }
 
 struct LaneTab {

@@ -41,7 +41,7 @@ __global__ __launch_bounds__(kBlock) void icrc_stream_kernel(StreamArgs a) {
   // The table entry's load goes first; with PIPE the wave's first packets are
   // requested before the tables are built (waiting for the table load leaves
   // them in flight), so the fill no longer sits in front of the first loads.
-  const uint32_t tab_v = table_entry(g_tab);
+  const TableRegs tab_v = table_load(g_tab);
 
   constexpr int NP = 4 * CPL;   // 16-byte pieces per lane
   constexpr int NW = 16 * CPL;  // words per lane
@@ -134,7 +134,7 @@ __global__ __launch_bounds__(kBlock) void icrc_stream_kernel(StreamArgs a) {
     load(it < last ? it : last, cur);      // unconditional: no branch join
     load(it + nwaves < last ? it + nwaves : last, nxt);
     __builtin_amdgcn_sched_barrier(0);
-    table_store(lds, tab_v);
+    table_write(lds, tab_v);
     __syncthreads();
     for (; it < a.n_iters; it += nwaves) {
       // Unconditional prefetch (past the end it re-loads the last step) so the
@@ -150,7 +150,7 @@ __global__ __launch_bounds__(kBlock) void icrc_stream_kernel(StreamArgs a) {
       }
     }
   } else {
-    table_store(lds, tab_v);
+    table_write(lds, tab_v);
     __syncthreads();
     for (uint64_t it = wave; it < a.n_iters; it += nwaves) {
       u32x4 v[NP];
@@ -554,6 +554,10 @@ __global__ __launch_bounds__(64 * W) void icrc_quad_kernel(QuadArgs a) {
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(a.base + (s < s_end ? b : 0), rem);
     return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 1024u * k + 16u * lane, 0, 2));
   };
+  // the table entries first (the ring's loads are then waited for in order
+  // behind them, not before them)
+  TableRegs tv{};
+  if constexpr (W == kWaves) tv = table_load(g_tab);
   u32x4 ring[4 * R];
 #pragma unroll
   for (int u = 0; u < 4 * R; ++u) {
@@ -561,8 +565,12 @@ __global__ __launch_bounds__(64 * W) void icrc_quad_kernel(QuadArgs a) {
     ring[u] = load(s_begin + (uint32_t)(u >> 2), (uint32_t)(u & 3));
   }
   __builtin_amdgcn_sched_barrier(0);
+  if constexpr (W == kWaves) {
+    table_write(tab, tv);
+  } else {
 #pragma unroll
-  for (uint32_t t = threadIdx.x; t < 1024u; t += 64u * W) table_store_at(tab, t, crc_table_value(t));
+    for (uint32_t t = threadIdx.x; t < 1024u; t += 64u * W) table_store_at(tab, t, crc_table_value(t));
+  }
   __syncthreads();
 
   const LaneTab lt{(lane & 31) << 2, ((lane & 31) << 2) | 0x10000u};

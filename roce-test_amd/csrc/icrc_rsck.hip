@@ -388,8 +388,9 @@ __device__ __forceinline__ void static_for(F &&f) {
 // 1 no table fold, 2 no finish, 8 no edge masks, 16 no result
 // slots / stores, 16384 no line loads,
 // 524288 per-wave s_memrealtime stamps into a.out, 8 words per wave: entry,
-// tables built, work split found, end, first line arrived, counters arrived,
-// the work of the wave's groups, its share.
+// tables built (the barrier), work split found, end, first line arrived,
+// counters arrived, table build's own instructions done, the work of the
+// wave's groups.
 template <int ABL>
 __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   // Result slots per wave (a round of 8 groups leaves in one store; a store
@@ -433,7 +434,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   // barrier: at C4's 8-GPU shard its waves found their share 11 us after
   // entry at the median, 27 us at worst, tools/microbench/shard.hip,
   // profiles/r05/s1_mb_shard_baseline.txt.)
-  const uint32_t tab_v = table_entry(g_tab128);
+  const TableRegs tab_v = table_load(g_tab128);
   const uint32_t tz_v = a.tzb[threadIdx.x < kTzWords ? threadIdx.x : 0];
   const RsCounters C = *a.ctr;
   constexpr int kBq = kPassBlocks / 64;  // pass blocks per lane
@@ -486,7 +487,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   const RsRun *R0 = a.runs + (uint64_t)b0 * kRsRuns, *R1 = a.runs + (uint64_t)b1 * kRsRuns;
   RsRun Q0 = R0[lane < n0 ? lane : 0u], Q1 = R1[lane < n1 ? lane : 0u];  // both in flight during the table build
 
-  table_store(tab, tab_v);
+  table_write(tab, tab_v);
   if (threadIdx.x < kTzWords) tzl[threadIdx.x] = tz_v;
   {  // entry (s, w, v) = (nibble v at bits 4w..4w+3) * x^(-128 s), where bit
      // j of a value stands for QS[s] x^(31 - j)
@@ -547,6 +548,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
     }
     return NG;  // (not reached: x < S lies in a run)
   };
+  const uint32_t t_tb = (ABL & 524288) ? (uint32_t)__builtin_amdgcn_s_memrealtime() : 0u;
   const uint32_t q_begin = group_at(x0, n0, R0, Q0), q_end = group_at(x1, n1, R1, Q1);
   const uint32_t t_split = (ABL & 524288) ? (uint32_t)__builtin_amdgcn_s_memrealtime() : 0u;
   const bool work = q_begin < q_end;  // wave-uniform
@@ -866,8 +868,8 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   if ((ABL & 524288) && lane == 0) {  // timing only: end stamp after every store has left
     __builtin_amdgcn_s_waitcnt(0);
     a.out[wave8 + 3] = (uint32_t)__builtin_amdgcn_s_memrealtime();
-    a.out[wave8 + 6] = done_work;
-    a.out[wave8 + 7] = (uint32_t)(x1 - x0);
+    a.out[wave8 + 6] = t_tb;
+    a.out[wave8 + 7] = done_work;
   }
 }
 
@@ -1134,7 +1136,8 @@ __global__ __launch_bounds__(kPassBlock) void rsck_gather(RsckArgs a) {
   constexpr bool split = SPLIT;  // a grid of 2 x nblk
   const bool small_side = split && blockIdx.x >= a.nblk;
   const uint32_t pb = small_side ? blockIdx.x - a.nblk : blockIdx.x;
-  const uint32_t tab_v = SMALL ? table_entry(g_tab) : 0u;
+  TableRegs tab_v{};
+  if (SMALL) tab_v = table_load(g_tab);
   // The counters are dead now (the bucket pass and both folds have read
   // them): zero them for the next call on this workspace.
   if (blockIdx.x == 0 && threadIdx.x == 0) *a.ctr = RsCounters{};
@@ -1148,7 +1151,7 @@ __global__ __launch_bounds__(kPassBlock) void rsck_gather(RsckArgs a) {
   // other loads; C4's shard blocks hold ~1 K one-line packets, one per thread
   auto small_desc = [&](uint32_t j) { return a.desc[B.small0 + (j < B.small ? j : B.small - 1u)]; };
   auto small_fold = [&](const RsDesc &sd0, auto store) {  // fold the block's small range, store(j, icrc)
-    table_store(tab, tab_v);
+    table_write(tab, tab_v);
     __syncthreads();
 #pragma unroll 1
     for (uint32_t j0 = 0; j0 < B.small; j0 += blockDim.x) {

@@ -131,7 +131,7 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
   // (the table load is issued first, so waiting for it leaves them in flight).
   const uint64_t t_start = (ABL & 64) ? __builtin_amdgcn_s_memrealtime() : 0u;
   xcd_record(a.xcd_rec);
-  const uint32_t tab_v = table_entry(g_tab128);
+  const TableRegs tab_v = table_load(g_tab128);
   u32x4 ring[D];
 #pragma unroll
   for (int k = 0; k < D; ++k) {  // in order: the loop's vmcnt waits assume it
@@ -139,7 +139,7 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
     ring[k] = load(k < L ? qcur : qnext, (uint32_t)(k % L));
   }
   __builtin_amdgcn_sched_barrier(0);
-  if (!(ABL & 128)) table_store(tab, tab_v);
+  if (!(ABL & 128)) table_write(tab, tab_v);
   if (!(ABL & 128)) {
     if (threadIdx.x < 128) {  // entry 16 w + v: (nibble v at bits 4w..4w+3) * x^-32
       const uint32_t w = threadIdx.x >> 4, v = threadIdx.x & 15u;

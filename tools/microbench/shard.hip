@@ -164,20 +164,9 @@ int main(int argc, char **argv) {
              pct(en, 0.5), pct(en, 0.9), pct(en, 0.99), pct(en, 1));
       printf("  counters arrived p50 %.1f max %.1f | first line arrived p10 %.1f p50 %.1f max %.1f\n", pct(c1, 0.5),
              pct(c1, 1), pct(l1, 0.1), pct(l1, 0.5), pct(l1, 1));
-      // the work each wave got (its groups' L + group cost, quarter line-steps) against its share
-      std::vector<double> ratio(nw);
-      for (int w = 0; w < nw; ++w) ratio[w] = st[8 * w + 7] ? (double)st[8 * w + 6] / st[8 * w + 7] : 0.0;
-      printf("  work / share: p1 %.3f p10 %.3f p50 %.3f p90 %.3f p99 %.3f max %.3f\n", pct(ratio, 0.01), pct(ratio, 0.1),
-             pct(ratio, 0.5), pct(ratio, 0.9), pct(ratio, 0.99), pct(ratio, 1));
-      // end time by work ratio decile: does the extra work explain the late waves?
-      std::vector<int> idx(nw); for (int w = 0; w < nw; ++w) idx[w] = w;
-      std::sort(idx.begin(), idx.end(), [&](int u, int v) { return ratio[u] < ratio[v]; });
-      printf("  mean end by work-ratio decile:");
-      for (int d = 0; d < 10; ++d) {
-        double m = 0; int n = 0;
-        for (int j = d * nw / 10; j < (d + 1) * nw / 10; ++j) { m += en[idx[j]]; ++n; }
-        printf(" %.1f", m / n);
-      }
+      std::vector<double> tb2(nw);
+      for (int w = 0; w < nw; ++w) tb2[w] = (int32_t)(st[8 * w + 6] - t0) / 100.0;
+      printf("  table build's instructions done p50 %.1f max %.1f", pct(tb2, 0.5), pct(tb2, 1));
       printf("\n  mean end by wave slot:");
       for (int sl = 0; sl < kWaves; ++sl) { double m = 0; for (int b = 0; b < grid; ++b) m += en[b * kWaves + sl]; printf(" %.0f", m / grid); }
       printf("\n");
