@@ -109,6 +109,7 @@ struct Dev {
   Knobs knobs;
   hipStream_t stream = nullptr;
   uint32_t *d_tzb = nullptr;   // [kTzWords]: basis words 4q of x^(-8 tz) at 2 tz + q (ragged strided-chain path)
+  uint32_t *d_fin = nullptr;   // [kFinSck + kFinFold]: the strided-chain kernels' finish tables (build_fin_tables)
   uint32_t *d_x8n = nullptr;   // x^(8 k), k < 65536 (incremental repair)
   // Pinned word where workgroup 0 of the SCK records its XCD; the next SCK
   // launch passes it as xcd_k (xcd_share in icrc_device.h).  (The ragged
@@ -216,6 +217,11 @@ int init_dev(Dev &d) {
   (void)hipGetLastError();
   HIP_TRY(hipMalloc(&d.d_tzb, tzb.size() * sizeof(uint32_t)));
   HIP_TRY(hipMemcpy(d.d_tzb, tzb.data(), tzb.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  std::vector<uint32_t> fin(kFinSck + kFinFold);
+  build_fin_tables(fin.data(), false);
+  build_fin_tables(fin.data() + kFinSck, true);
+  HIP_TRY(hipMalloc(&d.d_fin, fin.size() * sizeof(uint32_t)));
+  HIP_TRY(hipMemcpy(d.d_fin, fin.data(), fin.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
   std::vector<uint32_t> x8n(65536);  // x^(8 k): a repair's shift over the bytes after the rewrite
   uint32_t w = kOne;
   for (size_t k = 0; k < x8n.size(); ++k) {
@@ -269,6 +275,7 @@ void free_dev(Dev &d) {
   for (hipEvent_t e : d.pt_ev) (void)hipEventDestroy(e);
   d.pt_ev.clear();
   (void)hipFree(d.d_tzb);
+  (void)hipFree(d.d_fin);
   (void)hipFree(d.d_x8n);
   if (d.h_xcd) (void)hipDeviceSynchronize(), (void)hipHostFree(d.h_xcd);  // no kernel may still record into it
   if (d.stream) (void)hipStreamDestroy(d.stream);
@@ -401,22 +408,7 @@ int launch_rsck_range(Dev &d, const uint8_t *base, const uint64_t *off, const ui
   k.no_split = d.knobs.no_gather_split ? 1u : 0u;
   k.out = out;
   k.tzb = d.d_tzb;
-  // GF(2) constants of the fold's finish (the same for every call)
-  static const RsckArgs kc = [] {
-    RsckArgs c{};
-    const uint32_t xi = gf_xinv8n(4), xi2 = gf_xinv8n(8), xi3 = gf_xinv8n(12);
-    for (int j = 0; j < 32; ++j) {
-      c.XB[j] = gf_mul(xi, 1u << j);
-      c.XB2[j] = gf_mul(xi2, 1u << j);
-      c.XB3[j] = gf_mul(xi3, 1u << j);
-    }
-    for (int s = 0; s < 8; ++s) c.QS[s] = gf_xinv8n(16ull * s);
-    return c;
-  }();
-  memcpy(k.XB, kc.XB, sizeof k.XB);
-  memcpy(k.XB2, kc.XB2, sizeof k.XB2);
-  memcpy(k.XB3, kc.XB3, sizeof k.XB3);
-  memcpy(k.QS, kc.QS, sizeof k.QS);
+  k.fin = d.d_fin + kFinSck;  // the fold's finish tables
   Dev::Ws *ws = nullptr;
   const int wrc = ragged_ws(d, st, rs_workspace_bytes(count), &ws);
   if (wrc) return wrc;
@@ -506,9 +498,7 @@ int launch_batch_v4(Dev &d, const uint8_t *base, const uint64_t *off, const uint
       k.n = (uint32_t)stride;
       k.l3_offset = l3_offset;
       k.verify = verify ? 1u : 0u;
-      const uint32_t xi = gf_xinv8n(4);
-      for (int j = 0; j < 32; ++j) k.XB[j] = gf_mul(xi, 1u << j);
-      for (int s = 0; s < 8; ++s) k.QS[s] = gf_xinv8n(16ull * s + 4);
+      k.fin = d.d_fin;  // the SCK's finish tables
       const XcdWeights xw = xcd_weights(d.knobs, stride != 4096 ? 0 : sgrid < d.n_cu ? 25 : 50);
       for (int x = 0; x < 8; ++x) k.xw[x] = xw.w[x];
       k.xcd_k = xcd_start(d.h_xcd);

@@ -112,10 +112,7 @@ struct RsckArgs {
   uint32_t small_cap;   // count rounded up to 8
   uint32_t nblk;        // pass blocks of this call (launch_rsck sets it)
   const uint32_t *tzb;  // [kTzWords]: entry m = x^(31 - 4 m), i.e. basis word 4 q of x^(-8 tz) at m = 2 tz + q
-  uint32_t XB[32];      // basis of x^-32
-  uint32_t XB2[32];     // basis of x^-64
-  uint32_t XB3[32];     // basis of x^-96
-  uint32_t QS[8];       // x^(-8*16 s): lane slot s -> line start
+  const uint32_t *fin;  // the fold's finish tables (kFinFold words, icrc_math.h build_fin_tables), the context's
 };
 // Work of a group in line-steps: its L lines plus the per-group finish
 // (GF(2) multiplies through nibble tables, reductions, descriptor and slot

@@ -148,6 +148,46 @@ constexpr SliceTables<N> make_tables() {
   return s;
 }
 
+// The strided-chain kernels' finish tables, the first words of their LDS
+// (built on the host once per device, loaded by every workgroup): nibble
+// tables of GF(2) constants -- entry 16 w + v = (nibble v at bits
+// 4w..4w+3) * K, bit j of a value standing for x^(31 - j).
+//   [0, 128)               K = x^-32
+//   [128 + 132 s, + 128)   K = QS[s] = x^(-8 (16 s + trail)), lane slot s (rows padded to 132 words)
+//   kFinSck = 1216 words (the SCK: trail = 4, its trailer word); the ragged
+//   fold (trail = 0) adds [1184, 1216) its head masks (or, xor of word k)
+//   and [1216, 1344), [1344, 1472) K = x^-64, x^-96: kFinFold = 1472.
+constexpr uint32_t kFinQtStride = 132;
+constexpr uint32_t kFinSck = 128 + 8 * kFinQtStride + 32;
+constexpr uint32_t kFinFold = 128 + 8 * kFinQtStride + 32 + 256;
+inline uint32_t nibble_entry(uint32_t K, uint32_t w, uint32_t v) {
+  uint32_t e = 0;
+  for (int b = 0; b < 4; ++b)
+    if ((v >> b) & 1u) e ^= gf_mul(K, 1u << (4 * w + b));
+  return e;
+}
+inline void build_fin_tables(uint32_t *t, bool fold) {
+  const uint32_t n = fold ? kFinFold : kFinSck;
+  for (uint32_t i = 0; i < n; ++i) t[i] = 0;
+  uint32_t qs[8];
+  for (uint32_t s = 0; s < 8; ++s) qs[s] = gf_xinv8n(16ull * s + (fold ? 0 : 4));
+  const uint32_t x32 = gf_xinv8n(4), x64 = gf_xinv8n(8), x96 = gf_xinv8n(12);
+  for (uint32_t w = 0; w < 8; ++w)
+    for (uint32_t v = 0; v < 16; ++v) {
+      t[16 * w + v] = nibble_entry(x32, w, v);
+      for (uint32_t s = 0; s < 8; ++s) t[128 + kFinQtStride * s + 16 * w + v] = nibble_entry(qs[s], w, v);
+      if (fold) {
+        t[1216 + 16 * w + v] = nibble_entry(x64, w, v);
+        t[1344 + 16 * w + v] = nibble_entry(x96, w, v);
+      }
+    }
+  if (fold)
+    for (uint32_t k = 0; k < 16; ++k) {  // word k of the header (rel = 4k): IPv4 invariant fields -> 0xFF, the seed at 0
+      t[1184 + 2 * k] = k == 0 ? kMaskW0 : k == 2 ? kMaskW2 : k == 6 ? kMaskW6 : k == 8 ? kMaskW8 : 0u;
+      t[1184 + 2 * k + 1] = k == 0 ? kSeed : 0u;
+    }
+}
+
 static_assert(gf_mul(kXInv, kOne >> 1) == kOne, "x * x^-1 must be 1");
 static_assert(make_tables<1>().t[0][1] == 0x77073096u, "Sarwate table");
 

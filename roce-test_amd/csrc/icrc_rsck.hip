@@ -410,7 +410,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   // the banks) | head masks (32 words) | x^-64, x^-96 nibble tables (2 x 128
   // words) | 128 KiB slice-by-4 tables | 1 KiB tz bases | 1.5 KiB per wave =
   // 157.7 KiB.
-  constexpr uint32_t kQtStride = 132, kSmallWords = 128 + 8 * kQtStride + 32 + 256;  // 1472: a multiple of 32 words
+  constexpr uint32_t kQtStride = kFinQtStride, kSmallWords = kFinFold;  // 1472 (build_fin_tables): a multiple of 32 words
   __shared__ uint32_t lds[kSmallWords + kLdsWords + kTzWords + kWaves * kWaveWords];
   uint32_t *xtl = lds;
   uint32_t *qtl = lds + 128;
@@ -435,6 +435,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   // entry at the median, 27 us at worst, tools/microbench/shard.hip,
   // profiles/r05/s1_mb_shard_baseline.txt.)
   const TableRegs tab_v = table_load(g_tab128);
+  const uint32_t fin0 = a.fin[threadIdx.x], fin1 = a.fin[threadIdx.x + 1024u < kSmallWords ? threadIdx.x + 1024u : 0u];
   const uint32_t tz_v = a.tzb[threadIdx.x < kTzWords ? threadIdx.x : 0];
   const RsCounters C = *a.ctr;
   constexpr int kBq = kPassBlocks / 64;  // pass blocks per lane
@@ -485,46 +486,17 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   const uint32_t b0 = block_of(x0), b1 = block_of(x1);
   const uint32_t n0 = runs_of(b0), n1 = runs_of(b1);
   const RsRun *R0 = a.runs + (uint64_t)b0 * kRsRuns, *R1 = a.runs + (uint64_t)b1 * kRsRuns;
-  RsRun Q0 = R0[lane < n0 ? lane : 0u], Q1 = R1[lane < n1 ? lane : 0u];  // both in flight during the table build
+  RsRun Q0 = R0[lane < n0 ? lane : 0u], Q1 = R1[lane < n1 ? lane : 0u];  // in flight during the table stores
 
+  // The tables' words arrived with the counters: LDS stores only.  (Built
+  // in the kernel from kernel-argument bases, the finish tables indexed the
+  // arguments by lane -- vector loads from the argument segment, each
+  // waiting for every load before it, the runs included: ~4 us of the
+  // fold's start at C4's 8-GPU shard, profiles/r05/NOTES.md.)
   table_write(tab, tab_v);
   if (threadIdx.x < kTzWords) tzl[threadIdx.x] = tz_v;
-  {  // entry (s, w, v) = (nibble v at bits 4w..4w+3) * x^(-128 s), where bit
-     // j of a value stands for QS[s] x^(31 - j)
-    const uint32_t bs = threadIdx.x >> 7, w = (threadIdx.x >> 4) & 7u, v = threadIdx.x & 15u;
-    uint32_t p = a.QS[0];
-#pragma unroll
-    for (int k = 1; k < 8; ++k) p = bs == (uint32_t)k ? a.QS[k] : p;
-    for (uint32_t t = 0; t < 28u - 4u * w; ++t) p = gf_mulx(p);  // bit 4w + 3
-    uint32_t e = 0;
-#pragma unroll
-    for (int b = 3; b >= 0; --b) {
-      e ^= ((v >> b) & 1u) ? p : 0u;
-      p = gf_mulx(p);
-    }
-    qtl[bs * kQtStride + 16u * w + v] = e;
-  }
-  if (threadIdx.x < 16) {  // word k of the header (rel = 4k): IPv4 invariant fields -> 0xFF, the seed at 0
-    const uint32_t k = threadIdx.x;
-    const uint32_t orm = k == 0 ? kMaskW0 : k == 2 ? kMaskW2 : k == 6 ? kMaskW6 : k == 8 ? kMaskW8 : 0u;
-    etl[2 * k] = orm;
-    etl[2 * k + 1] = k == 0 ? kSeed : 0u;
-  }
-  if (threadIdx.x < 128) {  // entry 16 w + v: (nibble v at bits 4w..4w+3) * x^-32
-    const uint32_t w = threadIdx.x >> 4, v = threadIdx.x & 15u;
-    uint32_t t = 0;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) t ^= ((v >> b) & 1u) ? a.XB[4 * w + b] : 0u;
-    xtl[threadIdx.x] = t;
-    uint32_t t2 = 0, t3 = 0;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      t2 ^= ((v >> b) & 1u) ? a.XB2[4 * w + b] : 0u;
-      t3 ^= ((v >> b) & 1u) ? a.XB3[4 * w + b] : 0u;
-    }
-    x2tl[threadIdx.x] = t2;
-    x3tl[threadIdx.x] = t3;
-  }
+  lds[threadIdx.x] = fin0;  // the finish tables, built by the host (icrc_math.h build_fin_tables)
+  if (threadIdx.x + 1024u < kSmallWords) lds[threadIdx.x + 1024u] = fin1;
 
   // First group whose work starts at or after x: the run of the pass block
   // (b, its nr runs at R; Q = this lane's run of the first 64) holding x.

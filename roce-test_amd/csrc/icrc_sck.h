@@ -16,8 +16,7 @@ struct SckArgs {
   uint32_t n;        // == stride (the slot, for a framed ring)
   uint32_t l3_offset;  // 0, or a framed ring's L3 offset in each slot (<= kSckMaxL3)
   uint32_t verify;
-  uint32_t XB[32];   // basis of x^-32 (Horner step between a lane's chains)
-  uint32_t QS[8];    // x^(-32 (4 s + 1)): lane slot s's chain 0 -> packet end
+  const uint32_t *fin;  // finish tables (kFinSck words: x^-32 and x^(-32 (4 s + 1)) nibble tables), the context's
   uint32_t family;   // kFamV4 / kFamV6 / kFamAuto: masks applied by the kernel itself
   uint64_t *stamps;  // diagnostic builds only (tools/microbench); null in the product
   // Per-wave share of the groups by XCD (xcd_share): a wave on XCD x takes

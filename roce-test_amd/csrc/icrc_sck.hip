@@ -82,8 +82,8 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
   // finish tables | 128 KiB of slice-by-4 tables | result slots per wave
   constexpr uint32_t kSlots = 256;
   constexpr uint32_t kRoundMask = kSlots / 8 - 1;  // groups per round of slots - 1
-  constexpr uint32_t kQtStride = 132;  // words per lane slot's nibble table (padded across banks)
-  constexpr uint32_t kFin = 128 + 8 * kQtStride + 32;  // finish tables: a multiple of 32 words
+  constexpr uint32_t kQtStride = kFinQtStride;  // words per lane slot's nibble table (padded across banks)
+  constexpr uint32_t kFin = kFinSck;             // finish tables (build_fin_tables): a multiple of 32 words
   __shared__ uint32_t lds[kFin + kLdsWords + kWaves * kSlots];
   uint32_t *tab = lds + kFin;  // slice-by-4 tables
   const uint32_t *xtl = lds, *qtl = lds + 128;
@@ -132,6 +132,8 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
   const uint64_t t_start = (ABL & 64) ? __builtin_amdgcn_s_memrealtime() : 0u;
   xcd_record(a.xcd_rec);
   const TableRegs tab_v = table_load(g_tab128);
+  // the finish tables, built by the host (icrc_math.h build_fin_tables): two words per thread
+  const uint32_t fin0 = a.fin[threadIdx.x], fin1 = a.fin[threadIdx.x + 1024u < kFin ? threadIdx.x + 1024u : 0u];
   u32x4 ring[D];
 #pragma unroll
   for (int k = 0; k < D; ++k) {  // in order: the loop's vmcnt waits assume it
@@ -141,27 +143,8 @@ __global__ __launch_bounds__(kBlock) void icrc_sck_kernel(SckArgs a) {
   __builtin_amdgcn_sched_barrier(0);
   if (!(ABL & 128)) table_write(tab, tab_v);
   if (!(ABL & 128)) {
-    if (threadIdx.x < 128) {  // entry 16 w + v: (nibble v at bits 4w..4w+3) * x^-32
-      const uint32_t w = threadIdx.x >> 4, v = threadIdx.x & 15u;
-      uint32_t t = 0;
-#pragma unroll
-      for (int b = 0; b < 4; ++b) t ^= ((v >> b) & 1u) ? a.XB[4 * w + b] : 0u;
-      lds[threadIdx.x] = t;
-    }
-    // slot s, entry 16 w + v: (nibble v at bits 4w..4w+3) * QS[s], where bit
-    // j of a value stands for x^(31 - j)
-    const uint32_t bs = threadIdx.x >> 7, w = (threadIdx.x >> 4) & 7u, v = threadIdx.x & 15u;
-    uint32_t p = a.QS[0];
-#pragma unroll
-    for (int k = 1; k < 8; ++k) p = bs == (uint32_t)k ? a.QS[k] : p;
-    for (uint32_t t = 0; t < 28u - 4u * w; ++t) p = gf_mulx(p);  // bit 4w + 3
-    uint32_t e = 0;
-#pragma unroll
-    for (int b = 3; b >= 0; --b) {
-      e ^= ((v >> b) & 1u) ? p : 0u;
-      p = gf_mulx(p);
-    }
-    lds[128 + bs * kQtStride + 16u * w + v] = e;
+    lds[threadIdx.x] = fin0;
+    if (threadIdx.x + 1024u < kFin) lds[threadIdx.x + 1024u] = fin1;
   }
   __syncthreads();
 

@@ -26,6 +26,7 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 aos_probe.hip -o aos_probe
 #include "../../roce-test_amd/csrc/icrc_kernels.hip"
 #include "../../roce-test_amd/csrc/icrc_rsck.hip"
+#include "mb_fin.h"
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -223,8 +224,7 @@ int main() {
   RsckArgs a{};
   a.base = buf; a.off = d_off; a.len = d_len; a.count = count;
   a.out = out; a.tzb = tzb; a.group_cost = kRsGroupCost;
-  for (int j = 0; j < 32; ++j) { a.XB[j] = 0x85EBCA6Bu * (j + 3); a.XB2[j] = 0x27D4EB2Fu * (j + 5); a.XB3[j] = 0x165667B1u * (j + 7); }
-  for (int s = 0; s < 8; ++s) a.QS[s] = 0x9E3779B9u * (s + 1);
+  a.fin = mb_fin();
   void *ws; CK(hipMalloc(&ws, rs_workspace_bytes(count)));
   CK(rs_zero_counters(ws, 0));
   rs_bind_workspace(a, ws);

@@ -11,6 +11,7 @@
 #include "../../roce-test_amd/csrc/icrc_kernels.hip"
 #include "../../roce-test_amd/csrc/icrc_sck.hip"
 #include <stdint.h>
+#include "mb_fin.h"
 #include <stdio.h>
 #include <stdlib.h>
 using namespace ricrc;
@@ -71,8 +72,7 @@ int main() {
   }
   uint32_t *out; CK(hipMalloc(&out, 4ull << 22));
   SckArgs sa{}; sa.base = buf; sa.count = bytes / 4096; sa.out = out; sa.n = 4096;
-  for (int j = 0; j < 32; ++j) sa.XB[j] = 0x85EBCA6Bu * (j + 3);
-  for (int k = 0; k < 8; ++k) sa.QS[k] = 0x9E3779B9u * (k + 1);
+  sa.fin = mb_fin();
   uint32_t *sink; CK(hipMalloc(&sink, 4096));
   const int grid = 256;
   if (getenv("SIZE_SWEEP")) {  // SCK at 256 vs 240 workgroups by batch size (4 KiB packets), alternating

@@ -10,6 +10,7 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 overlap.hip -o overlap
 #include "../../roce-test_amd/csrc/icrc_kernels.hip"
 #include "../../roce-test_amd/csrc/icrc_sck.hip"
+#include "mb_fin.h"
 #include <stdio.h>
 #include <stdlib.h>
 using namespace ricrc;
@@ -50,8 +51,7 @@ int main() {
   const uint64_t gbytes = 28ull << 20;  // what one GPU receives of an 8-GPU all-gather of 4 MB shards
   u32x4 *gsrc, *gdst; CK(hipMalloc(&gsrc, gbytes)); CK(hipMalloc(&gdst, gbytes)); CK(hipMemset(gsrc, 1, gbytes));
   SckArgs sa{}; sa.base = buf; sa.count = count; sa.out = out; sa.n = 4096;
-  for (int j = 0; j < 32; ++j) sa.XB[j] = 0x85EBCA6Bu * (j + 3);
-  for (int k = 0; k < 8; ++k) sa.QS[k] = 0x9E3779B9u * (k + 1);
+  sa.fin = mb_fin();
   hipStream_t sk, sg; CK(hipStreamCreateWithFlags(&sk, hipStreamNonBlocking)); CK(hipStreamCreateWithFlags(&sg, hipStreamNonBlocking));
   const int K = 20;
   hipEvent_t done[K], e0, e1;

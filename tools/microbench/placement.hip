@@ -14,6 +14,7 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 placement.hip -o placement
 #include "../../roce-test_amd/csrc/icrc_kernels.hip"
 #include "../../roce-test_amd/csrc/icrc_rsck.hip"
+#include "mb_fin.h"
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -60,8 +61,7 @@ int main() {
     RsckArgs a{};
     a.base = buf[c]; a.off = d_off; a.len = d_len; a.count = count;
     a.out = out; a.tzb = tzb; a.group_cost = kRsGroupCost;
-    for (int j = 0; j < 32; ++j) { a.XB[j] = 0x85EBCA6Bu * (j + 3); a.XB2[j] = 0x27D4EB2Fu * (j + 5); a.XB3[j] = 0x165667B1u * (j + 7); }
-    for (int s = 0; s < 8; ++s) a.QS[s] = 0x9E3779B9u * (s + 1);
+    a.fin = mb_fin();
     rs_bind_workspace(a, ws[w]);
     for (int k = 0; k < 4; ++k) sum[k] = 0;
     for (int r = 0; r < 3 + reps; ++r) {
@@ -100,8 +100,7 @@ int main() {
     RsckArgs a{};
     a.base = buf[c]; a.off = d_off; a.len = d_len; a.count = count;
     a.out = out; a.tzb = tzb; a.group_cost = kRsGroupCost;
-    for (int j = 0; j < 32; ++j) { a.XB[j] = 0x85EBCA6Bu * (j + 3); a.XB2[j] = 0x27D4EB2Fu * (j + 5); a.XB3[j] = 0x165667B1u * (j + 7); }
-    for (int s = 0; s < 8; ++s) a.QS[s] = 0x9E3779B9u * (s + 1);
+    a.fin = mb_fin();
     rs_bind_workspace(a, ws[c]);
     for (int r = 0; r < 3; ++r) CK(launch_rsck(a, grid, 0, 0, nullptr));  // warm, back to back
     for (int i = 0; i < kB2B; ++i) CK(launch_rsck(a, grid, 0, 0, &bev[5 * i]));

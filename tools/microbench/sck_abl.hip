@@ -3,6 +3,7 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 sck_abl.hip -o sck_abl
 #include "../../roce-test_amd/csrc/icrc_kernels.hip"
 #include "../../roce-test_amd/csrc/icrc_sck.hip"
+#include "mb_fin.h"
 #include <stdio.h>
 #include <stdlib.h>
 using namespace ricrc;
@@ -26,8 +27,7 @@ int main(int argc, char **argv) {
   }
   hipDeviceProp_t p; CK(hipGetDeviceProperties(&p, 0));
   SckArgs a{}; a.base = buf; a.count = count; a.out = out; a.n = n;
-  for (int j = 0; j < 32; ++j) a.XB[j] = 0x85EBCA6Bu * (j + 3);
-  for (int s = 0; s < 8; ++s) a.QS[s] = 0x9E3779B9u * (s + 1);
+  a.fin = mb_fin();
   const int grid = p.multiProcessorCount;
   auto rep = [&](const char *nm, float ms) { printf("%-36s %7.3f ms  %7.1f GB/s\n", nm, ms, 4294967296.0 / (ms * 1e-3) / 1e9); };
   const bool quick = argc > 1 && argv[1][0] == 'x';  // "xt": finish-table variants only

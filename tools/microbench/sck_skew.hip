@@ -10,6 +10,7 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 sck_skew.hip -o sck_skew
 #include "../../roce-test_amd/csrc/icrc_kernels.hip"
 #include "../../roce-test_amd/csrc/icrc_sck.hip"
+#include "mb_fin.h"
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -40,8 +41,7 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&stamps, 16ull * waves));
   SckArgs a{};
   a.base = buf; a.count = count; a.out = out; a.n = (uint32_t)n;
-  for (int j = 0; j < 32; ++j) a.XB[j] = 0x85EBCA6Bu * (j + 3);
-  for (int s = 0; s < 8; ++s) a.QS[s] = 0x9E3779B9u * (s + 1);
+  a.fin = mb_fin();
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   auto launch = [&](const SckArgs &k, bool stamp) {
     if (L == 32) {

@@ -4,6 +4,7 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 sck_tail.hip -o sck_tail
 #include "../../roce-test_amd/csrc/icrc_kernels.hip"
 #include "../../roce-test_amd/csrc/icrc_sck.hip"
+#include "mb_fin.h"
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -16,8 +17,7 @@ template <int L>
 void run(uint8_t *buf, uint32_t *out, uint64_t count, int grid) {
   SckArgs a{};
   a.base = buf; a.count = count; a.out = out; a.n = 128 * L;
-  for (int j = 0; j < 32; ++j) a.XB[j] = 0x85EBCA6Bu * (j + 3);
-  for (int s = 0; s < 8; ++s) a.QS[s] = 0x9E3779B9u * (s + 1);
+  a.fin = mb_fin();
   const int waves = grid * kWaves;
   CK(hipMalloc(&a.stamps, 16ull * waves));
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));

@@ -7,6 +7,7 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 sck_xw.hip -o sck_xw
 #include "../../roce-test_amd/csrc/icrc_kernels.hip"
 #include "../../roce-test_amd/csrc/icrc_sck.hip"
+#include "mb_fin.h"
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -32,8 +33,7 @@ int main() {
   CK(hipMalloc(&stamps, 16ull * waves));
   SckArgs a{};
   a.base = buf; a.count = count; a.out = out; a.n = 4096; a.xcd_rec = d_rec;
-  for (int j = 0; j < 32; ++j) a.XB[j] = 0x85EBCA6Bu * (j + 3);
-  for (int s = 0; s < 8; ++s) a.QS[s] = 0x9E3779B9u * (s + 1);
+  a.fin = mb_fin();
   const uint32_t W[][8] = {
       {0, 0, 0, 0, 0, 0, 0, 0},
       {1025, 975, 1025, 975, 1025, 975, 1025, 975},

@@ -8,6 +8,7 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 xcd_fix.hip -o xcd_fix
 #include "../../roce-test_amd/csrc/icrc_kernels.hip"
 #include "../../roce-test_amd/csrc/icrc_sck.hip"
+#include "mb_fin.h"
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -40,8 +41,7 @@ int main(int argc, char **argv) {
   const int grid = 240;
   SckArgs a{};
   a.base = buf; a.count = count; a.out = out; a.n = 4096; a.xcd_rec = d_rec;
-  for (int j = 0; j < 32; ++j) a.XB[j] = 0x85EBCA6Bu * (j + 3);
-  for (int s = 0; s < 8; ++s) a.QS[s] = 0x9E3779B9u * (s + 1);
+  a.fin = mb_fin();
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   hipStream_t st = 0;
   auto run = [&](int v) {  // 0 equal shares, 1 skew assuming k = 0, 2 skew with the recorded k

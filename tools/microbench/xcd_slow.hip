@@ -10,6 +10,7 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 xcd_slow.hip -o xcd_slow
 #include "../../roce-test_amd/csrc/icrc_kernels.hip"
 #include "../../roce-test_amd/csrc/icrc_sck.hip"
+#include "mb_fin.h"
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -43,8 +44,7 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&stamps, 16ull * waves));
   SckArgs a{};
   a.base = buf; a.count = count; a.out = out; a.n = 4096; a.stamps = stamps;
-  for (int j = 0; j < 32; ++j) a.XB[j] = 0x85EBCA6Bu * (j + 3);
-  for (int s = 0; s < 8; ++s) a.QS[s] = 0x9E3779B9u * (s + 1);
+  a.fin = mb_fin();
   std::vector<uint32_t> hx(512);
   std::vector<uint64_t> st(2 * waves);
   uint32_t *sink; CK(hipMalloc(&sink, 4096));
