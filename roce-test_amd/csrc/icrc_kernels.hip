@@ -61,9 +61,13 @@ __global__ __launch_bounds__(kBlock) void icrc_stream_kernel(StreamArgs a) {
   const uint32_t m6 = first ? kMaskW6 : 0u, m8 = first ? kMaskW8 : 0u;
   const uint32_t x0 = first ? kSeed : 0u;
 
+  // The lane's re-alignment constant, requested with the table entries; its
+  // basis is built once the first steps' loads are in flight (an argument
+  // indexed by lane is a vector load: waiting for it before the prefetch
+  // would put a round trip in front of the first loads).
+  const uint32_t Kc = lane_valid ? a.K[c] : 0u;
   uint32_t Q[32];
   const bool multi = a.P > 1;
-  if (multi) make_basis(lane_valid ? a.K[c] : 0u, Q);
 
   const uint64_t wave = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
   const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
@@ -134,6 +138,7 @@ __global__ __launch_bounds__(kBlock) void icrc_stream_kernel(StreamArgs a) {
     load(it < last ? it : last, cur);      // unconditional: no branch join
     load(it + nwaves < last ? it + nwaves : last, nxt);
     __builtin_amdgcn_sched_barrier(0);
+    if (multi) make_basis(Kc, Q);
     table_write(lds, tab_v);
     __syncthreads();
     for (; it < a.n_iters; it += nwaves) {
@@ -150,6 +155,7 @@ __global__ __launch_bounds__(kBlock) void icrc_stream_kernel(StreamArgs a) {
       }
     }
   } else {
+    if (multi) make_basis(Kc, Q);
     table_write(lds, tab_v);
     __syncthreads();
     for (uint64_t it = wave; it < a.n_iters; it += nwaves) {
