@@ -220,7 +220,7 @@ KERNEL_ROLES = {
     "icrc_tsk_kernel": "transposed streaming ICRC kernel",
     "icrc_stream_kernel": "direct streaming ICRC kernel",
     "rsck_bucket": "bucket pass",
-    "icrc_rsck_kernel": "strided-chain fold of packets of >= 2 lines",
+    "icrc_rsck_kernel": "strided-chain fold (8 packets of >= 2 lines a group; one-line packets one a lane)",
     "icrc_rsmall_kernel": "one-line packets",
     "rsck_gather": "gather",
     "family_fix_kernel": "address-family fix-up",
@@ -239,13 +239,9 @@ def kernel_path(args, base=0x100000, count=1):
 
 
 def kernel_label(args, base=0x100000, count=1):
-    """Human-readable label of kernel_path: 'role (kernel) -> role (kernel)'.
-    Batches of up to 1 M packets fold their one-line packets in the gather
-    pass (no icrc_rsmall_kernel launch)."""
+    """Human-readable label of kernel_path: 'role (kernel) -> role (kernel)'."""
     ks = kernel_path(args, base, count).split("+")
-    role = lambda k: ("gather, folding the one-line packets" if k == "rsck_gather" and "rsck_bucket" in ks  # noqa: E731
-                      and "icrc_rsmall_kernel" not in ks else KERNEL_ROLES.get(k, k))
-    return " -> ".join(f"{role(k)} ({k})" for k in ks)
+    return " -> ".join(f"{KERNEL_ROLES.get(k, k)} ({k})" for k in ks)
 
 
 def rccl_version():

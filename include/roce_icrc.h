@@ -422,7 +422,8 @@ typedef struct {
   uint32_t start_xcd;      /* recorded by the last strided-chain kernel on this device */
   uint32_t pass_grid;      /* ragged: bucket / gather blocks (0 otherwise) */
   uint32_t pass_unroll;    /* ragged: packets per thread of those passes */
-  uint32_t fused;          /* ragged: 1 if the gather folds the one-line packets */
+  uint32_t one_line;       /* ragged: who folds the one-line packets: 2 the fold (default), 1 the gather,
+                              0 a separate one-line kernel (RICRC_ONE_LINE_IN_GATHER selects 1 or 0) */
   uint32_t gather_grid;    /* ragged: gather blocks (2 x pass_grid when one-line sides run beside them) */
 } ricrc_launch_info_t;
 int ricrc_launch_info(const ricrc_ctx *ctx, int dev, const void *d_base, const uint64_t *d_off,

@@ -53,6 +53,8 @@ struct Knobs {
   int sck_grid = 0;        // RICRC_SCK_GRID: cap the strided-chain grid (tests: many groups per wave)
   int rsck_grid = 0;       // RICRC_RSCK_GRID: cap the ragged fold grid (tests)
   uint32_t gcost = 0;      // RICRC_RS_GCOST: the ragged fold's per-group cost, quarter lines (0: kRsGroupCost)
+  bool one_line_in_gather = false;  // RICRC_ONE_LINE_IN_GATHER: the gather / a one-line kernel folds the one-line packets
+  int small_slots = -1;    // RICRC_SMALL_SLOTS: wave slots taking the fold's one-line packets (-1: kRsSmallSlots)
   int pass_grid = 0;       // RICRC_RS_PASS_GRID: cap the ragged bucket / gather pass grid (schedule studies)
   bool pass_times = false; // RICRC_PASS_TIMES: timing events between the ragged passes (ricrc_pass_times)
   long fail_chunk = -1;    // RICRC_FAIL_CHUNK: the next ricrc_batch_host fails after queueing chunk k (tests; once)
@@ -403,6 +405,8 @@ int launch_rsck_range(Dev &d, const uint8_t *base, const uint64_t *off, const ui
   k.l3_offset = l3_offset;
   k.verify = verify ? 1u : 0u;
   k.group_cost = d.knobs.gcost ? d.knobs.gcost : kRsGroupCost;
+  k.small_in_fold = d.knobs.one_line_in_gather ? 0u : 1u;
+  k.small_slots = d.knobs.small_slots < 0 ? kRsSmallSlots : (uint32_t)d.knobs.small_slots;
   const XcdWeights xw = xcd_weights(d.knobs, 40);
   for (int x = 0; x < 8; ++x) k.xw[x] = xw.w[x];
   k.no_split = d.knobs.no_gather_split ? 1u : 0u;
@@ -468,14 +472,14 @@ Path choose_path(const Knobs &kn, const uint8_t *base, const uint64_t *off, cons
   return cpl ? Path::kStream : Path::kRagged;
 }
 
-const char *path_kernels(Path p, bool fused) {
+const char *path_kernels(Path p, bool one_line_pass) {
   switch (p) {
     case Path::kSck:
     case Path::kSckFramed: return "icrc_sck_kernel";
     case Path::kQuad: return "icrc_quad_kernel";
     case Path::kTsk: return "icrc_tsk_kernel";
     case Path::kStream: return "icrc_stream_kernel";
-    default: return fused ? "rsck_bucket+icrc_rsck_kernel+rsck_gather" : "rsck_bucket+icrc_rsck_kernel+icrc_rsmall_kernel+rsck_gather";
+    default: return one_line_pass ? "rsck_bucket+icrc_rsck_kernel+icrc_rsmall_kernel+rsck_gather" : "rsck_bucket+icrc_rsck_kernel+rsck_gather";
   }
 }
 
@@ -735,6 +739,8 @@ Knobs read_knobs() {
   k.sck_grid = (int)std::max(0L, num("RICRC_SCK_GRID", 0));
   k.rsck_grid = (int)std::max(0L, num("RICRC_RSCK_GRID", 0));
   k.gcost = (uint32_t)std::min(1024L, std::max(0L, num("RICRC_RS_GCOST", 0)));  // the packed work counter's range
+  k.one_line_in_gather = getenv("RICRC_ONE_LINE_IN_GATHER") != nullptr;
+  k.small_slots = (int)std::min(16L, std::max(-1L, num("RICRC_SMALL_SLOTS", -1)));  // (16 waves a workgroup)
   k.pass_grid = (int)std::max(0L, num("RICRC_RS_PASS_GRID", 0));
   k.pass_times = getenv("RICRC_PASS_TIMES") != nullptr;
   k.fail_chunk = num("RICRC_FAIL_CHUNK", -1);
@@ -853,17 +859,18 @@ const char *ricrc_kernel_path(const ricrc_ctx *ctx, const void *d_base, const ui
   if ((!d_off && stride == 0) || (!d_len && stride <= l3_offset)) return nullptr;
   const Knobs kn = ctx ? ctx->knobs : Knobs{};
   const Path p = choose_path(kn, (const uint8_t *)d_base, d_off, d_len, stride, l3_offset);
-  // the ragged pipeline's first range (launch_batch_v4 cuts at kRsChunk) decides the one-line pass
-  const bool fused = rs_fused(std::min<uint64_t>(count, kRsChunk), kn.pass_grid);
-  if (flags == RICRC_F_IPV4 || p == Path::kSck) return path_kernels(p, fused);  // the SCK applies every family natively
+  // the ragged pipeline's first range (launch_batch_v4 cuts at kRsChunk) decides the one-line pass:
+  // none when the fold (the default) or the gather (a fused pass shape) folds those packets
+  const bool one_line_pass = kn.one_line_in_gather && !rs_fused(std::min<uint64_t>(count, kRsChunk), kn.pass_grid);
+  if (flags == RICRC_F_IPV4 || p == Path::kSck) return path_kernels(p, one_line_pass);  // the SCK applies every family natively
   switch (p) {  // IPv6 / AUTO: the IPv4-mask kernels, then the linear header fix-up
     case Path::kSckFramed: return "icrc_sck_kernel+family_fix_kernel";
     case Path::kQuad: return "icrc_quad_kernel+family_fix_kernel";
     case Path::kTsk: return "icrc_tsk_kernel+family_fix_kernel";
     case Path::kStream: return "icrc_stream_kernel+family_fix_kernel";
     default:
-      return fused ? "rsck_bucket+icrc_rsck_kernel+rsck_gather+family_fix_kernel"
-                   : "rsck_bucket+icrc_rsck_kernel+icrc_rsmall_kernel+rsck_gather+family_fix_kernel";
+      return one_line_pass ? "rsck_bucket+icrc_rsck_kernel+icrc_rsmall_kernel+rsck_gather+family_fix_kernel"
+                           : "rsck_bucket+icrc_rsck_kernel+rsck_gather+family_fix_kernel";
   }
 }
 
@@ -890,8 +897,9 @@ int ricrc_launch_info(const ricrc_ctx *ctx, int dev, const void *d_base, const u
                  &gg);
     info->pass_grid = (uint32_t)pg;
     info->pass_unroll = (uint32_t)pu;
-    info->fused = fused ? 1u : 0u;
-    info->gather_grid = (uint32_t)gg;
+    const bool in_fold = !d.knobs.one_line_in_gather;
+    info->one_line = in_fold ? 2u : fused ? 1u : 0u;
+    info->gather_grid = in_fold ? (uint32_t)pg : (uint32_t)gg;
   }
   for (int x = 0; x < 8; ++x) info->xcd_weights[x] = xw.w[x];
   return 0;

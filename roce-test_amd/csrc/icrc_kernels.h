@@ -98,6 +98,8 @@ struct RsckArgs {
   uint32_t group_cost;  // a group's finish in line-steps of the fold's work split (launch_rsck sets it)
   uint32_t xw[8];            // the fold's work split by XCD (xcd_share; xw[0] == 0: equal shares)
   uint32_t no_split;         // host: keep the fused gather on the pass grid (RICRC_NO_GATHER_SPLIT)
+  uint32_t small_in_fold;    // the fold takes the one-line packets (host: unless RICRC_ONE_LINE_IN_GATHER)
+  uint32_t small_slots;      // ... dealt to wave slots 0..s-1 (0: to every wave by its work)
   uint32_t *out;
   // device workspace (icrc_api.cpp sizes it: rs_workspace_bytes)
   RsCounters *ctr;      // zeroed on allocation and by the gather pass of every call
@@ -126,6 +128,10 @@ struct RsckArgs {
 // ab_c4_group_cost_quarters.txt).
 // (RICRC_RS_GCOST, read by ricrc_create, overrides it for schedule studies.)
 constexpr uint32_t kRsGroupCost = 12;  // quarter line-steps (3 lines)
+// The fold's one-line packets go to wave slots 0 .. kRsSmallSlots - 1 of
+// every workgroup (icrc_rsck_kernel; RICRC_SMALL_SLOTS overrides, 0: every
+// wave in proportion to its work).
+constexpr uint32_t kRsSmallSlots = 12;
 uint64_t rs_workspace_bytes(uint64_t count);
 // Carves the workspace (rs_workspace_bytes(count) bytes at ws) into a.
 void rs_bind_workspace(RsckArgs &a, void *ws);

@@ -156,10 +156,13 @@ constexpr SliceTables<N> make_tables() {
 //   [128 + 132 s, + 128)   K = QS[s] = x^(-8 (16 s + trail)), lane slot s (rows padded to 132 words)
 //   kFinSck = 1216 words (the SCK: trail = 4, its trailer word); the ragged
 //   fold (trail = 0) adds [1184, 1216) its head masks (or, xor of word k)
-//   and [1216, 1344), [1344, 1472) K = x^-64, x^-96: kFinFold = 1472.
+//   and [1216, 1344), [1344, 1472) K = x^-64, x^-96, and [1472, 1600)
+//   K = x^32 (one 4-byte CRC step for its one-line packets, whose 128 KiB
+//   LDS tables are the 128-byte-stride ones): kFinFold = 1600.
 constexpr uint32_t kFinQtStride = 132;
 constexpr uint32_t kFinSck = 128 + 8 * kFinQtStride + 32;
-constexpr uint32_t kFinFold = 128 + 8 * kFinQtStride + 32 + 256;
+constexpr uint32_t kFinFold = 128 + 8 * kFinQtStride + 32 + 384;
+constexpr uint32_t kFinStep4 = 1472;  // the fold's x^32 nibble table
 inline uint32_t nibble_entry(uint32_t K, uint32_t w, uint32_t v) {
   uint32_t e = 0;
   for (int b = 0; b < 4; ++b)
@@ -179,6 +182,7 @@ inline void build_fin_tables(uint32_t *t, bool fold) {
       if (fold) {
         t[1216 + 16 * w + v] = nibble_entry(x64, w, v);
         t[1344 + 16 * w + v] = nibble_entry(x96, w, v);
+        t[kFinStep4 + 16 * w + v] = nibble_entry(gf_x8n(4), w, v);
       }
     }
   if (fold)

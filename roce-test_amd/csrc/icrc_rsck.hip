@@ -391,6 +391,232 @@ __device__ __forceinline__ void static_for(F &&f) {
 // tables built (the barrier), work split found, end, first line arrived,
 // counters arrived, table build's own instructions done, the work of the
 // wave's groups.
+// =======================================================================
+// Small packets of the ragged path (<= kRsSmallL lines: the 64 / 256-byte
+// share of C4): ONE LANE PER PACKET, descriptors [0, ctr->small) of the
+// buckets.  8 lanes per packet (the fold above) is too coarse for them, and
+// the round-1 piece kernel (one 64-byte piece per lane; git history) paid a
+// GF(2) re-alignment, prefix XOR and end multiply per packet.  Here a lane folds its
+// packet's whole byte stream from a ZERO register with no multiply at all:
+//
+//   stream = 4 x 0xFF || masked L3[0, M)        (M = n - 4)
+//
+// (the CRC-32 init ~0 folded over the 8-byte 0xFF prefix of calc_icrc,
+// shuffle_egress.p4:465, is the zero register over 00 x 4 || FF x 4, and
+// leading zeros are free; tests/test_kernel_algebra.py::
+// test_small_lane_end_aligned_stream), ICRC = ~register.  The
+// stream is cut into 16-byte blocks that END at the packet's covered end
+// e = addr + M, so no trailing byte is ever folded; leading bytes before the
+// prefix are zeros, which a zero register ignores.  That lets every lane of
+// a wave fold the same number of blocks Kmax (a multiple of 4: lanes with
+// shorter packets start with all-zero blocks), so the loop has no divergence
+// and no exec-masked memory op.  Block j needs the 16-byte native units N and
+// N + 16 (N = e - (e & 15) - 16 (Kmax - j)), requested up to 17 at a time
+// before the fold (memory-level parallelism); loads are clamped to the units
+// that hold packet bytes (never another page) and whatever a clamped unit
+// holds is masked away by packet-relative offset.  A block's words come out
+// of the two units by a 2-level word funnel and v_alignbyte (phase e & 15).
+// =======================================================================
+__device__ __forceinline__ uint32_t small_word(uint32_t w, int r) {  // r = packet-relative offset of byte 0
+  const uint32_t keep = byte_span_mask(-r, 4);            // bytes at r >= 0: packet data
+  const uint32_t pre = byte_span_mask(-4 - r, -r);        // bytes at -4 <= r < 0: the 0xFF prefix
+  // invariant fields -> 0xFF; outside [0, 40) the shifted map is empty, so no
+  // range test (a select on r became a divergent branch)
+  const uint32_t sh = (uint32_t)(r + 3 < 0 ? 0 : r + 3 > 63 ? 63 : r + 3);
+  const uint32_t bits = (uint32_t)(((kMaskBits << 3) >> sh) & 0xFu);
+  return (w & keep) | pre | (expand_nibble(bits) & keep);
+}
+
+// small_word for a word-aligned r (a multiple of 4): whole-word keep, the
+// 0xFF prefix word at -4, the IPv4 mask words of offsets 0, 8, 24, 32.
+__device__ __forceinline__ uint32_t small_word_aligned(uint32_t w, int r) {
+  const uint32_t keep = (uint32_t)(r >= 0) * 0xFFFFFFFFu;
+  const uint32_t orm = ((uint32_t)(r == -4) * 0xFFFFFFFFu) | ((uint32_t)(r == 0) * kMaskW0) |
+                       ((uint32_t)(r == 8) * kMaskW2) | ((uint32_t)(r == 24) * kMaskW6) |
+                       ((uint32_t)(r == 32) * kMaskW8);
+  return (w & keep) | orm;
+}
+
+// One packet's stream in icrc_rsmall_kernel.
+struct SmallPk {
+  uint64_t ufirst, ulast, N0;  // the packet's first / last 16-byte unit, native unit of block 0
+  uint32_t sb, m2, m1;         // end phase: byte shift, word-shift selects (all ones / zero)
+  int rel;                     // packet-relative offset of the next block
+  uint32_t reg;
+
+  __device__ __forceinline__ void init(const RsDesc &d, uint32_t Kmax) {
+    const uint64_t addr = ((uint64_t)(d.hi & 0xFFFFu) << 32) | d.lo;
+    const uint32_t M = (d.hi >> 16) - 4u;
+    const uint64_t e = addr + M;
+    const uint32_t t = (uint32_t)(e & 15u);
+    sb = t & 3u;
+    m2 = 0u - ((t >> 3) & 1u);
+    m1 = 0u - ((t >> 2) & 1u);
+    ufirst = addr & ~15ull;
+    ulast = (e - 1u) & ~15ull;
+    N0 = e - t - 16ull * Kmax;
+    rel = (int)M - 16 * (int)Kmax;
+    reg = 0u;
+  }
+  __device__ __forceinline__ u32x4 unit(uint32_t k) const {  // native unit k, clamped to the packet's
+    uint64_t u = N0 + 16ull * k;
+    u = u < ufirst ? ufirst : (u > ulast ? ulast : u);
+    return gload16(u);  // plain: non-temporal scattered unit reads took 69 instead of 40 us on C4
+  }
+  // Blocks j0 .. j0 + KB - 1: all KB + 1 units they need are requested at
+  // once, then folded.  (A ring of 4-8 units in flight measured ~2x slower
+  // on C4's scattered small packets, tools/microbench/mb_scatter.hip: the
+  // memory-level parallelism of one lane is what these reads need.)
+  // WA: every packet of the wave starts and ends on a 4-byte word (the wave-
+  // uniform common case: C4, NIC rings): no byte shift, whole-word masks.
+  // MASK: which blocks get the head masks (prefix / invariant fields / bytes
+  // before the packet), branch-free: 1 = blocks 0..3 (the first chunk of a
+  // wave whose packets all start their heads there: M >= 16 Kmax - 24), 2 = all
+  // (lanes with shorter packets start later), 0 = none.  (A wave-uniform
+  // branch on "is some lane in its head" made the compiler wait for every
+  // outstanding load (vmcnt(0)) before each block: 2x slower.)
+  template <int KB, bool WA, int MASK, class Step>
+  __device__ __forceinline__ void chunk(const Step &step, uint32_t j0) {
+    u32x4 U[KB + 1];
+#pragma unroll
+    for (int k = 0; k <= KB; ++k) U[k] = unit(j0 + k);
+    blocks<KB, WA, MASK>(step, U);
+  }
+  // Fold blocks 0 .. KB-1 of units U (block j from units j, j + 1).
+  template <int KB, bool WA, int MASK, class Step>
+  __device__ __forceinline__ void blocks(const Step &step, const u32x4 (&U)[KB + 1]) {
+#pragma unroll
+    for (int j = 0; j < KB; ++j) {
+      // Block j's 4 words from units j, j + 1: X[k] = W[(t >> 2) + k] by
+      // bitwise selects (written as ternaries, the compiler turned the
+      // funnel into a dynamically indexed array in scratch), then
+      // v_alignbyte by the byte phase.
+      const u32x4 c = U[j], n = U[j + 1];
+      const uint32_t W[8] = {c[0], c[1], c[2], c[3], n[0], n[1], n[2], n[3]};
+      uint32_t V[6], X[5], w[4];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) V[k] = __builtin_amdgcn_bitop3_b32(m2, W[k + 2], W[k], 0xCA);
+#pragma unroll
+      for (int k = 0; k < 5; ++k) X[k] = __builtin_amdgcn_bitop3_b32(m1, V[k + 1], V[k], 0xCA);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) w[i] = WA ? X[i] : __builtin_amdgcn_alignbyte(X[i + 1], X[i], sb);
+      if (MASK == 2 || (MASK == 1 && j < 4)) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) w[i] = WA ? small_word_aligned(w[i], rel + 4 * i) : small_word(w[i], rel + 4 * i);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) reg = step(reg, w[i]);
+      rel += 16;
+    }
+  }
+};
+
+// small_icrc's CRC step over the slice-by-4 tables in LDS (fill_tables).
+struct Step4 {
+  const uint32_t *lds;
+  LaneTab lt;
+  __device__ __forceinline__ uint32_t operator()(uint32_t r, uint32_t w) const { return step4(lds, lt, r, w); }
+};
+// ... through the nibble table of x^32 (16 entries per nibble position, in 16
+// banks: conflict-free for any lane pattern): 8 lookups instead of 4, for
+// the fold kernel, whose 128 KiB of LDS tables advance 128 bytes a step.
+struct StepNib {
+  const uint32_t *t;  // [128]: entry 16 w + v = (nibble v at bits 4w..4w+3) * x^32
+  __device__ __forceinline__ uint32_t operator()(uint32_t r, uint32_t w) const {
+    const uint32_t v = r ^ w;
+    uint32_t e[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) e[k] = t[16 * k + __builtin_amdgcn_ubfe(v, 4 * k, 4)];
+    return xor3(xor3(e[0], e[1], e[2]), xor3(e[3], e[4], e[5]), e[6] ^ e[7]);
+  }
+};
+
+// The ICRC of every lane's one-line packet d: wave-collective (every lane of
+// the wave calls it together; a lane without a packet passes a copy of a
+// valid descriptor and ignores the result), since the wave's shape -- its
+// largest block count, whether every packet is word-aligned, half-line --
+// is decided by ballots.  step(r, w): the register after folding word w
+// into r (step4 over the slice-by-4 tables, fill_tables; or nibble lookups).
+template <class Step>
+__device__ __forceinline__ uint32_t small_icrc(const Step &step, const RsDesc &d, uint32_t lane) {
+  uint32_t K = (((d.hi >> 16) - 4u) + 4u + 15u) >> 4;  // this lane's blocks
+  // the wave's largest, rounded up to a multiple of 4: by ballots for
+  // one-line packets (K <= 8), a shuffle reduction beyond
+  uint32_t Kmax;
+  if (__builtin_amdgcn_ballot_w64(K > 4u) == 0) {
+    Kmax = 4u;
+  } else if (__builtin_amdgcn_ballot_w64(K > 8u) == 0) {
+    Kmax = 8u;
+  } else {
+#pragma unroll
+    for (int w = 32; w >= 1; w >>= 1) K = max(K, (uint32_t)__shfl_xor((int)K, w));
+    Kmax = __builtin_amdgcn_readfirstlane((K + 3u) & ~3u);
+  }
+  // wave-uniform variants: word-aligned packets; every packet's head in blocks 0..3
+  const bool wa = __builtin_amdgcn_ballot_w64(((d.lo | (d.hi >> 16)) & 3u) != 0) == 0;
+  // heads in blocks 0..3: rel_4 = M - 16 Kmax + 64 >= 40 for every lane
+  const bool uk = __builtin_amdgcn_ballot_w64((d.hi >> 16) - 4u + 24u < 16u * Kmax) == 0;
+  // Half-line packets: every covered byte in one aligned 64-byte half
+  // line hb .. hb + 63 whose last 16-byte unit holds the covered end, not
+  // at the half line's end (C4's 64-byte packets: 64-byte aligned, 60
+  // covered bytes).  For a wave of them the 5 units of the 4 blocks are
+  // the half line's units 0, 0, 1, 2, 3, and they are read coalesced: in
+  // load c the 4 lanes of quad p read units 0..3 of lane 4 p + c's half
+  // line (64 contiguous bytes), and a 4 x 4 quad transpose hands every lane
+  // its own -- instead of every lane reading its packet's units alone, 64
+  // lines apart (the access pattern that costs C1's direct kernel, see the
+  // quad kernel in icrc_kernels.hip).  (Kmax = 4: a half-line packet of
+  // 61..63 covered bytes needs a fifth block for its prefix.)
+  const uint64_t pa = ((uint64_t)(d.hi & 0xFFFFu) << 32) | d.lo;
+  const uint64_t pe = pa + ((d.hi >> 16) - 4u);
+  const uint64_t hb = (pe - 1u) & ~63ull;
+  const bool half = pa >= hb && ((uint32_t)pe & 63u) > 48u;
+  SmallPk P;
+  if (Kmax == 4u && __builtin_amdgcn_ballot_w64(!half) == 0) {  // wave-uniform: a wave of half-line packets
+    const uint32_t hlo = (uint32_t)hb, hhi = (uint32_t)(hb >> 32), q = lane & 3u;
+    auto at = [&](uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32 | lo) + 16u * q; };
+    u32x4 H[4];
+    H[0] = gload16(at(dpp_quad_bcast<0>(hlo), dpp_quad_bcast<0>(hhi)));
+    H[1] = gload16(at(dpp_quad_bcast<1>(hlo), dpp_quad_bcast<1>(hhi)));
+    H[2] = gload16(at(dpp_quad_bcast<2>(hlo), dpp_quad_bcast<2>(hhi)));
+    H[3] = gload16(at(dpp_quad_bcast<3>(hlo), dpp_quad_bcast<3>(hhi)));
+    quad_transpose(H, lane & 3u);
+    const u32x4 U[5] = {H[0], H[0], H[1], H[2], H[3]};
+    P.init(d, 4u);
+    if (wa && uk)
+      P.blocks<4, true, 1>(step, U);
+    else if (uk)
+      P.blocks<4, false, 1>(step, U);
+    else
+      P.blocks<4, false, 2>(step, U);
+    return ~P.reg;
+  }
+  P.init(d, Kmax);
+  auto run = [&](auto words, auto uniform) __attribute__((always_inline)) {
+    constexpr bool WA = decltype(words)::value;
+    constexpr int M1 = decltype(uniform)::value ? 1 : 2, M2 = decltype(uniform)::value ? 0 : 2;
+    // Kmax = 8 q + r (r = 0 or 4): a first chunk of r or 8 blocks, then
+    // chunks of 8 (one-line packets: M <= 124, Kmax <= 8 -- one chunk, at
+    // most 9 units = 36 VGPRs in flight)
+    uint32_t j = 0;
+    if ((Kmax & 7u) == 4u) {  // wave-uniform
+      P.chunk<4, WA, M1>(step, 0);
+      j = 4;
+    } else {
+      P.chunk<8, WA, M1>(step, 0);
+      j = 8;
+    }
+    for (; j < Kmax; j += 8) P.chunk<8, WA, M2>(step, j);
+  };
+  if (wa && uk)
+    run(std::true_type{}, std::true_type{});
+  else if (uk)
+    run(std::false_type{}, std::true_type{});
+  else
+    run(std::false_type{}, std::false_type{});
+  return ~P.reg;
+}
+
 template <int ABL>
 __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   // Result slots per wave (a round of 8 groups leaves in one store; a store
@@ -407,10 +633,10 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   // Finish tables first, so every lookup's constant part fits a ds_read's
   // 16-bit offset: x^-32 nibble table (128 words) | x^(-128 s) nibble tables
   // (8 x 132 words: rows padded by 4 words so the 8 lane slots spread over
-  // the banks) | head masks (32 words) | x^-64, x^-96 nibble tables (2 x 128
-  // words) | 128 KiB slice-by-4 tables | 1 KiB tz bases | 1.5 KiB per wave =
-  // 157.7 KiB.
-  constexpr uint32_t kQtStride = kFinQtStride, kSmallWords = kFinFold;  // 1472 (build_fin_tables): a multiple of 32 words
+  // the banks) | head masks (32 words) | x^-64, x^-96, x^32 nibble tables
+  // (3 x 128 words) | 128 KiB slice-by-4 tables | 1 KiB tz bases | 1.5 KiB
+  // per wave = 159.3 KiB.
+  constexpr uint32_t kQtStride = kFinQtStride, kSmallWords = kFinFold;  // 1600 (build_fin_tables): a multiple of 32 words
   __shared__ uint32_t lds[kSmallWords + kLdsWords + kTzWords + kWaves * kWaveWords];
   uint32_t *xtl = lds;
   uint32_t *qtl = lds + 128;
@@ -454,16 +680,23 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   // its runs split that range by class.
   const uint32_t NG = (uint32_t)(C.pool & ((1ull << kRsGroupBits) - 1u));
   const uint64_t S = C.pool >> kRsGroupBits;
-  if (NG == 0) return;  // no packet of >= 2 lines: every wave leaves here (no barrier above)
+  // The small pool's one-line packets (a.small_in_fold): rounds of 64, one
+  // lane per packet, split over the waves in the proportion of their big
+  // work (below) -- spread thin, as one round costs a wave two round trips
+  // that a wave with many of them could not hide.
+  const uint32_t NS = a.small_in_fold ? C.small : 0u;
+  const uint32_t NC = (NS + 63u) >> 6;
+  if (NG == 0 && NC == 0) return;  // nothing to fold: every wave leaves here (no barrier above)
   const uint32_t t_ctr = (ABL & 524288) ? (uint32_t)__builtin_amdgcn_s_memrealtime() : 0u;
 #pragma unroll
   for (int k = 0; k < kBq; ++k) brn[k] = 64u * (uint32_t)k + lane < a.nblk ? brn[k] : 0u;
   // This wave's groups: those whose first line lies in its share of the work.
   const uint64_t wave = (uint64_t)blockIdx.x * kWaves + wid;
   const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
-  const uint64_t share = (S + nwaves - 1) / nwaves;
-  uint64_t x0 = wave * share < S ? wave * share : S, x1 = x0 + share;
-  if (a.xw[0] != 0u) xcd_share(S, a.xw, C.xcd, wid, x0, x1);  // weighted by XCD
+  const uint64_t T = NG ? S : NC;  // the work split's total (the small rounds when no packet has >= 2 lines)
+  const uint64_t share = (T + nwaves - 1) / nwaves;
+  uint64_t x0 = wave * share < T ? wave * share : T, x1 = x0 + share;
+  if (a.xw[0] != 0u) xcd_share(T, a.xw, C.xcd, wid, x0, x1);  // weighted by XCD
   // the pass block whose work range holds x (ballots over the loaded ranges)
   auto block_of = [&](uint64_t x) -> uint32_t {
     uint32_t b = 0;
@@ -524,6 +757,28 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   const uint32_t q_begin = group_at(x0, n0, R0, Q0), q_end = group_at(x1, n1, R1, Q1);
   const uint32_t t_split = (ABL & 524288) ? (uint32_t)__builtin_amdgcn_s_memrealtime() : 0u;
   const bool work = q_begin < q_end;  // wave-uniform
+  // Small rounds [c_begin, c_end): dealt evenly to the waves of slots
+  // 0 .. small_slots - 1 (12: the four youngest slots of a workgroup, the
+  // last to finish their equal shares, take none; at C4's 8-GPU shard 0.1542
+  // -> 0.1512 ms per step against folding them in the gather, at C4 0.9825 ->
+  // 0.9730, where slots 0..15 measured 0.981 and a share by each wave's work
+  // 0.984, profiles/r05/NOTES.md), or -- small_slots = 0, or no packet of
+  // >= 2 lines -- the wave's fraction [x0, x1) / T of them (consecutive
+  // waves' fractions meet, so the rounds are dealt exactly once).
+  uint32_t c_begin = (uint32_t)((x0 < T ? x0 : T) * NC / T), c_end = (uint32_t)((x1 < T ? x1 : T) * NC / T);
+  if (a.small_slots != 0u && NG != 0u) {  // wave-uniform
+    const uint32_t sl = a.small_slots;
+    const uint64_t E = (uint64_t)gridDim.x * sl, e = (uint64_t)blockIdx.x * sl + wid;
+    c_begin = wid < sl ? (uint32_t)(e * NC / E) : 0u;
+    c_end = wid < sl ? (uint32_t)((e + 1u) * NC / E) : 0u;
+  }
+  auto small_desc = [&](uint32_t c) {
+    const uint32_t j = 64u * c + lane;
+    return a.desc[j < NS ? j : NS - 1u];
+  };
+  // the first round's descriptors, requested with the first descriptor blocks
+  RsDesc sd{0u, 0u};
+  if (c_begin < c_end) sd = small_desc(c_begin);
 
   const LaneTab lt{(lane & 31) << 2, ((lane & 31) << 2) | 0x10000u};
   const uint32_t *qrow = qtl + s * kQtStride;
@@ -619,434 +874,248 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
     a.out[wave8 + 4] = work ? q_end - q_begin : 0u;
     a.out[wave8 + 5] = t_ctr;
   }
-  if (!work) return;
-
-  uint32_t round_q0 = q_begin;  // first group of the current round of result slots
-  uint32_t sink = 0;             // timing ablations: values kept live
-  uint32_t done_work = 0;        // (ABL 524288: the work of the wave's groups)
-  auto flush = [&](uint32_t q_stop) {  // groups [round_q0, q_stop) of the round
-    const uint32_t valid = 8u * (q_stop - round_q0);
-    const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.bres + 8ull * round_q0, 4u * valid);
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the slot writes have landed
-    // slots past `valid` fall outside the range check
-    __builtin_amdgcn_raw_buffer_store_b32(slots[lane], ro, 4u * lane, 0, 16);
-  };
-  // A group's finish: its chain registers rr (after its last line), L lines,
-  // first-byte offsets ga and covered lengths gM of its 8 packets (per lane
-  // group), its position q in the big pool -> the ICRC into the wave's slot.
-  auto finish_group = [&](uint32_t (&rr)[4], uint32_t Lg, uint32_t ga, uint32_t gM, uint32_t q) {
-    uint32_t R;
-    if (ABL & 2) {
-      R = group_xor(rr[0] ^ rr[1] ^ rr[2] ^ rr[3], 3);
-    } else {
-      // Horner by x^-32 through the nibble table: 8 lookups per multiply
-      // (one copy: the 16 entries of a nibble position sit in 16 banks, so
-      // any lane pattern is conflict-free) instead of 32 bit-selects.
-      // v * (table's constant) ^ x: 8 nibble lookups, an XOR tree of 3-input XORs
-      auto nib_mul = [](const uint32_t *t, uint32_t v, uint32_t x) -> uint32_t {
-        uint32_t e[8];
+  // The wave's small rounds first, while its first lines are in flight.
+  // small_icrc is wave-collective: every lane folds one packet (lanes past
+  // the pool a copy of the last, result dropped).
+  if (c_begin < c_end) {  // wave-uniform
+    const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.res, 4u * NS);
+    const StepNib step{lds + kFinStep4};
+    auto put = [&](uint32_t c, uint32_t v) {
+      const uint32_t pos = 64u * c + lane;
+      __builtin_amdgcn_raw_buffer_store_b32(v, ro, pos < NS ? 4u * pos : 0x7FFFFFF0u, 0, 0);
+    };
+    RsDesc d = sd;
+#pragma unroll 1
+    for (uint32_t c = c_begin; c < c_end; ++c) {
+      const RsDesc dn = small_desc(c + 1u < c_end ? c + 1u : c);  // the next round's, in flight meanwhile
+      put(c, small_icrc(step, d, lane));
+      d = dn;
+    }
+  }
+  uint32_t done_work = 0;  // (ABL 524288: the work of the wave's groups)
+  if (work) {  // wave-uniform
+    uint32_t round_q0 = q_begin;  // first group of the current round of result slots
+    uint32_t sink = 0;             // timing ablations: values kept live
+    auto flush = [&](uint32_t q_stop) {  // groups [round_q0, q_stop) of the round
+      const uint32_t valid = 8u * (q_stop - round_q0);
+      const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.bres + 8ull * round_q0, 4u * valid);
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the slot writes have landed
+      // slots past `valid` fall outside the range check
+      __builtin_amdgcn_raw_buffer_store_b32(slots[lane], ro, 4u * lane, 0, 16);
+    };
+    // A group's finish: its chain registers rr (after its last line), L lines,
+    // first-byte offsets ga and covered lengths gM of its 8 packets (per lane
+    // group), its position q in the big pool -> the ICRC into the wave's slot.
+    auto finish_group = [&](uint32_t (&rr)[4], uint32_t Lg, uint32_t ga, uint32_t gM, uint32_t q) {
+      uint32_t R;
+      if (ABL & 2) {
+        R = group_xor(rr[0] ^ rr[1] ^ rr[2] ^ rr[3], 3);
+      } else {
+        // Horner by x^-32 through the nibble table: 8 lookups per multiply
+        // (one copy: the 16 entries of a nibble position sit in 16 banks, so
+        // any lane pattern is conflict-free) instead of 32 bit-selects.
+        // v * (table's constant) ^ x: 8 nibble lookups, an XOR tree of 3-input XORs
+        auto nib_mul = [](const uint32_t *t, uint32_t v, uint32_t x) -> uint32_t {
+          uint32_t e[8];
 #pragma unroll
-        for (int w = 0; w < 8; ++w) e[w] = t[16 * w + __builtin_amdgcn_ubfe(v, 4 * w, 4)];
-        return xor3(xor3(e[0], e[1], e[2]), xor3(e[3], e[4], e[5]), xor3(e[6], e[7], x));
-      };
-      // r3 x^-96 + r2 x^-64 + r1 x^-32 + r0: three independent multiplies
-      // (Horner chained them: four dependent LDS round trips per finish,
-      // which the 2-3-line groups of 256-byte packets could not hide)
-      const uint32_t u = nib_mul(x3tl, rr[3], nib_mul(x2tl, rr[2], nib_mul(xtl, rr[1], rr[0])));
-      R = group_xor(nib_mul(qrow, u, 0u), 3);  // u * x^(-128 s): lane slot s's nibble table
-      // x^(-8 tz), distributed: lane s takes bits 4s..4s+3 of R; basis word
-      // 4s from LDS, 4s+1..4s+3 by successive x^-1.
-      const uint32_t tz = 128u * Lg - ga - gM;
-      uint32_t bw = tzl[2u * tz + s], p = 0;
+          for (int w = 0; w < 8; ++w) e[w] = t[16 * w + __builtin_amdgcn_ubfe(v, 4 * w, 4)];
+          return xor3(xor3(e[0], e[1], e[2]), xor3(e[3], e[4], e[5]), xor3(e[6], e[7], x));
+        };
+        // r3 x^-96 + r2 x^-64 + r1 x^-32 + r0: three independent multiplies
+        // (Horner chained them: four dependent LDS round trips per finish,
+        // which the 2-3-line groups of 256-byte packets could not hide)
+        const uint32_t u = nib_mul(x3tl, rr[3], nib_mul(x2tl, rr[2], nib_mul(xtl, rr[1], rr[0])));
+        R = group_xor(nib_mul(qrow, u, 0u), 3);  // u * x^(-128 s): lane slot s's nibble table
+        // x^(-8 tz), distributed: lane s takes bits 4s..4s+3 of R; basis word
+        // 4s from LDS, 4s+1..4s+3 by successive x^-1.
+        const uint32_t tz = 128u * Lg - ga - gM;
+        uint32_t bw = tzl[2u * tz + s], p = 0;
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)R, (int)(4u * s + t), 1);
-        p = and_xor(m, bw, p);
-        bw = and_xor((uint32_t)((int32_t)bw >> 31), kXInv, bw << 1);
+        for (int t = 0; t < 4; ++t) {
+          const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)R, (int)(4u * s + t), 1);
+          p = and_xor(m, bw, p);
+          bw = and_xor((uint32_t)((int32_t)bw >> 31), kXInv, bw << 1);
+        }
+        R = group_xor(p, 3);
       }
-      R = group_xor(p, 3);
-    }
-    if (ABL & 524288) done_work += 4u * Lg + a.group_cost;
-    if (ABL & 16) {
-      sink ^= R;  // keep the value live
-      return;
-    }
-    slots[((q - round_q0) << 3) | g] = ~R;
-    if (q + 1 - round_q0 == kRound) {  // wave-uniform
-      flush(q + 1);
-      round_q0 = q + 1;
-    }
-  };
+      if (ABL & 524288) done_work += 4u * Lg + a.group_cost;
+      if (ABL & 16) {
+        sink ^= R;  // keep the value live
+        return;
+      }
+      slots[((q - round_q0) << 3) | g] = ~R;
+      if (q + 1 - round_q0 == kRound) {  // wave-uniform
+        flush(q + 1);
+        round_q0 = q + 1;
+      }
+    };
 
-  // The fold over groups [qb, qe): any mix of line counts, byte- or
-  // word-granular edges (two cursors, quiet blocks).
-  uint32_t fd_q = qb, fd_k = 0, fd_L, fd_a, fd_M;
-  auto fd_enter = [&](uint32_t q) {
-    const uint32_t v = fifo[((q & 7u) << 3) | g];
-    fd_a = v & 127u;
-    fd_M = v >> 7;
-    fd_L = __builtin_amdgcn_readfirstlane((fd_a + fd_M + 127u) >> 7);
-  };
-  fd_enter(fd_q);
-  // head lines of the group: 2 when some packet's header runs into line 1 (a
-  // plain uint32 so the edge test below is SALU arithmetic and one branch:
-  // short-circuit || on a ballot-derived bool compiled to five branches per
-  // step, and C4's fold ran 1.5 % slower)
-  uint32_t fd_hl = __ballot(fd_a > 88u) != 0 ? 2u : 1u;
-  // edge line <=> fd_k < fd_hl or fd_k == fd_L - 1 <=> (fd_k - fd_hl) >= fd_span, unsigned
-  uint32_t fd_span = fd_L - 1u > fd_hl ? fd_L - 1u - fd_hl : 0u;  // 0: every line is an edge line
+    // The fold over groups [qb, qe): any mix of line counts, byte- or
+    // word-granular edges (two cursors, quiet blocks).
+    uint32_t fd_q = qb, fd_k = 0, fd_L, fd_a, fd_M;
+    auto fd_enter = [&](uint32_t q) {
+      const uint32_t v = fifo[((q & 7u) << 3) | g];
+      fd_a = v & 127u;
+      fd_M = v >> 7;
+      fd_L = __builtin_amdgcn_readfirstlane((fd_a + fd_M + 127u) >> 7);
+    };
+    fd_enter(fd_q);
+    // head lines of the group: 2 when some packet's header runs into line 1 (a
+    // plain uint32 so the edge test below is SALU arithmetic and one branch:
+    // short-circuit || on a ballot-derived bool compiled to five branches per
+    // step, and C4's fold ran 1.5 % slower)
+    uint32_t fd_hl = __ballot(fd_a > 88u) != 0 ? 2u : 1u;
+    // edge line <=> fd_k < fd_hl or fd_k == fd_L - 1 <=> (fd_k - fd_hl) >= fd_span, unsigned
+    uint32_t fd_span = fd_L - 1u > fd_hl ? fd_L - 1u - fd_hl : 0u;  // 0: every line is an edge line
 
-  uint32_t r[4] = {0u, 0u, 0u, 0u};
-  // Two copies of the fold loop: one with whole-word edges when the bucket
-  // pass found every strided-chain packet word-aligned in start and length
-  // (a per-group choice inside the loop made the compiler rotate the load
-  // ring through copies and drain vmcnt(0) at the loop head).
-  // The fold keeps xr = r ^ (the current line's word), the lookup input: the
-  // XOR with the next line's word rides in the step's last 3-input XOR (as in
-  // the SCK), 4 VALU per line fewer.  An edge line corrects xr by
-  // w ^ masked(w) on its own step; a group's last line leaves the next
-  // group's first word alone in xr (its chains start from zero).
-  uint32_t xr[4] = {ring[0][0], ring[0][1], ring[0][2], ring[0][3]};
-  if ((ABL & 524288) && lane == 0) a.out[wave8 + 4] = (uint32_t)__builtin_amdgcn_s_memrealtime() + (xr[0] == 0x9E3779B9u);
-  // Quiet steps.  Per-step cursor control cost the fold 16 SALU and 4.5
-  // branches per wave step against 1.7 and 0.1 in the SCK (rocprofv3 --pmc,
-  // profiles/r03/pmc_insts.txt).  A run of steps in which neither cursor
-  // changes group and the fold cursor's line is no edge line (not a head
-  // line, not the group's last) needs none of it: a step is then the 16
-  // lookups, the XORs and a load.  Every full step computes the length of
-  // the run that follows it (quiet); a block of D steps that starts with a
-  // run of >= D ahead is D quiet steps with no per-step test at all, and
-  // shorter runs go through full steps (a per-step quiet / full branch
-  // measured 17 % slower: 1115 against 953 us, profiles/r03/fold_var.txt).
-  uint32_t quiet = 0;
-  auto quiet_step = [&](int u, uint32_t ahead) {  // ahead: lines the load cursor is past ld_k within the block
-    const u32x4 wn = ring[(u + 1) % D];
+    uint32_t r[4] = {0u, 0u, 0u, 0u};
+    // Two copies of the fold loop: one with whole-word edges when the bucket
+    // pass found every strided-chain packet word-aligned in start and length
+    // (a per-group choice inside the loop made the compiler rotate the load
+    // ring through copies and drain vmcnt(0) at the loop head).
+    // The fold keeps xr = r ^ (the current line's word), the lookup input: the
+    // XOR with the next line's word rides in the step's last 3-input XOR (as in
+    // the SCK), 4 VALU per line fewer.  An edge line corrects xr by
+    // w ^ masked(w) on its own step; a group's last line leaves the next
+    // group's first word alone in xr (its chains start from zero).
+    uint32_t xr[4] = {ring[0][0], ring[0][1], ring[0][2], ring[0][3]};
+    if ((ABL & 524288) && lane == 0) a.out[wave8 + 4] = (uint32_t)__builtin_amdgcn_s_memrealtime() + (xr[0] == 0x9E3779B9u);
+    // Quiet steps.  Per-step cursor control cost the fold 16 SALU and 4.5
+    // branches per wave step against 1.7 and 0.1 in the SCK (rocprofv3 --pmc,
+    // profiles/r03/pmc_insts.txt).  A run of steps in which neither cursor
+    // changes group and the fold cursor's line is no edge line (not a head
+    // line, not the group's last) needs none of it: a step is then the 16
+    // lookups, the XORs and a load.  Every full step computes the length of
+    // the run that follows it (quiet); a block of D steps that starts with a
+    // run of >= D ahead is D quiet steps with no per-step test at all, and
+    // shorter runs go through full steps (a per-step quiet / full branch
+    // measured 17 % slower: 1115 against 953 us, profiles/r03/fold_var.txt).
+    uint32_t quiet = 0;
+    auto quiet_step = [&](int u, uint32_t ahead) {  // ahead: lines the load cursor is past ld_k within the block
+      const u32x4 wn = ring[(u + 1) % D];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t t0 = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0400u));
-      const uint32_t t1 = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0500u) + 128);
-      const uint32_t t2 = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo1, 0x0C020600u));
-      const uint32_t t3 = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo1, 0x0C020700u) + 128);
-      xr[i] = xor3(t0, t1, xor3(t2, t3, wn[i]));
-    }
-    ring[u] = line_load(ld.line0 + 128ull * (ld_k + ahead));
-  };
-  auto fold_loop = [&](auto words) {
-    // One full step: edge masks, group finish and both cursors' group changes.
-    auto full_step = [&](int u, bool &done) {
-      const u32x4 wn = ring[(u + 1) % D];  // the next line, raw
-      if (!(ABL & 8) && fd_k - fd_hl >= fd_span) {  // wave-uniform: an edge line
-        const u32x4 wc = ring[u];
-        const int rel0 = (int)(128u * fd_k + 16u * s) - (int)fd_a;
-        if constexpr (decltype(words)::value) {
-          if (fd_k < fd_hl) {  // wave-uniform: a head line
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t t0 = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0400u));
+        const uint32_t t1 = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0500u) + 128);
+        const uint32_t t2 = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo1, 0x0C020600u));
+        const uint32_t t3 = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo1, 0x0C020700u) + 128);
+        xr[i] = xor3(t0, t1, xor3(t2, t3, wn[i]));
+      }
+      ring[u] = line_load(ld.line0 + 128ull * (ld_k + ahead));
+    };
+    auto fold_loop = [&](auto words) {
+      // One full step: edge masks, group finish and both cursors' group changes.
+      auto full_step = [&](int u, bool &done) {
+        const u32x4 wn = ring[(u + 1) % D];  // the next line, raw
+        if (!(ABL & 8) && fd_k - fd_hl >= fd_span) {  // wave-uniform: an edge line
+          const u32x4 wc = ring[u];
+          const int rel0 = (int)(128u * fd_k + 16u * s) - (int)fd_a;
+          if constexpr (decltype(words)::value) {
+            if (fd_k < fd_hl) {  // wave-uniform: a head line
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              // whole words: keep 0 <= rel < M by sign arithmetic (compare +
-              // select pairs needed hazard NOPs), head masks from a 16-entry
-              // table (rel >= 40 and rel < 0 index the zero entry 15)
-              const int rel = rel0 + 4 * i;
-              const uint32_t keep = (uint32_t)(((rel - (int)fd_M) & ~rel) >> 31);
-              const uint32_t k = __builtin_elementwise_min((uint32_t)rel >> 2, 15u);
-              typedef uint32_t u32x2e __attribute__((ext_vector_type(2)));
-              const u32x2e e = *reinterpret_cast<const u32x2e *>(etl + 2 * k);
-              xr[i] = xor3(xr[i], wc[i], ((wc[i] & keep) | e[0]) ^ e[1]);
+              for (int i = 0; i < 4; ++i) {
+                // whole words: keep 0 <= rel < M by sign arithmetic (compare +
+                // select pairs needed hazard NOPs), head masks from a 16-entry
+                // table (rel >= 40 and rel < 0 index the zero entry 15)
+                const int rel = rel0 + 4 * i;
+                const uint32_t keep = (uint32_t)(((rel - (int)fd_M) & ~rel) >> 31);
+                const uint32_t k = __builtin_elementwise_min((uint32_t)rel >> 2, 15u);
+                typedef uint32_t u32x2e __attribute__((ext_vector_type(2)));
+                const u32x2e e = *reinterpret_cast<const u32x2e *>(etl + 2 * k);
+                xr[i] = xor3(xr[i], wc[i], ((wc[i] & keep) | e[0]) ^ e[1]);
+              }
+            } else {
+              // the group's last line past its head lines: rel >= 40 (no head
+              // masks), only the bytes at rel >= M dropped -- 3 VALU a word
+              // instead of 10 and a table read
+              const int lim = (int)fd_M - 1 - rel0;
+#pragma unroll
+              for (int i = 0; i < 4; ++i) xr[i] ^= wc[i] & (uint32_t)((lim - 4 * i) >> 31);
             }
           } else {
-            // the group's last line past its head lines: rel >= 40 (no head
-            // masks), only the bytes at rel >= M dropped -- 3 VALU a word
-            // instead of 10 and a table read
-            const int lim = (int)fd_M - 1 - rel0;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) xr[i] ^= wc[i] & (uint32_t)((lim - 4 * i) >> 31);
+            for (int i = 0; i < 4; ++i) xr[i] = xor3(xr[i], wc[i], edge_word(wc[i], rel0 + 4 * i, (int)fd_M));
+          }
+        }
+        uint32_t t[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (ABL & 1) {
+            t[i][0] = __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0400u);
+            t[i][1] = xr[i] >> 7;
+            t[i][2] = 0u;
+            t[i][3] = 0u;
+          } else {
+            t[i][0] = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0400u));
+            t[i][1] = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0500u) + 128);
+            t[i][2] = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo1, 0x0C020600u));
+            t[i][3] = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo1, 0x0C020700u) + 128);
+          }
+        }
+        if (++fd_k == fd_L) {  // wave-uniform: group fd_q folded
+#pragma unroll
+          for (int i = 0; i < 4; ++i) r[i] = xor3(t[i][0], t[i][1], t[i][2] ^ t[i][3]);
+          finish_group(r, fd_L, fd_a, fd_M, fd_q);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) xr[i] = wn[i];
+          fd_k = 0;
+          if (fd_q + 1 < qe) {
+            ++fd_q;
+            fd_enter(fd_q);
+            fd_hl = __ballot(fd_a > 88u) != 0 ? 2u : 1u;
+            fd_span = fd_L - 1u > fd_hl ? fd_L - 1u - fd_hl : 0u;
+          } else {
+            done = true;
+            fd_L = 0xFFFFFFFFu;
           }
         } else {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) xr[i] = xor3(xr[i], wc[i], edge_word(wc[i], rel0 + 4 * i, (int)fd_M));
+          for (int i = 0; i < 4; ++i) xr[i] = xor3(t[i][0], t[i][1], xor3(t[i][2], t[i][3], wn[i]));
         }
-      }
-      uint32_t t[4][4];
+        // Refill after folding: the FIFO entry the fold just read may be
+        // rewritten by this step's load-cursor advance.
+        ring[u] = ld_issue();
+        ld_advance();
+        // The quiet run that follows: fold lines fd_k .. fd_L - 2 past the head
+        // lines, loads up to the line before the load cursor's group change
+        // (ld_L = 1 once every group is loaded: no run).
+        const uint32_t nf = (fd_k >= fd_hl && fd_k + 1 < fd_L) ? fd_L - 1u - fd_k : 0u;
+        const uint32_t nl = ld_L - 1u - ld_k;
+        quiet = nf < nl ? nf : nl;
+      };
+      bool done = false;
+      while (!done) {
+        if (!(ABL & 8) && quiet >= (uint32_t)D) {  // wave-uniform: D quiet steps, no per-step control
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if (ABL & 1) {
-          t[i][0] = __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0400u);
-          t[i][1] = xr[i] >> 7;
-          t[i][2] = 0u;
-          t[i][3] = 0u;
-        } else {
-          t[i][0] = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0400u));
-          t[i][1] = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0500u) + 128);
-          t[i][2] = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo1, 0x0C020600u));
-          t[i][3] = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo1, 0x0C020700u) + 128);
+          for (int u = 0; u < D; ++u) {
+            __builtin_amdgcn_sched_barrier(0);
+            quiet_step(u, (uint32_t)u);
+          }
+          quiet -= D;
+          fd_k += D;
+          ld_k += D;
+          continue;
         }
-      }
-      if (++fd_k == fd_L) {  // wave-uniform: group fd_q folded
 #pragma unroll
-        for (int i = 0; i < 4; ++i) r[i] = xor3(t[i][0], t[i][1], t[i][2] ^ t[i][3]);
-        finish_group(r, fd_L, fd_a, fd_M, fd_q);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) xr[i] = wn[i];
-        fd_k = 0;
-        if (fd_q + 1 < qe) {
-          ++fd_q;
-          fd_enter(fd_q);
-          fd_hl = __ballot(fd_a > 88u) != 0 ? 2u : 1u;
-          fd_span = fd_L - 1u > fd_hl ? fd_L - 1u - fd_hl : 0u;
-        } else {
-          done = true;
-          fd_L = 0xFFFFFFFFu;
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) xr[i] = xor3(t[i][0], t[i][1], xor3(t[i][2], t[i][3], wn[i]));
-      }
-      // Refill after folding: the FIFO entry the fold just read may be
-      // rewritten by this step's load-cursor advance.
-      ring[u] = ld_issue();
-      ld_advance();
-      // The quiet run that follows: fold lines fd_k .. fd_L - 2 past the head
-      // lines, loads up to the line before the load cursor's group change
-      // (ld_L = 1 once every group is loaded: no run).
-      const uint32_t nf = (fd_k >= fd_hl && fd_k + 1 < fd_L) ? fd_L - 1u - fd_k : 0u;
-      const uint32_t nl = ld_L - 1u - ld_k;
-      quiet = nf < nl ? nf : nl;
-    };
-    bool done = false;
-    while (!done) {
-      if (!(ABL & 8) && quiet >= (uint32_t)D) {  // wave-uniform: D quiet steps, no per-step control
-#pragma unroll
-        for (int u = 0; u < D; ++u) {
+        for (int u = 0; u < D; ++u) {  // full steps (correct in any state; each one measures the next run)
           __builtin_amdgcn_sched_barrier(0);
-          quiet_step(u, (uint32_t)u);
+          full_step(u, done);
         }
-        quiet -= D;
-        fd_k += D;
-        ld_k += D;
-        continue;
       }
-#pragma unroll
-      for (int u = 0; u < D; ++u) {  // full steps (correct in any state; each one measures the next run)
-        __builtin_amdgcn_sched_barrier(0);
-        full_step(u, done);
-      }
-    }
-  };
-  if (C.odd == 0)
-    fold_loop(std::true_type{});
-  else
-    fold_loop(std::false_type{});
-  if (!(ABL & 16) && q_end != round_q0) flush(q_end);
-  if ((ABL & 16) && sink == 0x12345678u) a.bres[0] = sink;
+    };
+    if (C.odd == 0)
+      fold_loop(std::true_type{});
+    else
+      fold_loop(std::false_type{});
+    if (!(ABL & 16) && q_end != round_q0) flush(q_end);
+    if ((ABL & 16) && sink == 0x12345678u) a.bres[0] = sink;
+  }
   if ((ABL & 524288) && lane == 0) {  // timing only: end stamp after every store has left
     __builtin_amdgcn_s_waitcnt(0);
     a.out[wave8 + 3] = (uint32_t)__builtin_amdgcn_s_memrealtime();
     a.out[wave8 + 6] = t_tb;
     a.out[wave8 + 7] = done_work;
   }
-}
-
-// =======================================================================
-// Small packets of the ragged path (<= kRsSmallL lines: the 64 / 256-byte
-// share of C4): ONE LANE PER PACKET, descriptors [0, ctr->small) of the
-// buckets.  8 lanes per packet (the fold above) is too coarse for them, and
-// the round-1 piece kernel (one 64-byte piece per lane; git history) paid a
-// GF(2) re-alignment, prefix XOR and end multiply per packet.  Here a lane folds its
-// packet's whole byte stream from a ZERO register with no multiply at all:
-//
-//   stream = 4 x 0xFF || masked L3[0, M)        (M = n - 4)
-//
-// (the CRC-32 init ~0 folded over the 8-byte 0xFF prefix of calc_icrc,
-// shuffle_egress.p4:465, is the zero register over 00 x 4 || FF x 4, and
-// leading zeros are free; tests/test_kernel_algebra.py::
-// test_small_lane_end_aligned_stream), ICRC = ~register.  The
-// stream is cut into 16-byte blocks that END at the packet's covered end
-// e = addr + M, so no trailing byte is ever folded; leading bytes before the
-// prefix are zeros, which a zero register ignores.  That lets every lane of
-// a wave fold the same number of blocks Kmax (a multiple of 4: lanes with
-// shorter packets start with all-zero blocks), so the loop has no divergence
-// and no exec-masked memory op.  Block j needs the 16-byte native units N and
-// N + 16 (N = e - (e & 15) - 16 (Kmax - j)), requested up to 17 at a time
-// before the fold (memory-level parallelism); loads are clamped to the units
-// that hold packet bytes (never another page) and whatever a clamped unit
-// holds is masked away by packet-relative offset.  A block's words come out
-// of the two units by a 2-level word funnel and v_alignbyte (phase e & 15).
-// =======================================================================
-__device__ __forceinline__ uint32_t small_word(uint32_t w, int r) {  // r = packet-relative offset of byte 0
-  const uint32_t keep = byte_span_mask(-r, 4);            // bytes at r >= 0: packet data
-  const uint32_t pre = byte_span_mask(-4 - r, -r);        // bytes at -4 <= r < 0: the 0xFF prefix
-  // invariant fields -> 0xFF; outside [0, 40) the shifted map is empty, so no
-  // range test (a select on r became a divergent branch)
-  const uint32_t sh = (uint32_t)(r + 3 < 0 ? 0 : r + 3 > 63 ? 63 : r + 3);
-  const uint32_t bits = (uint32_t)(((kMaskBits << 3) >> sh) & 0xFu);
-  return (w & keep) | pre | (expand_nibble(bits) & keep);
-}
-
-// small_word for a word-aligned r (a multiple of 4): whole-word keep, the
-// 0xFF prefix word at -4, the IPv4 mask words of offsets 0, 8, 24, 32.
-__device__ __forceinline__ uint32_t small_word_aligned(uint32_t w, int r) {
-  const uint32_t keep = (uint32_t)(r >= 0) * 0xFFFFFFFFu;
-  const uint32_t orm = ((uint32_t)(r == -4) * 0xFFFFFFFFu) | ((uint32_t)(r == 0) * kMaskW0) |
-                       ((uint32_t)(r == 8) * kMaskW2) | ((uint32_t)(r == 24) * kMaskW6) |
-                       ((uint32_t)(r == 32) * kMaskW8);
-  return (w & keep) | orm;
-}
-
-// One packet's stream in icrc_rsmall_kernel.
-struct SmallPk {
-  uint64_t ufirst, ulast, N0;  // the packet's first / last 16-byte unit, native unit of block 0
-  uint32_t sb, m2, m1;         // end phase: byte shift, word-shift selects (all ones / zero)
-  int rel;                     // packet-relative offset of the next block
-  uint32_t reg;
-
-  __device__ __forceinline__ void init(const RsDesc &d, uint32_t Kmax) {
-    const uint64_t addr = ((uint64_t)(d.hi & 0xFFFFu) << 32) | d.lo;
-    const uint32_t M = (d.hi >> 16) - 4u;
-    const uint64_t e = addr + M;
-    const uint32_t t = (uint32_t)(e & 15u);
-    sb = t & 3u;
-    m2 = 0u - ((t >> 3) & 1u);
-    m1 = 0u - ((t >> 2) & 1u);
-    ufirst = addr & ~15ull;
-    ulast = (e - 1u) & ~15ull;
-    N0 = e - t - 16ull * Kmax;
-    rel = (int)M - 16 * (int)Kmax;
-    reg = 0u;
-  }
-  __device__ __forceinline__ u32x4 unit(uint32_t k) const {  // native unit k, clamped to the packet's
-    uint64_t u = N0 + 16ull * k;
-    u = u < ufirst ? ufirst : (u > ulast ? ulast : u);
-    return gload16(u);  // plain: non-temporal scattered unit reads took 69 instead of 40 us on C4
-  }
-  // Blocks j0 .. j0 + KB - 1: all KB + 1 units they need are requested at
-  // once, then folded.  (A ring of 4-8 units in flight measured ~2x slower
-  // on C4's scattered small packets, tools/microbench/mb_scatter.hip: the
-  // memory-level parallelism of one lane is what these reads need.)
-  // WA: every packet of the wave starts and ends on a 4-byte word (the wave-
-  // uniform common case: C4, NIC rings): no byte shift, whole-word masks.
-  // MASK: which blocks get the head masks (prefix / invariant fields / bytes
-  // before the packet), branch-free: 1 = blocks 0..3 (the first chunk of a
-  // wave whose packets all start their heads there: M >= 16 Kmax - 24), 2 = all
-  // (lanes with shorter packets start later), 0 = none.  (A wave-uniform
-  // branch on "is some lane in its head" made the compiler wait for every
-  // outstanding load (vmcnt(0)) before each block: 2x slower.)
-  template <int KB, bool WA, int MASK>
-  __device__ __forceinline__ void chunk(const uint32_t *lds, const LaneTab &lt, uint32_t j0) {
-    u32x4 U[KB + 1];
-#pragma unroll
-    for (int k = 0; k <= KB; ++k) U[k] = unit(j0 + k);
-    blocks<KB, WA, MASK>(lds, lt, U);
-  }
-  // Fold blocks 0 .. KB-1 of units U (block j from units j, j + 1).
-  template <int KB, bool WA, int MASK>
-  __device__ __forceinline__ void blocks(const uint32_t *lds, const LaneTab &lt, const u32x4 (&U)[KB + 1]) {
-#pragma unroll
-    for (int j = 0; j < KB; ++j) {
-      // Block j's 4 words from units j, j + 1: X[k] = W[(t >> 2) + k] by
-      // bitwise selects (written as ternaries, the compiler turned the
-      // funnel into a dynamically indexed array in scratch), then
-      // v_alignbyte by the byte phase.
-      const u32x4 c = U[j], n = U[j + 1];
-      const uint32_t W[8] = {c[0], c[1], c[2], c[3], n[0], n[1], n[2], n[3]};
-      uint32_t V[6], X[5], w[4];
-#pragma unroll
-      for (int k = 0; k < 6; ++k) V[k] = __builtin_amdgcn_bitop3_b32(m2, W[k + 2], W[k], 0xCA);
-#pragma unroll
-      for (int k = 0; k < 5; ++k) X[k] = __builtin_amdgcn_bitop3_b32(m1, V[k + 1], V[k], 0xCA);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) w[i] = WA ? X[i] : __builtin_amdgcn_alignbyte(X[i + 1], X[i], sb);
-      if (MASK == 2 || (MASK == 1 && j < 4)) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) w[i] = WA ? small_word_aligned(w[i], rel + 4 * i) : small_word(w[i], rel + 4 * i);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) reg = step4(lds, lt, reg, w[i]);
-      rel += 16;
-    }
-  }
-};
-
-// The ICRC of every lane's one-line packet d: wave-collective (every lane of
-// the wave calls it together; a lane without a packet passes a copy of a
-// valid descriptor and ignores the result), since the wave's shape -- its
-// largest block count, whether every packet is word-aligned, half-line --
-// is decided by ballots.  lds: the slice-by-4 tables (fill_tables).
-__device__ __forceinline__ uint32_t small_icrc(const uint32_t *lds, const LaneTab &lt, const RsDesc &d,
-                                               uint32_t lane) {
-  uint32_t K = (((d.hi >> 16) - 4u) + 4u + 15u) >> 4;  // this lane's blocks
-  // the wave's largest, rounded up to a multiple of 4: by ballots for
-  // one-line packets (K <= 8), a shuffle reduction beyond
-  uint32_t Kmax;
-  if (__builtin_amdgcn_ballot_w64(K > 4u) == 0) {
-    Kmax = 4u;
-  } else if (__builtin_amdgcn_ballot_w64(K > 8u) == 0) {
-    Kmax = 8u;
-  } else {
-#pragma unroll
-    for (int w = 32; w >= 1; w >>= 1) K = max(K, (uint32_t)__shfl_xor((int)K, w));
-    Kmax = __builtin_amdgcn_readfirstlane((K + 3u) & ~3u);
-  }
-  // wave-uniform variants: word-aligned packets; every packet's head in blocks 0..3
-  const bool wa = __builtin_amdgcn_ballot_w64(((d.lo | (d.hi >> 16)) & 3u) != 0) == 0;
-  // heads in blocks 0..3: rel_4 = M - 16 Kmax + 64 >= 40 for every lane
-  const bool uk = __builtin_amdgcn_ballot_w64((d.hi >> 16) - 4u + 24u < 16u * Kmax) == 0;
-  // Half-line packets: every covered byte in one aligned 64-byte half
-  // line hb .. hb + 63 whose last 16-byte unit holds the covered end, not
-  // at the half line's end (C4's 64-byte packets: 64-byte aligned, 60
-  // covered bytes).  For a wave of them the 5 units of the 4 blocks are
-  // the half line's units 0, 0, 1, 2, 3, and they are read coalesced: in
-  // load c the 4 lanes of quad p read units 0..3 of lane 4 p + c's half
-  // line (64 contiguous bytes), and a 4 x 4 quad transpose hands every lane
-  // its own -- instead of every lane reading its packet's units alone, 64
-  // lines apart (the access pattern that costs C1's direct kernel, see the
-  // quad kernel in icrc_kernels.hip).
-  const uint64_t pa = ((uint64_t)(d.hi & 0xFFFFu) << 32) | d.lo;
-  const uint64_t pe = pa + ((d.hi >> 16) - 4u);
-  const uint64_t hb = (pe - 1u) & ~63ull;
-  const bool half = pa >= hb && ((uint32_t)pe & 63u) > 48u;
-  SmallPk P;
-  if (Kmax == 4u && __builtin_amdgcn_ballot_w64(!half) == 0) {  // wave-uniform: a wave of half-line packets
-    const uint32_t hlo = (uint32_t)hb, hhi = (uint32_t)(hb >> 32), q = lane & 3u;
-    auto at = [&](uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32 | lo) + 16u * q; };
-    u32x4 H[4];
-    H[0] = gload16(at(dpp_quad_bcast<0>(hlo), dpp_quad_bcast<0>(hhi)));
-    H[1] = gload16(at(dpp_quad_bcast<1>(hlo), dpp_quad_bcast<1>(hhi)));
-    H[2] = gload16(at(dpp_quad_bcast<2>(hlo), dpp_quad_bcast<2>(hhi)));
-    H[3] = gload16(at(dpp_quad_bcast<3>(hlo), dpp_quad_bcast<3>(hhi)));
-    quad_transpose(H, lane & 3u);
-    const u32x4 U[5] = {H[0], H[0], H[1], H[2], H[3]};
-    P.init(d, 4u);
-    if (wa && uk)
-      P.blocks<4, true, 1>(lds, lt, U);
-    else if (uk)
-      P.blocks<4, false, 1>(lds, lt, U);
-    else
-      P.blocks<4, false, 2>(lds, lt, U);
-    return ~P.reg;
-  }
-  P.init(d, Kmax);
-  auto run = [&](auto words, auto uniform) __attribute__((always_inline)) {
-    constexpr bool WA = decltype(words)::value;
-    constexpr int M1 = decltype(uniform)::value ? 1 : 2, M2 = decltype(uniform)::value ? 0 : 2;
-    // Kmax = 8 q + r (r = 0 or 4): a first chunk of r or 8 blocks, then
-    // chunks of 8 (one-line packets: M <= 124, Kmax <= 8 -- one chunk, at
-    // most 9 units = 36 VGPRs in flight)
-    uint32_t j = 0;
-    if ((Kmax & 7u) == 4u) {  // wave-uniform
-      P.chunk<4, WA, M1>(lds, lt, 0);
-      j = 4;
-    } else {
-      P.chunk<8, WA, M1>(lds, lt, 0);
-      j = 8;
-    }
-    for (; j < Kmax; j += 8) P.chunk<8, WA, M2>(lds, lt, j);
-  };
-  if (wa && uk)
-    run(std::true_type{}, std::true_type{});
-  else if (uk)
-    run(std::false_type{}, std::true_type{});
-  else
-    run(std::false_type{}, std::false_type{});
-  return ~P.reg;
 }
 
 // The small pool [0, ctr->small), one round of 64 packets per wave at a time
@@ -1071,7 +1140,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rsmall_kernel(RsckArgs a) {
   for (; base < count; base += step) {
     const RsDesc d = dn;
     dn = desc_at(base + step + lane);  // the next round's descriptors, in flight meanwhile
-    const uint32_t v = small_icrc(lds, lt, d, lane);
+    const uint32_t v = small_icrc(Step4{lds, lt}, d, lane);
     const uint32_t pos = base + lane;
     __builtin_amdgcn_raw_buffer_store_b32(v, ro, pos < count ? 4u * pos : 0x7FFFFFF0u, 0, 0);
   }
@@ -1129,7 +1198,7 @@ __global__ __launch_bounds__(kPassBlock) void rsck_gather(RsckArgs a) {
     for (uint32_t j0 = 0; j0 < B.small; j0 += blockDim.x) {
       const uint32_t j = j0 + threadIdx.x;
       if (j0 + (threadIdx.x & ~63u) < B.small) {  // wave-uniform
-        const uint32_t v = small_icrc(tab, lt, j0 ? small_desc(j) : sd0, lane);
+        const uint32_t v = small_icrc(Step4{tab, lt}, j0 ? small_desc(j) : sd0, lane);
         if (j < B.small) store(j, v);
       }
     }
@@ -1314,7 +1383,8 @@ hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, hipStream_t st, hipE
   if (a.count > kRsMaxCount) return hipErrorInvalidValue;
   // a.ctr is zero here: zeroed when the workspace was allocated, and again
   // by rsck_gather at the end of every call.
-  const PassShape ps = pass_shape(a.count, pass_cap, a.no_split != 0);
+  PassShape ps = pass_shape(a.count, pass_cap, a.no_split != 0);
+  if (a.small_in_fold) ps.fused = ps.split = false;  // the fold takes the one-line packets: a plain gather
   a.nblk = (uint32_t)ps.grid;
   // RICRC_PASS_TIMES: timing events between the passes on st (diagnostics)
   auto mark = [&](int k) { if (pass_ev) (void)hipEventRecord(pass_ev[k], st); };
@@ -1328,7 +1398,7 @@ hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, hipStream_t st, hipE
   // on 1/16 of the CUs on a second stream beside the fold instead: the step
   // took 1.050 against 0.999 ms -- its scattered half-line reads slowed the
   // fold by 60 us, profiles/r04/s2_*.)
-  if (!ps.fused) hipLaunchKernelGGL(icrc_rsmall_kernel, dim3(grid), dim3(kBlock), 0, st, a);
+  if (!ps.fused && !a.small_in_fold) hipLaunchKernelGGL(icrc_rsmall_kernel, dim3(grid), dim3(kBlock), 0, st, a);
   mark(3);
   launch_gather(a, ps, st);
   mark(4);

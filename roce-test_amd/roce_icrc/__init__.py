@@ -114,7 +114,7 @@ _SIG = {
 class LaunchInfo(ctypes.Structure):
     """``ricrc_launch_info_t`` (include/roce_icrc.h)."""
     _fields_ = [("grid", _u32), ("xcd_weights", _u32 * 8), ("start_xcd", _u32), ("pass_grid", _u32),
-                ("pass_unroll", _u32), ("fused", _u32), ("gather_grid", _u32)]
+                ("pass_unroll", _u32), ("one_line", _u32), ("gather_grid", _u32)]
 
 
 class ICRCError(RuntimeError):
@@ -546,8 +546,8 @@ class Context:
             raise ICRCError(rc, "ricrc_launch_info")
         d = {"grid": info.grid, "xcd_weights": list(info.xcd_weights), "start_xcd": info.start_xcd}
         if info.pass_grid:
-            d.update(pass_grid=info.pass_grid, pass_unroll=info.pass_unroll, one_line_in_gather=bool(info.fused),
-                     gather_grid=info.gather_grid)
+            d.update(pass_grid=info.pass_grid, pass_unroll=info.pass_unroll,
+                     one_line_in=("kernel", "gather", "fold")[info.one_line], gather_grid=info.gather_grid)
         return d
 
     def prime(self, usec: int = 20000, dev: int = 0) -> None:

@@ -137,14 +137,11 @@ def test_kernel_labels_follow_the_dispatch():
     assert "(icrc_tsk_kernel)" in lab("--size", "256")
     mixa = bench.parse(["--mix"])
     mix = bench.kernel_label(mixa, count=mixa.count)  # C4's 4 M packets: the ragged pipeline's passes, in launch order
-    assert mix.split(" -> ") == ["bucket pass (rsck_bucket)",
-                                 "strided-chain fold of packets of >= 2 lines (icrc_rsck_kernel)",
-                                 "one-line packets (icrc_rsmall_kernel)", "gather (rsck_gather)"]
-    # C4's 8-GPU shard (about 524 K packets): the gather folds the one-line packets
+    fold = "strided-chain fold (8 packets of >= 2 lines a group; one-line packets one a lane) (icrc_rsck_kernel)"
+    assert mix.split(" -> ") == ["bucket pass (rsck_bucket)", fold, "gather (rsck_gather)"]
+    # C4's 8-GPU shard (about 524 K packets): the same three passes
     shard = bench.kernel_label(bench.parse(["--mix", "--count", "524288"]), count=524288)
-    assert shard.split(" -> ") == ["bucket pass (rsck_bucket)",
-                                   "strided-chain fold of packets of >= 2 lines (icrc_rsck_kernel)",
-                                   "gather, folding the one-line packets (rsck_gather)"]
+    assert shard == mix
     # a framed 4 KiB NIC ring (L3 at 14): the SCK's framed variant over the slots
     assert "(icrc_sck_kernel)" in lab("--l3-offset", "14", "--stride", "4096")
     assert "(rsck_bucket)" in lab("--l3-offset", "14", "--stride", "1536")

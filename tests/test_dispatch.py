@@ -46,6 +46,8 @@ def test_rings_with_slot_lengths():
 
 
 def test_ragged_batches():
-    assert path(count=4 << 20, offsets=OFF, lengths=LEN) == \
-        "rsck_bucket+icrc_rsck_kernel+icrc_rsmall_kernel+rsck_gather"
+    """The fold kernel takes the one-line packets at every size (a separate
+    one-line kernel only under RICRC_ONE_LINE_IN_GATHER=1 beyond 524,288 packets,
+    tests/test_gpu_parity.py)."""
+    assert path(count=4 << 20, offsets=OFF, lengths=LEN) == "rsck_bucket+icrc_rsck_kernel+rsck_gather"
     assert path(count=524288, offsets=OFF, lengths=LEN) == "rsck_bucket+icrc_rsck_kernel+rsck_gather"

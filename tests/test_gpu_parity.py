@@ -256,14 +256,19 @@ def test_ragged_bucket_17_per_thread_one_round_unstaged(ctx, ctx_env):
 
 
 @pytest.mark.parametrize("count", [3000, 30_000, 200_000, 524_288])
-def test_gather_small_sides(ctx, ctx_env, count):
-    """Batches whose bucket pass runs on at most half the CUs (<= 524,288
-    packets: 4 per thread on <= 128 blocks) launch the gather on twice the
-    blocks: block nblk + b folds pass block b's one-line packets and writes
-    their out[i] itself, block b gathers the rest.  Every class (one-line,
-    2-3 lines, long), short packets finished in the gather (n < 44), invalid
-    lengths, verify mode -- the same words as with RICRC_NO_GATHER_SPLIT
-    (the pass grid's own blocks fold the one-line packets) and the oracle."""
+def test_one_line_packets_three_ways(ctx, ctx_env, count):
+    """The one-line packets of a ragged batch are folded by the fold kernel
+    (default: rounds of 64, one lane per packet, dealt to wave slots 0..11
+    before their groups; RICRC_SMALL_SLOTS=0: to every wave by its share of
+    the work), or, with
+    RICRC_ONE_LINE_IN_GATHER, by the gather: for batches whose bucket pass runs
+    on at most half the CUs (<= 524,288 packets: 4 per thread on <= 128
+    blocks) on twice the blocks, block nblk + b folding pass block b's
+    one-line packets and writing their out[i] itself ("small sides"), or with
+    RICRC_NO_GATHER_SPLIT too by the pass grid's own blocks.  Every class
+    (one-line, 2-3 lines, long), short packets finished in the gather
+    (n < 44), invalid lengths, verify mode -- the same words all three ways
+    and from the oracle."""
     import roce_icrc
 
     rng = np.random.default_rng(count)
@@ -277,14 +282,17 @@ def test_gather_small_sides(ctx, ctx_env, count):
     want = oracle_c.icrc_batch(buf, offsets=offs, lengths=lens, threads=16)
     want[bad] = 0
     d_buf, d_offs, d_lens = _dev(buf), _dev(offs), _dev(lens_dev)
-    whole = ctx_env(RICRC_NO_GATHER_SPLIT=1)
-    li, lw = ctx.launch_info(d_buf, count, offsets=d_offs, lengths=d_lens), \
-        whole.launch_info(d_buf, count, offsets=d_offs, lengths=d_lens)
-    assert li["one_line_in_gather"] and li["gather_grid"] == 2 * li["pass_grid"] <= 256
-    assert lw["gather_grid"] == lw["pass_grid"] == li["pass_grid"]
-    assert roce_icrc.kernel_path(d_buf, count, offsets=d_offs, lengths=d_lens, ctx=ctx) == \
-        "rsck_bucket+icrc_rsck_kernel+rsck_gather"
-    for c in (ctx, whole):
+    sides = ctx_env(RICRC_ONE_LINE_IN_GATHER=1)
+    whole = ctx_env(RICRC_ONE_LINE_IN_GATHER=1, RICRC_NO_GATHER_SPLIT=1)
+    prop = ctx_env(RICRC_SMALL_SLOTS=0)  # the fold's rounds dealt by each wave's work, not to slots 0..11
+    lf, li, lw = (c.launch_info(d_buf, count, offsets=d_offs, lengths=d_lens) for c in (ctx, sides, whole))
+    assert lf["one_line_in"] == "fold" and lf["gather_grid"] == lf["pass_grid"]
+    assert li["one_line_in"] == "gather" and li["gather_grid"] == 2 * li["pass_grid"] <= 256
+    assert lw["one_line_in"] == "gather" and lw["gather_grid"] == lw["pass_grid"] == li["pass_grid"]
+    for c in (ctx, sides, whole):
+        assert roce_icrc.kernel_path(d_buf, count, offsets=d_offs, lengths=d_lens, ctx=c) == \
+            "rsck_bucket+icrc_rsck_kernel+rsck_gather"
+    for c in (ctx, sides, whole, prop):
         out = _out(count)
         c.batch_device(d_buf, count, out, offsets=d_offs, lengths=d_lens, stream=_stream())
         np.testing.assert_array_equal(_host_u32(out), want)
@@ -295,11 +303,28 @@ def test_gather_small_sides(ctx, ctx_env, count):
             o = int(offs[i]) + int(lens[i]) - 4
             stamped[o:o + 4] = np.frombuffer(int(want[i]).to_bytes(4, "little"), np.uint8)
             want_v[i] = 1
-    for c in (ctx, whole):
+    for c in (ctx, sides, whole):
         out = _out(count)
         c.batch_device(_dev(stamped), count, out, offsets=d_offs, lengths=d_lens, stream=_stream(), verify=True)
         got = _host_u32(out)
         np.testing.assert_array_equal(got[::7], want_v[::7])
+
+
+@pytest.mark.parametrize("n", [60, 64, 65, 66, 67])
+def test_one_line_half_line_waves(ctx, n):
+    """One-line packets that each sit in one aligned 64-byte half line, a
+    whole wave of them: the coalesced half-line path folds 4 blocks, so only
+    packets of <= 60 covered bytes (n <= 64) may take it; n = 65..67 still
+    sit in one half line but need a fifth block for the 0xFF prefix."""
+    rng = np.random.default_rng(n)
+    count = 5000
+    offs = (np.arange(count, dtype=np.uint64) * 128) + (rng.integers(0, 2, size=count).astype(np.uint64) * 64)
+    lens = np.full(count, n, np.uint32)
+    buf = rng.integers(0, 256, size=count * 128 + 64, dtype=np.uint8)
+    want = oracle_c.icrc_batch(buf, offsets=offs, lengths=lens, threads=16)
+    out = _out(count)
+    ctx.batch_device(_dev(buf), count, out, offsets=_dev(offs), lengths=_dev(lens), stream=_stream())
+    np.testing.assert_array_equal(_host_u32(out), want)
 
 
 def test_ragged_kernel_offsets_only_and_lengths_only(ctx):

@@ -329,6 +329,21 @@ def test_ragged_finish_nibble_tables():
         assert _nib_mul(xt, u) == o.gf_mul(u, X)
 
 
+def test_fold_one_line_nibble_step():
+    """icrc_rsck.hip StepNib (the fold kernel's one-line packets, whose LDS
+    tables advance 128 bytes a step): the x^32 nibble table (icrc_math.h
+    build_fin_tables, kFinStep4) gives the slice-by-4 step's register,
+    r, w -> (r ^ w) x^32."""
+    rng = random.Random(32)
+    X32 = ONE
+    for _ in range(32):
+        X32 = o.gf_mul(X32, ONE >> 1)
+    xt = [o.gf_mul(X32, v << (4 * w)) for w in range(8) for v in range(16)]
+    for _ in range(300):
+        r, w = rng.getrandbits(32), rng.getrandbits(32)
+        assert _nib_mul(xt, r ^ w) == fold(r, w.to_bytes(4, "little"))
+
+
 def test_ragged_tz_bases_compact():
     """Basis word 4q of x^(-8 tz) is x^(-8 tz) x^(31 - 4q) = x^(31 - 4 (2 tz + q)),
     so the kernel's table needs one entry per m = 2 tz + q (264 words, host
