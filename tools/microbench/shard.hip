@@ -92,6 +92,7 @@ int main(int argc, char **argv) {
   RsckArgs a{};
   a.base = buf; a.off = d_off; a.len = d_len; a.count = count;
   a.out = out; a.tzb = tzb; a.group_cost = kRsGroupCost;
+  a.small_in_fold = 1u; a.small_slots = kRsSmallSlots;  // the product's defaults (icrc_api.cpp)
   a.fin = mb_fin();
   for (int k = 0; k < 8; ++k) a.xw[k] = 1000u + ((k & 1) ? -40 : 40);
   rs_bind_workspace(a, ws);
