@@ -50,7 +50,7 @@ struct RsDesc {
 // 8 packets of equal line count per group, folded as in the SCK.
 // Classes: 0 = not bucketed (n < 44 or n > 65535: done in the bucket pass);
 // 1 + P for packets spanning <= kRsSmallL lines, by their 64-byte piece count P
-// (one lane per packet, icrc_rsmall_kernel: 8 lanes per packet is too coarse
+// (one lane per packet, in the fold's small rounds: 8 lanes per packet is too coarse
 // for them); kRsBigBase + L for the rest, by line count L (the strided-chain
 // fold).
 #ifndef RICRC_RS_SMALL_L  // tools/microbench only
@@ -138,7 +138,7 @@ void rs_bind_workspace(RsckArgs &a, void *ws);
 // Zeroes a workspace's counters (on allocation; afterwards every call
 // leaves them zero).
 hipError_t rs_zero_counters(void *ws, hipStream_t st);
-// The whole ragged pipeline on `st`: bucket, fold, one-line fold, gather.
+// The whole ragged pipeline on `st`: bucket, fold (one-line packets included), gather.
 // count <= kRsMaxCount (the host cuts larger batches: the big pool's group
 // count must fit kRsGroupBits).
 constexpr uint64_t kRsMaxCount = 1ull << 28;

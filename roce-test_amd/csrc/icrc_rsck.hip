@@ -20,9 +20,11 @@
 //                   tables in LDS -- with a load cursor running ahead of the
 //                   fold cursor across group boundaries, descriptors read 64
 //                   at a time, waves splitting the big pool by weighted work;
-//  3. icrc_rsmall_kernel folds the one-line packets (C4's 64 B; 8 lanes per
-//                   packet is too coarse for them) one lane per packet;
-//  4. rsck_gather   out[i] = res[pos(i)] (verify mode: the trailer compared
+//                   and, in rounds of 64 on wave slots 0..11, the one-line
+//                   packets (C4's 64 B; 8 lanes per packet is too coarse for
+//                   them) one lane per packet (RICRC_ONE_LINE_IN_GATHER: a
+//                   separate icrc_rsmall_kernel, or the gather, folds them);
+//  3. rsck_gather   out[i] = res[pos(i)] (verify mode: the trailer compared
 //                   with it); packets too short for a RoCEv2 header
 //                   (4 <= n < 44) are computed here by a scalar loop, invalid
 //                   lengths yield 0.
@@ -1393,8 +1395,9 @@ hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, hipStream_t st, hipE
   mark(1);
   hipLaunchKernelGGL((icrc_rsck_kernel<0>), dim3(grid), dim3(kBlock), 0, st, a);
   mark(2);
-  // the small pool [0, ctr->small): one lane per packet, unless the gather
-  // folds each block's one-line packets itself (ps.fused).  (Round 4 ran it
+  // RICRC_ONE_LINE_IN_GATHER: the small pool [0, ctr->small) one lane per
+  // packet here, unless the gather folds each block's one-line packets
+  // itself (ps.fused); by default the fold took them.  (Round 4 ran it
   // on 1/16 of the CUs on a second stream beside the fold instead: the step
   // took 1.050 against 0.999 ms -- its scattered half-line reads slowed the
   // fold by 60 us, profiles/r04/s2_*.)
