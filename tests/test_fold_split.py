@@ -78,3 +78,43 @@ def test_wave_shares_partition_the_pool():
                 for q in range(first_at(blk, runs, NG, S, x0), first_at(blk, runs, NG, S, x1)):
                     seen[q] += 1
         assert seen == [1] * NG
+
+
+def small_rounds(NC, NG, S, grid, b, wid, x0, x1, slots):
+    """icrc_rsck_kernel's small rounds [c_begin, c_end) of wave wid of
+    workgroup b: dealt evenly to wave slots 0..slots-1, or (slots = 0, or
+    no big pool) the wave's fraction [x0, x1) / T of them."""
+    T = S if NG else NC
+    c0, c1 = min(x0, T) * NC // T, min(x1, T) * NC // T
+    if slots and NG:
+        E, e = grid * slots, b * slots + wid
+        c0, c1 = (e * NC // E, (e + 1) * NC // E) if wid < slots else (0, 0)
+    return c0, c1
+
+
+def test_small_rounds_partition_the_small_pool():
+    """The fold's rounds of 64 one-line packets: every round folded by exactly
+    one wave, for slot dealing (kRsSmallSlots = 12, RICRC_SMALL_SLOTS) and the
+    share-proportional rule, with and without a big pool and XCD weights."""
+    rng = random.Random(11)
+    for _ in range(300):
+        NC = rng.choice([1, 2, 63, 64, 2048, 16384, rng.randrange(1, 5000)])
+        NG = rng.choice([0, 1, 7, 1000])
+        S = NG * rng.choice([16, 20, 144])
+        T = S if NG else NC
+        grid = rng.choice([1, 3, 16, 256])
+        slots = rng.choice([0, 1, 4, 12, 16])
+        xw, xk = rng.choice([None, [1040, 960] * 4, [3, 7, 1, 8000, 2, 2, 5, 9]]), rng.randrange(8)
+        nw = grid * KW
+        share = (T + nw - 1) // nw
+        seen = [0] * NC
+        for b in range(grid):
+            for wid in range(KW):
+                x0 = min((b * KW + wid) * share, T)
+                x1 = x0 + share
+                if xw:
+                    x0, x1 = xcd_share(T, xw, xk, b, grid, wid)
+                c0, c1 = small_rounds(NC, NG, S, grid, b, wid, x0, x1, slots)
+                for c in range(c0, c1):
+                    seen[c] += 1
+        assert seen == [1] * NC, (NC, NG, grid, slots)
