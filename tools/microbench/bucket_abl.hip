@@ -11,6 +11,7 @@
 #include "mb_fin.h"
 #include <stdio.h>
 #include <stdlib.h>
+#include <string>
 #include <vector>
 #include <algorithm>
 using namespace ricrc;
@@ -58,7 +59,9 @@ __global__ void fill_random(uint64_t *p, uint64_t n) {
 int main(int argc, char **argv) {
   hipDeviceProp_t p; CK(hipGetDeviceProperties(&p, 0));
   const int grid = p.multiProcessorCount;
-  const uint64_t count = 4ull << 20;
+  // "shard": C4's 8-GPU shard, 524,288 packets, on the product's pass shape (U = 4, 128 blocks)
+  const bool shard = argc > 1 && std::string(argv[1]) == "shard";
+  const uint64_t count = shard ? 524288ull : 4ull << 20;
   std::vector<uint64_t> off(count); std::vector<uint32_t> len(count);
   uint64_t x = 0x1234567ull, pos = 0;
   const uint32_t sizes[4] = {64, 256, 1024, 4096};
@@ -82,7 +85,7 @@ int main(int argc, char **argv) {
   void *ws; CK(hipMalloc(&ws, rs_workspace_bytes(count)));
   CK(rs_zero_counters(ws, 0));
   rs_bind_workspace(a, ws);
-  const int pgrid = kPassBlocks;
+  const int pgrid = shard ? 128 : kPassBlocks;
   a.nblk = pgrid;
   printf("C4-shaped batch: %llu packets, %llu B; pass grid %d x %d, fold grid %d\n", (unsigned long long)count,
          (unsigned long long)pos, pgrid, kPassBlock, grid);
@@ -96,7 +99,8 @@ int main(int argc, char **argv) {
     constexpr int ABL = decltype(abl)::value;
     return timeit([&] {
       CK(rs_zero_counters(ws, 0));
-      hipLaunchKernelGGL((rsck_bucket<true, true, ABL>), dim3(pgrid), dim3(kPassBlock), 0, 0, a);
+      if (shard) hipLaunchKernelGGL((rsck_bucket<true, true, ABL, 4>), dim3(pgrid), dim3(kPassBlock), 0, 0, a);
+      else hipLaunchKernelGGL((rsck_bucket<true, true, ABL>), dim3(pgrid), dim3(kPassBlock), 0, 0, a);
     }, 20);
   };
   const float zero = timeit([&] { CK(rs_zero_counters(ws, 0)); }, 20);
@@ -114,6 +118,7 @@ int main(int argc, char **argv) {
     rep("bucket: full, no stores", bucket(std::integral_constant<int, 8 | 16>{}));
     rep("bucket: no staging, no pos_of stores", bucket(std::integral_constant<int, 32 | 8>{}));
     rep("bucket: no staging, no descriptor stores", bucket(std::integral_constant<int, 32 | 16>{}));
+    if (shard) continue;  // (the rest times the 4 M layout's other passes)
     // the rest of the pipeline on the product's layout
     CK(rs_zero_counters(ws, 0));
     hipLaunchKernelGGL((rsck_bucket<true, true, 0>), dim3(pgrid), dim3(kPassBlock), 0, 0, a);
