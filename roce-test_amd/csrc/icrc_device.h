@@ -24,9 +24,7 @@ static constexpr int kLdsWords = 32768;  // 128 KiB
 // workgroup b is on XCD (b + k) % 8.  w and k come from the host or from an
 // earlier kernel of the same stream, so every wave uses the same values: the
 // shares are contiguous, in wave order, and cover [0, total) for any k; a
-// wrong k costs speed, never a packet.  The products total * before stay
-// below 2^64: total < 2^39.01 (the ragged pool's bound) and the host caps
-// the weights (RICRC_XCD_WEIGHTS <= 8000 each, icrc_api.cpp).
+// wrong k costs speed, never a packet.
 __device__ __forceinline__ void xcd_share(uint64_t total, const uint32_t (&w)[8], uint32_t k, uint32_t wid,
                                           uint64_t &lo, uint64_t &hi) {
   const uint64_t b = blockIdx.x, nb = gridDim.x;
@@ -41,8 +39,17 @@ __device__ __forceinline__ void xcd_share(uint64_t total, const uint32_t (&w)[8]
   const uint64_t wb = w[(b + k) & 7u];
   const uint64_t before = (uint64_t)kWaves * cum(b) + wid * wb;
   const uint64_t wtot = (uint64_t)kWaves * cum(nb);
-  lo = total * before / wtot;
-  hi = total * (before + wb) / wtot;
+  // The boundary at weight x, total * x / wtot, in double precision: a
+  // 64-bit integer division is a long software expansion ahead of the
+  // wave's first loads.  Monotonic in x and the same for both waves that
+  // share a boundary, exact at 0 and at wtot: still a partition.
+  const double f = (double)total / (double)wtot;
+  auto at = [&](uint64_t x) -> uint64_t {
+    const uint64_t r = (uint64_t)((double)x * f);
+    return x >= wtot || r > total ? total : r;
+  };
+  lo = at(before);
+  hi = at(before + wb);
 }
 
 // Workgroup 0 records the XCD it runs on (HW_REG_XCC_ID) for the host's next

@@ -696,9 +696,14 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
   const uint64_t wave = (uint64_t)blockIdx.x * kWaves + wid;
   const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
   const uint64_t T = NG ? S : NC;  // the work split's total (the small rounds when no packet has >= 2 lines)
-  const uint64_t share = (T + nwaves - 1) / nwaves;
-  uint64_t x0 = wave * share < T ? wave * share : T, x1 = x0 + share;
-  if (a.xw[0] != 0u) xcd_share(T, a.xw, C.xcd, wid, x0, x1);  // weighted by XCD
+  uint64_t x0, x1;
+  if (a.xw[0] != 0u) {
+    xcd_share(T, a.xw, C.xcd, wid, x0, x1);  // weighted by XCD
+  } else {
+    const uint64_t share = (T + nwaves - 1) / nwaves;
+    x0 = wave * share < T ? wave * share : T;
+    x1 = x0 + share;
+  }
   // the pass block whose work range holds x (ballots over the loaded ranges)
   auto block_of = [&](uint64_t x) -> uint32_t {
     uint32_t b = 0;
@@ -747,8 +752,10 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
         const uint32_t L = __builtin_amdgcn_readlane(Q.L, r);
         const uint64_t s0 = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(Q.s0 >> 32), r) << 32) |
                             __builtin_amdgcn_readlane((uint32_t)Q.s0, r);
-        const uint64_t w = 4u * L + a.group_cost;  // quarter line-steps
-        const uint64_t q = g0 + (x - s0 + w - 1) / w;
+        // x - s0 < gs w < 2^24 (a pass block's run): a 32-bit division (a
+        // 64-bit one is a long expansion on the start-up's critical path)
+        const uint32_t w = 4u * L + a.group_cost;  // quarter line-steps
+        const uint64_t q = g0 + ((uint32_t)(x - s0) + w - 1u) / w;
         const uint32_t gend = g0 + gs < NG ? g0 + gs : NG;  // (never past the pool)
         return q < gend ? (uint32_t)q : gend;
       }

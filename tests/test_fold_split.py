@@ -27,7 +27,12 @@ def xcd_share(total, w, k, b, nb, wid):
     wb = w[(b + k) & 7]
     before = KW * cum(b) + wid * wb
     wtot = KW * cum(nb)
-    return total * before // wtot, total * (before + wb) // wtot
+    f = float(total) / float(wtot)  # double precision, as the kernel (a monotonic map, exact at 0 and wtot)
+
+    def at(x):
+        r = int(float(x) * f)
+        return total if x >= wtot or r > total else r
+    return at(before), at(before + wb)
 
 
 def layout(rng, nblk):
@@ -78,6 +83,25 @@ def test_wave_shares_partition_the_pool():
                 for q in range(first_at(blk, runs, NG, S, x0), first_at(blk, runs, NG, S, x1)):
                     seen[q] += 1
         assert seen == [1] * NG
+
+
+def test_xcd_shares_tile_large_totals():
+    """xcd_share's double-precision boundaries at the ragged pool's full range
+    (total < 2^39.01) and the weight cap (8000): contiguous, ordered shares
+    from 0 to total, wave after wave."""
+    rng = random.Random(3)
+    for _ in range(60):
+        total = rng.choice([1, 7, 4096, rng.randrange(1, 1 << 39), (1 << 39) - 1])
+        grid = rng.choice([1, 3, 240, 256])
+        w = rng.choice([[1040, 960] * 4, [1025, 975] * 4, [8000] * 8, [rng.randrange(1, 8001) for _ in range(8)]])
+        k = rng.randrange(8)
+        prev = 0
+        for b in range(grid):
+            for wid in range(KW):
+                lo, hi = xcd_share(total, w, k, b, grid, wid)
+                assert lo == prev and lo <= hi <= total
+                prev = hi
+        assert prev == total
 
 
 def small_rounds(NC, NG, S, grid, b, wid, x0, x1, slots):
