@@ -24,9 +24,11 @@ its shard on its own device from the global packet index):
 
 Prints ONE JSON line on rank 0 (the task's bench contract) with a
 ``roofline`` block (rank 0's kernel bytes / HIP-event kernel time vs 8 TB/s)
-and, at N = 1, a ``cpu_baseline`` block (the C oracle port on this host's CPU
-share over a bounded sample of the same packets) plus the C0 per-packet CPU
-latency of the product's ricrc_one.  Every rank checks a sample of EVERY
+and, at N = 1, a ``cpu_baseline`` block (the product's own CPU batch path,
+ricrc_batch_cpu, on this host's CPU share over a bounded sample of the same
+packets; the C oracle port's figure beside it), the C0 per-packet CPU latency
+of the product's ricrc_one, and ``e2e``: the headline batch through
+ricrc_batch_host from pinned host memory (host in, host out, PCIe included).  Every rank checks a sample of EVERY
 rank's gathered ICRCs against the oracle restatement of the generator (after
 the timed region), so "bit-exact" holds at every N.
 """
@@ -61,7 +63,7 @@ QUAD_SOURCES = ("icrc_kernels.hip", "icrc_kernels.h", "icrc_device.h", "icrc_mat
 RAGGED_KERNELS = ("rsck_bucket", "icrc_rsck_kernel", "icrc_rsmall_kernel", "rsck_gather")
 
 
-def traffic_record(mix, size, count=None, l3_offset=0, stride=None):
+def traffic_record(mix, size, count=None, l3_offset=0, stride=None, slot_lengths=None):
     """(profiles/ file, kernel sources, kernel names) of the PMC traffic
     record for a workload of `count` packets on this rank (tools/pmc_traffic.py
     writes it), or None.  The BASELINE counts (1 M fixed-size packets, 4 M
@@ -70,6 +72,9 @@ def traffic_record(mix, size, count=None, l3_offset=0, stride=None):
     slot and L3 offset."""
     std = (4 << 20) if mix else (1 << 20)
     tag = "" if count in (None, std) else f"_{count}"
+    if slot_lengths is not None:  # a ring with a length per slot: the ragged pipeline
+        lo, hi = slot_lengths
+        return f"pmc_traffic_ring{l3_offset}_{stride or size}_len{lo}-{hi}{tag}.json", RAGGED_SOURCES, RAGGED_KERNELS
     if l3_offset:  # 1, 2 and 4 KiB slots with the L3 start in line 0: the SCK's framed variant
         name = f"pmc_traffic_ring{l3_offset}_{stride or size}{tag}.json"
         if (stride or size) in (1024, 2048, 4096) and l3_offset <= 92:
@@ -134,6 +139,11 @@ def parse(argv=None):
     # in each, stride - l3_offset bytes long.
     ap.add_argument("--l3-offset", type=int, default=0, help="L3 start inside each slot (14: Ethernet framing)")
     ap.add_argument("--stride", type=int, default=None, help="slot bytes of a framed ring (default --size)")
+    # ... with a completion length per slot (a NIC receive ring): the packet
+    # lengths uniform over [lo, hi] (PCG64 on the seed), a uint32 lengths array
+    # beside the ring (the ragged pipeline).
+    ap.add_argument("--slot-lengths", default=None, metavar="LO:HI",
+                    help="framed ring with per-slot packet lengths uniform over [LO, HI] (needs --stride)")
     # The other BASELINE configs, measured by the same command after the
     # headline: N = 1 adds c1 (1 M x 64 B), c2 (1 M x
     # 1 KiB) and c4 (the 4 M mix); N > 1 adds c3_strong (4 M x 4 KiB in all)
@@ -150,7 +160,15 @@ def parse(argv=None):
         ap.error("--l3-offset / --stride describe fixed-slot rings, not --mix")
     if not 0 <= a.l3_offset < a.stride:
         ap.error("--l3-offset must lie inside the slot")
-    a.pkt = a.stride - a.l3_offset  # L3 bytes per packet
+    a.pkt = a.stride - a.l3_offset  # L3 bytes per packet (the largest, with --slot-lengths)
+    if a.slot_lengths is not None:
+        try:
+            lo, hi = (int(x) for x in a.slot_lengths.split(":"))
+        except ValueError:
+            ap.error("--slot-lengths takes LO:HI")
+        if a.mix or not 44 <= lo <= hi <= a.pkt:
+            ap.error(f"--slot-lengths: need 44 <= LO <= HI <= stride - l3_offset = {a.pkt} (and no --mix)")
+        a.slot_lengths = (lo, hi)
     return a
 
 
@@ -195,7 +213,7 @@ def load_traffic(args, count):
     """HBM bytes per launch measured by separate rocprofv3 --pmc passes
     (profiles/pmc_traffic*.json, from tools/pmc_traffic.py) on this very
     workload and kernel source, or None."""
-    rec = traffic_record(args.mix, args.size, count, args.l3_offset, args.stride)
+    rec = traffic_record(args.mix, args.size, count, args.l3_offset, args.stride, args.slot_lengths)
     if args.family != "v4" or rec is None:
         return None
     name, srcs, _ = rec
@@ -206,6 +224,7 @@ def load_traffic(args, count):
         same = d.get("count") == count and d.get("kernel_src") == kernel_source_hash(srcs)
         same = same and (d.get("size") == "mix" if args.mix else d.get("size") == args.size)
         same = same and d.get("l3_offset", 0) == args.l3_offset and d.get("stride", args.size) == args.stride
+        same = same and d.get("slot_lengths") == (list(args.slot_lengths) if args.slot_lengths else None)
         if same:
             return d.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
@@ -235,7 +254,8 @@ def kernel_path(args, base=0x100000, count=1):
 
     if args.mix:
         return roce_icrc.kernel_path(base, count, offsets=8, lengths=8, family=args.family)
-    return roce_icrc.kernel_path(base, count, stride=args.stride, l3_offset=args.l3_offset, family=args.family)
+    return roce_icrc.kernel_path(base, count, stride=args.stride, l3_offset=args.l3_offset, family=args.family,
+                                 lengths=8 if args.slot_lengths else None)
 
 
 def kernel_label(args, base=0x100000, count=1):
@@ -349,10 +369,12 @@ def product_cpu(sample_host, got_sample, size, budget_s, threads, offsets=None, 
 
 
 def cpu_baseline(sample_host, got_sample, size, budget_s, offsets=None, lengths=None, family="v4"):
-    """Time the C oracle (slice-by-8, pthreads over this host's CPU share) on a
-    sample of the batch, check the GPU's ICRCs on it, and add a 1-core zlib
-    figure (the Python oracle, zlib.crc32 per packet) and the product's own
-    CPU batch path (slice-by-16, same threads)."""
+    """The cpu_baseline block: ``value`` is the product's own CPU batch path
+    (ricrc_batch_cpu, slice-by-16, pthreads over this host's CPU share; SURVEY
+    §8(d)(3)) on a sample of the batch.  The C oracle (slice-by-8, same
+    threads) checks the GPU's ICRCs on the sample first and is timed beside it
+    (``oracle_port_GiBs``), with a 1-core zlib figure (the Python oracle,
+    zlib.crc32 per packet)."""
     import numpy as np
 
     oracle_c, icrc_oracle = _oracle()
@@ -447,7 +469,11 @@ def shard_plan(args, world):
     if args.mix:
         lens_g = np.random.default_rng(args.seed).choice(np.array(MIX_SIZES, np.uint32), size=T)
         return T, byte_balanced_cuts(lens_g, world), lens_g
-    return T, [shard_range(T, world, r)[0] for r in range(world)] + [T], None
+    cuts = [shard_range(T, world, r)[0] for r in range(world)] + [T]
+    if args.slot_lengths:  # ring slots: equal slot counts per rank, a length per slot
+        lo, hi = args.slot_lengths
+        return T, cuts, np.random.default_rng(args.seed).integers(lo, hi + 1, size=T).astype(np.uint32)
+    return T, cuts, None
 
 
 def build_batch(torch, np, ctx, dev, stream, args, world, rank):
@@ -471,16 +497,20 @@ def build_batch(torch, np, ctx, dev, stream, args, world, rank):
         ctx.synth_ragged_device(buf, args.seed, lo, len(lens), d_offs, d_lens, stream=stream)
         b.update(buf=buf, d_offs=d_offs, d_lens=d_lens, h_offs=offs, h_lens=lens, lens_global=lens_g,
                  rank_bytes=nbytes)
-    elif args.l3_offset:  # a framed ring: the L3 packet at l3_offset in each stride-byte slot
+    elif args.l3_offset or args.slot_lengths:  # a framed ring: the L3 packet at l3_offset in each stride-byte slot
         n = hi - lo
         buf = torch.zeros(max(n * args.stride, 1), dtype=torch.uint8, device=dev)
+        h_lens = np.ascontiguousarray(lens_g[lo:hi]) if args.slot_lengths else np.full(n, args.pkt, np.uint32)
+        d_lens = torch.from_numpy(h_lens.view(np.int32)).to(dev) if n else None
         if n:
             offs = torch.arange(n, dtype=torch.int64, device=dev) * args.stride + args.l3_offset
-            lens = torch.full((n,), args.pkt, dtype=torch.int32, device=dev)
-            ctx.synth_ragged_device(buf, args.seed, lo, n, offs, lens, stream=stream)
+            ctx.synth_ragged_device(buf, args.seed, lo, n, offs, d_lens, stream=stream)
             stream.synchronize()
-            del offs, lens
-        b.update(buf=buf, d_offs=None, d_lens=None, lens_global=None, rank_bytes=n * args.pkt)
+            del offs
+        if not args.slot_lengths:  # every packet runs to its slot's end: no lengths array
+            d_lens = None
+        b.update(buf=buf, d_offs=None, d_lens=d_lens, h_lens=h_lens, lens_global=lens_g,
+                 rank_bytes=int(h_lens.sum(dtype=np.uint64)))
     else:
         buf = torch.empty(max((hi - lo) * args.size, 1), dtype=torch.uint8, device=dev)
         ctx.synth_device(buf, args.seed, lo, hi - lo, args.size, stream=stream)
@@ -539,6 +569,11 @@ def metric_for(args, T, count):
         scope = f"{_count_label(T)} in all" if args.global_count is not None else f"{_count_label(args.count)} per GPU"
         return (f"device-resident ICRC GiB/s on mixed-MTU (64/256/1024/4096 B) RoCE packets ({scope}); "
                 "bit-exact vs reference")
+    if args.slot_lengths:
+        scope = f"{_count_label(T)} in all" if args.global_count is not None else f"{_count_label(args.count)} per GPU"
+        lo, hi = args.slot_lengths
+        return (f"device-resident ICRC GiB/s on {lo}-{hi}B RoCE packets in {args.stride}B ring slots with a length "
+                f"per slot (L3 at offset {args.l3_offset}; {scope}); bit-exact vs reference")
     if args.l3_offset:
         scope = f"{_count_label(T)} in all" if args.global_count is not None else f"{_count_label(args.count)} per GPU"
         return (f"device-resident ICRC GiB/s on {args.pkt}B RoCE packets in {args.stride}B Ethernet-framed ring slots "
@@ -588,7 +623,7 @@ class HipBackend:
                                   family=args.family)
         else:
             self.ctx.batch_device(b["buf"], count, out, stride=args.stride, l3_offset=args.l3_offset,
-                                  stream=self.stream, family=args.family)
+                                  lengths=b["d_lens"], stream=self.stream, family=args.family)
 
     def sync(self):
         self.torch.cuda.synchronize()
@@ -611,7 +646,8 @@ class HipBackend:
         per-XCD work-split weights and the recorded start XCD."""
         if args.mix:
             return self.ctx.launch_info(b["buf"], count, offsets=b["d_offs"], lengths=b["d_lens"])
-        return self.ctx.launch_info(b["buf"], count, stride=args.stride, l3_offset=args.l3_offset)
+        return self.ctx.launch_info(b["buf"], count, stride=args.stride, l3_offset=args.l3_offset,
+                                    lengths=b["d_lens"])
 
     def release(self):
         self.torch.cuda.synchronize()
@@ -619,6 +655,33 @@ class HipBackend:
 
     def host_bytes(self, b, nbytes):
         return b["buf"][:nbytes].cpu().numpy()
+
+    # -- the host route (e2e): host in, host out --------------------------
+    def host_pinned(self, b, nbytes):
+        """A pinned host copy (ricrc_host_alloc) of the batch's first nbytes."""
+        arr = self.ctx.host_alloc(nbytes)
+        self.torch.from_numpy(arr).copy_(b["buf"][:nbytes])
+        return arr
+
+    def host_free(self, arr):
+        self.ctx.host_free(arr)
+
+    def host_batch(self, arr, args, count):
+        return self.ctx.batch_host(arr, stride=args.size, count=count, family=args.family)
+
+    def h2d_ms(self, arr, b, reps):
+        """The host-to-device copy alone of the whole pinned batch (ms per copy)."""
+        src = self.torch.from_numpy(arr)
+        dst = b["buf"][:arr.size]
+        e0, e1 = self.event(), self.event()
+        dst.copy_(src, non_blocking=True)
+        self.sync()
+        self.record(e0)
+        for _ in range(reps):
+            dst.copy_(src, non_blocking=True)
+        self.record(e1)
+        self.sync()
+        return e0.elapsed_time(e1) / reps
 
     def close(self):
         self.ctx.close()
@@ -777,7 +840,23 @@ def run(args, world, rank, be, distributed):
         raise SystemExit(f"bench: rank {rank}: {bad} sampled ICRCs differ from the oracle")
 
     all_bytes = rank_bytes
+    ranks = None
     if distributed:
+        # every rank's own kernel time, wall time and shard:
+        # a shortfall of the driver's multi-GPU run can then be pinned on one
+        # slow rank, an unequal byte cut or the collective
+        mine = torch.tensor([kern_ms, elapsed * 1e3 / max(args.steps, 1), float(rank_bytes), float(count)],
+                            dtype=torch.float64, device=be.dev)
+        every = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(every, mine)
+        every = [[float(x) for x in t.cpu()] for t in every]
+        km = [e[0] for e in every]
+        sb = [int(e[2]) for e in every]
+        ranks = {"kernel_ms": [round(v, 4) for v in km], "ms_per_step": [round(e[1], 4) for e in every],
+                 "shard_bytes": sb, "shard_packets": [int(e[3]) for e in every],
+                 "kernel_ms_min": round(min(km), 4), "kernel_ms_max": round(max(km), 4),
+                 "slowest_rank": int(max(range(world), key=lambda r: km[r])),
+                 "shard_bytes_min": min(sb), "shard_bytes_max": max(sb)}
         keys = sorted(split)
         t = torch.tensor([elapsed, kern_ms] + [split[k] for k in keys], dtype=torch.float64, device=be.dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -789,7 +868,8 @@ def run(args, world, rank, be, distributed):
 
     value = all_bytes * args.steps / elapsed / 2**30
     # per launch: packets read + ICRCs written (+ 12 B of offset/length descriptors per packet, ragged)
-    alg_bytes = rank_bytes + 4 * count + (12 * count if args.mix else 0)
+    # (+ 4 B of length per slot, rings with a length per slot)
+    alg_bytes = rank_bytes + 4 * count + (12 * count if args.mix else 4 * count if args.slot_lengths else 0)
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
     traffic = load_traffic(args, count)
 
@@ -801,6 +881,10 @@ def run(args, world, rank, be, distributed):
                     "lengths uniform over 64/256/1024/4096 B, packed, uint64 offsets + uint32 lengths, "
                     f"shards cut at equal bytes; rank 0: {sizes[0]} packets, {rank_bytes if rank == 0 else '?'} B; "
                     f"device-resident, ragged path: {label}")
+    elif args.slot_lengths:
+        workload = (f"{b['T']} RoCEv2 packets of {args.slot_lengths[0]}-{args.slot_lengths[1]} B in all ({count} on "
+                    f"rank 0, {rank_bytes if rank == 0 else '?'} B), each at offset {args.l3_offset} of a "
+                    f"{args.stride} B ring slot, uint32 length per slot, device-resident, ragged path: {label}")
     elif args.l3_offset:
         workload = (f"{b['T']} x {args.pkt} B RoCEv2 packets in all ({count} on rank 0), each at offset "
                     f"{args.l3_offset} of a {args.stride} B Ethernet-framed ring slot, device-resident, " + label)
@@ -823,7 +907,8 @@ def run(args, world, rank, be, distributed):
         "dtype": "u8",
         "data": "synthetic (device-generated RoCEv2 SEND_ONLY packets, seeded; reference P4 header template)",
         "config": {"workload": workload, "packets_total": b["T"], "packets_rank0": sizes[0], "family": args.family,
-                   "packet_bytes": "mix 64/256/1024/4096" if args.mix else args.pkt,
+                   "packet_bytes": ("mix 64/256/1024/4096" if args.mix else
+                                    f"{args.slot_lengths[0]}-{args.slot_lengths[1]}" if args.slot_lengths else args.pkt),
                    "parallelism": f"dp{world}" + (" (all-gather u32 results)" if do_gather else "")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -836,7 +921,7 @@ def run(args, world, rank, be, distributed):
                    "timing": "one HIP event pair around the K steps on the kernels' stream; value from wall "
                              "time between barrier + synchronize"},
     }
-    if args.l3_offset:
+    if args.l3_offset or args.slot_lengths:
         result["config"].update(l3_offset=args.l3_offset, slot_bytes=args.stride)
     if hasattr(be, "launch_info") and count:
         try:
@@ -849,15 +934,86 @@ def run(args, world, rank, be, distributed):
         result["collective_backend"] = dist.get_backend()
         result["rccl_version"] = rccl_version()
         result.update(split)
+        result["ranks"] = ranks
     return result, full_h, b
+
+
+def e2e_route(be, b, args, count, want, reps=5):
+    """The headline batch through ricrc_batch_host from pinned host memory
+    (ricrc_host_alloc): host in, host out, PCIe included -- the north_star's
+    end-to-end rate (the path starts and ends in host memory,
+    python/simulator.py:49-55).  The library cuts the batch into <= 256 MiB
+    chunks, double-buffered on two streams (H2D of chunk k+1 overlaps the
+    kernel of chunk k), and copies the 4-byte results back.  Reported beside
+    the host-to-device copy alone of the same bytes and the device-resident
+    kernel time; the ICRCs are checked equal to the device-resident run's."""
+    import numpy as np
+
+    nbytes = count * args.size
+    arr = be.host_pinned(b, nbytes)
+    try:
+        got = be.host_batch(arr, args, count)  # (warm: first-touch of the staging and the chunk plan)
+        if not np.array_equal(got, want[:count]):
+            raise SystemExit("bench: e2e host-route ICRCs differ from the device-resident run")
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            be.host_batch(arr, args, count)
+        dt = (time.perf_counter() - t0) / reps
+        h2d = be.h2d_ms(arr, b, reps)
+    finally:
+        be.host_free(arr)
+    return {"value": round(nbytes / dt / 2**30, 2), "unit": "GiB/s", "ms_per_batch": round(dt * 1e3, 3),
+            "reps": reps, "h2d_ms": round(h2d, 3), "h2d_GiBs": round(nbytes / (h2d * 1e-3) / 2**30, 2),
+            "d2h_bytes": 4 * count, "route": "ricrc_batch_host, pinned host buffer (ricrc_host_alloc): "
+            "hipMemcpyAsync H2D in <= 256 MiB chunks on two streams, each chunk's kernel behind its copy, "
+            "4-byte results D2H; host wall time per call",
+            "config": f"{count} x {args.size} B (the headline batch), host in, host out, ICRCs checked"}
+
+
+def n1_extras(args, be, result, full_h, b):
+    """N = 1 only: cpu_baseline, the C0 latency and (headline shape) e2e."""
+    import numpy as np
+
+    count = b["sizes"][0]
+    ns = min(count, 32768)
+    got = full_h[:ns]
+    if args.mix:
+        h_offs, h_lens = b["h_offs"], b["h_lens"]
+        span = int(h_offs[ns - 1]) + int(h_lens[ns - 1])
+        sample = be.host_bytes(b, span)
+        result["cpu_baseline"] = cpu_baseline(sample, got, args.size, args.cpu_seconds,
+                                              offsets=h_offs[:ns].copy(), lengths=h_lens[:ns].copy(),
+                                              family=args.family)
+    elif args.slot_lengths:  # ring slots with a length each
+        sample = be.host_bytes(b, ns * args.stride)
+        offs = np.arange(ns, dtype=np.uint64) * args.stride + args.l3_offset
+        result["cpu_baseline"] = cpu_baseline(sample, got, args.pkt, args.cpu_seconds, offsets=offs,
+                                              lengths=b["h_lens"][:ns].copy(), family=args.family)
+    else:  # (a framed ring: its slots' L3 packets, contiguous on the host)
+        sample = be.host_bytes(b, ns * args.stride).reshape(ns, args.stride)[:, args.l3_offset:]
+        result["cpu_baseline"] = cpu_baseline(np.ascontiguousarray(sample), got, args.pkt, args.cpu_seconds,
+                                              family=args.family)
+    result["c0"] = c0_latency()
+    if not (args.mix or args.l3_offset or args.slot_lengths) and hasattr(be, "host_batch"):
+        try:
+            result["e2e"] = e2e_route(be, b, args, count, full_h)
+        except (Exception, SystemExit) as e:
+            result["e2e"] = {"error": f"{type(e).__name__}: {e}"}
 
 
 # BASELINE.json's other configs (SURVEY 8(d)): measured after the main
 # workload in the same process, each with its own warm phase and K steps.
-SIDE_N1 = (("c1", ["--size", "64"]), ("c2", ["--size", "1024"]), ("c4", ["--mix"]))
+# N = 1 also carries the anchors of the 8-GPU run (VERDICT r5 item 3): C3's
+# 4 M x 4 KiB on one GPU (the denominator of its strong-scaling curve), C4's
+# 524,288-packet shard stand-in, the 4 KiB framed NIC ring, and a NIC ring of
+# 1 KiB slots with a length per slot (64-1010 B, the ragged pipeline).
+SIDE_N1 = (("c1", ["--size", "64"]), ("c2", ["--size", "1024"]), ("c4", ["--mix"]),
+           ("c3", ["--global-count", str(4 << 20)]), ("c4s", ["--mix", "--count", str(512 << 10)]),
+           ("ring", ["--l3-offset", "14", "--stride", "4096"]),
+           ("ring_len", ["--l3-offset", "14", "--stride", "1024", "--slot-lengths", "64:1010"]))
 SIDE_NX = (("c3_strong", ["--global-count", str(4 << 20)]), ("c4_strong", ["--mix", "--global-count", str(4 << 20)]))
 SIDE_KEYS = ("metric", "value", "unit", "ms_per_step", "scaling", "compute_only_ms_per_step", "gather_ms",
-             "oracle_sampled_all_ranks", "launch")
+             "oracle_sampled_all_ranks", "launch", "ranks")
 
 
 def side_args(args, extra):
@@ -883,12 +1039,20 @@ def run_side(args, world, rank, be, distributed):
     out = {}
     for name, extra in (SIDE_N1 if world == 1 else SIDE_NX):
         sa = side_args(args, extra)
-        r, _, sb = run(sa, world, rank, be, distributed)
+        try:
+            r, _, sb = run(sa, world, rank, be, distributed)
+            del sb
+        except (Exception, SystemExit) as e:  # N = 1: one side config's failure must not lose the main line
+            if distributed:  # the other ranks may wait in a collective: fail the job as before
+                raise
+            out[name] = {"error": f"{type(e).__name__}: {e}"}
+            if hasattr(be, "release"):
+                be.release()
+            continue
         d = {k: r[k] for k in SIDE_KEYS if k in r}
         d["config"] = {k: r["config"][k] for k in ("workload", "packets_total", "packets_rank0")}
         d["roofline"] = {k: r["roofline"][k] for k in ("achieved", "frac", "traffic", "kernel_ms", "alg_bytes_per_launch")}
         out[name] = d
-        del sb
         if hasattr(be, "release"):
             be.release()
     return out
@@ -919,20 +1083,7 @@ def main(argv=None):
     count = b["sizes"][rank]
 
     if world == 1 and not args.no_cpu:
-        ns = min(count, 32768)
-        got = full_h[:ns]
-        if args.mix:
-            h_offs, h_lens = b["h_offs"], b["h_lens"]
-            span = int(h_offs[ns - 1]) + int(h_lens[ns - 1])
-            sample = be.host_bytes(b, span)
-            result["cpu_baseline"] = cpu_baseline(sample, got, args.size, args.cpu_seconds,
-                                                  offsets=h_offs[:ns].copy(), lengths=h_lens[:ns].copy(),
-                                                  family=args.family)
-        else:  # (a framed ring: its slots' L3 packets, contiguous on the host)
-            sample = be.host_bytes(b, ns * args.stride).reshape(ns, args.stride)[:, args.l3_offset:]
-            result["cpu_baseline"] = cpu_baseline(np.ascontiguousarray(sample), got, args.pkt, args.cpu_seconds,
-                                                  family=args.family)
-        result["c0"] = c0_latency()
+        n1_extras(args, be, result, full_h, b)
 
     if not args.no_side:  # the other BASELINE configs, by the same command
         del full_h, b

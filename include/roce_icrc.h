@@ -187,8 +187,9 @@ int ricrc_device_count(const ricrc_ctx *ctx);
  * reported as -EINVAL.  Callers whose descriptors are not trusted use
  * ricrc_batch_device_bounded / ricrc_batch_host_bounded below.
  * ricrc_batch_host checks the descriptors against the buffer when it knows
- * the buffer's size -- base inside a ricrc_host_alloc / ricrc_host_register
- * range -- and returns -EINVAL (reading nothing) for one past its end. */
+ * the buffer's size -- base inside a ricrc_host_alloc'd buffer -- and returns
+ * -EINVAL (reading nothing) for one past its end.  A ricrc_host_register'ed
+ * range bounds nothing (it may be one part of a larger caller buffer). */
 int ricrc_batch_host(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *off, const uint32_t *len,
                      uint32_t stride, uint64_t count, uint32_t l3_offset, uint32_t *out);
 int ricrc_batch_device(ricrc_ctx *ctx, int dev, const void *d_base, const uint64_t *d_off,
@@ -414,7 +415,9 @@ const char *ricrc_kernel_path(const ricrc_ctx *ctx, const void *d_base, const ui
  * few per cent slower), the XCD the device's last strided-chain launch
  * started on (the next launch's k in the split), and for the ragged
  * pipeline its bucket / gather pass blocks, packets per thread and whether
- * the gather folds the one-line packets.  bench.py reports it next to its
+ * the gather folds the one-line packets; for every path the lanes that fold
+ * one packet.  ctx may be NULL (dev 0): the dispatch on a 256-CU MI355X
+ * with the default knobs, no GPU needed.  bench.py reports it next to its
  * numbers.  0, or -EINVAL as ricrc_kernel_path's NULL. */
 typedef struct {
   uint32_t grid;           /* workgroups of the main kernel (0: not reported for this path) */
@@ -425,6 +428,9 @@ typedef struct {
   uint32_t one_line;       /* ragged: who folds the one-line packets: 2 the fold (default), 1 the gather,
                               0 a separate one-line kernel (RICRC_ONE_LINE_IN_GATHER selects 1 or 0) */
   uint32_t gather_grid;    /* ragged: gather blocks (2 x pass_grid when one-line sides run beside them) */
+  uint32_t lanes_per_packet; /* lanes of a wave that fold one packet (SCK and the ragged fold 8, the quad
+                                kernel 4, TSK n / 32, the streaming kernel its chunk lanes; the ragged
+                                pipeline's one-line packets take one lane each) */
 } ricrc_launch_info_t;
 int ricrc_launch_info(const ricrc_ctx *ctx, int dev, const void *d_base, const uint64_t *d_off,
                       const uint32_t *d_len, uint32_t stride, uint64_t count, uint32_t l3_offset,

@@ -483,6 +483,26 @@ const char *path_kernels(Path p, bool one_line_pass) {
   }
 }
 
+// Grids of the fixed-length kernels (one decision for the launch and
+// ricrc_launch_info): one 1024-thread workgroup per CU at most, 16 waves of
+// work per workgroup.
+int quad_grid(const Dev &d, uint64_t count) {  // a wave step reads 4 KiB (64 packets)
+  const uint64_t steps = (count * 64 + 4095) / 4096;
+  return (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)d.n_cu, (steps + 15) / 16));
+}
+int tsk_grid(const Dev &d, uint64_t count, uint64_t stride) {  // a wave step re-lays a 4 KiB region
+  const uint64_t n_iters = (count * stride + 4095) / 4096;
+  return (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)d.n_cu, (n_iters + 15) / 16));
+}
+// The direct streaming kernel's packets: P lanes of 64 cpl bytes each,
+// 64 >> log2(P) packets per wave step.
+uint32_t stream_lanes(uint32_t fixed_len, int cpl) { return (fixed_len - 4 + 64u * cpl - 1) / (64u * cpl); }
+int stream_grid(const Dev &d, uint64_t count, uint32_t P) {
+  const uint64_t ppw = 64u >> ilog2_ceil(P);
+  const uint64_t n_iters = (count + ppw - 1) / ppw;
+  return (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)d.n_cu, (n_iters + 15) / 16));
+}
+
 int launch_batch_v4(Dev &d, const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
                     uint64_t count, uint32_t l3_offset, uint32_t *out, hipStream_t st, bool verify,
                     uint32_t family = kFamV4) {
@@ -516,9 +536,7 @@ int launch_batch_v4(Dev &d, const uint8_t *base, const uint64_t *off, const uint
       q.count = count;
       q.out = out;
       q.verify = verify ? 1u : 0u;
-      const uint64_t steps = (count * 64 + 4095) / 4096;
-      const int qgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)d.n_cu, (steps + 15) / 16));
-      return hip_err(launch_quad(q, qgrid, st));
+      return hip_err(launch_quad(q, quad_grid(d, count), st));
     }
     const int cpl = stream_cpl(fixed_len);
     if (path == Path::kTsk) {
@@ -536,9 +554,7 @@ int launch_batch_v4(Dev &d, const uint8_t *base, const uint64_t *off, const uint
       }
       const uint32_t y = gf_x8n(2048);
       for (int j = 0; j < 32; ++j) t.YB[j] = gf_mul(y, 1u << j);
-      const uint64_t tw = (t.n_iters + 15) / 16;
-      const int tgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)d.n_cu, tw));
-      return hip_err(launch_tsk(t, tgrid, st));
+      return hip_err(launch_tsk(t, tsk_grid(d, count, stride), st));
     }
     {  // Path::kStream: any other fixed length up to 16 KiB, lanes fold 64 CPL-byte chunks
       StreamArgs a{};
@@ -548,7 +564,7 @@ int launch_batch_v4(Dev &d, const uint8_t *base, const uint64_t *off, const uint
       a.count = count;
       a.out = out;
       a.len = fixed_len;
-      a.P = (M + chunk - 1) / chunk;
+      a.P = stream_lanes(fixed_len, cpl);
       a.log2P2 = (uint32_t)ilog2_ceil(a.P);
       a.nw_last = (M - chunk * (a.P - 1)) / 4;
       const uint64_t ppw = 64u >> a.log2P2;
@@ -558,9 +574,7 @@ int launch_batch_v4(Dev &d, const uint8_t *base, const uint64_t *off, const uint
         if (c >= a.P) a.K[c] = 0;
         else a.K[c] = x8n_host((uint64_t)M - std::min<uint64_t>((uint64_t)chunk * (c + 1), M));
       }
-      const uint64_t want = (a.n_iters + 15) / 16;
-      const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)d.n_cu, want));
-      return hip_err(launch_stream(a, cpl, grid, st));
+      return hip_err(launch_stream(a, cpl, stream_grid(d, count, a.P), st));
     }
   }
   // Everything else (offsets, lengths, any alignment, Ethernet framing): the
@@ -877,18 +891,35 @@ const char *ricrc_kernel_path(const ricrc_ctx *ctx, const void *d_base, const ui
 int ricrc_launch_info(const ricrc_ctx *ctx, int dev, const void *d_base, const uint64_t *d_off,
                       const uint32_t *d_len, uint32_t stride, uint64_t count, uint32_t l3_offset,
                       ricrc_launch_info_t *info) {
-  if (!ctx || !info || dev < 0 || dev >= (int)ctx->devs.size() || !d_base || count == 0) return -EINVAL;
+  if (!info || dev < 0 || (ctx && dev >= (int)ctx->devs.size()) || (!ctx && dev != 0) || !d_base || count == 0)
+    return -EINVAL;
   if ((!d_off && stride == 0) || (!d_len && stride <= l3_offset)) return -EINVAL;
-  const Dev &d = ctx->devs[dev];
+  // ctx NULL: the dispatch on a 256-CU MI355X with the default knobs (no GPU needed)
+  Dev nodev{};
+  nodev.n_cu = 256;
+  const Dev &d = ctx ? ctx->devs[dev] : nodev;
   *info = ricrc_launch_info_t{};
   info->start_xcd = xcd_start(d.h_xcd);
   const uint8_t *base = (const uint8_t *)d_base;
-  const Path p = choose_path(ctx->knobs, base, d_off, d_len, stride, l3_offset);
+  const Path p = choose_path(d.knobs, base, d_off, d_len, stride, l3_offset);
   XcdWeights xw{};
+  const uint32_t fixed_len = stride > l3_offset ? (uint32_t)std::min<uint64_t>(stride - l3_offset, 0xFFFFFFFFu) : 0u;
   if (p == Path::kSck || p == Path::kSckFramed) {
     info->grid = (uint32_t)sck_grid(d, base, d_off, d_len, stride, count, l3_offset);
-    xw = xcd_weights(ctx->knobs, stride != 4096 ? 0 : (int)info->grid < d.n_cu ? 25 : 50);
+    xw = xcd_weights(d.knobs, stride != 4096 ? 0 : (int)info->grid < d.n_cu ? 25 : 50);
+    info->lanes_per_packet = 8;  // lane 8 g + s: slot s of every line of packet g
+  } else if (p == Path::kQuad) {
+    info->grid = (uint32_t)quad_grid(d, count);
+    info->lanes_per_packet = 4;  // a lane quad per 64-byte packet
+  } else if (p == Path::kTsk) {
+    info->grid = (uint32_t)tsk_grid(d, count, stride);
+    info->lanes_per_packet = fixed_len / 32;  // contiguous 32-byte chunks per lane
+  } else if (p == Path::kStream) {
+    const uint32_t P = stream_lanes(fixed_len, stream_cpl(fixed_len));
+    info->grid = (uint32_t)stream_grid(d, count, P);
+    info->lanes_per_packet = 1u << ilog2_ceil(P);  // P chunk lanes, padded to a power of two
   } else if (p == Path::kRagged) {
+    info->lanes_per_packet = 8;  // the fold's groups (one-line packets: one lane each)
     info->grid = (uint32_t)(d.knobs.rsck_grid > 0 ? std::min(d.n_cu, d.knobs.rsck_grid) : d.n_cu);
     xw = xcd_weights(d.knobs, 40);
     int pg = 0, pu = 0, gg = 0;
@@ -1302,9 +1333,13 @@ static int batch_host_impl(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *
   if (!base || !out) return -EINVAL;
   if (!off && stride == 0) return -EINVAL;
   if (!len && stride <= l3_offset) return -EINVAL;
+  // The plain calls know the buffer's size only for a buffer the context
+  // allocated (ricrc_host_alloc): a registered range may be a part of a
+  // larger caller buffer (or one of several adjacent ones), so it bounds
+  // nothing.
   if (extent == 0)
     for (const HostRange &r : ctx->pinned)
-      if ((uintptr_t)base >= r.lo && (uintptr_t)base < r.hi) extent = r.hi - (uintptr_t)base;
+      if (r.owned && (uintptr_t)base >= r.lo && (uintptr_t)base < r.hi) extent = r.hi - (uintptr_t)base;
   auto len_ok = [](uint64_t n) { return n >= kMinLen && n <= kMaxLen; };
   auto frame = [&](uint64_t i) -> uint64_t { return off ? off[i] : i * (uint64_t)stride; };
   // packet i's descriptor bytes [frame + l3_offset, + n) inside the extent
@@ -1402,19 +1437,34 @@ static int batch_host_impl(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *
         Slot &sl = d.slot[s];
         const uint64_t lo = c.next;
         // Span plan: the largest [lo, hi) whose frames ascend without overlap
-        // and whose byte span [frame(lo), end of hi-1) fits the slot with at
-        // most 25 % slack.  The span lands at d_buf + pad so that packet lo's
-        // L3 header is 16-byte aligned on the device (so are the others when
-        // the frames are 16 apart, e.g. a fixed stride).
-        const uint64_t s_lo = frame(lo);
+        // and whose byte span [first frame, end of the last packet) fits the
+        // slot with at most 25 % slack.  The span lands at d_buf + pad so that
+        // its first packet's L3 header is 16-byte aligned on the device (so
+        // are the others when the frames are 16 apart, e.g. a fixed stride).
+        // A packet staged as 0 bytes (with a status array: a bad length, or a
+        // frame outside the extent) is read by nobody: it neither starts,
+        // stretches nor ends a span, so no byte outside the extent is copied
+        // (its device descriptor is length 0 at the span's start).
         const uint64_t pad = (16u - (l3_offset & 15u)) & 15u;
-        uint64_t hi = lo, s_hi = s_lo, used = 0;
+        uint64_t hi = lo, s_lo = 0, s_hi = 0, used = 0;
+        bool any = false, empty = false;
         while (hi < c.end && hi - lo < kStagePkts) {
-          const uint64_t fs = frame(hi), fe = fs + l3_offset + pkt_len(hi);
-          if (fs < s_hi && hi > lo) break;  // not ascending / overlapping
+          const uint64_t n = pkt_len(hi);
+          if (n == 0) {
+            empty = true;
+            ++hi;
+            continue;
+          }
+          const uint64_t fs = frame(hi), fe = fs + l3_offset + n;
+          if (!any) {
+            s_lo = s_hi = fs;
+            any = true;
+          } else if (fs < s_hi) {
+            break;  // not ascending / overlapping
+          }
           if (fe - s_lo > kStageBytes) break;
           s_hi = fe;
-          used += pkt_len(hi);
+          used += n;
           ++hi;
         }
         const bool span = hi > lo && (s_hi - s_lo) <= used + used / 4 + 64;
@@ -1430,8 +1480,8 @@ static int batch_host_impl(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *
             par_for(bytes, T, 4u << 20, [&](uint64_t a, uint64_t b) { memcpy(sl.h_buf + a, src + a, b - a); });
             HIP_TRY(hipMemcpyAsync(sl.d_buf + pad, sl.h_buf, bytes, hipMemcpyHostToDevice, sl.st));
           }
-          if (off || len || f.framelen)
-            for (uint64_t i = lo; i < hi; ++i) sl.h_off[i - lo] = frame(i) - s_lo + pad;
+          if (off || len || f.framelen || empty)
+            for (uint64_t i = lo; i < hi; ++i) sl.h_off[i - lo] = pkt_len(i) ? frame(i) - s_lo + pad : pad;
         } else {
           // Gather: packed L3 packets, 16-byte aligned each (after `pre`
           // EtherType bytes when those are checked).
@@ -1455,7 +1505,8 @@ static int batch_host_impl(ricrc_ctx *ctx, const uint8_t *base, const uint64_t *
           HIP_TRY(hipMemcpyAsync(sl.d_buf, sl.h_buf, bytes, hipMemcpyHostToDevice, sl.st));
           kl3 = pre;
         }
-        const bool fixed = span && !off && !len && !f.framelen;  // frames at i*stride from d_buf + pad
+        // frames at i*stride from d_buf + pad (no packet staged as 0 bytes: those need their length 0)
+        const bool fixed = span && !off && !len && !f.framelen && !empty;
         const uint8_t *dbase = fixed ? sl.d_buf + pad : sl.d_buf;
         const uint64_t *doff = nullptr;
         const uint32_t *dlen = nullptr;

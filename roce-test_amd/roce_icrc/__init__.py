@@ -114,7 +114,7 @@ _SIG = {
 class LaunchInfo(ctypes.Structure):
     """``ricrc_launch_info_t`` (include/roce_icrc.h)."""
     _fields_ = [("grid", _u32), ("xcd_weights", _u32 * 8), ("start_xcd", _u32), ("pass_grid", _u32),
-                ("pass_unroll", _u32), ("one_line", _u32), ("gather_grid", _u32)]
+                ("pass_unroll", _u32), ("one_line", _u32), ("gather_grid", _u32), ("lanes_per_packet", _u32)]
 
 
 class ICRCError(RuntimeError):
@@ -544,11 +544,7 @@ class Context:
                                          l3_offset, ctypes.byref(info))
         if rc:
             raise ICRCError(rc, "ricrc_launch_info")
-        d = {"grid": info.grid, "xcd_weights": list(info.xcd_weights), "start_xcd": info.start_xcd}
-        if info.pass_grid:
-            d.update(pass_grid=info.pass_grid, pass_unroll=info.pass_unroll,
-                     one_line_in=("kernel", "gather", "fold")[info.one_line], gather_grid=info.gather_grid)
-        return d
+        return _launch_dict(info)
 
     def prime(self, usec: int = 20000, dev: int = 0) -> None:
         """``ricrc_prime``: bring the device out of its idle power state."""
@@ -611,6 +607,26 @@ class Context:
         rc = self._lib.ricrc_host_unregister(self._h, arr.ctypes.data)
         if rc:
             raise ICRCError(rc, "ricrc_host_unregister")
+
+
+def _launch_dict(info: LaunchInfo) -> dict:
+    d = {"grid": info.grid, "xcd_weights": list(info.xcd_weights), "start_xcd": info.start_xcd,
+         "lanes_per_packet": info.lanes_per_packet}
+    if info.pass_grid:
+        d.update(pass_grid=info.pass_grid, pass_unroll=info.pass_unroll,
+                 one_line_in=("kernel", "gather", "fold")[info.one_line], gather_grid=info.gather_grid)
+    return d
+
+
+def launch_info(base, count: int, stride: int = 0, offsets=None, lengths=None, l3_offset: int = 0) -> dict:
+    """``ricrc_launch_info`` without a context: how the dispatch launches a
+    batch of this shape on a 256-CU MI355X (default knobs; no GPU needed)."""
+    info = LaunchInfo()
+    rc = hip_lib().ricrc_launch_info(None, 0, _ptr(base), _ptr(offsets), _ptr(lengths), stride, count, l3_offset,
+                                     ctypes.byref(info))
+    if rc:
+        raise ICRCError(rc, "ricrc_launch_info")
+    return _launch_dict(info)
 
 
 def kernel_path(base, count: int, stride: int = 0, offsets=None, lengths=None, l3_offset: int = 0,

@@ -228,7 +228,12 @@ def test_side_configs_are_the_baseline_configs():
     each with the main run's K, W and seed."""
     a = bench.parse(["--steps", "7", "--warmup", "2", "--seed", "11"])
     got = {n: bench.side_args(a, x) for n, x in bench.SIDE_N1}
-    assert set(got) == {"c1", "c2", "c4"}
+    assert set(got) == {"c1", "c2", "c4", "c3", "c4s", "ring", "ring_len"}
+    # the 8-GPU run's anchors at N = 1 (VERDICT r5 item 3)
+    assert (got["c3"].global_count, got["c3"].size, got["c3"].mix) == (4 << 20, 4096, False)
+    assert got["c4s"].mix and got["c4s"].count == 524288
+    assert (got["ring"].l3_offset, got["ring"].stride, got["ring"].count) == (14, 4096, 1 << 20)
+    assert (got["ring_len"].l3_offset, got["ring_len"].stride, got["ring_len"].slot_lengths) == (14, 1024, (64, 1010))
     assert (got["c1"].size, got["c1"].count, got["c1"].mix) == (64, 1 << 20, False)
     assert (got["c2"].size, got["c2"].count, got["c2"].mix) == (1024, 1 << 20, False)
     assert got["c4"].mix and got["c4"].count == 4 << 20 and got["c4"].global_count is None
@@ -249,12 +254,77 @@ def test_side_configs_run_at_n1_on_cpu_stand_in():
 
     a = bench.parse(["--steps", "2", "--warmup", "1", "--prime-ms", "0", "--warm-ms", "0", "--side-count", "1500"])
     res = bench.run_side(a, 1, 0, CpuOracleBackend(), False)
-    assert set(res) == {"c1", "c2", "c4"}
+    assert set(res) == {"c1", "c2", "c4", "c3", "c4s", "ring", "ring_len"}
+    assert not any("error" in d for d in res.values()), res
     for name, d in res.items():
         assert d["value"] > 0 and d["ms_per_step"] > 0 and d["oracle_sampled_all_ranks"], name
         assert d["roofline"]["frac"] > 0 and d["roofline"]["kernel_ms"] > 0 and "traffic" in d["roofline"], name
         assert d["config"]["packets_total"] == 1500, name
     assert "mixed-MTU" in res["c4"]["metric"] and "64B" in res["c1"]["metric"] and "1024B" in res["c2"]["metric"]
+    assert "fixed total" in res["c3"]["metric"] and "mixed-MTU" in res["c4s"]["metric"]
+    assert "framed" in res["ring"]["metric"] and "length per slot" in res["ring_len"]["metric"]
+    # the ring with a length per slot counts its packets' bytes and its lengths array
+    rl = res["ring_len"]["roofline"]
+    assert rl["alg_bytes_per_launch"] > 8 * 1500 and rl["alg_bytes_per_launch"] < 1500 * (1010 + 8)
+
+
+def test_side_config_failure_keeps_the_main_line(monkeypatch):
+    """A side config that raises is recorded as an error key (N = 1); the
+    others still run (the headline must never be lost)."""
+    from test_bench_dist import CpuOracleBackend
+
+    a = bench.parse(["--steps", "1", "--warmup", "0", "--prime-ms", "0", "--warm-ms", "0", "--side-count", "600"])
+    real = bench.run
+
+    def flaky(sa, *rest):
+        if sa.mix and flaky.n == 0:  # c4, the first mixed side config
+            flaky.n += 1
+            raise RuntimeError("out of memory (test)")
+        return real(sa, *rest)
+    flaky.n = 0
+    monkeypatch.setattr(bench, "run", flaky)
+    res = bench.run_side(a, 1, 0, CpuOracleBackend(), False)
+    assert "error" in res["c4"] and "out of memory" in res["c4"]["error"]
+    assert res["c1"]["value"] > 0 and res["c4s"]["value"] > 0
+
+
+def test_n1_extras_carry_cpu_baseline_c0_and_e2e():
+    """N = 1: cpu_baseline, C0, and the headline batch through the host route
+    (e2e: host in, host out) -- on the CPU stand-in."""
+    from test_bench_dist import CpuOracleBackend
+
+    be = CpuOracleBackend()
+    a = bench.parse(["--steps", "1", "--warmup", "0", "--prime-ms", "0", "--warm-ms", "0", "--count", "700",
+                     "--size", "1024", "--cpu-seconds", "0.05"])
+    res, full_h, b = bench.run(a, 1, 0, be, False)
+    bench.n1_extras(a, be, res, full_h, b)
+    assert res["cpu_baseline"]["value"] > 0 and res["c0"]["us_per_packet_ctypes_call"] > 0
+    e = res["e2e"]
+    assert "error" not in e, e
+    assert e["value"] > 0 and e["h2d_ms"] > 0 and e["d2h_bytes"] == 4 * 700 and "ricrc_batch_host" in e["route"]
+    # a ring with a length per slot: its CPU baseline takes offsets + lengths; no e2e (not the headline shape)
+    a = bench.parse(["--steps", "1", "--warmup", "0", "--prime-ms", "0", "--warm-ms", "0", "--count", "500",
+                     "--l3-offset", "14", "--stride", "1024", "--slot-lengths", "64:1010", "--cpu-seconds", "0.05"])
+    res, full_h, b = bench.run(a, 1, 0, be, False)
+    bench.n1_extras(a, be, res, full_h, b)
+    assert res["cpu_baseline"]["value"] > 0 and "e2e" not in res
+
+
+def test_slot_lengths_flag():
+    """--slot-lengths LO:HI: a NIC ring with a completion length per slot
+    (VERDICT r5 item 2), lengths uniform over [LO, HI] from the seed."""
+    a = bench.parse(["--l3-offset", "14", "--stride", "1024", "--slot-lengths", "64:1010"])
+    assert a.slot_lengths == (64, 1010) and a.pkt == 1010
+    T, cuts, lens = bench.shard_plan(a, 1)
+    assert T == 1 << 20 and cuts == [0, T] and lens.min() >= 64 and lens.max() <= 1010
+    assert "(rsck_bucket)" in bench.kernel_label(a)
+    assert bench.traffic_record(False, a.size, a.count, 14, 1024, (64, 1010))[0] == \
+        "pmc_traffic_ring14_1024_len64-1010.json"
+    for bad in (["--stride", "1024", "--slot-lengths", "64:1011", "--l3-offset", "14"],
+                ["--stride", "1024", "--slot-lengths", "30:100"], ["--mix", "--slot-lengths", "64:100"],
+                ["--stride", "1024", "--slot-lengths", "64"]):
+        with pytest.raises(SystemExit):
+            bench.parse(bad)
 
 
 def test_framed_ring_flags():

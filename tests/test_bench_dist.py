@@ -55,6 +55,12 @@ class CpuOracleBackend:
             lens = np.ascontiguousarray(lens_g[lo:hi])
             buf, offs = oracle_c.synth_ragged(args.seed, lo, lens)
             b = dict(buf=buf, h_offs=offs, h_lens=lens, lens_global=lens_g, rank_bytes=int(lens.sum(dtype=np.uint64)))
+        elif args.l3_offset or args.slot_lengths:  # ring slots (a length per slot with --slot-lengths)
+            n = hi - lo
+            lens = np.ascontiguousarray(lens_g[lo:hi]) if args.slot_lengths else np.full(n, args.pkt, np.uint32)
+            offs = np.arange(n, dtype=np.uint64) * args.stride + args.l3_offset
+            buf, _ = oracle_c.synth_ragged(args.seed, lo, lens, offsets=offs, size=n * args.stride)
+            b = dict(buf=buf, h_offs=offs, h_lens=lens, lens_global=lens_g, rank_bytes=int(lens.sum(dtype=np.uint64)))
         else:
             buf = oracle_c.synth_batch(args.seed, lo, hi - lo, args.size)
             b = dict(buf=buf, lens_global=None, rank_bytes=(hi - lo) * args.size)
@@ -64,7 +70,7 @@ class CpuOracleBackend:
     def compute(self, b, count, out, args):
         import oracle_c
 
-        if args.mix:
+        if b.get("h_offs") is not None:
             v = oracle_c.icrc_batch(b["buf"], offsets=b["h_offs"], lengths=b["h_lens"], family=args.family)
         else:
             v = oracle_c.icrc_batch(b["buf"], stride=args.size, family=args.family)
@@ -81,6 +87,27 @@ class CpuOracleBackend:
 
     def prime(self, ms):
         pass
+
+    def host_bytes(self, b, nbytes):
+        return b["buf"][:nbytes]
+
+    # the host route (bench.e2e_route), on the CPU
+    def host_pinned(self, b, nbytes):
+        return np.array(b["buf"][:nbytes])
+
+    def host_free(self, arr):
+        pass
+
+    def host_batch(self, arr, args, count):
+        import oracle_c
+
+        return oracle_c.icrc_batch(arr, stride=args.size, count=count, family=args.family)
+
+    def h2d_ms(self, arr, b, reps):
+        t = time.perf_counter()
+        for _ in range(reps):
+            np.copyto(b["buf"][:arr.size], arr)
+        return (time.perf_counter() - t) * 1e3 / reps
 
     def close(self):
         pass
@@ -182,6 +209,12 @@ def test_bench_run_world2_gloo(argv, scaling, total):
     # group's own world size, the collective library's version (None on gloo)
     assert res["world_size"] == 2 and res["collective_backend"] == "gloo" and "rccl_version" in res
     assert res["compute_only_ms_per_step"] > 0 and res["gather_ms"] > 0
+    # every rank's own kernel time and shard, with their spread
+    rk = res["ranks"]
+    assert len(rk["kernel_ms"]) == 2 and len(rk["shard_bytes"]) == 2 and rk["slowest_rank"] in (0, 1)
+    assert rk["kernel_ms_min"] == min(rk["kernel_ms"]) and rk["kernel_ms_max"] == max(rk["kernel_ms"])
+    assert rk["shard_bytes_min"] == min(rk["shard_bytes"]) and rk["shard_bytes_max"] == max(rk["shard_bytes"])
+    assert rk["shard_packets"] == got[0][2] and rk["kernel_ms_max"] == res["roofline"]["kernel_ms"]
     sizes = got[0][2]
     assert sum(sizes) == total
     if "--mix" in argv:
@@ -216,4 +249,5 @@ def test_bench_side_configs_world2_gloo():
         assert d["compute_only_ms_per_step"] > 0 and d["gather_ms"] > 0 and d["oracle_sampled_all_ranks"], k
         assert d["roofline"]["frac"] > 0 and d["value"] > 0, k
         assert got[1][0][k]["value"] == d["value"], k  # one number on every rank
+        assert len(d["ranks"]["kernel_ms"]) == 2 and sum(d["ranks"]["shard_packets"]) == 3001, k
     assert "mixed-MTU" in res["c4_strong"]["metric"] and "fixed total" in res["c3_strong"]["metric"]

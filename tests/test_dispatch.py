@@ -51,3 +51,24 @@ def test_ragged_batches():
     tests/test_gpu_parity.py)."""
     assert path(count=4 << 20, offsets=OFF, lengths=LEN) == "rsck_bucket+icrc_rsck_kernel+rsck_gather"
     assert path(count=524288, offsets=OFF, lengths=LEN) == "rsck_bucket+icrc_rsck_kernel+rsck_gather"
+
+
+def test_launch_info_reports_every_path():
+    """ricrc_launch_info names the grid and the lanes per packet of every
+    kernel path, so a C1 regression is attributable from
+    the bench line; ctx = NULL: the dispatch on a 256-CU MI355X."""
+    li = lambda count, **kw: roce_icrc.launch_info(BASE, count, **kw)  # noqa: E731
+    c1 = li(1 << 20, stride=64)  # C1: 1 M x 64 B, the quad kernel
+    assert c1["grid"] == 256 and c1["lanes_per_packet"] == 4
+    assert li(1000, stride=64)["grid"] == 1  # 1000 packets: one 4 KiB wave step per 64 packets, 16 waves
+    tsk = li(1 << 20, stride=256)
+    assert tsk["grid"] == 256 and tsk["lanes_per_packet"] == 8
+    st = li(1 << 20, stride=1504)  # the direct streaming kernel: 1500-byte chunks over 64-byte lanes
+    assert st["grid"] == 256 and st["lanes_per_packet"] == 32
+    head = li(1 << 20, stride=4096)  # the headline: 240 of 256 CUs, XCD-weighted
+    assert head["grid"] == 240 and head["lanes_per_packet"] == 8 and head["xcd_weights"][0] > head["xcd_weights"][1]
+    rag = li(4 << 20, offsets=OFF, lengths=LEN)
+    assert rag["grid"] == 256 and rag["pass_grid"] == 256 and rag["one_line_in"] == "fold"
+    assert rag["lanes_per_packet"] == 8
+    with pytest.raises(roce_icrc.ICRCError):
+        li(0, stride=64)

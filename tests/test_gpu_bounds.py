@@ -7,11 +7,17 @@ caller's allocation is the caller's fault.  The extent-checked calls take the
 buffer's size: ricrc_batch_host_bounded returns -EINVAL (status NULL) or
 RICRC_ST_BADLEN per packet, ricrc_batch_device_bounded reports
 RICRC_ST_BADLEN with out = 0 and never reads the packet; ricrc_batch_host
-itself checks descriptors against a ricrc_host_alloc'd buffer's size.  In
-these tests every "outside" descriptor still points into memory the process
-owns (the device buffer is allocated larger than the extent declared), so a
-read past the extent would be a wrong answer, not a fault."""
+itself checks descriptors against a ricrc_host_alloc'd buffer's size.
+
+What each test can see: on the device call the status pass sets out[i] = 0
+for every RICRC_ST_BADLEN packet whatever was read, so the device tests check
+statuses and the other packets' ICRCs (the device buffer is allocated larger
+than the extent declared: a stray read there is neither a fault nor visible).
+That no byte past the extent is READ is asserted on the host route, whose
+buffer ends at a PROT_NONE guard page: a read past it is a SIGSEGV."""
+import ctypes
 import errno
+import mmap
 
 import numpy as np
 import pytest
@@ -112,3 +118,53 @@ def test_batch_device_bounded_flags_out_of_range_packets(ctx, framelen):
     with pytest.raises(roce_icrc.ICRCError) as e:
         ctx.batch_device_bounded(d, 4096 * 3 - 1, 3, out, st, stride=4096, stream=s)
     assert e.value.rc == -errno.EINVAL
+
+
+def _guarded(nbytes):
+    """A writable host array of nbytes that ends exactly at a PROT_NONE page."""
+    page = mmap.PAGESIZE
+    total = ((nbytes + page - 1) // page + 1) * page
+    mm = mmap.mmap(-1, total, prot=mmap.PROT_READ | mmap.PROT_WRITE)
+    addr = ctypes.addressof(ctypes.c_char.from_buffer(mm))
+    libc = ctypes.CDLL(None, use_errno=True)
+    assert libc.mprotect(ctypes.c_void_p(addr + total - page), ctypes.c_size_t(page), 0) == 0
+    arr = np.frombuffer(mm, np.uint8, count=total - page)[total - page - nbytes:]
+    return mm, arr
+
+
+@pytest.mark.parametrize("l3_offset", [0, 14])
+def test_batch_host_never_reads_past_the_extent(ctx, l3_offset):
+    """a trailing descriptor a little past the buffer (or a frame
+    starting within l3_offset bytes of its end) is RICRC_ST_BADLEN and none of
+    its bytes is read -- the buffer ends at a guard page, so the span copy of
+    the host route would fault if it stretched over such a packet."""
+    rng = np.random.default_rng(7 + l3_offset)
+    count = 3000
+    lens = rng.choice(np.array([64, 256, 1024, 1500], np.uint32), size=count)
+    frames = lens.astype(np.uint64) + l3_offset
+    offs = np.zeros(count, np.uint64)
+    offs[1:] = np.cumsum(frames[:-1])
+    extent = int(offs[-1] + frames[-1])
+    mm, buf = _guarded(extent)
+    buf[:] = rng.integers(0, 256, size=extent, dtype=np.uint8)
+    want = oracle_c.icrc_batch(buf, offsets=offs, lengths=lens, l3_offset=l3_offset, threads=16)
+    got = ctx.batch_host_bounded(buf, extent, offsets=offs, lengths=lens, l3_offset=l3_offset)
+    np.testing.assert_array_equal(got, want)
+    cases = [  # (last offset, last length): just past the end; the frame inside, its L3 packet past it
+        (extent - 10, 64), (extent - max(l3_offset, 1) + 0, 64), (extent + 64, 64), (extent - int(frames[-1]), 65)]
+    for last_off, last_len in cases:
+        o, n = offs.copy(), lens.copy()
+        o[-1], n[-1] = last_off, last_len
+        out, st = ctx.batch_host_bounded(buf, extent, offsets=o, lengths=n, l3_offset=l3_offset, status=True)
+        assert st[-1] == roce_icrc.ST_BADLEN and out[-1] == 0, (last_off, last_len)
+        assert (st[:-1] == roce_icrc.ST_OK).all()
+        np.testing.assert_array_equal(out[:-1], want[:-1])
+    # a bad descriptor in the middle of an ascending ring does not break it for the rest
+    o = offs.copy()
+    o[1500] = np.uint64(2**64 - 8)
+    out, st = ctx.batch_host_bounded(buf, extent, offsets=o, lengths=lens, l3_offset=l3_offset, status=True)
+    assert st[1500] == roce_icrc.ST_BADLEN and out[1500] == 0
+    ok = np.ones(count, bool)
+    ok[1500] = False
+    np.testing.assert_array_equal(out[ok], want[ok])
+    del buf

@@ -171,7 +171,7 @@ def _want_slots(frames, lens, stride, count, l3, family="v4"):
     return want
 
 
-@pytest.mark.parametrize("stride", [2048, 4096])
+@pytest.mark.parametrize("stride", [1024, 2048, 4096])
 @pytest.mark.parametrize("l3", [0, 14, 18, 92])
 def test_slot_lengths_match_oracle(ctx, ctx_env, stride, l3):
     """Slots with per-slot lengths, every odd length case, against the oracle;
@@ -195,7 +195,7 @@ def test_slot_lengths_match_oracle(ctx, ctx_env, stride, l3):
 
 @pytest.mark.parametrize("count", [1, 7, 9, 65, 8 * 16 * 3 + 5, 70001])
 def test_slot_lengths_tails(ctx, count):
-    for stride in (2048, 4096):
+    for stride in (1024, 2048, 4096):
         rng = np.random.default_rng(count * 3 + stride)
         frames = rng.integers(0, 256, size=count * stride + 4096, dtype=np.uint8)
         lens = _slot_lens(rng, count, stride, 14, odd=count > 8)
@@ -278,3 +278,30 @@ def test_slot_lengths_full_size_bit_exact(ctx):
     ctx.batch_device(d, count, out, stride=stride, lengths=_dev(lens), l3_offset=l3)
     np.testing.assert_array_equal(_host_u32(out), oracle_c.icrc_batch(d.cpu().numpy(), lengths=lens, stride=stride,
                                                                       count=count, l3_offset=l3, threads=16))
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("lo,hi", [(64, 1010), (200, 200), (450, 450)])
+def test_slot_lengths_1k_full_size_bit_exact(ctx, lo, hi):
+    """1,048,576 slots of 1 KiB behind a 14-byte Ethernet header with a
+    completion length per slot (the NIC receive ring of
+    small buffers; uniform 64-1010 B, and single lengths of two and four
+    lines), every ICRC against the C oracle on the same device-generated
+    bytes, then every trailer stamped and verified."""
+    count, stride, l3 = 1 << 20, 1024, 14
+    lens = np.random.default_rng(lo * 7 + hi).integers(lo, hi + 1, size=count).astype(np.uint32)
+    d = torch.zeros(count * stride, dtype=torch.uint8, device="cuda")
+    offs = np.arange(count, dtype=np.uint64) * stride + l3
+    ctx.synth_ragged_device(d, SEED ^ 9, 0, count, _dev(offs), _dev(lens))
+    d_len = _dev(lens)
+    out = _out(count)
+    ctx.batch_device(d, count, out, stride=stride, lengths=d_len, l3_offset=l3)
+    got = _host_u32(out)
+    host = d.cpu().numpy()
+    np.testing.assert_array_equal(got, oracle_c.icrc_batch(host, lengths=lens, stride=stride, count=count,
+                                                           l3_offset=l3, threads=16))
+    tail = (offs + lens.astype(np.uint64) - 4).astype(np.int64)
+    host[(tail[:, None] + np.arange(4, dtype=np.int64)[None, :]).reshape(-1)] = got.view(np.uint8)
+    d.copy_(torch.from_numpy(host))
+    ctx.batch_device(d, count, out, stride=stride, lengths=d_len, l3_offset=l3, verify=True)
+    assert int(_host_u32(out).astype(np.uint64).sum()) == count

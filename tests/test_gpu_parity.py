@@ -577,9 +577,11 @@ def test_c4_shard_full_size_bit_exact(ctx, shard):
     (--mix --count 524288: the first 524,288 packets of the bench seed's mix)
     and rank 7 of C4 strong-scaled over 8 GPUs (4 M packets cut at equal
     bytes).  Both take the shard's pipeline -- the bucket pass at 4 packets
-    per thread on <= 128 blocks, the gather folding the one-line packets --
-    and every ICRC is compared with the C oracle on the very same bytes, then
-    every trailer stamped and verified."""
+    per thread on <= 128 blocks, the fold kernel folding the one-line packets
+    (one lane each, on wave slots 0..11) before its groups, a plain gather
+    (ricrc_launch_info: one_line_in "fold") -- and every ICRC is compared
+    with the C oracle on the very same bytes, then every trailer stamped and
+    verified."""
     import bench
     import roce_icrc
     from roce_icrc.dist import byte_balanced_cuts
@@ -596,6 +598,8 @@ def test_c4_shard_full_size_bit_exact(ctx, shard):
     d_offs, d_lens = _dev(offs), _dev(lens)
     assert roce_icrc.kernel_path(d, count, offsets=d_offs, lengths=d_lens, ctx=ctx) == \
         "rsck_bucket+icrc_rsck_kernel+rsck_gather"
+    li = ctx.launch_info(d, count, offsets=d_offs, lengths=d_lens)
+    assert li["one_line_in"] == "fold" and li["pass_unroll"] == 4 and li["pass_grid"] <= 128
     ctx.synth_ragged_device(d, bench.SEED, lo, count, d_offs, d_lens, stream=_stream())
     out = _out(count)
     ctx.batch_device(d, count, out, offsets=d_offs, lengths=d_lens, stream=_stream())

@@ -9,7 +9,7 @@ the C oracle.  Kernel time from HIP events around `--reps` back-to-back
 batches after a 100 ms warm phase; algorithmic bytes = the packets' bytes + 4
 written (+ 4 read from the lengths array) per slot.  One JSON line per case.
 
-    python tools/ring_bench.py [--count N] [--reps R]
+    python tools/ring_bench.py [--count N] [--reps R] [--cases 1024:64-1010,1024:200]
 """
 from __future__ import annotations
 
@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--count", type=int, default=1 << 20)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--l3", type=int, default=14)
+    ap.add_argument("--cases", default="",
+                    help="comma-separated slot:lengths cases, lengths 'full', 'lo-hi' or n (default: CASES)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -45,7 +47,15 @@ def main():
     dev = torch.device("cuda", 0)
     s = torch.cuda.current_stream()
     rng = np.random.default_rng(0x1CEC0DE)
-    for slot, spec in CASES:
+    cases = CASES
+    if a.cases:
+        cases = []
+        for c in a.cases.split(","):
+            slot, spec = c.split(":")
+            if spec != "full":
+                spec = tuple(int(x) for x in spec.split("-")) if "-" in spec else int(spec)
+            cases.append((int(slot), spec))
+    for slot, spec in cases:
         n_slots = a.count
         buf = torch.empty(n_slots * slot, dtype=torch.uint8, device=dev)
         ctx.synth_device(buf, 7, 0, n_slots, slot, stream=s)  # random-looking bytes in every slot
