@@ -752,10 +752,14 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
         const uint32_t L = __builtin_amdgcn_readlane(Q.L, r);
         const uint64_t s0 = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(Q.s0 >> 32), r) << 32) |
                             __builtin_amdgcn_readlane((uint32_t)Q.s0, r);
-        // x - s0 < gs w < 2^24 (a pass block's run): a 32-bit division (a
-        // 64-bit one is a long expansion on the start-up's critical path)
+        // x - s0 < gs w, the run's work: below 2^31 for every product shape
+        // (a one-round pass block holds <= 17 K packets, gs w < 2^23), so a
+        // 32-bit division (a 64-bit one is a long expansion on the start-up's
+        // critical path); blocks of several rounds (RICRC_RS_PASS_GRID) can
+        // hold runs past it: 64 bits there (wave-uniform)
         const uint32_t w = 4u * L + a.group_cost;  // quarter line-steps
-        const uint64_t q = g0 + ((uint32_t)(x - s0) + w - 1u) / w;
+        const uint64_t dx = x - s0;
+        const uint64_t q = g0 + (dx < (1ull << 31) ? ((uint32_t)dx + w - 1u) / w : (dx + w - 1u) / w);
         const uint32_t gend = g0 + gs < NG ? g0 + gs : NG;  // (never past the pool)
         return q < gend ? (uint32_t)q : gend;
       }
@@ -1041,9 +1045,21 @@ __global__ __launch_bounds__(kBlock) void icrc_rsck_kernel(RsckArgs a) {
 #pragma unroll
               for (int i = 0; i < 4; ++i) xr[i] ^= wc[i] & (uint32_t)((lim - 4 * i) >> 31);
             }
-          } else {
+          } else if (fd_k < fd_hl) {  // wave-uniform: a head line (byte-granular)
 #pragma unroll
             for (int i = 0; i < 4; ++i) xr[i] = xor3(xr[i], wc[i], edge_word(wc[i], rel0 + 4 * i, (int)fd_M));
+          } else {
+            // the group's last line past its head lines, byte-granular: rel
+            // >= 40 (no head masks), only the bytes at rel >= M dropped -- the
+            // word keeps its low clamp(M - rel, 0, 4) bytes (5 VALU a word
+            // instead of edge_word's ~20)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int r = (int)fd_M - (rel0 + 4 * i);
+              const uint32_t c = 8u * (uint32_t)__builtin_elementwise_min(__builtin_elementwise_max(r, 0), 4);
+              const uint32_t keep = (uint32_t)((1ull << c) - 1u);
+              xr[i] ^= wc[i] & ~keep;
+            }
           }
         }
         uint32_t t[4][4];

@@ -151,7 +151,8 @@ def test_batch_host_never_reads_past_the_extent(ctx, l3_offset):
     got = ctx.batch_host_bounded(buf, extent, offsets=offs, lengths=lens, l3_offset=l3_offset)
     np.testing.assert_array_equal(got, want)
     cases = [  # (last offset, last length): just past the end; the frame inside, its L3 packet past it
-        (extent - 10, 64), (extent - max(l3_offset, 1) + 0, 64), (extent + 64, 64), (extent - int(frames[-1]), 65)]
+        (extent - 10, 64), (extent - max(l3_offset, 1) + 0, 64), (extent + 64, 64),
+        (extent - int(frames[-1]), int(lens[-1]) + 1)]
     for last_off, last_len in cases:
         o, n = offs.copy(), lens.copy()
         o[-1], n[-1] = last_off, last_len
