@@ -60,7 +60,7 @@ RAGGED_SOURCES = ("icrc_rsck.hip", "icrc_kernels.h", "icrc_sck.h", "icrc_device.
 QUAD_SOURCES = ("icrc_kernels.hip", "icrc_kernels.h", "icrc_device.h", "icrc_math.h", "icrc_api.cpp")
 
 
-RAGGED_KERNELS = ("rsck_bucket", "icrc_rsck_kernel", "icrc_rsmall_kernel", "rsck_gather")
+RAGGED_KERNELS = ("rsck_bucket", "icrc_rsck_kernel", "icrc_rsmall_kernel", "rsck_gather", "icrc_rswg_kernel")
 
 
 def traffic_record(mix, size, count=None, l3_offset=0, stride=None, slot_lengths=None):
@@ -242,6 +242,7 @@ KERNEL_ROLES = {
     "icrc_rsck_kernel": "strided-chain fold (8 packets of >= 2 lines a group; one-line packets one a lane)",
     "icrc_rsmall_kernel": "one-line packets",
     "rsck_gather": "gather",
+    "icrc_rswg_kernel": "workgroup-local ragged kernel (classify, fold, write in one launch)",
     "family_fix_kernel": "address-family fix-up",
 }
 

@@ -55,6 +55,8 @@ struct Knobs {
   uint32_t gcost = 0;      // RICRC_RS_GCOST: the ragged fold's per-group cost, quarter lines (0: kRsGroupCost)
   bool one_line_in_gather = false;  // RICRC_ONE_LINE_IN_GATHER: the gather / a one-line kernel folds the one-line packets
   int small_slots = -1;    // RICRC_SMALL_SLOTS: wave slots taking the fold's one-line packets (-1: kRsSmallSlots)
+  int wg_chunks = 2;       // RICRC_WG_CHUNKS: ragged batches of up to this many kRsWgCap chunks per workgroup take
+                           // the workgroup-local kernel (0: never; RICRC_NO_WG = 0)
   int pass_grid = 0;       // RICRC_RS_PASS_GRID: cap the ragged bucket / gather pass grid (schedule studies)
   bool pass_times = false; // RICRC_PASS_TIMES: timing events between the ragged passes (ricrc_pass_times)
   long fail_chunk = -1;    // RICRC_FAIL_CHUNK: the next ricrc_batch_host fails after queueing chunk k (tests; once)
@@ -390,6 +392,24 @@ int sck_grid(const Dev &d, const uint8_t *base, const uint64_t *off, const uint3
   return g;
 }
 
+// Whether a ragged range of `count` packets takes the workgroup-local kernel
+// (icrc_rswg_kernel, one launch) rather than the bucket / fold / gather
+// pipeline: up to RICRC_WG_CHUNKS (default 2) chunks of kRsWgCap packets on
+// the most loaded workgroup -- C4's 8-GPU shard (524,288 packets) and NIC
+// rings of up to ~1.1 M slots on 256 CUs.  Same-box A/B (profiles/r06/,
+// session 5): the shard 0.148 -> 0.134 ms of kernel per step, 1 M x 1 KiB
+// slots of 64-1010 B (two chunks) 0.155 -> 0.149; C4's 4 M (eight chunks)
+// 0.968 against 0.976 on the pipeline, which keeps the large batches.
+// One decision for the launch, ricrc_kernel_path and ricrc_launch_info.
+bool rs_use_wg(const Dev &d, uint64_t count) {
+  if (d.knobs.wg_chunks <= 0 || count == 0) return false;
+  if (d.knobs.one_line_in_gather || d.knobs.pass_grid > 0) return false;  // (knobs of the three-pass pipeline)
+  int rgrid = d.n_cu;
+  if (d.knobs.rsck_grid > 0) rgrid = std::min(rgrid, d.knobs.rsck_grid);
+  const XcdWeights xw = xcd_weights(d.knobs, 40);
+  return rs_wg_chunks(count, rgrid, xw.w) <= (uint64_t)d.knobs.wg_chunks;
+}
+
 // The ragged strided-chain pipeline (icrc_rsck.hip) on packets [0, count) of
 // the batch, count < 2^31.
 int launch_rsck_range(Dev &d, const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
@@ -413,12 +433,18 @@ int launch_rsck_range(Dev &d, const uint8_t *base, const uint64_t *off, const ui
   k.out = out;
   k.tzb = d.d_tzb;
   k.fin = d.d_fin + kFinSck;  // the fold's finish tables
-  Dev::Ws *ws = nullptr;
-  const int wrc = ragged_ws(d, st, rs_workspace_bytes(count), &ws);
-  if (wrc) return wrc;
-  rs_bind_workspace(k, ws->p);
   int rgrid = d.n_cu;
   if (d.knobs.rsck_grid > 0) rgrid = std::min(rgrid, d.knobs.rsck_grid);
+  const bool wg = rs_use_wg(d, count);
+  Dev::Ws *ws = nullptr;
+  if (!wg) {
+    const int wrc = ragged_ws(d, st, rs_workspace_bytes(count), &ws);
+    if (wrc) return wrc;
+    rs_bind_workspace(k, ws->p);
+  } else {
+    k.xcd_k = xcd_start(d.h_xcd);
+    k.xcd_rec = d.d_xcd_rec;
+  }
   hipEvent_t *pev = nullptr;
   if (d.knobs.pass_times && count > 0 && count <= kRsMaxCount) {  // (launch_rsck records all five events then)
     if (d.pt_ev.empty()) {
@@ -429,6 +455,7 @@ int launch_rsck_range(Dev &d, const uint8_t *base, const uint64_t *off, const ui
     d.pt_next = (d.pt_next + 1) % Dev::kPtSets;
     d.pt_used = std::min(d.pt_used + 1, Dev::kPtSets);
   }
+  if (wg) return hip_err(launch_rswg(k, rgrid, st, pev));  // no workspace
   const hipError_t e = launch_rsck(k, rgrid, d.knobs.pass_grid, st, pev);
   if (e != hipSuccess) ws->dirty = true;
   const hipError_t e2 = hipEventRecord(ws->done, st);
@@ -472,14 +499,16 @@ Path choose_path(const Knobs &kn, const uint8_t *base, const uint64_t *off, cons
   return cpl ? Path::kStream : Path::kRagged;
 }
 
-const char *path_kernels(Path p, bool one_line_pass) {
+const char *path_kernels(Path p, bool one_line_pass, bool wg = false) {
   switch (p) {
     case Path::kSck:
     case Path::kSckFramed: return "icrc_sck_kernel";
     case Path::kQuad: return "icrc_quad_kernel";
     case Path::kTsk: return "icrc_tsk_kernel";
     case Path::kStream: return "icrc_stream_kernel";
-    default: return one_line_pass ? "rsck_bucket+icrc_rsck_kernel+icrc_rsmall_kernel+rsck_gather" : "rsck_bucket+icrc_rsck_kernel+rsck_gather";
+    default:
+      if (wg) return "icrc_rswg_kernel";
+      return one_line_pass ? "rsck_bucket+icrc_rsck_kernel+icrc_rsmall_kernel+rsck_gather" : "rsck_bucket+icrc_rsck_kernel+rsck_gather";
   }
 }
 
@@ -755,6 +784,7 @@ Knobs read_knobs() {
   k.gcost = (uint32_t)std::min(1024L, std::max(0L, num("RICRC_RS_GCOST", 0)));  // the packed work counter's range
   k.one_line_in_gather = getenv("RICRC_ONE_LINE_IN_GATHER") != nullptr;
   k.small_slots = (int)std::min(16L, std::max(-1L, num("RICRC_SMALL_SLOTS", -1)));  // (16 waves a workgroup)
+  k.wg_chunks = getenv("RICRC_NO_WG") ? 0 : (int)std::min(64L, std::max(0L, num("RICRC_WG_CHUNKS", 2)));
   k.pass_grid = (int)std::max(0L, num("RICRC_RS_PASS_GRID", 0));
   k.pass_times = getenv("RICRC_PASS_TIMES") != nullptr;
   k.fail_chunk = num("RICRC_FAIL_CHUNK", -1);
@@ -876,7 +906,13 @@ const char *ricrc_kernel_path(const ricrc_ctx *ctx, const void *d_base, const ui
   // the ragged pipeline's first range (launch_batch_v4 cuts at kRsChunk) decides the one-line pass:
   // none when the fold (the default) or the gather (a fused pass shape) folds those packets
   const bool one_line_pass = kn.one_line_in_gather && !rs_fused(std::min<uint64_t>(count, kRsChunk), kn.pass_grid);
-  if (flags == RICRC_F_IPV4 || p == Path::kSck) return path_kernels(p, one_line_pass);  // the SCK applies every family natively
+  // ... and whether it takes the workgroup-local kernel (ctx NULL: a 256-CU MI355X)
+  Dev nodev{};
+  nodev.n_cu = 256;
+  nodev.knobs = kn;
+  const bool wg = rs_use_wg(ctx && !ctx->devs.empty() ? ctx->devs[0] : nodev, std::min<uint64_t>(count, kRsChunk));
+  if (flags == RICRC_F_IPV4 || p == Path::kSck) return path_kernels(p, one_line_pass, wg);  // the SCK applies every family natively
+  if (p == Path::kRagged && wg) return "icrc_rswg_kernel+family_fix_kernel";
   switch (p) {  // IPv6 / AUTO: the IPv4-mask kernels, then the linear header fix-up
     case Path::kSckFramed: return "icrc_sck_kernel+family_fix_kernel";
     case Path::kQuad: return "icrc_quad_kernel+family_fix_kernel";
@@ -918,6 +954,11 @@ int ricrc_launch_info(const ricrc_ctx *ctx, int dev, const void *d_base, const u
     const uint32_t P = stream_lanes(fixed_len, stream_cpl(fixed_len));
     info->grid = (uint32_t)stream_grid(d, count, P);
     info->lanes_per_packet = 1u << ilog2_ceil(P);  // P chunk lanes, padded to a power of two
+  } else if (p == Path::kRagged && rs_use_wg(d, std::min<uint64_t>(count, kRsChunk))) {
+    info->lanes_per_packet = 8;  // the fold's groups (one-line packets: one lane each)
+    info->grid = (uint32_t)(d.knobs.rsck_grid > 0 ? std::min(d.n_cu, d.knobs.rsck_grid) : d.n_cu);
+    xw = xcd_weights(d.knobs, 40);
+    info->one_line = 2;  // folded by the kernel; no bucket / gather passes (pass_grid 0)
   } else if (p == Path::kRagged) {
     info->lanes_per_packet = 8;  // the fold's groups (one-line packets: one lane each)
     info->grid = (uint32_t)(d.knobs.rsck_grid > 0 ? std::min(d.n_cu, d.knobs.rsck_grid) : d.n_cu);

@@ -115,6 +115,8 @@ struct RsckArgs {
   uint32_t nblk;        // pass blocks of this call (launch_rsck sets it)
   const uint32_t *tzb;  // [kTzWords]: entry m = x^(31 - 4 m), i.e. basis word 4 q of x^(-8 tz) at m = 2 tz + q
   const uint32_t *fin;  // the fold's finish tables (kFinFold words, icrc_math.h build_fin_tables), the context's
+  uint32_t xcd_k;       // icrc_rswg_kernel: the start XCD of its work split (the SCK's record, xcd_share)
+  uint32_t *xcd_rec;    // ... where its workgroup 0 records its XCD for the next launch
 };
 // Work of a group in line-steps: its L lines plus the per-group finish
 // (GF(2) multiplies through nibble tables, reductions, descriptor and slot
@@ -151,6 +153,16 @@ hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, hipStream_t st, hipE
 bool rs_fused(uint64_t count, int pass_cap);
 // The bucket / gather passes' blocks and packets per thread for such a batch (ricrc_launch_info).
 void rs_pass_info(uint64_t count, int pass_cap, bool no_split, int *grid, int *unroll, bool *fused, int *ggrid);
+// The workgroup-local ragged kernel (icrc_rswg_kernel: classify, lay out,
+// fold and write out[] in one launch, no workspace) on `grid` workgroups.
+// Any count <= kRsMaxCount is exact (a workgroup takes its packets in chunks
+// of kRsWgCap); the dispatch sends it batches of about one chunk per
+// workgroup (rs_wg_chunks).
+constexpr uint32_t kRsWgCap = 2304;
+hipError_t launch_rswg(const RsckArgs &a, int grid, hipStream_t st, hipEvent_t *pass_ev = nullptr);
+// Chunks the most loaded workgroup takes for a batch of `count` packets on
+// `grid` workgroups with the XCD weights w (0: equal shares).
+uint64_t rs_wg_chunks(uint64_t count, int grid, const uint32_t (&w)[8]);
 
 struct SynthArgs {
   uint8_t *buf;

@@ -1171,6 +1171,432 @@ __global__ __launch_bounds__(kBlock) void icrc_rsmall_kernel(RsckArgs a) {
   }
 }
 
+// =======================================================================
+// The ragged path in ONE launch, workgroup-local (icrc_rswg_kernel): for
+// batches of up to about kWgCap packets per workgroup (C4's 8-GPU shard:
+// 524,288 packets on 256 CUs).  The three-pass pipeline above pays, at that
+// size, the bucket pass (~11 us), the gather (~4.5 us), two launch
+// boundaries and the fold's start-up of four dependent round trips (counters
+// and block ranges, runs, descriptor blocks, lines: ~10 us), for ~130 us of
+// streaming (profiles/r05/NOTES.md).  Here each workgroup takes a contiguous
+// range of the batch (XCD-weighted packet counts) and, per chunk of <=
+// kWgCap packets:
+//   1. reads its descriptors (3 per thread), classifies them as rsck_bucket
+//      does (rs_class) and ranks each in its class by an LDS atomic;
+//   2. scans the class counts -- one-line classes first, then the big
+//      classes by DESCENDING line count, so the groups claimed last are the
+//      short ones -- and lays the descriptors out in LDS (no padding: a
+//      class's last group repeats its last packet in the lanes past its
+//      end); each packet's layout position goes to out[i] (scratch);
+//   3. folds: the one-line packets in rounds of 64 on wave slots 0..11
+//      (small_icrc, as the fold kernel), then the groups of 8 equal-L
+//      packets, CLAIMED one at a time from an LDS counter -- the waves of a
+//      workgroup end within a group of each other, instead of spreading by
+//      wave slot as static shares do (the memory system serves a SIMD's
+//      older waves first: mean end by slot 104 -> 124 us at the shard, r6s1);
+//      the result of each packet overwrites its layout entry;
+//   4. writes out[i] from the layout (out[i] held its position), computing
+//      the packets not bucketed (n < 44: Sarwate loop; invalid: 0) there.
+// The fold loop is the fold kernel's (two cursors, quiet blocks, edge masks,
+// the finish through nibble tables); a group's descriptors come from the
+// layout in LDS instead of global descriptor blocks, and the fold cursor
+// reads (a, M) of each group from the layout too (a per-wave FIFO carries the
+// group's layout range from the load cursor).
+// =======================================================================
+constexpr uint32_t kWgCap = kRsWgCap;                             // packets per workgroup chunk
+constexpr uint32_t kWgPer = (kWgCap + kBlock - 1) / kBlock;       // ... per thread
+constexpr uint32_t kWgFifo = 8;                                   // group ranges between the cursors, per wave
+template <int ABL>
+__global__ __launch_bounds__(kBlock) void icrc_rswg_kernel(RsckArgs a) {
+  constexpr int D = 6;  // lines in flight per wave (as the fold kernel)
+  constexpr uint32_t kLayW = 2 * kWgCap;          // (lo, hi) per layout entry; lo <- the ICRC once folded
+  constexpr uint32_t kScrW = 2 * kRsClasses;      // class counts | class starts; then the runs
+  constexpr uint32_t kFifoW = kWaves * kWgFifo * 2;
+  constexpr uint32_t kMiscW = 16;
+  __shared__ uint32_t lds[kFinFold + kLdsWords + kTzWords + kLayW + kScrW + kFifoW + kMiscW];
+  uint32_t *xtl = lds;
+  uint32_t *qtl = lds + 128;
+  uint32_t *etl = lds + 128 + 8 * kFinQtStride;  // whole-word head masks: (or, xor) of word k = rel / 4
+  uint32_t *x2tl = etl + 32, *x3tl = etl + 160;  // nibble tables of x^-64, x^-96
+  uint32_t *tab = lds + kFinFold;
+  uint32_t *tzl = tab + kLdsWords;
+  uint32_t *lay = tzl + kTzWords;
+  uint32_t *hcnt = lay + kLayW, *cstart = hcnt + kRsClasses;
+  uint32_t *runs = hcnt;  // after the placement: run r = (g0 | L << 16, e0 | cnt << 16)
+  uint32_t *fifo_all = hcnt + kScrW;
+  uint32_t *misc = fifo_all + kFifoW;  // 0 groups, 1 one-line packets, 2 claim counter, 3.. scan totals
+  static_assert(sizeof(lds) <= 160 * 1024, "LDS");
+  static_assert(kWgCap < 65536 && kRsClasses <= kBlock, "16-bit layout fields, one class per thread");
+
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t s = lane & 7, g = lane >> 3;
+  xcd_record(a.xcd_rec);
+  const TableRegs tab_v = table_load(g_tab128);
+  const uint32_t fin0 = a.fin[threadIdx.x], fin1 = a.fin[threadIdx.x + 1024u < kFinFold ? threadIdx.x + 1024u : 0u];
+  const uint32_t tz_v = a.tzb[threadIdx.x < kTzWords ? threadIdx.x : 0];
+  // This workgroup's packets: the union of its waves' XCD-weighted shares.
+  uint64_t w_lo, w_hi;
+  {
+    uint64_t l0, h0, l1, h1;
+    if (a.xw[0] != 0u) {
+      xcd_share(a.count, a.xw, a.xcd_k, 0, l0, h0);
+      xcd_share(a.count, a.xw, a.xcd_k, kWaves - 1, l1, h1);
+    } else {
+      const uint64_t per = (a.count + gridDim.x - 1) / gridDim.x;
+      l0 = (uint64_t)blockIdx.x * per < a.count ? (uint64_t)blockIdx.x * per : a.count;
+      h1 = l0 + per < a.count ? l0 + per : a.count;
+    }
+    w_lo = l0;
+    w_hi = h1;
+  }
+  table_write(tab, tab_v);
+  if (threadIdx.x < kTzWords) tzl[threadIdx.x] = tz_v;
+  lds[threadIdx.x] = fin0;  // the finish tables, built by the host (icrc_math.h build_fin_tables)
+  if (threadIdx.x + 1024u < kFinFold) lds[threadIdx.x + 1024u] = fin1;
+
+  const LaneTab lt{(lane & 31) << 2, ((lane & 31) << 2) | 0x10000u};
+  const uint32_t *qrow = qtl + s * kFinQtStride;
+  uint32_t *fifo = fifo_all + wid * (kWgFifo * 2);
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  auto lay_at = [&](uint32_t e) -> u32x2 { return *reinterpret_cast<const u32x2 *>(lay + 2u * e); };
+
+  for (uint64_t c0 = w_lo; c0 < w_hi; c0 += kWgCap) {  // workgroup-uniform: chunks of <= kWgCap packets
+    const uint32_t P = (uint32_t)(w_hi - c0 < kWgCap ? w_hi - c0 : kWgCap);
+    for (uint32_t t = threadIdx.x; t < kRsClasses; t += kBlock) hcnt[t] = 0;
+    if (threadIdx.x < kMiscW) misc[threadIdx.x] = 0;
+    __syncthreads();  // (the first chunk: the tables are written too)
+
+    // 1. descriptors, classes, ranks (loads first, index clamped: issued back to back)
+    uint64_t addr[kWgPer];
+    uint32_t n[kWgPer], cr[kWgPer];
+#pragma unroll
+    for (int k = 0; k < (int)kWgPer; ++k) {
+      const uint32_t j = (uint32_t)k * kBlock + threadIdx.x;
+      const uint64_t i = c0 + (j < P ? j : P - 1u);
+      addr[k] = a.off ? a.off[i] : i * a.stride;
+      n[k] = a.len ? a.len[i] : a.fixed_len;
+    }
+    int odd = 0;
+#pragma unroll
+    for (int k = 0; k < (int)kWgPer; ++k) {
+      const uint32_t j = (uint32_t)k * kBlock + threadIdx.x;
+      addr[k] += (uint64_t)(uintptr_t)a.base + a.l3_offset;
+      const uint32_t c = j < P ? rs_class(addr[k], n[k]) : 0u;
+      const uint32_t rk = c ? atomicAdd(&hcnt[c], 1u) : 0u;
+      odd |= (c > (uint32_t)kRsBigBase && ((addr[k] | n[k]) & 3u)) ? 1 : 0;
+      cr[k] = c | (rk << 10);
+    }
+    const bool words = __syncthreads_or(odd) == 0;  // (a barrier: the counts are complete)
+
+    // 2. scan by key: one-line classes 1..kRsBigBase (keys 0..7), then the big
+    //    classes by descending L (key 8 + j: class kRsClasses - 1 - j)
+    const uint32_t t = threadIdx.x, wv = t >> 6;
+    const bool key = t < (uint32_t)kRsClasses - 1u;
+    const uint32_t c = !key ? 0u : t < (uint32_t)kRsBigBase ? t + 1u : (uint32_t)kRsClasses - 1u - (t - kRsBigBase);
+    const bool big = c > (uint32_t)kRsBigBase;
+    const uint32_t cnt = key ? hcnt[c] : 0u;
+    const uint32_t G = big ? (cnt + 7u) >> 3 : 0u;
+    const uint32_t f = (big && cnt) ? 1u : 0u;
+    const uint32_t Sm = big ? 0u : cnt;
+    uint32_t ie = wave_scan(cnt), ig = wave_scan(G), ir = wave_scan(f), is = wave_scan(Sm);
+    uint32_t *wt = fifo_all;  // per-wave totals (the FIFOs are not in use yet)
+    if (lane == 63) {
+      wt[4 * wv] = ie;
+      wt[4 * wv + 1] = ig;
+      wt[4 * wv + 2] = ir;
+      wt[4 * wv + 3] = is;
+    }
+    __syncthreads();
+    for (uint32_t w = 0; w < wv; ++w) {  // wave-uniform
+      ie += wt[4 * w];
+      ig += wt[4 * w + 1];
+      ir += wt[4 * w + 2];
+      is += wt[4 * w + 3];
+    }
+    const uint32_t e0 = ie - cnt, g0 = ig - G, r0 = ir - f;  // exclusive prefixes
+    if (key) cstart[c] = e0;
+    if (t == kBlock - 1) {
+      misc[0] = ig;  // groups
+      misc[1] = is;  // one-line packets: layout entries [0, is)
+    }
+    __syncthreads();
+    // placement; out[i] <- the packet's layout position (or ~0: not bucketed)
+#pragma unroll
+    for (int k = 0; k < (int)kWgPer; ++k) {
+      const uint32_t j = (uint32_t)k * kBlock + threadIdx.x;
+      if (j >= P) continue;
+      const uint32_t ck = cr[k] & 1023u;
+      uint32_t pos = 0xFFFFFFFFu;
+      if (ck) {
+        pos = cstart[ck] + (cr[k] >> 10);
+        *reinterpret_cast<u32x2 *>(lay + 2u * pos) =
+            u32x2{(uint32_t)addr[k], (uint32_t)(addr[k] >> 32) | (n[k] << 16)};
+      }
+      __builtin_nontemporal_store(pos, a.out + c0 + j);
+    }
+    __syncthreads();
+    if (f) {  // the runs, in key order (g0 ascending)
+      runs[2u * r0] = g0 | ((c - (uint32_t)kRsBigBase) << 16);
+      runs[2u * r0 + 1u] = e0 | (cnt << 16);
+    }
+    __syncthreads();
+    const uint32_t NG = misc[0], NS = misc[1];
+
+    // 3a. the one-line packets: rounds of 64 dealt evenly to wave slots 0..11
+    {
+      const uint32_t NC = (NS + 63u) >> 6;
+      const uint32_t sl = kRsSmallSlots;
+      const uint32_t cb = wid < sl ? wid * NC / sl : 0u, ce = wid < sl ? (wid + 1u) * NC / sl : 0u;
+      const StepNib step{lds + kFinStep4};
+#pragma unroll 1
+      for (uint32_t cc = cb; cc < ce; ++cc) {  // wave-uniform
+        const uint32_t jj = 64u * cc + lane;
+        const u32x2 dv = lay_at(jj < NS ? jj : NS - 1u);
+        const uint32_t v = small_icrc(step, RsDesc{dv[0], dv[1]}, lane);
+        if (jj < NS) lay[2u * jj] = v;
+      }
+    }
+
+    // 3b. the groups, claimed one at a time
+    auto claim = [&]() -> uint32_t {
+      uint32_t v = 0;
+      if (lane == 0) v = atomicAdd(&misc[2], 1u);
+      return v;  // (readfirstlane when used: the atomic's return lands meanwhile)
+    };
+    uint32_t run_i = 0;  // the run of the load cursor's group (runs in g0 order, groups claimed ascending)
+    uint32_t run_g0 = 0, run_L = 0, run_e0 = 0, run_cnt = 0, run_g1 = 0;
+    auto run_load = [&](uint32_t r) {
+      const u32x2 rv = *reinterpret_cast<const u32x2 *>(runs + 2u * r);
+      run_g0 = __builtin_amdgcn_readfirstlane(rv[0] & 0xFFFFu);
+      run_L = __builtin_amdgcn_readfirstlane(rv[0] >> 16);
+      run_e0 = __builtin_amdgcn_readfirstlane(rv[1] & 0xFFFFu);
+      run_cnt = __builtin_amdgcn_readfirstlane(rv[1] >> 16);
+      run_g1 = run_g0 + ((run_cnt + 7u) >> 3);
+    };
+    if (NG != 0u) run_load(0);
+    uint32_t q_pend = claim();  // (lane 0's claim in flight)
+    const uint32_t q_first = __builtin_amdgcn_readfirstlane(q_pend);
+    if (q_first < NG) {  // wave-uniform
+      uint32_t q_next = q_first;
+      q_pend = claim();
+      uint32_t ld_seq = 0;  // groups the load cursor entered - 1
+      struct LInfo {
+        uint64_t line0;
+      } ld;
+      // Load cursor enters claimed group q: its layout range, line base and L;
+      // the range goes into the FIFO slot of its sequence number.
+      auto ld_enter = [&](uint32_t q, uint32_t seq) -> uint32_t {
+        while (q >= run_g1) run_load(++run_i);  // wave-uniform (claims ascend)
+        const uint32_t eb = run_e0 + 8u * (q - run_g0), el = run_e0 + run_cnt - 1u;
+        const uint32_t e = eb + g < el ? eb + g : el;
+        const u32x2 dv = lay_at(e);
+        const uint64_t ad = ((uint64_t)(dv[1] & 0xFFFFu) << 32) | dv[0];
+        ld.line0 = (ad & ~127ull) + 16u * s;
+        if (lane == 0) *reinterpret_cast<u32x2 *>(fifo + 2u * (seq & (kWgFifo - 1u))) = u32x2{eb, el};
+        return run_L;
+      };
+      auto line_load = [&](uint64_t ad) -> u32x4 {
+        if (ABL & 16384) return u32x4{(uint32_t)ad, (uint32_t)(ad >> 7), lane, (uint32_t)ad * 3u};
+        return gload16_nt(ad);
+      };
+      uint32_t ld_k = 0, ld_L = ld_enter(q_next, 0);
+      bool ld_more = true;  // a claimed group follows the load cursor's current one
+      auto ld_issue = [&]() -> u32x4 { return line_load(ld.line0 + 128ull * ld_k); };
+      auto ld_advance = [&]() {
+        if (++ld_k == ld_L) {  // wave-uniform
+          ld_k = 0;
+          if (ld_more) {
+            const uint32_t qn = __builtin_amdgcn_readfirstlane(q_pend);
+            if (qn < NG) {
+              q_pend = claim();
+              ++ld_seq;
+              ld_L = ld_enter(qn, ld_seq);
+              return;
+            }
+            ld_more = false;
+          }
+          ld_L = 1;  // done: re-read line 0 of the last group (ld_k wraps to 0 every step)
+        }
+      };
+      u32x4 ring[D];
+#pragma unroll
+      for (int u = 0; u < D; ++u) {
+        __builtin_amdgcn_sched_barrier(0);
+        ring[u] = ld_issue();
+        ld_advance();
+      }
+      __builtin_amdgcn_sched_barrier(0);
+
+      // A group's finish (the fold kernel's): chains rr after its last line,
+      // L lines, first-byte offsets ga and covered lengths gM per lane group,
+      // its layout entry e -> ~ICRC into lay[2 e].
+      auto finish_group = [&](uint32_t (&rr)[4], uint32_t Lg, uint32_t ga, uint32_t gM, uint32_t e) {
+        uint32_t R;
+        if (ABL & 2) {
+          R = group_xor(rr[0] ^ rr[1] ^ rr[2] ^ rr[3], 3);
+        } else {
+          auto nib_mul = [](const uint32_t *tb, uint32_t v, uint32_t x) -> uint32_t {
+            uint32_t ev[8];
+#pragma unroll
+            for (int w = 0; w < 8; ++w) ev[w] = tb[16 * w + __builtin_amdgcn_ubfe(v, 4 * w, 4)];
+            return xor3(xor3(ev[0], ev[1], ev[2]), xor3(ev[3], ev[4], ev[5]), xor3(ev[6], ev[7], x));
+          };
+          const uint32_t u = nib_mul(x3tl, rr[3], nib_mul(x2tl, rr[2], nib_mul(xtl, rr[1], rr[0])));
+          R = group_xor(nib_mul(qrow, u, 0u), 3);
+          const uint32_t tz = 128u * Lg - ga - gM;
+          uint32_t bw = tzl[2u * tz + s], p = 0;
+#pragma unroll
+          for (int tt = 0; tt < 4; ++tt) {
+            const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)R, (int)(4u * s + tt), 1);
+            p = and_xor(m, bw, p);
+            bw = and_xor((uint32_t)((int32_t)bw >> 31), kXInv, bw << 1);
+          }
+          R = group_xor(p, 3);
+        }
+        if (ABL & 16) return;
+        if (s == 0) lay[2u * e] = ~R;  // (the group's entries are dead: both cursors are past it)
+      };
+
+      uint32_t fd_seq = 0, fd_k = 0, fd_L, fd_a, fd_M, fd_e;
+      auto fd_enter = [&](uint32_t seq) {
+        const u32x2 rg = *reinterpret_cast<const u32x2 *>(fifo + 2u * (seq & (kWgFifo - 1u)));
+        const uint32_t eb = __builtin_amdgcn_readfirstlane(rg[0]), el = __builtin_amdgcn_readfirstlane(rg[1]);
+        fd_e = eb + g < el ? eb + g : el;
+        const u32x2 dv = lay_at(fd_e);
+        fd_a = dv[0] & 127u;
+        fd_M = (dv[1] >> 16) - 4u;
+        fd_L = __builtin_amdgcn_readfirstlane((fd_a + fd_M + 127u) >> 7);
+      };
+      fd_enter(0);
+      uint32_t fd_hl = __ballot(fd_a > 88u) != 0 ? 2u : 1u;
+      uint32_t fd_span = fd_L - 1u > fd_hl ? fd_L - 1u - fd_hl : 0u;
+      uint32_t r[4] = {0u, 0u, 0u, 0u};
+      uint32_t xr[4] = {ring[0][0], ring[0][1], ring[0][2], ring[0][3]};
+      uint32_t quiet = 0;
+      auto quiet_step = [&](int u, uint32_t ahead) {
+        const u32x4 wn = ring[(u + 1) % D];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t t0 = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0400u));
+          const uint32_t t1 = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0500u) + 128);
+          const uint32_t t2 = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo1, 0x0C020600u));
+          const uint32_t t3 = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo1, 0x0C020700u) + 128);
+          xr[i] = xor3(t0, t1, xor3(t2, t3, wn[i]));
+        }
+        ring[u] = line_load(ld.line0 + 128ull * (ld_k + ahead));
+      };
+      auto fold_loop = [&](auto wordsv) {
+        auto full_step = [&](int u, bool &done) {
+          const u32x4 wn = ring[(u + 1) % D];
+          if (!(ABL & 8) && fd_k - fd_hl >= fd_span) {  // wave-uniform: an edge line
+            const u32x4 wc = ring[u];
+            const int rel0 = (int)(128u * fd_k + 16u * s) - (int)fd_a;
+            if constexpr (decltype(wordsv)::value) {
+              if (fd_k < fd_hl) {  // wave-uniform: a head line
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                  const int rel = rel0 + 4 * i;
+                  const uint32_t keep = (uint32_t)(((rel - (int)fd_M) & ~rel) >> 31);
+                  const uint32_t k = __builtin_elementwise_min((uint32_t)rel >> 2, 15u);
+                  const u32x2 ev = *reinterpret_cast<const u32x2 *>(etl + 2 * k);
+                  xr[i] = xor3(xr[i], wc[i], ((wc[i] & keep) | ev[0]) ^ ev[1]);
+                }
+              } else {
+                const int lim = (int)fd_M - 1 - rel0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) xr[i] ^= wc[i] & (uint32_t)((lim - 4 * i) >> 31);
+              }
+            } else if (fd_k < fd_hl) {  // wave-uniform: a head line (byte-granular)
+#pragma unroll
+              for (int i = 0; i < 4; ++i) xr[i] = xor3(xr[i], wc[i], edge_word(wc[i], rel0 + 4 * i, (int)fd_M));
+            } else {  // the last line past the head lines: the word keeps its low clamp(M - rel, 0, 4) bytes
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                const int rb = (int)fd_M - (rel0 + 4 * i);
+                const uint32_t cb = 8u * (uint32_t)__builtin_elementwise_min(__builtin_elementwise_max(rb, 0), 4);
+                xr[i] ^= wc[i] & ~(uint32_t)((1ull << cb) - 1u);
+              }
+            }
+          }
+          uint32_t tl[4][4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            tl[i][0] = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0400u));
+            tl[i][1] = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo0, 0x0C0C0500u) + 128);
+            tl[i][2] = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo1, 0x0C020600u));
+            tl[i][3] = lds_at(tab, __builtin_amdgcn_perm(xr[i], lt.lo1, 0x0C020700u) + 128);
+          }
+          if (++fd_k == fd_L) {  // wave-uniform: the group is folded
+#pragma unroll
+            for (int i = 0; i < 4; ++i) r[i] = xor3(tl[i][0], tl[i][1], tl[i][2] ^ tl[i][3]);
+            finish_group(r, fd_L, fd_a, fd_M, fd_e);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) xr[i] = wn[i];
+            fd_k = 0;
+            if (fd_seq < ld_seq) {  // wave-uniform: the load cursor entered a next group
+              ++fd_seq;
+              fd_enter(fd_seq);
+              fd_hl = __ballot(fd_a > 88u) != 0 ? 2u : 1u;
+              fd_span = fd_L - 1u > fd_hl ? fd_L - 1u - fd_hl : 0u;
+            } else {
+              done = true;
+              fd_L = 0xFFFFFFFFu;
+            }
+          } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) xr[i] = xor3(tl[i][0], tl[i][1], xor3(tl[i][2], tl[i][3], wn[i]));
+          }
+          ring[u] = ld_issue();
+          ld_advance();
+          const uint32_t nf = (fd_k >= fd_hl && fd_k + 1 < fd_L) ? fd_L - 1u - fd_k : 0u;
+          const uint32_t nl = ld_L - 1u - ld_k;
+          quiet = nf < nl ? nf : nl;
+        };
+        bool done = false;
+        while (!done) {
+          if (!(ABL & 8) && quiet >= (uint32_t)D) {  // wave-uniform: D quiet steps, no per-step control
+#pragma unroll
+            for (int u = 0; u < D; ++u) {
+              __builtin_amdgcn_sched_barrier(0);
+              quiet_step(u, (uint32_t)u);
+            }
+            quiet -= D;
+            fd_k += D;
+            ld_k += D;
+            continue;
+          }
+#pragma unroll
+          for (int u = 0; u < D; ++u) {
+            __builtin_amdgcn_sched_barrier(0);
+            full_step(u, done);
+          }
+        }
+      };
+      if (words)
+        fold_loop(std::true_type{});
+      else
+        fold_loop(std::false_type{});
+    }
+    // 4. out[i] from the layout (out[i] held the packet's position)
+    uint32_t pv[kWgPer];
+#pragma unroll
+    for (int k = 0; k < (int)kWgPer; ++k) {
+      const uint32_t j = (uint32_t)k * kBlock + threadIdx.x;
+      pv[k] = j < P ? __builtin_nontemporal_load(a.out + c0 + j) : 0xFFFFFFFFu;
+    }
+    __syncthreads();  // every group folded
+#pragma unroll
+    for (int k = 0; k < (int)kWgPer; ++k) {
+      const uint32_t j = (uint32_t)k * kBlock + threadIdx.x;
+      if (j >= P) continue;
+      const uint32_t v = pv[k] != 0xFFFFFFFFu ? lay[2u * pv[k]] : 0u;
+      __builtin_nontemporal_store(gather_one(a, c0 + j, pv[k], v), a.out + c0 + j);
+    }
+    __syncthreads();  // the layout is read: the next chunk may overwrite it
+  }
+}
+
 // Gather: block b serves pass block b's packets.  A staged block's results
 // sit in two contiguous ranges (its small range, its big range): they are
 // read coalesced into LDS in the block's layout order and pos_of indexes
@@ -1400,6 +1826,33 @@ static void launch_gather(const RsckArgs &a, const PassShape &ps, hipStream_t st
     case kPassUnroll: hipLaunchKernelGGL((rsck_gather<kPassUnroll, false>), dim3(ps.grid), dim3(kPassBlock), 0, st, a); break;
     default: hipLaunchKernelGGL((rsck_gather<kPassUnrollBig, false>), dim3(ps.grid), dim3(kPassBlock), 0, st, a); break;
   }
+}
+
+hipError_t launch_rswg(const RsckArgs &a, int grid, hipStream_t st, hipEvent_t *pass_ev) {
+  (void)hipGetLastError();  // a stale error of an earlier, unrelated HIP call must not fail this launch
+  if (a.count == 0) return hipSuccess;
+  if (a.count > kRsMaxCount) return hipErrorInvalidValue;
+  // RICRC_PASS_TIMES: the one kernel counts as the fold (bucket, one-line and gather 0)
+  if (pass_ev) {
+    (void)hipEventRecord(pass_ev[0], st);
+    (void)hipEventRecord(pass_ev[1], st);
+  }
+  hipLaunchKernelGGL((icrc_rswg_kernel<0>), dim3(grid), dim3(kBlock), 0, st, a);
+  if (pass_ev)
+    for (int k = 2; k < 5; ++k) (void)hipEventRecord(pass_ev[k], st);
+  return hipGetLastError();
+}
+
+uint64_t rs_wg_chunks(uint64_t count, int grid, const uint32_t (&w)[8]) {
+  // the heaviest workgroup's share: count x w_max / w_mean (xcd_share), rounded up
+  uint64_t wsum = 0, wmax = 0;
+  for (int x = 0; x < 8; ++x) {
+    wsum += w[x];
+    wmax = w[x] > wmax ? w[x] : wmax;
+  }
+  const uint64_t g = grid > 0 ? (uint64_t)grid : 1u;
+  const uint64_t share = wsum ? (count * wmax * 8u + wsum * g - 1u) / (wsum * g) + 1u : (count + g - 1u) / g;
+  return (share + kWgCap - 1u) / kWgCap;
 }
 
 hipError_t launch_rsck(RsckArgs &a, int grid, int pass_cap, hipStream_t st, hipEvent_t *pass_ev) {

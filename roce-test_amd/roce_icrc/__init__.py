@@ -615,6 +615,8 @@ def _launch_dict(info: LaunchInfo) -> dict:
     if info.pass_grid:
         d.update(pass_grid=info.pass_grid, pass_unroll=info.pass_unroll,
                  one_line_in=("kernel", "gather", "fold")[info.one_line], gather_grid=info.gather_grid)
+    elif info.one_line == 2:  # the workgroup-local ragged kernel: one launch, no bucket / gather passes
+        d.update(one_line_in="fold", passes=1)
     return d
 
 

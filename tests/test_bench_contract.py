@@ -139,12 +139,12 @@ def test_kernel_labels_follow_the_dispatch():
     mix = bench.kernel_label(mixa, count=mixa.count)  # C4's 4 M packets: the ragged pipeline's passes, in launch order
     fold = "strided-chain fold (8 packets of >= 2 lines a group; one-line packets one a lane) (icrc_rsck_kernel)"
     assert mix.split(" -> ") == ["bucket pass (rsck_bucket)", fold, "gather (rsck_gather)"]
-    # C4's 8-GPU shard (about 524 K packets): the same three passes
+    # C4's 8-GPU shard (about 524 K packets): the ragged path in one workgroup-local launch
     shard = bench.kernel_label(bench.parse(["--mix", "--count", "524288"]), count=524288)
-    assert shard == mix
+    assert shard == "workgroup-local ragged kernel (classify, fold, write in one launch) (icrc_rswg_kernel)"
     # a framed 4 KiB NIC ring (L3 at 14): the SCK's framed variant over the slots
     assert "(icrc_sck_kernel)" in lab("--l3-offset", "14", "--stride", "4096")
-    assert "(rsck_bucket)" in lab("--l3-offset", "14", "--stride", "1536")
+    assert "(icrc_rswg_kernel)" in lab("--l3-offset", "14", "--stride", "1536")
     assert "family_fix_kernel" in lab("--size", "64", "--family", "v6")
     assert "family_fix_kernel" not in lab("--family", "v6")  # the SCK applies IPv6 masks natively
     assert "count/plan" not in mix and "scatter" not in mix
@@ -317,7 +317,7 @@ def test_slot_lengths_flag():
     assert a.slot_lengths == (64, 1010) and a.pkt == 1010
     T, cuts, lens = bench.shard_plan(a, 1)
     assert T == 1 << 20 and cuts == [0, T] and lens.min() >= 64 and lens.max() <= 1010
-    assert "(rsck_bucket)" in bench.kernel_label(a)
+    assert "(icrc_rswg_kernel)" in bench.kernel_label(a, count=a.count)  # 1 M slots: two chunks a workgroup
     assert bench.traffic_record(False, a.size, a.count, 14, 1024, (64, 1010))[0] == \
         "pmc_traffic_ring14_1024_len64-1010.json"
     for bad in (["--stride", "1024", "--slot-lengths", "64:1011", "--l3-offset", "14"],

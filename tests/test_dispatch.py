@@ -8,6 +8,7 @@ roce_icrc = pytest.importorskip("roce_icrc")
 
 BASE = 1 << 20  # 16-byte aligned
 OFF, LEN = 0x10000, 0x20000  # "some device array"
+RAGGED = ("rsck_bucket", "icrc_rswg_kernel")  # the three-pass pipeline, or its one-launch workgroup-local form
 
 
 def path(count=1000, **kw):
@@ -30,9 +31,9 @@ def test_framed_rings_full_slots():
     for slot in (1024, 2048, 4096):
         for l3 in (1, 14, 18, 22, 92):
             assert path(stride=slot, l3_offset=l3) == "icrc_sck_kernel", (slot, l3)
-    assert path(stride=4096, l3_offset=93).startswith("rsck_bucket")  # a mask byte past line 0
-    assert path(stride=1536, l3_offset=14).startswith("rsck_bucket")
-    assert path(base=BASE + 2, stride=4096, l3_offset=14).startswith("rsck_bucket")
+    assert path(stride=4096, l3_offset=93).startswith(RAGGED)  # a mask byte past line 0
+    assert path(stride=1536, l3_offset=14).startswith(RAGGED)
+    assert path(base=BASE + 2, stride=4096, l3_offset=14).startswith(RAGGED)
     assert path(stride=4096, l3_offset=14, family="auto") == "icrc_sck_kernel+family_fix_kernel"
 
 
@@ -41,8 +42,8 @@ def test_rings_with_slot_lengths():
     strided-chain variant that stops each lane at its packet's end measured
     no faster overall; profiles/r05/NOTES.md)."""
     for slot in (1024, 2048, 4096):
-        assert path(stride=slot, l3_offset=14, lengths=LEN).startswith("rsck_bucket")
-    assert path(stride=4096, lengths=LEN, offsets=OFF).startswith("rsck_bucket")
+        assert path(stride=slot, l3_offset=14, lengths=LEN).startswith(RAGGED)
+    assert path(stride=4096, lengths=LEN, offsets=OFF).startswith(RAGGED)
 
 
 def test_ragged_batches():
@@ -50,7 +51,12 @@ def test_ragged_batches():
     one-line kernel only under RICRC_ONE_LINE_IN_GATHER=1 beyond 524,288 packets,
     tests/test_gpu_parity.py)."""
     assert path(count=4 << 20, offsets=OFF, lengths=LEN) == "rsck_bucket+icrc_rsck_kernel+rsck_gather"
-    assert path(count=524288, offsets=OFF, lengths=LEN) == "rsck_bucket+icrc_rsck_kernel+rsck_gather"
+    # up to one chunk of 2304 packets per workgroup (C4's 8-GPU shard): one launch, workgroup-local
+    assert path(count=524288, offsets=OFF, lengths=LEN) == "icrc_rswg_kernel"
+    assert path(count=540_000, offsets=OFF, lengths=LEN) == "icrc_rswg_kernel"  # C4 strong, its largest rank
+    assert path(count=1 << 20, stride=1024, l3_offset=14, lengths=LEN) == "icrc_rswg_kernel"  # 1 M ring slots: 2 chunks
+    assert path(count=4 << 20, stride=1024, l3_offset=14, lengths=LEN).startswith("rsck_bucket")  # 4 M: the pipeline
+    assert path(count=3, offsets=OFF, lengths=LEN) == "icrc_rswg_kernel"
 
 
 def test_launch_info_reports_every_path():
@@ -70,5 +76,7 @@ def test_launch_info_reports_every_path():
     rag = li(4 << 20, offsets=OFF, lengths=LEN)
     assert rag["grid"] == 256 and rag["pass_grid"] == 256 and rag["one_line_in"] == "fold"
     assert rag["lanes_per_packet"] == 8
+    wg = li(524288, offsets=OFF, lengths=LEN)  # the workgroup-local kernel: no bucket / gather passes
+    assert wg["grid"] == 256 and "pass_grid" not in wg and wg["passes"] == 1 and wg["one_line_in"] == "fold"
     with pytest.raises(roce_icrc.ICRCError):
         li(0, stride=64)

@@ -69,7 +69,7 @@ def test_framed_ring_same_as_ragged_pipeline(ctx, ctx_env):
     frames = np.random.default_rng(5).integers(0, 256, size=count * stride, dtype=np.uint8)
     d = _dev(frames)
     rag = ctx_env(RICRC_NO_FRAMED=1)
-    assert roce_icrc.kernel_path(d, count, stride=stride, l3_offset=18, ctx=rag).startswith("rsck_bucket")
+    assert roce_icrc.kernel_path(d, count, stride=stride, l3_offset=18, ctx=rag).startswith(("rsck_bucket", "icrc_rswg_kernel"))
     a, b = _out(count), _out(count)
     ctx.batch_device(d, count, a, stride=stride, l3_offset=18)
     rag.batch_device(d, count, b, stride=stride, l3_offset=18)
@@ -84,11 +84,11 @@ def test_framed_ring_not_taken(ctx):
     d = torch.zeros(4096 * 8 + 16, dtype=torch.uint8, device="cuda")
     path = lambda **kw: roce_icrc.kernel_path(kw.pop("base", d), 8, ctx=ctx, **kw)  # noqa: E731
     assert path(stride=4096, l3_offset=14) == "icrc_sck_kernel"
-    assert path(stride=1536, l3_offset=14).startswith("rsck_bucket")
-    assert path(stride=4096, l3_offset=93).startswith("rsck_bucket")
-    assert path(base=d[2:], stride=4096, l3_offset=14).startswith("rsck_bucket")
+    assert path(stride=1536, l3_offset=14).startswith(("rsck_bucket", "icrc_rswg_kernel"))
+    assert path(stride=4096, l3_offset=93).startswith(("rsck_bucket", "icrc_rswg_kernel"))
+    assert path(base=d[2:], stride=4096, l3_offset=14).startswith(("rsck_bucket", "icrc_rswg_kernel"))
     lens = torch.full((8,), 1000, dtype=torch.int32, device="cuda")
-    assert path(stride=4096, l3_offset=14, lengths=lens).startswith("rsck_bucket")
+    assert path(stride=4096, l3_offset=14, lengths=lens).startswith(("rsck_bucket", "icrc_rswg_kernel"))
 
 
 def test_framed_ring_verify_mode(ctx):
@@ -181,13 +181,13 @@ def test_slot_lengths_match_oracle(ctx, ctx_env, stride, l3):
     frames = rng.integers(0, 256, size=count * stride + 4096, dtype=np.uint8)  # slack: packets past the last slot
     lens = _slot_lens(rng, count, stride, l3)
     d, d_len = _dev(frames), _dev(lens)
-    assert roce_icrc.kernel_path(d, count, stride=stride, lengths=d_len, l3_offset=l3, ctx=ctx).startswith("rsck_bucket")
+    assert roce_icrc.kernel_path(d, count, stride=stride, lengths=d_len, l3_offset=l3, ctx=ctx).startswith(("rsck_bucket", "icrc_rswg_kernel"))
     want = _want_slots(frames, lens, stride, count, l3)
     out = _out(count)
     ctx.batch_device(d, count, out, stride=stride, lengths=d_len, l3_offset=l3)
     np.testing.assert_array_equal(_host_u32(out), want)
     rag = ctx_env(RICRC_NO_FRAMED=1)
-    assert roce_icrc.kernel_path(d, count, stride=stride, lengths=d_len, l3_offset=l3, ctx=rag).startswith("rsck_bucket")
+    assert roce_icrc.kernel_path(d, count, stride=stride, lengths=d_len, l3_offset=l3, ctx=rag).startswith(("rsck_bucket", "icrc_rswg_kernel"))
     out2 = _out(count)
     rag.batch_device(d, count, out2, stride=stride, lengths=d_len, l3_offset=l3)
     np.testing.assert_array_equal(_host_u32(out2), want)

@@ -282,17 +282,19 @@ def test_one_line_packets_three_ways(ctx, ctx_env, count):
     want = oracle_c.icrc_batch(buf, offsets=offs, lengths=lens, threads=16)
     want[bad] = 0
     d_buf, d_offs, d_lens = _dev(buf), _dev(offs), _dev(lens_dev)
+    pipe = ctx_env(RICRC_NO_WG=1)  # the three-pass pipeline (default here: the workgroup-local kernel)
     sides = ctx_env(RICRC_ONE_LINE_IN_GATHER=1)
     whole = ctx_env(RICRC_ONE_LINE_IN_GATHER=1, RICRC_NO_GATHER_SPLIT=1)
-    prop = ctx_env(RICRC_SMALL_SLOTS=0)  # the fold's rounds dealt by each wave's work, not to slots 0..11
-    lf, li, lw = (c.launch_info(d_buf, count, offsets=d_offs, lengths=d_lens) for c in (ctx, sides, whole))
+    prop = ctx_env(RICRC_SMALL_SLOTS=0, RICRC_NO_WG=1)  # the fold's rounds dealt by each wave's work
+    lf, li, lw = (c.launch_info(d_buf, count, offsets=d_offs, lengths=d_lens) for c in (pipe, sides, whole))
     assert lf["one_line_in"] == "fold" and lf["gather_grid"] == lf["pass_grid"]
     assert li["one_line_in"] == "gather" and li["gather_grid"] == 2 * li["pass_grid"] <= 256
     assert lw["one_line_in"] == "gather" and lw["gather_grid"] == lw["pass_grid"] == li["pass_grid"]
-    for c in (ctx, sides, whole):
+    for c in (pipe, sides, whole):
         assert roce_icrc.kernel_path(d_buf, count, offsets=d_offs, lengths=d_lens, ctx=c) == \
             "rsck_bucket+icrc_rsck_kernel+rsck_gather"
-    for c in (ctx, sides, whole, prop):
+    assert roce_icrc.kernel_path(d_buf, count, offsets=d_offs, lengths=d_lens, ctx=ctx) == "icrc_rswg_kernel"
+    for c in (ctx, pipe, sides, whole, prop):
         out = _out(count)
         c.batch_device(d_buf, count, out, offsets=d_offs, lengths=d_lens, stream=_stream())
         np.testing.assert_array_equal(_host_u32(out), want)
@@ -303,7 +305,7 @@ def test_one_line_packets_three_ways(ctx, ctx_env, count):
             o = int(offs[i]) + int(lens[i]) - 4
             stamped[o:o + 4] = np.frombuffer(int(want[i]).to_bytes(4, "little"), np.uint8)
             want_v[i] = 1
-    for c in (ctx, sides, whole):
+    for c in (ctx, pipe, sides, whole):
         out = _out(count)
         c.batch_device(_dev(stamped), count, out, offsets=d_offs, lengths=d_lens, stream=_stream(), verify=True)
         got = _host_u32(out)
@@ -571,16 +573,18 @@ def test_c4_full_size_bit_exact(ctx):
 
 
 @pytest.mark.slow
+@pytest.mark.parametrize("route", ["wg", "pipeline"])
 @pytest.mark.parametrize("shard", ["c4s", "c4_strong_rank7"])
-def test_c4_shard_full_size_bit_exact(ctx, shard):
+def test_c4_shard_full_size_bit_exact(ctx, ctx_env, shard, route):
     """C4's 8-GPU shard at full size, as bench.py builds it: the stand-in
     (--mix --count 524288: the first 524,288 packets of the bench seed's mix)
     and rank 7 of C4 strong-scaled over 8 GPUs (4 M packets cut at equal
-    bytes).  Both take the shard's pipeline -- the bucket pass at 4 packets
-    per thread on <= 128 blocks, the fold kernel folding the one-line packets
-    (one lane each, on wave slots 0..11) before its groups, a plain gather
-    (ricrc_launch_info: one_line_in "fold") -- and every ICRC is compared
-    with the C oracle on the very same bytes, then every trailer stamped and
+    bytes).  Both take the workgroup-local kernel (one launch: classify, lay
+    out in LDS, fold with groups claimed from an LDS counter, write out[]);
+    with RICRC_NO_WG=1 the three-pass pipeline -- the bucket pass at 4
+    packets per thread on <= 128 blocks, the fold kernel folding the one-line
+    packets before its groups, a plain gather.  Every ICRC is compared with
+    the C oracle on the very same bytes, then every trailer stamped and
     verified."""
     import bench
     import roce_icrc
@@ -596,10 +600,14 @@ def test_c4_shard_full_size_bit_exact(ctx, shard):
     offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
     d = torch.empty(int(offs[-1] + lens[-1]), dtype=torch.uint8, device="cuda")
     d_offs, d_lens = _dev(offs), _dev(lens)
-    assert roce_icrc.kernel_path(d, count, offsets=d_offs, lengths=d_lens, ctx=ctx) == \
-        "rsck_bucket+icrc_rsck_kernel+rsck_gather"
-    li = ctx.launch_info(d, count, offsets=d_offs, lengths=d_lens)
-    assert li["one_line_in"] == "fold" and li["pass_unroll"] == 4 and li["pass_grid"] <= 128
+    if route == "pipeline":
+        ctx = ctx_env(RICRC_NO_WG=1)
+        assert roce_icrc.kernel_path(d, count, offsets=d_offs, lengths=d_lens, ctx=ctx) == \
+            "rsck_bucket+icrc_rsck_kernel+rsck_gather"
+        li = ctx.launch_info(d, count, offsets=d_offs, lengths=d_lens)
+        assert li["one_line_in"] == "fold" and li["pass_unroll"] == 4 and li["pass_grid"] <= 128
+    else:
+        assert roce_icrc.kernel_path(d, count, offsets=d_offs, lengths=d_lens, ctx=ctx) == "icrc_rswg_kernel"
     ctx.synth_ragged_device(d, bench.SEED, lo, count, d_offs, d_lens, stream=_stream())
     out = _out(count)
     ctx.batch_device(d, count, out, offsets=d_offs, lengths=d_lens, stream=_stream())
