@@ -1231,6 +1231,16 @@ __global__ __launch_bounds__(kBlock) void icrc_rswg_kernel(RsckArgs a) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t s = lane & 7, g = lane >> 3;
+  // ABL 524288 (timing only, tools/microbench/wg.hip): per-wave s_memrealtime
+  // stamps into a.pos_of, 8 words per wave: entry, layout done, one-line
+  // rounds done, fold done, end, descriptors in, ranks counted (the first
+  // chunk's), the XCD
+  uint32_t st_w[8] = {};
+  auto stamp = [&](int k) {
+    if (ABL & 524288) st_w[k] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
+  if (ABL & 524288) st_w[7] = (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID
   xcd_record(a.xcd_rec);
   const TableRegs tab_v = table_load(g_tab128);
   const uint32_t fin0 = a.fin[threadIdx.x], fin1 = a.fin[threadIdx.x + 1024u < kFinFold ? threadIdx.x + 1024u : 0u];
@@ -1278,6 +1288,10 @@ __global__ __launch_bounds__(kBlock) void icrc_rswg_kernel(RsckArgs a) {
       n[k] = a.len ? a.len[i] : a.fixed_len;
     }
     int odd = 0;
+    if (ABL & 524288) {  // (timing: the descriptors' arrival)
+      __builtin_amdgcn_s_waitcnt(0);
+      if (c0 == w_lo) stamp(5);
+    }
 #pragma unroll
     for (int k = 0; k < (int)kWgPer; ++k) {
       const uint32_t j = (uint32_t)k * kBlock + threadIdx.x;
@@ -1288,6 +1302,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rswg_kernel(RsckArgs a) {
       cr[k] = c | (rk << 10);
     }
     const bool words = __syncthreads_or(odd) == 0;  // (a barrier: the counts are complete)
+    if (c0 == w_lo) stamp(6);
 
     // 2. scan by key: one-line classes 1..kRsBigBase (keys 0..7), then the big
     //    classes by descending L (key 8 + j: class kRsClasses - 1 - j)
@@ -1342,6 +1357,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rswg_kernel(RsckArgs a) {
     }
     __syncthreads();
     const uint32_t NG = misc[0], NS = misc[1];
+    if (c0 == w_lo) stamp(1);
 
     // 3a. the one-line packets: rounds of 64 dealt evenly to wave slots 0..11
     {
@@ -1358,6 +1374,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rswg_kernel(RsckArgs a) {
       }
     }
 
+    if (c0 == w_lo) stamp(2);
     // 3b. the groups, claimed one at a time
     auto claim = [&]() -> uint32_t {
       uint32_t v = 0;
@@ -1578,6 +1595,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rswg_kernel(RsckArgs a) {
       else
         fold_loop(std::false_type{});
     }
+    stamp(3);
     // 4. out[i] from the layout (out[i] held the packet's position)
     uint32_t pv[kWgPer];
 #pragma unroll
@@ -1594,6 +1612,13 @@ __global__ __launch_bounds__(kBlock) void icrc_rswg_kernel(RsckArgs a) {
       __builtin_nontemporal_store(gather_one(a, c0 + j, pv[k], v), a.out + c0 + j);
     }
     __syncthreads();  // the layout is read: the next chunk may overwrite it
+  }
+  if ((ABL & 524288) && lane == 0) {
+    __builtin_amdgcn_s_waitcnt(0);
+    stamp(4);
+    const uint64_t w8 = 8ull * ((uint64_t)blockIdx.x * kWaves + wid);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a.pos_of[w8 + k] = st_w[k];
   }
 }
 
