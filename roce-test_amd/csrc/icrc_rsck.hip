@@ -373,6 +373,19 @@ __device__ __forceinline__ uint32_t edge_word(uint32_t w, int rel, int M) {
   return ((w & keep) | orm) ^ sx;
 }
 
+// edge_word with no end (M past the word) as two masks for a word at offset
+// rel: edge_word(w, rel, inf) = (w & ~drop) ^ set, so a fold that XORed w in
+// whole fixes it with xr ^= (w & drop) ^ set.
+__device__ __forceinline__ uint32_t __attribute__((ext_vector_type(2))) head_masks(int rel) {
+  const uint32_t keep = byte_span_mask(-rel, 4);
+  const uint32_t sh = (uint32_t)(rel + 3 < 0 ? 0 : rel + 3 > 63 ? 63 : rel + 3);
+  const uint32_t bits = (uint32_t)(((kMaskBits << 3) >> sh) & 0xFu);
+  const uint32_t orm = (rel > -4 && rel < 40) ? (expand_nibble(bits) & keep) : 0u;
+  const uint64_t s64 = (uint64_t)kSeed << 24;
+  const uint32_t sx = (rel > -4 && rel < 4) ? (uint32_t)(s64 >> (8u * (sh & 7u))) : 0u;
+  return {~(keep & ~orm), orm ^ sx};
+}
+
 
 }  // namespace
 
@@ -1213,7 +1226,9 @@ __global__ __launch_bounds__(kBlock) void icrc_rswg_kernel(RsckArgs a) {
   constexpr uint32_t kScrW = 2 * kRsClasses;      // class counts | class starts; then the runs
   constexpr uint32_t kFifoW = kWaves * kWgFifo * 2;
   constexpr uint32_t kMiscW = 16;
-  __shared__ uint32_t lds[kFinFold + kLdsWords + kTzWords + kLayW + kScrW + kFifoW + kMiscW];
+  constexpr int kHeadLo = -16, kHeadHi = 44;  // head words' offsets: rel0 clamped to [lo, hi], + 4 i
+  constexpr uint32_t kHeadN = kHeadHi + 12 - kHeadLo + 1, kHeadW = 2 * kHeadN;
+  __shared__ uint32_t lds[kFinFold + kLdsWords + kTzWords + kLayW + kScrW + kFifoW + kMiscW + kHeadW];
   uint32_t *xtl = lds;
   uint32_t *qtl = lds + 128;
   uint32_t *etl = lds + 128 + 8 * kFinQtStride;  // whole-word head masks: (or, xor) of word k = rel / 4
@@ -1225,6 +1240,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rswg_kernel(RsckArgs a) {
   uint32_t *runs = hcnt;  // after the placement: run r = (g0 | L << 16, e0 | cnt << 16)
   uint32_t *fifo_all = hcnt + kScrW;
   uint32_t *misc = fifo_all + kFifoW;  // 0 groups, 1 one-line packets, 2 claim counter, 3.. scan totals
+  uint32_t *htl = misc + kMiscW;       // byte-granular head words: (drop, set) by offset (head_masks)
   static_assert(sizeof(lds) <= 160 * 1024, "LDS");
   static_assert(kWgCap < 65536 && kRsClasses <= kBlock, "16-bit layout fields, one class per thread");
 
@@ -1264,6 +1280,11 @@ __global__ __launch_bounds__(kBlock) void icrc_rswg_kernel(RsckArgs a) {
   if (threadIdx.x < kTzWords) tzl[threadIdx.x] = tz_v;
   lds[threadIdx.x] = fin0;  // the finish tables, built by the host (icrc_math.h build_fin_tables)
   if (threadIdx.x + 1024u < kFinFold) lds[threadIdx.x + 1024u] = fin1;
+  if (threadIdx.x < kHeadN) {
+    const auto hm = head_masks((int)threadIdx.x + kHeadLo);
+    htl[2u * threadIdx.x] = hm[0];
+    htl[2u * threadIdx.x + 1u] = hm[1];
+  }
 
   const LaneTab lt{(lane & 31) << 2, ((lane & 31) << 2) | 0x10000u};
   const uint32_t *qrow = qtl + s * kFinQtStride;
@@ -1524,15 +1545,24 @@ __global__ __launch_bounds__(kBlock) void icrc_rswg_kernel(RsckArgs a) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) xr[i] ^= wc[i] & (uint32_t)((lim - 4 * i) >> 31);
               }
-            } else if (fd_k < fd_hl) {  // wave-uniform: a head line (byte-granular)
+            } else {
+              if (fd_k < fd_hl) {  // wave-uniform: a head line (byte-granular): the word -> (word & ~drop) ^ set
+                const int rc = __builtin_elementwise_min(__builtin_elementwise_max(rel0, kHeadLo), kHeadHi);
+                const uint32_t *h = htl + 2 * (rc - kHeadLo);
 #pragma unroll
-              for (int i = 0; i < 4; ++i) xr[i] = xor3(xr[i], wc[i], edge_word(wc[i], rel0 + 4 * i, (int)fd_M));
-            } else {  // the last line past the head lines: the word keeps its low clamp(M - rel, 0, 4) bytes
+                for (int i = 0; i < 4; ++i) {
+                  const u32x2 dm = *reinterpret_cast<const u32x2 *>(h + 8 * i);
+                  xr[i] ^= (wc[i] & dm[0]) ^ dm[1];
+                }
+              }
+              if (fd_k >= fd_hl || fd_k + 1u == fd_L) {  // wave-uniform: the last line: bytes past M dropped
+                // (past M >= 40 the head masks are identity, so the two apply in turn)
 #pragma unroll
-              for (int i = 0; i < 4; ++i) {
-                const int rb = (int)fd_M - (rel0 + 4 * i);
-                const uint32_t cb = 8u * (uint32_t)__builtin_elementwise_min(__builtin_elementwise_max(rb, 0), 4);
-                xr[i] ^= wc[i] & ~(uint32_t)((1ull << cb) - 1u);
+                for (int i = 0; i < 4; ++i) {
+                  const int rb = (int)fd_M - (rel0 + 4 * i);
+                  const uint32_t cb = 8u * (uint32_t)__builtin_elementwise_min(__builtin_elementwise_max(rb, 0), 4);
+                  xr[i] ^= wc[i] & ~(uint32_t)((1ull << cb) - 1u);
+                }
               }
             }
           }
