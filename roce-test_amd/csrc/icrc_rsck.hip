@@ -1474,10 +1474,19 @@ __global__ __launch_bounds__(kBlock) void icrc_rswg_kernel(RsckArgs a) {
         if (ABL & 2) {
           R = group_xor(rr[0] ^ rr[1] ^ rr[2] ^ rr[3], 3);
         } else {
+          // v * (table's constant) ^ x: nibble w's entry at byte 64 w + 4 n_w of
+          // the tables; the 4 n_w sit in the bytes of two masked shifts of v, one
+          // byte extract (or SDWA add to a lane's base) per lookup
           auto nib_mul = [](const uint32_t *tb, uint32_t v, uint32_t x) -> uint32_t {
+            uint32_t lo4 = (v << 2) & 0x3C3C3C3Cu, hi4 = (v >> 2) & 0x3C3C3C3Cu;
+            asm volatile("" : "+v"(lo4), "+v"(hi4));  // (else folded back into a shift and mask per nibble)
+            const char *tc = reinterpret_cast<const char *>(tb);
             uint32_t ev[8];
 #pragma unroll
-            for (int w = 0; w < 8; ++w) ev[w] = tb[16 * w + __builtin_amdgcn_ubfe(v, 4 * w, 4)];
+            for (int k = 0; k < 4; ++k) {
+              ev[2 * k] = *reinterpret_cast<const uint32_t *>(tc + 128 * k + ((lo4 >> (8 * k)) & 0xFFu));
+              ev[2 * k + 1] = *reinterpret_cast<const uint32_t *>(tc + 128 * k + 64 + ((hi4 >> (8 * k)) & 0xFFu));
+            }
             return xor3(xor3(ev[0], ev[1], ev[2]), xor3(ev[3], ev[4], ev[5]), xor3(ev[6], ev[7], x));
           };
           const uint32_t u = nib_mul(x3tl, rr[3], nib_mul(x2tl, rr[2], nib_mul(xtl, rr[1], rr[0])));
@@ -1556,12 +1565,15 @@ __global__ __launch_bounds__(kBlock) void icrc_rswg_kernel(RsckArgs a) {
                 }
               }
               if (fd_k >= fd_hl || fd_k + 1u == fd_L) {  // wave-uniform: the last line: bytes past M dropped
-                // (past M >= 40 the head masks are identity, so the two apply in turn)
+                // (past M >= 40 the head masks are identity, so the two apply in turn);
+                // word i keeps its low clamp(M - rel0 - 4 i, 0, 4) bytes
+                const int rb8 = 8 * ((int)fd_M - rel0);
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                  const int rb = (int)fd_M - (rel0 + 4 * i);
-                  const uint32_t cb = 8u * (uint32_t)__builtin_elementwise_min(__builtin_elementwise_max(rb, 0), 4);
-                  xr[i] ^= wc[i] & ~(uint32_t)((1ull << cb) - 1u);
+                  int t8 = rb8 - 32 * i;
+                  asm volatile("" : "+v"(t8));  // (one med3, not max/sub/min)
+                  const uint32_t cb = (uint32_t)__builtin_elementwise_min(__builtin_elementwise_max(t8, 0), 32);
+                  xr[i] ^= wc[i] & (uint32_t)(~0ull << cb);
                 }
               }
             }
