@@ -1614,16 +1614,17 @@ __global__ __launch_bounds__(kBlock) void icrc_rswg_kernel(RsckArgs a) {
         };
         bool done = false;
         while (!done) {
-          if (!(ABL & 8) && quiet >= (uint32_t)D) {  // wave-uniform: D quiet steps, no per-step control
+          if (!(ABL & 8)) {
+            while (quiet >= (uint32_t)D) {  // wave-uniform: D quiet steps, no per-step control
 #pragma unroll
-            for (int u = 0; u < D; ++u) {
-              __builtin_amdgcn_sched_barrier(0);
-              quiet_step(u, (uint32_t)u);
+              for (int u = 0; u < D; ++u) {
+                __builtin_amdgcn_sched_barrier(0);
+                quiet_step(u, (uint32_t)u);
+              }
+              quiet -= D;
+              fd_k += D;
+              ld_k += D;
             }
-            quiet -= D;
-            fd_k += D;
-            ld_k += D;
-            continue;
           }
 #pragma unroll
           for (int u = 0; u < D; ++u) {
