@@ -55,7 +55,7 @@ struct Knobs {
   uint32_t gcost = 0;      // RICRC_RS_GCOST: the ragged fold's per-group cost, quarter lines (0: kRsGroupCost)
   bool one_line_in_gather = false;  // RICRC_ONE_LINE_IN_GATHER: the gather / a one-line kernel folds the one-line packets
   int small_slots = -1;    // RICRC_SMALL_SLOTS: wave slots taking the fold's one-line packets (-1: kRsSmallSlots)
-  int wg_chunks = 2;       // RICRC_WG_CHUNKS: ragged batches of up to this many kRsWgCap chunks per workgroup take
+  int wg_chunks = 8;       // RICRC_WG_CHUNKS: ragged batches of up to this many kRsWgCap chunks per workgroup take
                            // the workgroup-local kernel (0: never; RICRC_NO_WG = 0)
   int pass_grid = 0;       // RICRC_RS_PASS_GRID: cap the ragged bucket / gather pass grid (schedule studies)
   bool pass_times = false; // RICRC_PASS_TIMES: timing events between the ragged passes (ricrc_pass_times)
@@ -394,12 +394,12 @@ int sck_grid(const Dev &d, const uint8_t *base, const uint64_t *off, const uint3
 
 // Whether a ragged range of `count` packets takes the workgroup-local kernel
 // (icrc_rswg_kernel, one launch) rather than the bucket / fold / gather
-// pipeline: up to RICRC_WG_CHUNKS (default 2) chunks of kRsWgCap packets on
-// the most loaded workgroup -- C4's 8-GPU shard (524,288 packets) and NIC
-// rings of up to ~1.1 M slots on 256 CUs.  Same-box A/B (profiles/r06/,
-// session 5): the shard 0.148 -> 0.134 ms of kernel per step, 1 M x 1 KiB
-// slots of 64-1010 B (two chunks) 0.155 -> 0.149; C4's 4 M (eight chunks)
-// 0.968 against 0.976 on the pipeline, which keeps the large batches.
+// pipeline: up to RICRC_WG_CHUNKS (default 8) chunks of kRsWgCap packets on
+// the most loaded workgroup -- every batch up to ~4.6 M packets on 256 CUs
+// (C4, its 8-GPU shard, NIC rings of up to 4 M slots).  Same-box A/B
+// (profiles/r06/): the shard 0.148 -> 0.131 ms of kernel per step, C4's 4 M
+// (eight chunks) 0.971-0.974 -> 0.963-0.967 (session 20), 4 M x 4 KiB ring
+// slots of 64-4082 B 1.46 -> 1.40; larger batches keep the pipeline.
 // One decision for the launch, ricrc_kernel_path and ricrc_launch_info.
 bool rs_use_wg(const Dev &d, uint64_t count) {
   if (d.knobs.wg_chunks <= 0 || count == 0) return false;
@@ -784,7 +784,7 @@ Knobs read_knobs() {
   k.gcost = (uint32_t)std::min(1024L, std::max(0L, num("RICRC_RS_GCOST", 0)));  // the packed work counter's range
   k.one_line_in_gather = getenv("RICRC_ONE_LINE_IN_GATHER") != nullptr;
   k.small_slots = (int)std::min(16L, std::max(-1L, num("RICRC_SMALL_SLOTS", -1)));  // (16 waves a workgroup)
-  k.wg_chunks = getenv("RICRC_NO_WG") ? 0 : (int)std::min(64L, std::max(0L, num("RICRC_WG_CHUNKS", 2)));
+  k.wg_chunks = getenv("RICRC_NO_WG") ? 0 : (int)std::min(64L, std::max(0L, num("RICRC_WG_CHUNKS", 8)));
   k.pass_grid = (int)std::max(0L, num("RICRC_RS_PASS_GRID", 0));
   k.pass_times = getenv("RICRC_PASS_TIMES") != nullptr;
   k.fail_chunk = num("RICRC_FAIL_CHUNK", -1);

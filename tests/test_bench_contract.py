@@ -136,12 +136,16 @@ def test_kernel_labels_follow_the_dispatch():
     assert lab("--size", "64") == "quad ICRC kernel (64-byte packets, lane-quad transposes) (icrc_quad_kernel)"
     assert "(icrc_tsk_kernel)" in lab("--size", "256")
     mixa = bench.parse(["--mix"])
-    mix = bench.kernel_label(mixa, count=mixa.count)  # C4's 4 M packets: the ragged pipeline's passes, in launch order
+    mix = bench.kernel_label(mixa, count=mixa.count)  # C4's 4 M packets: eight chunks a workgroup, one launch
+    wg = "workgroup-local ragged kernel (classify, fold, write in one launch) (icrc_rswg_kernel)"
+    assert mix == wg
+    # past ~4.6 M packets on 256 CUs: the three-pass pipeline, in launch order
+    big = bench.kernel_label(bench.parse(["--mix", "--count", str(8 << 20)]), count=8 << 20)
     fold = "strided-chain fold (8 packets of >= 2 lines a group; one-line packets one a lane) (icrc_rsck_kernel)"
-    assert mix.split(" -> ") == ["bucket pass (rsck_bucket)", fold, "gather (rsck_gather)"]
-    # C4's 8-GPU shard (about 524 K packets): the ragged path in one workgroup-local launch
+    assert big.split(" -> ") == ["bucket pass (rsck_bucket)", fold, "gather (rsck_gather)"]
+    # C4's 8-GPU shard (about 524 K packets): one chunk a workgroup
     shard = bench.kernel_label(bench.parse(["--mix", "--count", "524288"]), count=524288)
-    assert shard == "workgroup-local ragged kernel (classify, fold, write in one launch) (icrc_rswg_kernel)"
+    assert shard == wg
     # a framed 4 KiB NIC ring (L3 at 14): the SCK's framed variant over the slots
     assert "(icrc_sck_kernel)" in lab("--l3-offset", "14", "--stride", "4096")
     assert "(icrc_rswg_kernel)" in lab("--l3-offset", "14", "--stride", "1536")
@@ -258,7 +262,8 @@ def test_side_configs_run_at_n1_on_cpu_stand_in():
     assert not any("error" in d for d in res.values()), res
     for name, d in res.items():
         assert d["value"] > 0 and d["ms_per_step"] > 0 and d["oracle_sampled_all_ranks"], name
-        assert d["roofline"]["frac"] > 0 and d["roofline"]["kernel_ms"] > 0 and "traffic" in d["roofline"], name
+        # (frac is rounded to 4 places: a CPU stand-in on a loaded host can round to 0)
+        assert d["roofline"]["frac"] >= 0 and d["roofline"]["kernel_ms"] > 0 and "traffic" in d["roofline"], name
         assert d["config"]["packets_total"] == 1500, name
     assert "mixed-MTU" in res["c4"]["metric"] and "64B" in res["c1"]["metric"] and "1024B" in res["c2"]["metric"]
     assert "fixed total" in res["c3"]["metric"] and "mixed-MTU" in res["c4s"]["metric"]

@@ -50,12 +50,13 @@ def test_ragged_batches():
     """The fold kernel takes the one-line packets at every size (a separate
     one-line kernel only under RICRC_ONE_LINE_IN_GATHER=1 beyond 524,288 packets,
     tests/test_gpu_parity.py)."""
-    assert path(count=4 << 20, offsets=OFF, lengths=LEN) == "rsck_bucket+icrc_rsck_kernel+rsck_gather"
+    assert path(count=4 << 20, offsets=OFF, lengths=LEN) == "icrc_rswg_kernel"  # C4: eight chunks a workgroup
+    assert path(count=8 << 20, offsets=OFF, lengths=LEN) == "rsck_bucket+icrc_rsck_kernel+rsck_gather"
     # up to one chunk of 2304 packets per workgroup (C4's 8-GPU shard): one launch, workgroup-local
     assert path(count=524288, offsets=OFF, lengths=LEN) == "icrc_rswg_kernel"
     assert path(count=540_000, offsets=OFF, lengths=LEN) == "icrc_rswg_kernel"  # C4 strong, its largest rank
     assert path(count=1 << 20, stride=1024, l3_offset=14, lengths=LEN) == "icrc_rswg_kernel"  # 1 M ring slots: 2 chunks
-    assert path(count=4 << 20, stride=1024, l3_offset=14, lengths=LEN).startswith("rsck_bucket")  # 4 M: the pipeline
+    assert path(count=8 << 20, stride=1024, l3_offset=14, lengths=LEN).startswith("rsck_bucket")  # 8 M: the pipeline
     assert path(count=3, offsets=OFF, lengths=LEN) == "icrc_rswg_kernel"
 
 
@@ -73,10 +74,10 @@ def test_launch_info_reports_every_path():
     assert st["grid"] == 256 and st["lanes_per_packet"] == 32
     head = li(1 << 20, stride=4096)  # the headline: 240 of 256 CUs, XCD-weighted
     assert head["grid"] == 240 and head["lanes_per_packet"] == 8 and head["xcd_weights"][0] > head["xcd_weights"][1]
-    rag = li(4 << 20, offsets=OFF, lengths=LEN)
+    rag = li(8 << 20, offsets=OFF, lengths=LEN)  # past eight chunks a workgroup: the three-pass pipeline
     assert rag["grid"] == 256 and rag["pass_grid"] == 256 and rag["one_line_in"] == "fold"
     assert rag["lanes_per_packet"] == 8
-    wg = li(524288, offsets=OFF, lengths=LEN)  # the workgroup-local kernel: no bucket / gather passes
+    wg = li(4 << 20, offsets=OFF, lengths=LEN)  # C4: the workgroup-local kernel, no bucket / gather passes
     assert wg["grid"] == 256 and "pass_grid" not in wg and wg["passes"] == 1 and wg["one_line_in"] == "fold"
     with pytest.raises(roce_icrc.ICRCError):
         li(0, stride=64)
