@@ -15,6 +15,8 @@
 #   c3s       512 K x 4096 B (C3's shard at N = 8)
 #   c4s       512 K mixed (C4's shard at N = 8: 4 M mixed over 8 GPUs)
 #   ring      1 M x 4096 B Ethernet-framed NIC ring slots, the L3 packet at 14
+#   ring_len  1 M x 1024 B ring slots, L3 at 14, a length per slot of 64..1010 B
+#   ringbench tools/ring_bench.py (every ring row)   pathbench tools/path_bench.py
 # Every GPU step runs under its own timeout; the session stops at the first
 # step that crashes, aborts or times out (rc >= 2); a plain test failure
 # (rc 1) lets the rest run.
@@ -40,6 +42,7 @@ cfg_args() {
     c3s) echo "--count 524288" ;;
     c4s) echo "--mix --count 524288" ;;
     ring) echo "--l3-offset 14 --stride 4096" ;;
+    ring_len) echo "--l3-offset 14 --stride 1024 --slot-lengths 64:1010" ;;
     *) echo "BAD" ;;
   esac
 }
@@ -53,6 +56,7 @@ pmc_args() {
     c3s) echo "--count 524288" ;;
     c4s) echo "--mix --count 524288" ;;
     ring) echo "--l3-offset 14 --stride 4096" ;;
+    ring_len) echo "--l3-offset 14 --stride 1024 --slot-lengths 64:1010" ;;
     *) echo "BAD" ;;
   esac
 }
@@ -99,6 +103,14 @@ print('$cfg', d['value'], d['ms_per_step'], r['kernel_ms'], r['frac'], r.get('tr
       ok $? "pmc $cfg"
       python3 -c "import json; d=json.load(open('$OUT/pmc_$cfg.json')); print('pmc $cfg', d['kernel_src'], \
 round(d['traffic_over_algorithmic'], 5))" | tee -a "$OUT/session.txt" ;;
+    ringbench)
+      timeout -k 10 300 python tools/ring_bench.py > "$OUT/ring_bench.jsonl" 2> "$OUT/ring_bench.err"
+      ok $? ringbench
+      cut -c1-160 "$OUT/ring_bench.jsonl" | tee -a "$OUT/session.txt" ;;
+    pathbench)
+      timeout -k 10 600 python tools/path_bench.py ${PATH_ARGS:-} > "$OUT/path_bench.jsonl" 2> "$OUT/path_bench.err"
+      ok $? pathbench
+      cut -c1-200 "$OUT/path_bench.jsonl" | tee -a "$OUT/session.txt" ;;
     microbench)
       (cd tools/microbench && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 "$cfg.hip" -o "$cfg" \
         > "../../$OUT/mb_${cfg}_build.log" 2>&1)
