@@ -183,7 +183,8 @@ def main():
             buf[ix] = rows[c:c + step].reshape(-1)
         del tmp, rows, starts
     out = torch.empty(count, dtype=torch.int32, device=dev)
-    paths = [(lbl, knob) for key, lbl, knob in (("rsck", "ragged pipeline (C4 mix)", None),)
+    kp = roce_icrc.kernel_path(buf, count, offsets=d_offs, lengths=d_lens, ctx=ctx)
+    paths = [(lbl, knob) for key, lbl, knob in (("rsck", f"ragged, C4 mix ({kp})", None),)
              if key in args.ragged_paths.split(",")]
     for label, knob in paths:
         if knob:
