@@ -247,7 +247,8 @@ def test_bench_side_configs_world2_gloo():
         d = res[k]
         assert d["scaling"] == "strong" and d["config"]["packets_total"] == 3001, k
         assert d["compute_only_ms_per_step"] > 0 and d["gather_ms"] > 0 and d["oracle_sampled_all_ranks"], k
-        assert d["roofline"]["frac"] > 0 and d["value"] > 0, k
+        # (frac is rounded to 4 places: a CPU stand-in on a loaded host can round to 0)
+        assert d["roofline"]["frac"] >= 0 and d["roofline"]["kernel_ms"] > 0 and d["value"] > 0, k
         assert got[1][0][k]["value"] == d["value"], k  # one number on every rank
         assert len(d["ranks"]["kernel_ms"]) == 2 and sum(d["ranks"]["shard_packets"]) == 3001, k
     assert "mixed-MTU" in res["c4_strong"]["metric"] and "fixed total" in res["c3_strong"]["metric"]
