@@ -1258,9 +1258,6 @@ __global__ __launch_bounds__(kBlock) void icrc_rswg_kernel(RsckArgs a) {
   stamp(0);
   if (ABL & 524288) st_w[7] = (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID
   xcd_record(a.xcd_rec);
-  const TableRegs tab_v = table_load(g_tab128);
-  const uint32_t fin0 = a.fin[threadIdx.x], fin1 = a.fin[threadIdx.x + 1024u < kFinFold ? threadIdx.x + 1024u : 0u];
-  const uint32_t tz_v = a.tzb[threadIdx.x < kTzWords ? threadIdx.x : 0];
   // This workgroup's packets: the union of its waves' XCD-weighted shares.
   uint64_t w_lo, w_hi;
   {
@@ -1276,6 +1273,23 @@ __global__ __launch_bounds__(kBlock) void icrc_rswg_kernel(RsckArgs a) {
     w_lo = l0;
     w_hi = h1;
   }
+  // The first chunk's descriptor lines, one load a 128-byte line, requested
+  // before the tables: their HBM round trip runs beside the tables' and the
+  // chunk's own descriptor loads find them in L2.
+  uint32_t pf = 0;
+  if (w_lo < w_hi) {
+    const uint64_t P0 = w_hi - w_lo < kWgCap ? w_hi - w_lo : kWgCap;
+    const uint32_t t = threadIdx.x;
+    const uint32_t no = a.off ? (uint32_t)((8u * P0 + 127u) >> 7) + 1u : 0u;
+    const uint32_t nl = a.len ? (uint32_t)((4u * P0 + 127u) >> 7) + 1u : 0u;
+    if (t < no)
+      pf = (uint32_t)a.off[w_lo + (16ull * t < P0 ? 16ull * t : P0 - 1u)];
+    else if (t < no + nl)
+      pf = a.len[w_lo + (32ull * (t - no) < P0 ? 32ull * (t - no) : P0 - 1u)];
+  }
+  const TableRegs tab_v = table_load(g_tab128);
+  const uint32_t fin0 = a.fin[threadIdx.x], fin1 = a.fin[threadIdx.x + 1024u < kFinFold ? threadIdx.x + 1024u : 0u];
+  const uint32_t tz_v = a.tzb[threadIdx.x < kTzWords ? threadIdx.x : 0];
   table_write(tab, tab_v);
   if (threadIdx.x < kTzWords) tzl[threadIdx.x] = tz_v;
   lds[threadIdx.x] = fin0;  // the finish tables, built by the host (icrc_math.h build_fin_tables)
@@ -1285,6 +1299,7 @@ __global__ __launch_bounds__(kBlock) void icrc_rswg_kernel(RsckArgs a) {
     htl[2u * threadIdx.x] = hm[0];
     htl[2u * threadIdx.x + 1u] = hm[1];
   }
+  asm volatile("" ::"v"(pf));  // (the prefetch lands here, not in the chunk loop)
 
   const LaneTab lt{(lane & 31) << 2, ((lane & 31) << 2) | 0x10000u};
   const uint32_t *qrow = qtl + s * kFinQtStride;
